@@ -1,0 +1,53 @@
+"""Build libicap.so for gfx950 with hipcc (in-tree, so it travels to the GPU box)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+LIB = HERE / "libicap.so"
+SOURCES = ["gemm.hip", "rows.hip", "attention.hip", "head.hip", "icap.cpp"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+         "-Wno-unused-variable", "-munsafe-fp-atomics"]
+
+
+def _stale() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    deps = [CSRC / s for s in SOURCES] + list(CSRC.glob("*.h")) + [HERE.parent / "include" / "icap.h"]
+    return any(p.stat().st_mtime > t for p in deps)
+
+
+def build(force: bool = False, verbose: bool = True) -> Path:
+    if not force and not _stale():
+        return LIB
+    objs = []
+    obj_dir = HERE / "build"
+    obj_dir.mkdir(exist_ok=True)
+    procs = []
+    for src in SOURCES:
+        obj = obj_dir / (src + ".o")
+        objs.append(obj)
+        cmd = [HIPCC, *FLAGS, "-x", "hip", "-c", str(CSRC / src), "-o", str(obj)]
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+    for cmd, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            sys.stderr.write(out.decode())
+            raise RuntimeError("hipcc failed: " + " ".join(cmd))
+        if verbose and out.strip():
+            sys.stderr.write(out.decode())
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,381 @@
+// Attention kernels of the captioning hot path.
+//
+// enc_attention: encoder self-attention (ViT N=197 x 12 heads, Grid N=49 x 8 heads; hd = 64,
+//   non-causal).  One workgroup per (image, head), 4 waves.  K and V of the head are staged in
+//   LDS once; each wave takes 16-query tiles.  Scores are computed transposed, S^T = K·Q^T,
+//   with v_mfma_f32_16x16x32_bf16 so a query sits on the lane and its keys in the accumulator
+//   registers: the softmax row-reduce is per-lane + two xor-shuffles, and the S^T accumulators
+//   are used directly as the B operand of O^T = V^T·P^T (k order permuted consistently), with
+//   V^T fragments delivered by ds_read_b64_tr_b16 transposed LDS reads.  In split mode every
+//   product carries the three terms hi·hi + lo·hi + hi·lo (activations are hi/lo bf16 planes).
+//
+// dec_self_attn: one decode step's causal self-attention over an fp32 KV cache (t <= max_len
+//   keys, one wave per (image, head), exact fp32 VALU math).
+//
+// cross_attn_absorbed: decoder cross-attention with the key projection absorbed into the query,
+//   score_h(s) = (q_h · Wk_h) · mem_s / sqrt(hd) (the q·bk term is constant over s and cancels
+//   in the softmax), context c_h = sum_s p_h(s) mem_s; the caller applies Wv_h and bv (sum p = 1).
+//   Memory (B,S,512) fp32 is read directly - it stays resident in the 256 MiB Infinity Cache
+//   across the 6 layers x 29 steps instead of 6 per-layer K/V projections.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+__device__ __forceinline__ void st_planes(bf16_t* base, long idx, long lo, int nsplit, float v) {
+  bf16_t hi, l;
+  split_bf(v, hi, l);
+  base[idx] = hi;
+  if (nsplit == 2) base[idx + lo] = l;
+}
+
+// Two ds_read_b64_tr_b16 (4 keys x 16 d each) concatenated into one 8-element MFMA operand.
+// Built with whole-vector shuffles/bit-casts: per-element short->__bf16 bit-casts miscompile
+// (hipcc ROCm 7.2 duplicated dwords via v_perm; found by tools/attn_debug.hip).
+__device__ __forceinline__ bf16x8 tr_pair(const char* p0, const char* p1) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)p0);
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)p1);
+  const s16x8 c = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+template <int NKT, bool SPLIT>
+__global__ __launch_bounds__(256) void enc_attention_kernel(const bf16_t* __restrict__ qkv, long ld, long lo,
+                                                            int N, int H, float scale, bf16_t* out,
+                                                            long out_ld, long out_lo) {
+  constexpr int NP = NKT * 16;           // padded keys (multiple of 32)
+  constexpr int MAT = NP * 128;           // bytes of one [NP][64] bf16 matrix
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kh = smem;
+  char* Vh = smem + MAT;
+  char* Kl = smem + 2 * MAT;
+  char* Vl = smem + 3 * MAT;
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int D = H * 64;
+  const bf16_t* base = qkv + (long)b * N * ld;
+
+  // stage K and V (zero-padded rows >= N); K swizzled for row-fragment reads, V plain for tr reads
+  for (int c = tid; c < NP * 8; c += 256) {
+    const int row = c >> 3, ch = c & 7;
+    u32x4 kh = {0, 0, 0, 0}, vh = kh, kl = kh, vl = kh;
+    if (row < N) {
+      const bf16_t* src = base + (long)row * ld + h * 64 + ch * 8;
+      kh = *(const u32x4*)(src + D);
+      vh = *(const u32x4*)(src + 2 * D);
+      if (SPLIT) {
+        kl = *(const u32x4*)(src + lo + D);
+        vl = *(const u32x4*)(src + lo + 2 * D);
+      }
+    }
+    const int ko = row * 128 + ((ch ^ (row & 7)) << 4), vo = row * 128 + ch * 16;
+    *(u32x4*)(Kh + ko) = kh;
+    *(u32x4*)(Vh + vo) = vh;
+    if (SPLIT) {
+      *(u32x4*)(Kl + ko) = kl;
+      *(u32x4*)(Vl + vo) = vl;
+    }
+  }
+  __syncthreads();
+
+  const int fr = lane & 15, g = lane >> 4;
+  const int nqt = (N + 15) / 16;
+  for (int qt = wave; qt < nqt; qt += 4) {
+    const int q = min(qt * 16 + fr, N - 1);
+    bf16x8 qh[2], ql[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16_t* src = base + (long)q * ld + h * 64 + ks * 32 + g * 8;
+      qh[ks] = *(const bf16x8*)src;
+      if (SPLIT) ql[ks] = *(const bf16x8*)(src + lo);
+    }
+    f32x4 s[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int row = kt * 16 + fr;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int off = row * 128 + (((ks * 4 + g) ^ (row & 7)) << 4);
+        const bf16x8 kh = *(const bf16x8*)(Kh + off);
+        acc = mfma16(kh, qh[ks], acc);
+        if (SPLIT) {
+          const bf16x8 kl = *(const bf16x8*)(Kl + off);
+          acc = mfma16(kl, qh[ks], acc);
+          acc = mfma16(kh, ql[ks], acc);
+        }
+      }
+      s[kt] = acc;
+    }
+    // softmax over keys for query (lane & 15): key of s[kt][r] = 16 kt + 4 g + r
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * 16 + g * 4 + r;
+        const float v = key < N ? s[kt][r] * scale : -INFINITY;
+        s[kt][r] = v;
+        m = fmaxf(m, v);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(s[kt][r] - m);
+        s[kt][r] = e;
+        l += e;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
+
+    // O^T[d][q] = sum_k V^T[d][k] P^T[k][q]
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int q4 = fr >> 2, p4 = fr & 3;
+#pragma unroll
+    for (int i = 0; i < NKT / 2; ++i) {
+      bf16x8 ph, pl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ph[j] = (__bf16)s[2 * i][j];
+        ph[4 + j] = (__bf16)s[2 * i + 1][j];
+        if (SPLIT) {
+          pl[j] = (__bf16)(s[2 * i][j] - (float)ph[j]);
+          pl[4 + j] = (__bf16)(s[2 * i + 1][j] - (float)ph[4 + j]);
+        }
+      }
+      const int key0 = 32 * i + 4 * g + q4;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int off0 = key0 * 128 + (dt * 16 + 4 * p4) * 2, off1 = off0 + 16 * 128;
+        const bf16x8 vh = tr_pair(Vh + off0, Vh + off1);
+        o[dt] = mfma16(vh, ph, o[dt]);
+        if (SPLIT) {
+          const bf16x8 vl = tr_pair(Vl + off0, Vl + off1);
+          o[dt] = mfma16(vl, ph, o[dt]);
+          o[dt] = mfma16(vh, pl, o[dt]);
+        }
+      }
+    }
+    const int qq = qt * 16 + fr;
+    if (qq < N) {
+      bf16_t* dst = out + ((long)b * N + qq) * out_ld + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16_t hv[4], lv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) split_bf(o[dt][r] * inv, hv[r], lv[r]);
+        const int d = dt * 16 + 4 * g;
+        *(u32x2*)(dst + d) = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+        if (SPLIT)
+          *(u32x2*)(dst + out_lo + d) =
+              (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// qkv rows: (b * n_new + i) with [q | k | v] of width 3D.  Cache kc/vc: [B][H][Lmax][64] fp32.
+__global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restrict__ qkv, int n_new, int t0,
+                                                           int H, float* kc, float* vc, int Lmax, int causal,
+                                                           float scale, bf16_t* out, long lo, int nsplit) {
+  __shared__ float sq[64];
+  __shared__ float sp[512];
+  const int h = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  float* kcb = kc + ((long)b * H + h) * Lmax * 64;
+  float* vcb = vc + ((long)b * H + h) * Lmax * 64;
+  const float* rows = qkv + (long)b * n_new * ld;
+  for (int i = 0; i < n_new; ++i) {
+    kcb[(long)(t0 + i) * 64 + lane] = rows[i * ld + D + h * 64 + lane];
+    vcb[(long)(t0 + i) * 64 + lane] = rows[i * ld + 2 * D + h * 64 + lane];
+  }
+  for (int i = 0; i < n_new; ++i) {
+    const int pos = t0 + i;
+    const int nkeys = causal ? pos + 1 : t0 + n_new;
+    __syncthreads();
+    sq[lane] = rows[i * ld + h * 64 + lane];
+    __syncthreads();
+    float m = -INFINITY;
+    for (int k0 = 0; k0 < nkeys; k0 += 64) {
+      const int key = k0 + lane;
+      float sc = -INFINITY;
+      if (key < nkeys) {
+        const float* kv = key < t0 ? kcb + (long)key * 64 : rows + (key - t0) * ld + D + h * 64;
+        float acc = 0.f;
+#pragma unroll 16
+        for (int d = 0; d < 64; ++d) acc = fmaf(sq[d], kv[d], acc);
+        sc = acc * scale;
+        sp[key] = sc;
+      }
+      m = fmaxf(m, sc);
+    }
+    m = wave_max(m);
+    float l = 0.f;
+    for (int k0 = 0; k0 < nkeys; k0 += 64) {
+      const int key = k0 + lane;
+      if (key < nkeys) {
+        const float e = __expf(sp[key] - m);
+        sp[key] = e;
+        l += e;
+      }
+    }
+    l = wave_sum(l);
+    __syncthreads();
+    float acc = 0.f;
+    for (int key = 0; key < nkeys; ++key) {
+      const float* vv = key < t0 ? vcb + (long)key * 64 : rows + (key - t0) * ld + 2 * D + h * 64;
+      acc = fmaf(sp[key], vv[lane], acc);
+    }
+    st_planes(out, ((long)b * n_new + i) * D + h * 64 + lane, lo, nsplit, acc / l);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// One workgroup (512 threads) per query row r; image = r / rows_per_image.
+// qt: [rows][H*Dm] fp32, mem: [images][S][Dm] fp32, out planes: [rows][H*Dm].
+constexpr int XH = 8;  // heads (d_model 512 / 64)
+__global__ __launch_bounds__(512) void cross_attn_absorbed_kernel(const float* __restrict__ qt,
+                                                                  const float* __restrict__ mem, int rows_per_image,
+                                                                  int S, int Dm, float scale, bf16_t* out, long lo,
+                                                                  int nsplit) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  float* sq = xs;                 // [Dm][XH]
+  float* sp = xs + Dm * XH;       // [256][XH] scores / probs
+  float* part = sp + 256 * XH;    // [256][XH] partial sums of the second d-half
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const float* qrow = qt + (long)r * XH * Dm;
+  const float* mb = mem + (long)(r / rows_per_image) * S * Dm;
+  for (int i = tid; i < XH * Dm; i += 512) {
+    const int h = i / Dm, d = i % Dm;
+    sq[d * XH + h] = qrow[i];
+  }
+  __syncthreads();
+  // scores: thread (s, half) dots over half of d
+  {
+    const int s = tid & 255, half = tid >> 8;
+    float acc[XH];
+#pragma unroll
+    for (int h = 0; h < XH; ++h) acc[h] = 0.f;
+    if (s < S) {
+      const float* mr = mb + (long)s * Dm;
+      const int d0 = half * (Dm / 2), d1 = d0 + Dm / 2;
+      for (int d = d0; d < d1; d += 4) {
+        const f32x4 mv = *(const f32x4*)(mr + d);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x4 qa = *(const f32x4*)(sq + (d + k) * XH);
+          const f32x4 qb = *(const f32x4*)(sq + (d + k) * XH + 4);
+          acc[0] = fmaf(qa[0], mv[k], acc[0]); acc[1] = fmaf(qa[1], mv[k], acc[1]);
+          acc[2] = fmaf(qa[2], mv[k], acc[2]); acc[3] = fmaf(qa[3], mv[k], acc[3]);
+          acc[4] = fmaf(qb[0], mv[k], acc[4]); acc[5] = fmaf(qb[1], mv[k], acc[5]);
+          acc[6] = fmaf(qb[2], mv[k], acc[6]); acc[7] = fmaf(qb[3], mv[k], acc[7]);
+        }
+      }
+      float* dst = (half ? part : sp) + s * XH;
+#pragma unroll
+      for (int h = 0; h < XH; ++h) dst[h] = acc[h];
+    }
+  }
+  __syncthreads();
+  // softmax per head: wave w handles head w (8 waves, 8 heads)
+  {
+    const int w = tid >> 6, lane = tid & 63;
+    float v[4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int s = c * 64 + lane;
+      v[c] = s < S ? (sp[s * XH + w] + part[s * XH + w]) * scale : -INFINITY;
+      m = fmaxf(m, v[c]);
+    }
+    m = wave_max(m);
+    float l = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      v[c] = (c * 64 + lane) < S ? __expf(v[c] - m) : 0.f;
+      l += v[c];
+    }
+    l = wave_sum(l);
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int s = c * 64 + lane;
+      if (s < S) sp[s * XH + w] = v[c] * inv;
+    }
+  }
+  __syncthreads();
+  // context: thread owns column d, all heads
+  for (int d = tid; d < Dm; d += 512) {
+    float acc[XH];
+#pragma unroll
+    for (int h = 0; h < XH; ++h) acc[h] = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const float mv = mb[(long)s * Dm + d];
+      const f32x4 pa = *(const f32x4*)(sp + s * XH), pb = *(const f32x4*)(sp + s * XH + 4);
+      acc[0] = fmaf(pa[0], mv, acc[0]); acc[1] = fmaf(pa[1], mv, acc[1]);
+      acc[2] = fmaf(pa[2], mv, acc[2]); acc[3] = fmaf(pa[3], mv, acc[3]);
+      acc[4] = fmaf(pb[0], mv, acc[4]); acc[5] = fmaf(pb[1], mv, acc[5]);
+      acc[6] = fmaf(pb[2], mv, acc[6]); acc[7] = fmaf(pb[3], mv, acc[7]);
+    }
+#pragma unroll
+    for (int h = 0; h < XH; ++h) st_planes(out, (long)r * XH * Dm + h * Dm + d, lo, nsplit, acc[h]);
+  }
+}
+
+template <int NKT, bool SPLIT>
+hipError_t run_enc(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale, bf16_t* out,
+                   long out_ld, long out_lo, hipStream_t s) {
+  const int lds = NKT * 16 * 128 * (SPLIT ? 4 : 2);
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_kernel<NKT, SPLIT>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((enc_attention_kernel<NKT, SPLIT>), dim3(H, B), dim3(256), lds, s, qkv, ld, lo, N, H,
+                     scale, out, out_ld, out_lo);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale,
+                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s) {
+  if (N <= 0 || B <= 0) return hipErrorInvalidValue;
+  if (N <= 64) {
+    return nsplit == 2 ? run_enc<4, true>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s)
+                       : run_enc<4, false>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s);
+  }
+  if (N <= 224) {
+    return nsplit == 2 ? run_enc<14, true>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s)
+                       : run_enc<14, false>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int H, float* kc, float* vc, int Lmax,
+                                int causal, float scale, bf16_t* out, long lo, int nsplit, hipStream_t s) {
+  if (t0 + n_new > Lmax || t0 + n_new > 512) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dec_self_attn_kernel, dim3(H, B), dim3(64), 0, s, qkv, n_new, t0, H, kc, vc, Lmax, causal,
+                     scale, out, lo, nsplit);
+  return hipGetLastError();
+}
+
+hipError_t launch_cross_attn_absorbed(const float* qt, const float* mem, int rows, int rows_per_image, int S, int H,
+                                      int Dm, float scale, bf16_t* out, long lo, int nsplit, hipStream_t s) {
+  if (H != XH || S > 256 || Dm % 8) return hipErrorInvalidValue;
+  const int lds = (Dm * XH + 2 * 256 * XH) * 4;
+  hipLaunchKernelGGL(cross_attn_absorbed_kernel, dim3(rows), dim3(512), lds, s, qt, mem, rows_per_image, S, Dm,
+                     scale, out, lo, nsplit);
+  return hipGetLastError();
+}

@@ -1,0 +1,105 @@
+// Output head of a decode step: fc_out (512 -> V=109) in exact fp32,
+// then either argmax (greedy, first index on ties like torch CPU argmax; vit:315-316) or an
+// inverse-CDF categorical sample on an injected uniform with its log-probability
+// (`_sample_with_log_probs`, scst_loss:229-239), and the next step's embedding
+// emb[tok] * sqrt(d) + pe[t+1] (vit:166-169) so the following layer GEMM can start at once.
+// One 128-thread workgroup per image row.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+__global__ __launch_bounds__(128) void head_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float hs[];
+  float* xs = hs;             // [Dm]
+  float* lg = hs + a.Dm;      // [128]
+  __shared__ int s_tok;
+  __shared__ float s_red[4];
+  __shared__ int s_idx[2];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* x = a.x + (long)r * a.Dm;
+  for (int d = tid; d < a.Dm; d += 128) xs[d] = x[d];
+  __syncthreads();
+  float logit = -INFINITY;
+  if (tid < a.V) {
+    const float* wr = a.W + (long)tid * a.Dm;
+    float acc = 0.f;
+    for (int d = 0; d < a.Dm; d += 4) {
+      const f32x4 wv = *(const f32x4*)(wr + d);
+      const f32x4 xv = *(const f32x4*)(xs + d);
+      acc = fmaf(xv[0], wv[0], acc);
+      acc = fmaf(xv[1], wv[1], acc);
+      acc = fmaf(xv[2], wv[2], acc);
+      acc = fmaf(xv[3], wv[3], acc);
+    }
+    logit = acc + a.bias[tid];
+    if (a.logits) a.logits[(long)r * a.ld_logits + tid] = logit;
+  }
+  lg[tid] = logit;
+  // argmax (value, lowest index on ties) within each wave, then across the two waves
+  float bv = logit;
+  int bi = tid < a.V ? tid : 0x7fffffff;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  if (lane == 0) { s_red[w] = bv; s_idx[w] = bi; }
+  __syncthreads();
+  const float mx = fmaxf(s_red[0], s_red[1]);
+  if (a.uniforms == nullptr) {
+    if (tid == 0) {
+      int tok = s_idx[0];
+      if (s_red[1] > s_red[0] || (s_red[1] == s_red[0] && s_idx[1] < s_idx[0])) tok = s_idx[1];
+      s_tok = tok;
+    }
+  } else {
+    // softmax + inverse CDF: idx = #{v : cdf[v] <= u * cdf[V-1]}, sequential prefix like torch.cumsum
+    const float e = tid < a.V ? __expf(logit - mx) : 0.f;
+    lg[tid] = e;
+    __syncthreads();
+    if (tid == 0) {
+      float c = 0.f;
+      for (int v = 0; v < a.V; ++v) { c += lg[v]; lg[v] = c; }
+      const float total = c;
+      const float thr = a.uniforms[r] * total;
+      int idx = 0;
+      for (int v = 0; v < a.V; ++v) idx += (lg[v] <= thr) ? 1 : 0;
+      idx = min(idx, a.V - 1);
+      s_tok = idx;
+      s_red[2] = logf(total);  // log-sum-exp offset for log_softmax of the chosen token
+    }
+    __syncthreads();
+    if (tid == s_tok) {
+      float lp = (logit - mx) - s_red[2];
+      const bool fin = a.finished[r] != 0;
+      a.logp[(long)r * a.ld_logp] = fin ? 0.f : lp;
+    }
+  }
+  __syncthreads();
+  const int tok = s_tok;
+  if (tid == 0) {
+    a.ids[(long)r * a.ld_ids + a.id_col] = tok;
+    if (a.finished) a.finished[r] = (uint8_t)(a.finished[r] | (tok == a.end_token));
+  }
+  if (a.emb) {
+    const long base = (long)r * a.Dm;
+    for (int d = tid; d < a.Dm; d += 128) {
+      const float v = a.emb[(long)tok * a.Dm + d] * a.emb_scale + a.pe[(long)a.pe_pos * a.Dm + d];
+      a.x_next[base + d] = v;
+      bf16_t hi, lo;
+      split_bf(v, hi, lo);
+      a.a_next[base + d] = hi;
+      if (a.nsplit == 2) a.a_next[base + d + a.lo] = lo;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_head(const HeadArgs& h, hipStream_t s) {
+  if (h.V > 128 || h.Dm % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_kernel, dim3(h.rows), dim3(128), (h.Dm + 128) * 4, s, h);
+  return hipGetLastError();
+}

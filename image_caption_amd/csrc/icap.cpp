@@ -1,0 +1,544 @@
+// libicap runtime: weight packing, workspace, and the launch schedules of the captioning hot
+// path (ViT / Grid encoders, KV-cached greedy and sampled decode, full-prefix decoder forward).
+// The C ABI is declared in include/icap.h; the reference functions each entry replaces are
+// cited there.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/icap.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Fail : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(x)                                                                                    \
+  do {                                                                                               \
+    hipError_t e_ = (x);                                                                             \
+    if (e_ != hipSuccess) throw Fail(std::string(#x) + ": " + hipGetErrorString(e_));                \
+  } while (0)
+#define REQUIRE(c, msg)                       \
+  do {                                        \
+    if (!(c)) throw Fail(std::string(msg)); \
+  } while (0)
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+  } catch (...) {
+    g_err = "unknown error";
+  }
+  return 1;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  void ensure(size_t bytes) {
+    if (bytes <= n) return;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    n = 0;
+    HIPCHK(hipMalloc(&p, bytes));
+    n = bytes;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+struct Lin {  // packed nn.Linear: bf16 W [N][K] + fp32 bias
+  bf16_t* w = nullptr;
+  float* b = nullptr;
+  int N = 0, K = 0;
+};
+struct LN {
+  float *w = nullptr, *b = nullptr;
+};
+struct VitLayer {
+  LN ln1, ln2;
+  Lin qkv, out, mlp0, mlp3;
+};
+struct EncLayer {
+  Lin qkv, out, lin1, lin2;
+  LN n1, n2;
+};
+struct DecLayer {
+  Lin sa_qkv, sa_out, ca_q, ca_out, lin1, lin2;
+  bf16_t* ca_kT = nullptr;  // [H][d_model][64]: W_k,h^T for the key absorption
+  bf16_t* ca_v = nullptr;   // [d_model][d_model] = rows [2d, 3d) of in_proj (per-head slices of 64 rows)
+  float* ca_vb = nullptr;   // bias rows [2d, 3d)
+  LN n1, n2, n3;
+};
+
+}  // namespace
+
+struct icap_handle {
+  icap_model_desc d{};
+  int ns = 2;  // activation planes (1 = bf16, 2 = hi/lo)
+  std::vector<void*> owned;
+  // decoder
+  float *emb = nullptr, *pe = nullptr, *fc_w = nullptr, *fc_b = nullptr;
+  std::vector<DecLayer> dec;
+  // vit
+  float *cls = nullptr, *pos = nullptr, *vit_ln_w = nullptr, *vit_ln_b = nullptr;
+  Lin conv, proj;
+  std::vector<VitLayer> vit;
+  // grid
+  float* enc_pe = nullptr;
+  std::vector<EncLayer> enc;
+  // workspaces
+  DevBuf e_x, e_a, e_qkv, e_h, e_patch;  // encoder
+  DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin;  // decoder
+
+  ~icap_handle() {
+    for (void* p : owned) (void)hipFree(p);
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_x, &d_a, &d_qkv, &d_q, &d_qt, &d_c, &d_o, &d_h,
+                      &d_kv, &d_fin})
+      b->release();
+  }
+
+  void* alloc(size_t bytes) {
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, bytes));
+    owned.push_back(p);
+    return p;
+  }
+  float* own_f32(const float* src, size_t n, hipStream_t s) {
+    REQUIRE(src != nullptr, "missing parameter pointer");
+    float* p = (float*)alloc(n * 4);
+    HIPCHK(hipMemcpyAsync(p, src, n * 4, hipMemcpyDeviceToDevice, s));
+    return p;
+  }
+  bf16_t* own_bf16(const float* src, size_t n, hipStream_t s) {
+    REQUIRE(src != nullptr, "missing parameter pointer");
+    bf16_t* p = (bf16_t*)alloc(n * 2);
+    HIPCHK(launch_f32_to_bf16(src, p, (long)n, s));
+    return p;
+  }
+  Lin lin(const float* w, const float* b, int N, int K, hipStream_t s) {
+    Lin l;
+    l.w = own_bf16(w, (size_t)N * K, s);
+    l.b = b ? own_f32(b, N, s) : nullptr;
+    l.N = N;
+    l.K = K;
+    return l;
+  }
+  LN ln(const icap_ln_w& p, int D, hipStream_t s) { return LN{own_f32(p.w, D, s), own_f32(p.b, D, s)}; }
+
+  // ---------------------------------------------------------------- GEMM helper
+  void gemm(const bf16_t* A, long lda, long a_lo, const Lin& W, int M, void* C, long ldc, long c_lo, int epi,
+            int out, hipStream_t s) {
+    GemmArgs g = gemm_args();
+    g.A = A; g.lda = lda; g.a_lo = a_lo;
+    g.W = W.w; g.ldw = W.K;
+    g.bias = W.b;
+    g.C = C; g.ldc = ldc; g.c_lo = c_lo;
+    g.M = M; g.N = W.N; g.K = W.K; g.nsplit = ns; g.c_planes = ns;
+    g.epi = epi; g.out = out;
+    HIPCHK(launch_gemm(g, s));
+  }
+};
+
+namespace {
+
+void pack(icap_handle* h, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  const int D = d.d_model, F = d.dim_ff;
+  REQUIRE(d.nhead * 64 == D && d.nhead == 8, "decoder must have 8 heads of 64");
+  REQUIRE(d.vocab <= 128, "vocab > 128 unsupported by the head kernel");
+  h->emb = h->own_f32(d.emb, (size_t)d.vocab * D, s);
+  h->pe = h->own_f32(d.pe, (size_t)d.pe_len * D, s);
+  h->fc_w = h->own_f32(d.fc_w, (size_t)d.vocab * D, s);
+  h->fc_b = h->own_f32(d.fc_b, d.vocab, s);
+  for (int i = 0; i < d.n_dec_layers; ++i) {
+    const icap_dec_layer_w& L = d.dec_layers[i];
+    DecLayer o;
+    o.sa_qkv = h->lin(L.self_attn.in_w, L.self_attn.in_b, 3 * D, D, s);
+    o.sa_out = h->lin(L.self_attn.out_w, L.self_attn.out_b, D, D, s);
+    o.ca_q = h->lin(L.cross_attn.in_w, L.cross_attn.in_b, D, D, s);
+    o.ca_kT = (bf16_t*)h->alloc((size_t)D * D * 2);
+    HIPCHK(launch_transpose_heads_bf16(L.cross_attn.in_w + (size_t)D * D, d.nhead, 64, D, o.ca_kT, s));
+    o.ca_v = h->own_bf16(L.cross_attn.in_w + (size_t)2 * D * D, (size_t)D * D, s);
+    o.ca_vb = h->own_f32(L.cross_attn.in_b + 2 * D, D, s);
+    o.ca_out = h->lin(L.cross_attn.out_w, L.cross_attn.out_b, D, D, s);
+    o.lin1 = h->lin(L.lin1_w, L.lin1_b, F, D, s);
+    o.lin2 = h->lin(L.lin2_w, L.lin2_b, D, F, s);
+    o.n1 = h->ln(L.norm1, D, s);
+    o.n2 = h->ln(L.norm2, D, s);
+    o.n3 = h->ln(L.norm3, D, s);
+    h->dec.push_back(o);
+  }
+  if (d.kind == ICAP_KIND_VIT) {
+    const int V = d.vit_dim, np = (d.image / d.patch) * (d.image / d.patch);
+    REQUIRE(d.vit_heads * 64 == V, "ViT heads must be 64 wide");
+    h->cls = h->own_f32(d.cls, V, s);
+    h->pos = h->own_f32(d.pos, (size_t)(np + 1) * V, s);
+    h->conv = h->lin(d.conv_w, d.conv_b, V, 3 * d.patch * d.patch, s);
+    for (int i = 0; i < d.vit_layers; ++i) {
+      const icap_vit_layer_w& L = d.vit_layers_w[i];
+      VitLayer o;
+      o.ln1 = h->ln(L.ln_1, V, s);
+      o.qkv = h->lin(L.attn.in_w, L.attn.in_b, 3 * V, V, s);
+      o.out = h->lin(L.attn.out_w, L.attn.out_b, V, V, s);
+      o.ln2 = h->ln(L.ln_2, V, s);
+      o.mlp0 = h->lin(L.mlp0_w, L.mlp0_b, d.vit_mlp, V, s);
+      o.mlp3 = h->lin(L.mlp3_w, L.mlp3_b, V, d.vit_mlp, s);
+      h->vit.push_back(o);
+    }
+    h->vit_ln_w = h->own_f32(d.vit_ln_w, V, s);
+    h->vit_ln_b = h->own_f32(d.vit_ln_b, V, s);
+    h->proj = h->lin(d.proj_w, d.proj_b, D, V, s);
+  } else if (d.kind == ICAP_KIND_GRID) {
+    h->proj = h->lin(d.proj_w, d.proj_b, D, d.cnn_dim, s);
+    h->enc_pe = h->own_f32(d.enc_pe, (size_t)d.grid_tokens * D, s);
+    for (int i = 0; i < d.n_enc_layers; ++i) {
+      const icap_enc_layer_w& L = d.enc_layers[i];
+      EncLayer o;
+      o.qkv = h->lin(L.attn.in_w, L.attn.in_b, 3 * D, D, s);
+      o.out = h->lin(L.attn.out_w, L.attn.out_b, D, D, s);
+      o.lin1 = h->lin(L.lin1_w, L.lin1_b, F, D, s);
+      o.lin2 = h->lin(L.lin2_w, L.lin2_b, D, F, s);
+      o.n1 = h->ln(L.norm1, D, s);
+      o.n2 = h->ln(L.norm2, D, s);
+      h->enc.push_back(o);
+    }
+  } else {
+    throw Fail("unknown model kind");
+  }
+}
+
+// Post-LN transformer encoder layer (nn.TransformerEncoderLayer, eval) over M rows of D.
+void enc_layer_postln(icap_handle* h, const EncLayer& L, int B, int N, float* x, bf16_t* a, bf16_t* qkv, bf16_t* hb,
+                      hipStream_t s) {
+  const int D = h->d.d_model, F = h->d.dim_ff, M = B * N;
+  const long aL = (long)M * D, qL = (long)M * 3 * D, hL = (long)M * F;
+  h->gemm(a, D, aL, L.qkv, M, qkv, 3 * D, qL, EPI_NONE, OUT_SPLIT, s);
+  HIPCHK(launch_enc_attention(qkv, 3 * D, qL, B, N, D / 64, 0.125f, a, D, aL, h->ns, s));
+  h->gemm(a, D, aL, L.out, M, x, D, 0, EPI_NONE, OUT_F32_RESID, s);
+  HIPCHK(launch_layernorm(x, D, M, D, 0, 0, 0, L.n1.w, L.n1.b, 1e-5f, x, D, a, D, aL, h->ns, s));
+  h->gemm(a, D, aL, L.lin1, M, hb, F, hL, EPI_RELU, OUT_SPLIT, s);
+  h->gemm(hb, F, hL, L.lin2, M, x, D, 0, EPI_NONE, OUT_F32_RESID, s);
+  HIPCHK(launch_layernorm(x, D, M, D, 0, 0, 0, L.n2.w, L.n2.b, 1e-5f, x, D, a, D, aL, h->ns, s));
+}
+
+void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  const int V = d.vit_dim, g = d.image / d.patch, np = g * g, T = np + 1, M = B * T, Dm = d.d_model;
+  const int Kp = 3 * d.patch * d.patch, ns = h->ns;
+  h->e_patch.ensure((size_t)B * np * Kp * 2 * ns);
+  h->e_x.ensure((size_t)M * V * 4);
+  h->e_a.ensure((size_t)M * V * 2 * ns);
+  h->e_qkv.ensure((size_t)M * 3 * V * 2 * ns);
+  h->e_h.ensure((size_t)M * d.vit_mlp * 2 * ns);
+  bf16_t* patch = h->e_patch.as<bf16_t>();
+  float* x = h->e_x.as<float>();
+  bf16_t* a = h->e_a.as<bf16_t>();
+  bf16_t* qkv = h->e_qkv.as<bf16_t>();
+  bf16_t* hb = h->e_h.as<bf16_t>();
+  const long pL = (long)B * np * Kp, aL = (long)M * V, qL = (long)M * 3 * V, hL = (long)M * d.vit_mlp;
+
+  HIPCHK(launch_im2col_patches(img, B, 3, d.image, d.patch, patch, pL, ns, s));
+  {  // patch-embed GEMM: rows (b, p) -> x[b*T + 1 + p] with conv bias + pos[1 + p]
+    GemmArgs ga = gemm_args();
+    ga.A = patch; ga.lda = Kp; ga.a_lo = pL;
+    ga.W = h->conv.w; ga.ldw = Kp; ga.bias = h->conv.b;
+    ga.C = x; ga.ldc = V;
+    ga.M = B * np; ga.N = V; ga.K = Kp; ga.nsplit = ns;
+    ga.epi = EPI_NONE; ga.out = OUT_F32;
+    ga.rm_group = np; ga.rm_stride = T; ga.rm_off = 1;
+    ga.addend = h->pos; ga.add_ld = V; ga.add_group = np; ga.add_off = 1;
+    HIPCHK(launch_gemm(ga, s));
+  }
+  HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
+  for (const VitLayer& L : h->vit) {
+    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
+    h->gemm(a, V, aL, L.qkv, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s);
+    HIPCHK(launch_enc_attention(qkv, 3 * V, qL, B, T, d.vit_heads, 0.125f, a, V, aL, ns, s));
+    h->gemm(a, V, aL, L.out, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s);
+    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
+    h->gemm(a, V, aL, L.mlp0, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);
+    h->gemm(hb, d.vit_mlp, hL, L.mlp3, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s);
+  }
+  // final LN on patch rows only (drop CLS), then projection 768 -> d_model
+  const long a2L = (long)B * np * V;
+  HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, nullptr, 0, a, V, a2L, ns, s));
+  h->gemm(a, V, a2L, h->proj, B * np, memory, Dm, 0, EPI_NONE, OUT_F32, s);
+}
+
+void encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  const int D = d.d_model, N = d.grid_tokens, M = B * N, C = d.cnn_dim, ns = h->ns;
+  h->e_patch.ensure((size_t)M * C * 2 * ns);
+  h->e_a.ensure((size_t)M * D * 2 * ns);
+  h->e_qkv.ensure((size_t)M * 3 * D * 2 * ns);
+  h->e_h.ensure((size_t)M * d.dim_ff * 2 * ns);
+  bf16_t* rows = h->e_patch.as<bf16_t>();
+  bf16_t* a = h->e_a.as<bf16_t>();
+  const long rL = (long)M * C;
+  HIPCHK(launch_nchw_to_rows(feats, B, C, N, rows, rL, ns, s));
+  {  // 1x1 conv projection + positional encoding
+    GemmArgs ga = gemm_args();
+    ga.A = rows; ga.lda = C; ga.a_lo = rL;
+    ga.W = h->proj.w; ga.ldw = C; ga.bias = h->proj.b;
+    ga.C = memory; ga.ldc = D;
+    ga.M = M; ga.N = D; ga.K = C; ga.nsplit = ns;
+    ga.epi = EPI_NONE; ga.out = OUT_F32;
+    ga.addend = h->enc_pe; ga.add_ld = D; ga.add_group = N; ga.add_off = 0;
+    HIPCHK(launch_gemm(ga, s));
+  }
+  // activation planes of x for the first encoder layer's QKV GEMM
+  HIPCHK(launch_split_f32(memory, (long)M * D, a, (long)M * D, ns, s));
+  for (const EncLayer& L : h->enc)
+    enc_layer_postln(h, L, B, N, memory, a, h->e_qkv.as<bf16_t>(), h->e_h.as<bf16_t>(), s);
+}
+
+struct DecodeBufs {
+  float *x, *qkv, *qt, *kc, *vc;
+  bf16_t *a, *q, *c, *o, *hb;
+  long aL, qL, cL, hL;
+};
+
+DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax) {
+  const icap_model_desc& d = h->d;
+  const int D = d.d_model, ns = h->ns, H = d.nhead;
+  h->d_x.ensure((size_t)rows * D * 4);
+  h->d_a.ensure((size_t)rows * D * 2 * ns);
+  h->d_qkv.ensure((size_t)rows * 3 * D * 4);
+  h->d_q.ensure((size_t)rows * D * 2 * ns);
+  h->d_qt.ensure((size_t)rows * H * D * 4);
+  h->d_c.ensure((size_t)rows * H * D * 2 * ns);
+  h->d_o.ensure((size_t)rows * D * 2 * ns);
+  h->d_h.ensure((size_t)rows * d.dim_ff * 2 * ns);
+  h->d_kv.ensure((size_t)2 * d.n_dec_layers * B * H * Lmax * 64 * 4);
+  DecodeBufs b;
+  b.x = h->d_x.as<float>(); b.a = h->d_a.as<bf16_t>(); b.qkv = h->d_qkv.as<float>();
+  b.q = h->d_q.as<bf16_t>(); b.qt = h->d_qt.as<float>(); b.c = h->d_c.as<bf16_t>();
+  b.o = h->d_o.as<bf16_t>(); b.hb = h->d_h.as<bf16_t>();
+  b.kc = h->d_kv.as<float>();
+  b.vc = b.kc + (size_t)d.n_dec_layers * B * H * Lmax * 64;
+  b.aL = (long)rows * D; b.qL = (long)rows * D; b.cL = (long)rows * H * D; b.hL = (long)rows * d.dim_ff;
+  return b;
+}
+
+// One pass of all decoder layers over `rows` query rows (n_new per image, positions t0..t0+n_new).
+void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int Lmax, int causal,
+                    const float* mem, int S, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  const int D = d.d_model, H = d.nhead, F = d.dim_ff, rows = B * n_new, ns = h->ns;
+  const size_t kv_layer = (size_t)B * H * Lmax * 64;
+  for (int l = 0; l < d.n_dec_layers; ++l) {
+    const DecLayer& L = h->dec[l];
+    // self-attention block: x = LN1(x + SA(x))
+    h->gemm(b.a, D, b.aL, L.sa_qkv, rows, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, s);
+    HIPCHK(launch_dec_self_attn(b.qkv, B, n_new, t0, H, b.kc + l * kv_layer, b.vc + l * kv_layer, Lmax, causal,
+                                0.125f, b.o, b.aL, ns, s));
+    h->gemm(b.o, D, b.aL, L.sa_out, rows, b.x, D, 0, EPI_NONE, OUT_F32_RESID, s);
+    HIPCHK(launch_layernorm(b.x, D, rows, D, 0, 0, 0, L.n1.w, L.n1.b, 1e-5f, b.x, D, b.a, D, b.aL, ns, s));
+    // cross-attention block (key-absorbed): x = LN2(x + CA(x, mem))
+    h->gemm(b.a, D, b.aL, L.ca_q, rows, b.q, D, b.qL, EPI_NONE, OUT_SPLIT, s);
+    {
+      GemmArgs g = gemm_args();  // qt[:, h*D:(h+1)*D] = q[:, h*64:(h+1)*64] · Wk_h
+      g.A = b.q; g.lda = D; g.a_batch = 64; g.a_lo = b.qL;
+      g.W = L.ca_kT; g.ldw = 64; g.w_batch = (long)D * 64;
+      g.C = b.qt; g.ldc = (long)H * D; g.c_batch = D;
+      g.M = rows; g.N = D; g.K = 64; g.nsplit = ns; g.batch = H;
+      g.epi = EPI_NONE; g.out = OUT_F32;
+      HIPCHK(launch_gemm(g, s));
+    }
+    HIPCHK(launch_cross_attn_absorbed(b.qt, mem, rows, n_new, S, H, D, 0.125f, b.c, b.cL, ns, s));
+    {
+      GemmArgs g = gemm_args();  // o[:, h*64:(h+1)*64] = c_h · Wv_h^T + bv_h
+      g.A = b.c; g.lda = (long)H * D; g.a_batch = D; g.a_lo = b.cL;
+      g.W = L.ca_v; g.ldw = D; g.w_batch = 64L * D;
+      g.bias = L.ca_vb; g.bias_batch = 64;
+      g.C = b.o; g.ldc = D; g.c_batch = 64; g.c_lo = b.aL;
+      g.M = rows; g.N = 64; g.K = D; g.nsplit = ns; g.batch = H; g.c_planes = ns;
+      g.epi = EPI_NONE; g.out = OUT_SPLIT;
+      HIPCHK(launch_gemm(g, s));
+    }
+    h->gemm(b.o, D, b.aL, L.ca_out, rows, b.x, D, 0, EPI_NONE, OUT_F32_RESID, s);
+    HIPCHK(launch_layernorm(b.x, D, rows, D, 0, 0, 0, L.n2.w, L.n2.b, 1e-5f, b.x, D, b.a, D, b.aL, ns, s));
+    // feed-forward block: x = LN3(x + W2 relu(W1 x))
+    h->gemm(b.a, D, b.aL, L.lin1, rows, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, s);
+    h->gemm(b.hb, F, b.hL, L.lin2, rows, b.x, D, 0, EPI_NONE, OUT_F32_RESID, s);
+    HIPCHK(launch_layernorm(b.x, D, rows, D, 0, 0, 0, L.n3.w, L.n3.b, 1e-5f, b.x, D, b.a, D, b.aL, ns, s));
+  }
+}
+
+void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
+                 float* step_logits, const float* uniforms, float* logp, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  REQUIRE(B > 0 && max_len >= 1, "bad batch / max_len");
+  REQUIRE(max_len <= d.pe_len, "max_len exceeds the positional-encoding table (PositionalEncoding max_len)");
+  REQUIRE(S > 0 && S <= 256, "memory length must be in [1, 256]");
+  const int D = d.d_model;
+  DecodeBufs b = dec_bufs(h, B, B, max_len);
+  const float scale = std::sqrt((float)D) == 0 ? 0.f : (float)std::sqrt((double)D);
+  HIPCHK(launch_fill_col(ids, B, max_len, 0, start, s));
+  HIPCHK(launch_embed(nullptr, 0, start, B, 1, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
+  uint8_t* fin = nullptr;
+  if (uniforms) {
+    h->d_fin.ensure((size_t)B);
+    fin = h->d_fin.as<uint8_t>();
+    HIPCHK(hipMemsetAsync(fin, 0, B, s));
+  }
+  for (int t = 0; t + 1 < max_len; ++t) {
+    decoder_layers(h, b, B, 1, t, max_len, 1, mem, S, s);
+    HeadArgs ha{};
+    ha.x = b.x; ha.rows = B; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = d.vocab;
+    ha.logits = step_logits ? step_logits + (size_t)t * B * d.vocab : nullptr;
+    ha.ld_logits = d.vocab;
+    ha.ids = ids; ha.ld_ids = max_len; ha.id_col = t + 1;
+    ha.uniforms = uniforms ? uniforms + (size_t)t * B : nullptr;
+    ha.logp = logp ? logp + t : nullptr; ha.ld_logp = max_len - 1;
+    ha.finished = fin; ha.end_token = end;
+    if (t + 2 < max_len) {
+      ha.emb = h->emb; ha.pe = h->pe; ha.pe_pos = t + 1; ha.emb_scale = scale;
+      ha.x_next = b.x; ha.a_next = b.a; ha.lo = b.aL; ha.nsplit = h->ns;
+    }
+    HIPCHK(launch_head(ha, s));
+  }
+}
+
+}  // namespace
+
+// ================================================================================== C ABI
+extern "C" {
+
+int icap_abi_version(void) { return ICAP_ABI_VERSION; }
+const char* icap_last_error(void) { return g_err.c_str(); }
+
+int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
+  return guarded([&] {
+    REQUIRE(desc && out, "null argument");
+    REQUIRE(desc->precision == ICAP_PREC_BF16 || desc->precision == ICAP_PREC_BF16X2, "bad precision");
+    icap_handle* h = new icap_handle();
+    try {
+      h->d = *desc;
+      h->ns = desc->precision == ICAP_PREC_BF16X2 ? 2 : 1;
+      pack(h, (hipStream_t)stream);
+      HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    // layer pointers in the desc belong to the caller; drop them
+    h->d.dec_layers = nullptr;
+    h->d.vit_layers_w = nullptr;
+    h->d.enc_layers = nullptr;
+    *out = h;
+  });
+}
+
+int icap_destroy(icap_handle* h) {
+  return guarded([&] {
+    if (h) {
+      (void)hipDeviceSynchronize();
+      delete h;
+    }
+  });
+}
+
+int icap_encode_vit(icap_handle* h, const float* images, int B, float* memory, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && images && memory && B > 0, "bad arguments");
+    REQUIRE(h->d.kind == ICAP_KIND_VIT, "handle is not a ViT model");
+    encode_vit(h, images, B, memory, (hipStream_t)stream);
+  });
+}
+
+int icap_encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && feats && memory && B > 0, "bad arguments");
+    REQUIRE(h->d.kind == ICAP_KIND_GRID, "handle is not a Grid model");
+    encode_grid_tail(h, feats, B, memory, (hipStream_t)stream);
+  });
+}
+
+int icap_decode_greedy(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                       int end_token, int32_t* ids, float* step_logits, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && memory && ids, "bad arguments");
+    decode_loop(h, memory, B, S, max_len, start_token, end_token, ids, step_logits, nullptr, nullptr,
+                (hipStream_t)stream);
+  });
+}
+
+int icap_decode_sample(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                       int end_token, const float* uniforms, int32_t* ids, float* logp, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && memory && ids && uniforms && logp, "bad arguments");
+    decode_loop(h, memory, B, S, max_len, start_token, end_token, ids, nullptr, uniforms, logp,
+                (hipStream_t)stream);
+  });
+}
+
+int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const float* memory, int S, int causal,
+                         float* logits, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && tgt && memory && logits && B > 0 && T > 0, "bad arguments");
+    REQUIRE(T <= h->d.pe_len, "sequence longer than the positional-encoding table");
+    REQUIRE(S > 0 && S <= 256, "memory length must be in [1, 256]");
+    hipStream_t s = (hipStream_t)stream;
+    const int D = h->d.d_model, rows = B * T;
+    DecodeBufs b = dec_bufs(h, rows, B, T);
+    const float scale = (float)std::sqrt((double)D);
+    HIPCHK(launch_embed(tgt, T, 0, rows, T, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
+    decoder_layers(h, b, B, T, 0, T, causal, memory, S, s);
+    HeadArgs ha{};
+    ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = h->d.vocab;
+    ha.logits = logits; ha.ld_logits = h->d.vocab;
+    h->d_fin.ensure((size_t)rows * 4);  // scratch ids
+    ha.ids = h->d_fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
+    HIPCHK(launch_head(ha, s));
+  });
+}
+
+int icap_op_gemm(const uint16_t* A, long lda, long a_lo, int nsplit, const uint16_t* W, const float* bias, void* C,
+                 long ldc, long c_lo, int M, int N, int K, int epi, int out, void* stream) {
+  return guarded([&] {
+    GemmArgs g = gemm_args();
+    g.A = A; g.lda = lda; g.a_lo = a_lo; g.nsplit = nsplit;
+    g.W = W; g.ldw = K; g.bias = bias;
+    g.C = C; g.ldc = ldc; g.c_lo = c_lo;
+    g.M = M; g.N = N; g.K = K; g.epi = epi; g.out = out;
+    HIPCHK(launch_gemm(g, (hipStream_t)stream));
+  });
+}
+
+int icap_op_layernorm(const float* x, int rows, int D, const float* w, const float* b, float eps, float* out_f32,
+                      uint16_t* out_bf, long bf_lo, int nsplit, void* stream) {
+  return guarded([&] {
+    HIPCHK(launch_layernorm(x, D, rows, D, 0, 0, 0, w, b, eps, out_f32, D, out_bf, D, bf_lo, nsplit,
+                            (hipStream_t)stream));
+  });
+}
+
+int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uint16_t* out, long out_lo, int nsplit,
+                          void* stream) {
+  return guarded([&] {
+    HIPCHK(launch_enc_attention(qkv, 3L * H * 64, lo, B, N, H, 0.125f, out, (long)H * 64, out_lo, nsplit,
+                                (hipStream_t)stream));
+  });
+}
+
+}  // extern "C"

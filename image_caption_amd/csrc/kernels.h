@@ -1,0 +1,69 @@
+// Host-side launch wrappers for the captioning kernels (all asynchronous on `stream`).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+
+// Epilogue / output selectors shared by kernels and the host dispatcher.
+enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RELU = 2 };
+enum { OUT_F32 = 0, OUT_BF16 = 1, OUT_SPLIT = 2, OUT_F32_RESID = 3 };
+
+// C[b] (+)= epi(A[b] · W[b]^T + bias[b] + addend) with A given as `nsplit` bf16 planes
+// (plane p of row r at A + p*a_lo + r*lda); W is [N][K] bf16 (nn.Linear layout).
+struct GemmArgs {
+  const bf16_t* A; long lda; long a_batch; long a_lo;
+  const bf16_t* W; long ldw; long w_batch;
+  const float* bias; long bias_batch;
+  void* C; long ldc; long c_batch; long c_lo; int c_planes;  // OUT_SPLIT: 1 = hi only, 2 = hi + lo
+  int M, N, K, nsplit, batch;
+  int epi, out;
+  int rm_group; long rm_stride; long rm_off;          // output row remap (0 = identity)
+  const float* addend; long add_ld; int add_group; int add_off;
+};
+inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
+hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
+
+// LayerNorm over rows of D fp32 values; optional fp32 output (may alias input) and
+// bf16 hi(/lo) planes.  Input row r is read from (r / in_group) * in_stride + in_off + r % in_group.
+hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_group, long in_stride,
+                            long in_off, const float* w, const float* b, float eps, float* out_f32,
+                            long ld_f32, bf16_t* out_bf, long ld_bf, long bf_lo, int nsplit,
+                            hipStream_t s);
+
+hipError_t launch_im2col_patches(const float* img, int B, int C, int HW, int P, bf16_t* out, long lo,
+                                 int nsplit, hipStream_t s);
+hipError_t launch_cls_rows(const float* cls, const float* pos, float* x, int B, int tokens, int D,
+                           hipStream_t s);
+hipError_t launch_nchw_to_rows(const float* feats, int B, int C, int S, bf16_t* out, long lo, int nsplit,
+                               hipStream_t s);
+// x[r] = emb[tok] * scale + pe[t0 + r % T], tok = tok_ptr[(r / T) * tok_ld + r % T] (or fixed_tok if null)
+hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0, const float* emb,
+                        const float* pe, int D, float scale, float* x, bf16_t* a, long lo, int nsplit, hipStream_t s);
+hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hipStream_t s);
+hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int nsplit, hipStream_t s);
+hipError_t launch_f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);
+hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s);
+
+// Encoder self-attention (non-causal) over N tokens, heads of 64, MFMA bf16 (nsplit 1 or 2).
+hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale,
+                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s);
+// Decoder self-attention with fp32 KV cache; n_new query rows per image starting at t0.
+hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int H, float* kc, float* vc,
+                                int Lmax, int causal, float scale, bf16_t* out, long lo, int nsplit,
+                                hipStream_t s);
+// Cross-attention in the key-absorbed form: qt rows hold q_h·Wk_h (H × Dm); mem (images,S,Dm) fp32.
+hipError_t launch_cross_attn_absorbed(const float* qt, const float* mem, int rows, int rows_per_image,
+                                      int S, int H, int Dm, float scale, bf16_t* out, long lo, int nsplit,
+                                      hipStream_t s);
+// fc_out + argmax (greedy) or inverse-CDF sample; writes ids[r*ld_ids + col], optional logits, and
+// (if emb != null) the next step's embedded token into x/a.
+struct HeadArgs {
+  const float* x; int rows; int Dm; const float* W; const float* bias; int V;
+  float* logits; long ld_logits;
+  int32_t* ids; long ld_ids; int id_col;
+  const float* uniforms;  // null => argmax
+  float* logp; long ld_logp; uint8_t* finished; int end_token;
+  const float* emb; const float* pe; int pe_pos; float emb_scale; float* x_next; bf16_t* a_next; long lo; int nsplit;
+};
+hipError_t launch_head(const HeadArgs& h, hipStream_t s);

@@ -1,0 +1,227 @@
+// Row-wise kernels: LayerNorm (SURVEY.md §2.1 K3 and the decoder/grid post-LNs), patch
+// unfolding for the ViT patch-embed GEMM (K1), class-token rows (K2), grid feature-map
+// transposition (K14), token embedding + sinusoidal PE (K7), weight packing helpers.
+//
+// All are HBM-streaming kernels: 16-byte vector accesses, one wave per row where a row
+// reduction is needed (wave64 shuffles), fp32 arithmetic throughout.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+__device__ __forceinline__ void store_planes(bf16_t* base, long idx, long lo, int nsplit, float v) {
+  bf16_t hi, l;
+  split_bf(v, hi, l);
+  base[idx] = hi;
+  if (nsplit == 2) base[idx + lo] = l;
+}
+
+// One wave per row, PER = D / 64 values per lane (D = 512 -> 8, 768 -> 12).
+template <int PER>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, long ldx, int rows,
+                                                        int in_group, long in_stride, long in_off,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ b, float eps,
+                                                        float* out_f32, long ld_f32, bf16_t* out_bf,
+                                                        long ld_bf, long bf_lo, int nsplit) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = PER * 64;
+  const long irow = in_group ? (long)(row / in_group) * in_stride + in_off + row % in_group : (long)row;
+  const float* xr = x + irow * ldx;
+  float v[PER];
+  // lane owns columns [4*lane + 256*c, +4)
+#pragma unroll
+  for (int c = 0; c < PER / 4; ++c) {
+    f32x4 t = *(const f32x4*)(xr + c * 256 + lane * 4);
+    v[c * 4 + 0] = t[0]; v[c * 4 + 1] = t[1]; v[c * 4 + 2] = t[2]; v[c * 4 + 3] = t[3];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) s += v[i];
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { const float d = v[i] - mean; q += d * d; }
+  const float var = wave_sum(q) / (float)D;
+  const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+  for (int c = 0; c < PER / 4; ++c) {
+    const int col = c * 256 + lane * 4;
+    f32x4 wv = *(const f32x4*)(w + col), bv = *(const f32x4*)(b + col), y;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) y[k] = (v[c * 4 + k] - mean) * rstd * wv[k] + bv[k];
+    if (out_f32) *(f32x4*)(out_f32 + (long)row * ld_f32 + col) = y;
+    if (out_bf) {
+      bf16_t h[4], l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) split_bf(y[k], h[k], l[k]);
+      bf16_t* o = out_bf + (long)row * ld_bf + col;
+      *(u32x2*)o = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+      if (nsplit == 2)
+        *(u32x2*)(o + bf_lo) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
+    }
+  }
+}
+
+// img (B,C,HW,HW) -> rows (B*np, C*P*P) in (c, kh, kw) order == torchvision conv_proj weight order.
+__global__ void im2col_kernel(const float* __restrict__ img, int B, int C, int HW, int P, bf16_t* out,
+                              long lo, int nsplit) {
+  const int g = HW / P, np = g * g, K = C * P * P, chunks = K / 8;
+  const long total = (long)B * np * chunks;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % chunks);
+    const long r = i / chunks;
+    const int p = (int)(r % np), b = (int)(r / np);
+    const int k0 = ch * 8, c = k0 / (P * P), kh = (k0 / P) % P, kw = k0 % P;
+    const int y = (p / g) * P + kh, xx = (p % g) * P + kw;
+    const float* src = img + (((long)b * C + c) * HW + y) * HW + xx;
+    f32x4 a = *(const f32x4*)src, bq = *(const f32x4*)(src + 4);
+    float v[8] = {a[0], a[1], a[2], a[3], bq[0], bq[1], bq[2], bq[3]};
+    bf16_t h[8], l[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) split_bf(v[k], h[k], l[k]);
+    u32x4 H, L;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      H[k] = (uint32_t)h[2 * k] | ((uint32_t)h[2 * k + 1] << 16);
+      L[k] = (uint32_t)l[2 * k] | ((uint32_t)l[2 * k + 1] << 16);
+    }
+    *(u32x4*)(out + r * K + k0) = H;
+    if (nsplit == 2) *(u32x4*)(out + lo + r * K + k0) = L;
+  }
+}
+
+__global__ void cls_rows_kernel(const float* cls, const float* pos, float* x, int B, int tokens, int D) {
+  const long total = (long)B * D;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D), b = (int)(i / D);
+    x[(long)b * tokens * D + d] = cls[d] + pos[d];
+  }
+}
+
+// feats (B, C, S) -> rows (B*S, C) as bf16 planes
+__global__ void nchw_to_rows_kernel(const float* __restrict__ f, int B, int C, int S, bf16_t* out, long lo,
+                                    int nsplit) {
+  const long total = (long)B * S * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long r = i / C;
+    const int s = (int)(r % S), b = (int)(r / S);
+    store_planes(out, i, lo, nsplit, f[((long)b * C + c) * S + s]);
+  }
+}
+
+// x[r] = emb[tok[r]] * scale + pe[t0 + r % T]  (TransformerDecoder.forward, vit:166-169)
+__global__ void embed_kernel(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0,
+                             const float* emb, const float* pe, int D, float scale, float* x, bf16_t* a, long lo,
+                             int nsplit) {
+  const long total = (long)rows * D;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D), r = (int)(i / D);
+    const int t = tok ? tok[(long)(r / T) * tok_ld + r % T] : fixed_tok;
+    const float v = emb[(long)t * D + d] * scale + pe[(long)(t0 + r % T) * D + d];
+    x[i] = v;
+    store_planes(a, i, lo, nsplit, v);
+  }
+}
+
+__global__ void fill_col_kernel(int32_t* ids, int B, long ld, int col, int value) {
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x) ids[(long)b * ld + col] = value;
+}
+
+__global__ void split_f32_kernel(const float* src, long n, bf16_t* dst, long lo, int nsplit) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    store_planes(dst, i, lo, nsplit, src[i]);
+}
+
+__global__ void f32_to_bf16_kernel(const float* src, bf16_t* dst, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = f2bf(src[i]);
+}
+
+// wk rows [h*hd + i][d] (i < hd, d < D)  ->  dst[h][d][i]   (W_h^T packing for the key absorption)
+__global__ void transpose_heads_kernel(const float* wk, int H, int hd, int D, bf16_t* dst) {
+  const long total = (long)H * hd * D;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ii = (int)(i % hd);
+    const long r = i / hd;
+    const int d = (int)(r % D), h = (int)(r / D);
+    dst[i] = f2bf(wk[((long)h * hd + ii) * D + d]);
+  }
+}
+
+inline int grid_for(long n, int block = 256) {
+  long g = (n + block - 1) / block;
+  return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
+}
+
+}  // namespace
+
+hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_group, long in_stride,
+                            long in_off, const float* w, const float* b, float eps, float* out_f32,
+                            long ld_f32, bf16_t* out_bf, long ld_bf, long bf_lo, int nsplit,
+                            hipStream_t s) {
+  dim3 grid((rows + 3) / 4);
+  if (D == 512)
+    hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off,
+                       w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit);
+  else if (D == 768)
+    hipLaunchKernelGGL(layernorm_kernel<12>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off,
+                       w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit);
+  else if (D == 256)
+    hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off,
+                       w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_im2col_patches(const float* img, int B, int C, int HW, int P, bf16_t* out, long lo,
+                                 int nsplit, hipStream_t s) {
+  if (HW % P || P % 8) return hipErrorInvalidValue;
+  const long n = (long)B * (HW / P) * (HW / P) * (C * P * P / 8);
+  hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(n)), dim3(256), 0, s, img, B, C, HW, P, out, lo, nsplit);
+  return hipGetLastError();
+}
+
+hipError_t launch_cls_rows(const float* cls, const float* pos, float* x, int B, int tokens, int D,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(cls_rows_kernel, dim3(grid_for((long)B * D)), dim3(256), 0, s, cls, pos, x, B, tokens, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_nchw_to_rows(const float* feats, int B, int C, int S, bf16_t* out, long lo, int nsplit,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(nchw_to_rows_kernel, dim3(grid_for((long)B * C * S)), dim3(256), 0, s, feats, B, C, S,
+                     out, lo, nsplit);
+  return hipGetLastError();
+}
+
+hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0, const float* emb,
+                        const float* pe, int D, float scale, float* x, bf16_t* a, long lo, int nsplit, hipStream_t s) {
+  hipLaunchKernelGGL(embed_kernel, dim3(grid_for((long)rows * D)), dim3(256), 0, s, tok, tok_ld, fixed_tok, rows, T,
+                     t0, emb, pe, D, scale, x, a, lo, nsplit);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hipStream_t s) {
+  hipLaunchKernelGGL(fill_col_kernel, dim3(grid_for(B)), dim3(256), 0, s, ids, B, ld, col, value);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int nsplit, hipStream_t s) {
+  hipLaunchKernelGGL(split_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, n, dst, lo, nsplit);
+  return hipGetLastError();
+}
+
+hipError_t launch_f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t s) {
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, dst, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s) {
+  hipLaunchKernelGGL(transpose_heads_kernel, dim3(grid_for((long)H * hd * D)), dim3(256), 0, s, wk, H, hd, D, dst);
+  return hipGetLastError();
+}

@@ -1,0 +1,211 @@
+"""Host side of the HIP hot path: packs a captioning model's state_dict into a libicap handle
+and runs the encoders / decode loops on the current torch stream.
+
+This mirrors the reference's operator surface for the path (models/vit_transformer_model.py):
+`encode` = VisionTransformerEncoder.forward (vit:71-100) / GridFeatureEncoder.forward tail
+(grid:97-108); `greedy` = the `_greedy_search` loop (vit:306-325) including its batch-global
+stop rule; `sample` = SCSTLoss._sample_with_log_probs (scst_loss:202-254) with injected
+uniforms; `decoder_forward` = TransformerDecoder.forward (vit:155-182).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import (DecLayerW, EncLayerW, LnW, MhaW, ModelDesc, VitLayerW, check, stream_ptr)
+
+DEFAULT_PRECISION = "bf16x2"
+
+
+def _ln(sd, p):
+    return LnW(sd[p + ".weight"].data_ptr(), sd[p + ".bias"].data_ptr())
+
+
+def _mha(sd, p):
+    return MhaW(sd[p + ".in_proj_weight"].data_ptr(), sd[p + ".in_proj_bias"].data_ptr(),
+                sd[p + ".out_proj.weight"].data_ptr(), sd[p + ".out_proj.bias"].data_ptr())
+
+
+def apply_stop_rule(ids: torch.Tensor, end_token: int) -> torch.Tensor:
+    """Truncate fixed-length greedy output to the reference's length: `_greedy_search` breaks
+    after the first step at which every sample's newest token is <end> (vit:321-323)."""
+    all_end = (ids[:, 1:] == end_token).all(dim=0)
+    if bool(all_end.any()):
+        L = int(torch.nonzero(all_end)[0, 0]) + 2
+        return ids[:, :L]
+    return ids
+
+
+class Engine:
+    """One packed model on one device.  Not thread-safe (a handle per thread)."""
+
+    def __init__(self, state_dict: Dict[str, torch.Tensor], kind: str, config: dict,
+                 precision: str = DEFAULT_PRECISION, device: torch.device | str | None = None):
+        self.lib = _lib.load()
+        if precision not in _lib.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}")
+        device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if device.type != "cuda":
+            raise _lib.IcapError("the HIP engine needs a GPU device")
+        self.device = device
+        self.kind = kind
+        self.precision = precision
+        sd = {k: v.detach().to(device=device, dtype=torch.float32).contiguous()
+              for k, v in state_dict.items() if torch.is_floating_point(v)}
+        self.d_model = int(config.get("d_model", 512))
+        self.nhead = int(config.get("nhead", 8))
+        emb = sd["decoder.embedding.weight"]
+        self.vocab = emb.shape[0]
+        self.pe_len = sd["decoder.pos_encoder.pe"].shape[1]
+        n_dec = 0
+        while f"decoder.transformer_decoder.layers.{n_dec}.norm1.weight" in sd:
+            n_dec += 1
+        dec = (DecLayerW * n_dec)()
+        for i in range(n_dec):
+            p = f"decoder.transformer_decoder.layers.{i}"
+            dec[i] = DecLayerW(_mha(sd, p + ".self_attn"), _mha(sd, p + ".multihead_attn"),
+                               sd[p + ".linear1.weight"].data_ptr(), sd[p + ".linear1.bias"].data_ptr(),
+                               sd[p + ".linear2.weight"].data_ptr(), sd[p + ".linear2.bias"].data_ptr(),
+                               _ln(sd, p + ".norm1"), _ln(sd, p + ".norm2"), _ln(sd, p + ".norm3"))
+        dim_ff = sd["decoder.transformer_decoder.layers.0.linear1.weight"].shape[0]
+        desc = ModelDesc()
+        desc.precision = _lib.PRECISIONS[precision]
+        desc.d_model, desc.nhead, desc.dim_ff = self.d_model, self.nhead, dim_ff
+        desc.n_dec_layers, desc.vocab, desc.pe_len = n_dec, self.vocab, self.pe_len
+        desc.emb = emb.data_ptr()
+        desc.pe = sd["decoder.pos_encoder.pe"].data_ptr()
+        desc.fc_w = sd["decoder.fc_out.weight"].data_ptr()
+        desc.fc_b = sd["decoder.fc_out.bias"].data_ptr()
+        desc.dec_layers = ctypes.cast(dec, ctypes.POINTER(DecLayerW))
+        keep = [dec]
+        if kind == "vit":
+            P = "encoder.vit."
+            conv = sd[P + "conv_proj.weight"]
+            n_vit = 0
+            while f"{P}encoder.layers.encoder_layer_{n_vit}.ln_1.weight" in sd:
+                n_vit += 1
+            vl = (VitLayerW * n_vit)()
+            for i in range(n_vit):
+                L = f"{P}encoder.layers.encoder_layer_{i}"
+                vl[i] = VitLayerW(_ln(sd, L + ".ln_1"), _mha(sd, L + ".self_attention"), _ln(sd, L + ".ln_2"),
+                                  sd[L + ".mlp.0.weight"].data_ptr(), sd[L + ".mlp.0.bias"].data_ptr(),
+                                  sd[L + ".mlp.3.weight"].data_ptr(), sd[L + ".mlp.3.bias"].data_ptr())
+            keep.append(vl)
+            desc.kind = _lib.KIND_VIT
+            desc.vit_dim = conv.shape[0]
+            desc.vit_heads = conv.shape[0] // 64
+            desc.vit_mlp = sd[f"{P}encoder.layers.encoder_layer_0.mlp.0.weight"].shape[0]
+            desc.vit_layers = n_vit
+            desc.patch = conv.shape[-1]
+            desc.image = 224
+            desc.cls = sd[P + "class_token"].data_ptr()
+            desc.conv_w = conv.data_ptr()
+            desc.conv_b = sd[P + "conv_proj.bias"].data_ptr()
+            desc.pos = sd[P + "encoder.pos_embedding"].data_ptr()
+            desc.vit_ln_w = sd[P + "encoder.ln.weight"].data_ptr()
+            desc.vit_ln_b = sd[P + "encoder.ln.bias"].data_ptr()
+            desc.vit_layers_w = ctypes.cast(vl, ctypes.POINTER(VitLayerW))
+            desc.proj_w = sd["encoder.projection.weight"].data_ptr()
+            desc.proj_b = sd["encoder.projection.bias"].data_ptr()
+            self.mem_tokens = (224 // desc.patch) ** 2
+        elif kind == "grid":
+            n_enc = 0
+            while f"encoder.transformer_encoder.layers.{n_enc}.norm1.weight" in sd:
+                n_enc += 1
+            el = (EncLayerW * n_enc)()
+            for i in range(n_enc):
+                L = f"encoder.transformer_encoder.layers.{i}"
+                el[i] = EncLayerW(_mha(sd, L + ".self_attn"), sd[L + ".linear1.weight"].data_ptr(),
+                                  sd[L + ".linear1.bias"].data_ptr(), sd[L + ".linear2.weight"].data_ptr(),
+                                  sd[L + ".linear2.bias"].data_ptr(), _ln(sd, L + ".norm1"), _ln(sd, L + ".norm2"))
+            keep.append(el)
+            pw = sd["encoder.projection.weight"]
+            desc.kind = _lib.KIND_GRID
+            desc.proj_w = pw.data_ptr()
+            desc.proj_b = sd["encoder.projection.bias"].data_ptr()
+            desc.cnn_dim = pw.shape[1]
+            desc.grid_tokens = 49
+            desc.n_enc_layers = n_enc
+            desc.enc_pe = sd["encoder.pos_encoder.pe"].data_ptr()
+            desc.enc_layers = ctypes.cast(el, ctypes.POINTER(EncLayerW))
+            self.mem_tokens = 49
+        else:
+            raise ValueError(f"unknown model kind {kind!r}")
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            check(self.lib.icap_create(ctypes.byref(desc), stream_ptr(device), ctypes.byref(handle)), "icap_create")
+        self.handle = handle
+        del keep, sd
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.lib.icap_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    # ------------------------------------------------------------------ encoders
+    def encode(self, images: torch.Tensor) -> torch.Tensor:
+        """ViT: images (B,3,224,224) -> memory (B,196,d).  Grid: trunk features (B,2048,7,7)."""
+        x = images.to(device=self.device, dtype=torch.float32).contiguous()
+        B = x.shape[0]
+        mem = torch.empty(B, self.mem_tokens, self.d_model, device=self.device, dtype=torch.float32)
+        if self.kind == "vit":
+            if tuple(x.shape[1:]) != (3, 224, 224):
+                raise ValueError(f"expected (B,3,224,224) images, got {tuple(x.shape)}")
+            check(self.lib.icap_encode_vit(self.handle, x.data_ptr(), B, mem.data_ptr(), stream_ptr(self.device)),
+                  "icap_encode_vit")
+        else:
+            if x.dim() != 4 or x.shape[2] * x.shape[3] != self.mem_tokens:
+                raise ValueError(f"expected (B,C,7,7) trunk features, got {tuple(x.shape)}")
+            check(self.lib.icap_encode_grid_tail(self.handle, x.data_ptr(), B, mem.data_ptr(),
+                                                 stream_ptr(self.device)), "icap_encode_grid_tail")
+        return mem
+
+    # ------------------------------------------------------------------ decoders
+    def greedy_raw(self, memory: torch.Tensor, start: int, end: int, max_len: int,
+                   want_logits: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        mem = memory.to(device=self.device, dtype=torch.float32).contiguous()
+        B, S = mem.shape[0], mem.shape[1]
+        ids = torch.empty(B, max_len, device=self.device, dtype=torch.int32)
+        logits = (torch.empty(max_len - 1, B, self.vocab, device=self.device, dtype=torch.float32)
+                  if want_logits else None)
+        check(self.lib.icap_decode_greedy(self.handle, mem.data_ptr(), B, S, max_len, int(start), int(end),
+                                          ids.data_ptr(), _lib.ptr(logits), stream_ptr(self.device)),
+              "icap_decode_greedy")
+        return ids, logits
+
+    def greedy(self, memory: torch.Tensor, start: int, end: int, max_len: int) -> torch.Tensor:
+        """Reference-identical greedy output (int64, stop rule applied)."""
+        ids, _ = self.greedy_raw(memory, start, end, max_len)
+        return apply_stop_rule(ids.long(), end)
+
+    def sample(self, memory: torch.Tensor, uniforms: torch.Tensor, start: int, end: int,
+               max_len: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Sampled ids (B,max_len) int32 and per-step log-probs (B,max_len-1), no early stop."""
+        mem = memory.to(device=self.device, dtype=torch.float32).contiguous()
+        B, S = mem.shape[0], mem.shape[1]
+        u = uniforms.to(device=self.device, dtype=torch.float32).contiguous()
+        if tuple(u.shape) != (max_len - 1, B):
+            raise ValueError("uniforms must be (max_len-1, B)")
+        ids = torch.empty(B, max_len, device=self.device, dtype=torch.int32)
+        logp = torch.empty(B, max_len - 1, device=self.device, dtype=torch.float32)
+        check(self.lib.icap_decode_sample(self.handle, mem.data_ptr(), B, S, max_len, int(start), int(end),
+                                          u.data_ptr(), ids.data_ptr(), logp.data_ptr(), stream_ptr(self.device)),
+              "icap_decode_sample")
+        return ids, logp
+
+    def decoder_forward(self, tgt: torch.Tensor, memory: torch.Tensor, causal: bool) -> torch.Tensor:
+        t = tgt.to(device=self.device, dtype=torch.int32).contiguous()
+        mem = memory.to(device=self.device, dtype=torch.float32).contiguous()
+        B, T = t.shape
+        logits = torch.empty(B, T, self.vocab, device=self.device, dtype=torch.float32)
+        check(self.lib.icap_decoder_forward(self.handle, t.data_ptr(), B, T, mem.data_ptr(), mem.shape[1],
+                                            int(bool(causal)), logits.data_ptr(), stream_ptr(self.device)),
+              "icap_decoder_forward")
+        return logits

@@ -1,0 +1,127 @@
+/*
+ * icap.h — C ABI of the MI355X-native image-captioning hot path (libicap.so).
+ *
+ * The reference (wonder-dream/image_caption) is pure PyTorch; its "plugin API" for this path is
+ * the nn.Module surface of models/{vit,grid}_transformer_model.py.  These entry points are what
+ * that surface binds through ctypes (image_caption_amd/_lib.py); each one cites the reference
+ * function it replaces.  Conventions:
+ *   - plain pointers and sizes only; every tensor pointer is caller-owned DEVICE memory
+ *     (row-major, contiguous); `stream` is a hipStream_t (may be NULL = legacy stream);
+ *   - the library owns only packed weights and its workspace;
+ *   - every call returns 0 on success, non-zero on error, with icap_last_error() describing it;
+ *     no C++ exception crosses the ABI; calls are asynchronous on `stream`;
+ *   - a handle is not thread-safe.
+ */
+#ifndef ICAP_H_
+#define ICAP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ICAP_ABI_VERSION 1
+
+#define ICAP_KIND_VIT 0   /* ViTTransformerCaptioning  (models/vit_transformer_model.py:185)  */
+#define ICAP_KIND_GRID 1  /* GridTransformerCaptioning (models/grid_transformer_model.py:161) */
+
+#define ICAP_PREC_BF16 1   /* bf16 operands, fp32 accumulate                                  */
+#define ICAP_PREC_BF16X2 2 /* activations as hi+lo bf16 pairs (~16 mantissa bits), fp32 acc  */
+
+typedef struct icap_handle icap_handle;
+
+/* Parameter pointers are device fp32 tensors with the reference state_dict shapes. */
+typedef struct { const float *w, *b; } icap_ln_w;                                 /* nn.LayerNorm */
+typedef struct { const float *in_w, *in_b, *out_w, *out_b; } icap_mha_w;         /* nn.MultiheadAttention */
+
+typedef struct { /* torchvision EncoderBlock: encoder.vit.encoder.layers.encoder_layer_{i} */
+  icap_ln_w ln_1;
+  icap_mha_w attn;
+  icap_ln_w ln_2;
+  const float *mlp0_w, *mlp0_b, *mlp3_w, *mlp3_b;
+} icap_vit_layer_w;
+
+typedef struct { /* nn.TransformerEncoderLayer (post-LN, ReLU): encoder.transformer_encoder.layers.{i} */
+  icap_mha_w attn;
+  const float *lin1_w, *lin1_b, *lin2_w, *lin2_b;
+  icap_ln_w norm1, norm2;
+} icap_enc_layer_w;
+
+typedef struct { /* nn.TransformerDecoderLayer (post-LN, ReLU): decoder.transformer_decoder.layers.{i} */
+  icap_mha_w self_attn, cross_attn;
+  const float *lin1_w, *lin1_b, *lin2_w, *lin2_b;
+  icap_ln_w norm1, norm2, norm3;
+} icap_dec_layer_w;
+
+typedef struct {
+  int kind, precision;
+  /* decoder (TransformerDecoder, vit:103-182) */
+  int d_model, nhead, dim_ff, n_dec_layers, vocab, pe_len;
+  const float *emb, *pe, *fc_w, *fc_b;
+  const icap_dec_layer_w* dec_layers;
+  /* ViT-B/16 trunk + projection (VisionTransformerEncoder, vit:36-100) */
+  int vit_dim, vit_heads, vit_mlp, vit_layers, patch, image;
+  const float *cls, *conv_w, *conv_b, *pos, *vit_ln_w, *vit_ln_b;
+  const icap_vit_layer_w* vit_layers_w;
+  /* encoder.projection: Linear(768->d) for ViT, Conv2d(2048->d, 1x1) for Grid */
+  const float *proj_w, *proj_b;
+  /* Grid tail (GridFeatureEncoder after self.cnn, grid:97-108) */
+  int cnn_dim, grid_tokens, n_enc_layers;
+  const float* enc_pe;
+  const icap_enc_layer_w* enc_layers;
+} icap_model_desc;
+
+int icap_abi_version(void);
+const char* icap_last_error(void);
+
+/* Packs the model's weights (bf16 GEMM operands + fp32 small params) into handle-owned memory.
+ * Replaces: build_model(...) + load_state_dict(...) + .to(device)
+ * (models/vit_transformer_model.py:423-444, scripts/inference_vit_transformer.py:50-52). */
+int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out);
+int icap_destroy(icap_handle* h);
+
+/* images (B,3,224,224) fp32 normalised -> memory (B,196,d_model) fp32.
+ * Replaces: VisionTransformerEncoder.forward, models/vit_transformer_model.py:71-100. */
+int icap_encode_vit(icap_handle* h, const float* images, int B, float* memory, void* stream);
+
+/* ResNet trunk features (B,cnn_dim,7,7) fp32 -> memory (B,49,d_model) fp32.
+ * Replaces: GridFeatureEncoder.forward after self.cnn, models/grid_transformer_model.py:97-108. */
+int icap_encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, void* stream);
+
+/* Greedy decode of max_len-1 steps with a KV cache: ids (B,max_len) int32, column 0 = start.
+ * step_logits (max_len-1,B,vocab) fp32 is optional (NULL to skip).  The reference's batch-global
+ * stop rule (break when every latest token == end) is applied by the caller on the returned ids.
+ * Replaces: _greedy_search loop, models/vit_transformer_model.py:306-325 (grid:237-249). */
+int icap_decode_greedy(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                       int end_token, int32_t* ids, float* step_logits, void* stream);
+
+/* Sampled decode with injected uniforms (max_len-1,B) in [0,1): ids (B,max_len) int32 and
+ * log-probs (B,max_len-1) fp32, zeroed after a sample has emitted end (masked_fill semantics).
+ * Replaces: SCSTLoss._sample_with_log_probs, utils/scst_loss.py:202-254 (torch.multinomial ->
+ * inverse CDF on the injected uniforms). */
+int icap_decode_sample(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                       int end_token, const float* uniforms, int32_t* ids, float* logp, void* stream);
+
+/* Full-prefix decoder forward: tgt (B,T) int32 -> logits (B,T,vocab) fp32, causal or unmasked.
+ * Replaces: TransformerDecoder.forward, models/vit_transformer_model.py:155-182 (no padding masks;
+ * causal=0 is the scripts/inference.py:79 call without tgt_mask). */
+int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const float* memory, int S,
+                         int causal, float* logits, void* stream);
+
+/* ---- op-level entry points (kernel parity tests) ---- */
+/* C = epi(A·W^T + bias); A = nsplit bf16 planes (plane stride a_lo); W (N,K) bf16.
+ * epi: 0 none, 1 GELU(erf), 2 ReLU.  out: 0 fp32, 1 bf16, 2 split bf16 planes, 3 fp32 +=. */
+int icap_op_gemm(const uint16_t* A, long lda, long a_lo, int nsplit, const uint16_t* W, const float* bias,
+                 void* C, long ldc, long c_lo, int M, int N, int K, int epi, int out, void* stream);
+int icap_op_layernorm(const float* x, int rows, int D, const float* w, const float* b, float eps,
+                      float* out_f32, uint16_t* out_bf, long bf_lo, int nsplit, void* stream);
+/* qkv planes (B*N, 3*H*64) -> out planes (B*N, H*64), non-causal softmax(QK^T/8)V. */
+int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uint16_t* out, long out_lo,
+                          int nsplit, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ICAP_H_ */

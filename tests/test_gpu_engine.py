@@ -1,0 +1,40 @@
+"""End-to-end parity of the HIP engine against the CPU oracle (oracle/captioner.py)."""
+import numpy as np
+import pytest
+import torch
+
+from image_caption_amd import weights as W
+from oracle import captioner as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def vit_sd():
+    return W.to_torch(W.vit_state_dict(0))
+
+
+@pytest.mark.parametrize("precision", ["bf16x2", "bf16"])
+def test_vit_encode_and_greedy(cuda, vit_sd, precision):
+    from image_caption_amd.engine import Engine
+
+    eng = Engine(vit_sd, "vit", {}, precision=precision, device=cuda)
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=3))
+    mem_ref = O.vit_encode(vit_sd, imgs)
+    mem = eng.encode(imgs.to(cuda)).cpu()
+    err = (mem - mem_ref).abs().max().item()
+    tol = 1e-3 if precision == "bf16x2" else 5e-2
+    assert err < tol, err
+    ids, logits = eng.greedy_raw(mem_ref.to(cuda), 107, 108, 30, want_logits=True)
+    ids = ids.cpu().long()
+    ref_ids, ref_tr = O.greedy_from_memory(vit_sd, mem_ref, 107, 108, 30, return_trace=True)
+    # teacher-forced logits on the reference prefix
+    tf = O.teacher_forced_logits(vit_sd, mem_ref, ref_ids)
+    tf_hip = eng.decoder_forward(ref_ids[:, :-1].to(cuda), mem_ref.to(cuda), causal=True).cpu()
+    lerr = (tf_hip - tf).abs().max().item()
+    if precision == "bf16x2":
+        assert lerr < 1e-3, lerr
+        assert torch.equal(ids[:, : ref_ids.shape[1]], ref_ids)
+        assert (logits.cpu()[: ref_tr.shape[0]] - ref_tr).abs().max().item() < 1e-3
+    else:
+        assert lerr < 1e-1, lerr

@@ -1,0 +1,116 @@
+"""Kernel-level parity of the HIP ops against fp64 torch references of the same op.
+
+Inputs are hi/lo bf16 planes (the engine's activation format), so the exact value the kernel
+sees is hi+lo; tolerances are written per test."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from image_caption_amd import _lib
+
+    return _lib, _lib.load()
+
+
+def planes(x: torch.Tensor, nsplit: int) -> torch.Tensor:
+    hi = x.to(torch.bfloat16)
+    if nsplit == 1:
+        return hi.contiguous()
+    lo = (x - hi.float()).to(torch.bfloat16)
+    return torch.stack([hi, lo]).contiguous()
+
+
+def value(p: torch.Tensor, nsplit: int) -> torch.Tensor:
+    return p.double() if nsplit == 1 else p[0].double() + p[1].double()
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (64, 64, 64), (8192, 1024, 768), (50, 512, 2048)])
+@pytest.mark.parametrize("nsplit", [1, 2])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm(cuda, M, N, K, nsplit, epi):
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K + epi)
+    a = torch.randn(M, K, generator=g).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    A = planes(a, nsplit)
+    ref = value(A, nsplit) @ w.double().t() + bias.double()
+    if epi == 1:
+        ref = torch.nn.functional.gelu(ref)
+    elif epi == 2:
+        ref = torch.relu(ref)
+    # fp32 output
+    C = torch.empty(M, N, device=cuda)
+    L.check(lib.icap_op_gemm(A.data_ptr(), K, M * K, nsplit, w.data_ptr(), bias.data_ptr(), C.data_ptr(), N, 0,
+                             M, N, K, epi, 0, L.stream_ptr()), "gemm")
+    torch.cuda.synchronize()
+    err = (C.double() - ref).abs().max().item()
+    assert err < 2e-4 * max(1.0, ref.abs().max().item()), err
+    # split-plane output, residual accumulate
+    Cs = torch.empty(2, M, N, device=cuda, dtype=torch.bfloat16)
+    L.check(lib.icap_op_gemm(A.data_ptr(), K, M * K, nsplit, w.data_ptr(), bias.data_ptr(), Cs.data_ptr(), N, M * N,
+                             M, N, K, epi, 2, L.stream_ptr()), "gemm split")
+    R = torch.randn(M, N, generator=g).to(cuda)
+    R0 = R.clone()
+    L.check(lib.icap_op_gemm(A.data_ptr(), K, M * K, nsplit, w.data_ptr(), bias.data_ptr(), R.data_ptr(), N, 0,
+                             M, N, K, epi, 3, L.stream_ptr()), "gemm resid")
+    torch.cuda.synchronize()
+    assert (value(Cs, 2) - C.double()).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())
+    assert (R.double() - R0.double() - C.double()).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())
+
+
+def test_gemm_identity_asymmetric(cuda):
+    """A = I, asymmetric W: catches a transposed C write (cdna_hip_programming.md §3)."""
+    L, lib = _lib()
+    n = 128
+    A = torch.eye(n, device=cuda).to(torch.bfloat16).contiguous()
+    w = (torch.arange(n * n, device=cuda, dtype=torch.float32).reshape(n, n) % 251).to(torch.bfloat16)
+    C = torch.empty(n, n, device=cuda)
+    L.check(lib.icap_op_gemm(A.data_ptr(), n, 0, 1, w.data_ptr(), None, C.data_ptr(), n, 0, n, n, n, 0, 0,
+                             L.stream_ptr()), "gemm")
+    torch.cuda.synchronize()
+    assert torch.equal(C, w.float().t())
+
+
+@pytest.mark.parametrize("D", [512, 768])
+@pytest.mark.parametrize("nsplit", [1, 2])
+def test_layernorm(cuda, D, nsplit):
+    L, lib = _lib()
+    rows = 333
+    x = (torch.randn(rows, D, device=cuda) * 3 + 1).contiguous()
+    w = torch.randn(D, device=cuda)
+    b = torch.randn(D, device=cuda)
+    ref = torch.nn.functional.layer_norm(x.double(), (D,), w.double(), b.double(), 1e-6)
+    y = torch.empty_like(x)
+    yb = torch.empty(nsplit, rows, D, device=cuda, dtype=torch.bfloat16)
+    L.check(lib.icap_op_layernorm(x.data_ptr(), rows, D, w.data_ptr(), b.data_ptr(), 1e-6, y.data_ptr(),
+                                  yb.data_ptr(), rows * D, nsplit, L.stream_ptr()), "ln")
+    torch.cuda.synchronize()
+    assert (y.double() - ref).abs().max().item() < 1e-5
+    # bf16 hi plane: |err| <= 2^-9 |y|; hi+lo: ~2^-17 |y|
+    rel = 2.0 ** -8 if nsplit == 1 else 2.0 ** -15
+    got = value(yb if nsplit == 2 else yb[0], nsplit)
+    assert ((got - ref).abs() <= rel * ref.abs() + 1e-6).all()
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (3, 49, 8), (1, 7, 2)])
+@pytest.mark.parametrize("nsplit", [1, 2])
+def test_enc_attention(cuda, B, N, H, nsplit):
+    L, lib = _lib()
+    D = H * 64
+    g = torch.Generator(device="cpu").manual_seed(B * N + H)
+    qkv = (torch.randn(B * N, 3 * D, generator=g) * 1.5).to(cuda)
+    P = planes(qkv, nsplit)
+    v = value(P, nsplit).view(B, N, 3, H, 64)
+    q, k, vv = v[:, :, 0].transpose(1, 2), v[:, :, 1].transpose(1, 2), v[:, :, 2].transpose(1, 2)
+    ref = torch.softmax(q @ k.transpose(-1, -2) / 8.0, -1) @ vv
+    ref = ref.transpose(1, 2).reshape(B * N, D)
+    out = torch.zeros(nsplit, B * N, D, device=cuda, dtype=torch.bfloat16)
+    L.check(lib.icap_op_enc_attention(P.data_ptr(), B * N * 3 * D, B, N, H, out.data_ptr(), B * N * D, nsplit,
+                                      L.stream_ptr()), "attn")
+    torch.cuda.synchronize()
+    got = value(out if nsplit == 2 else out[0], nsplit)
+    tol = 3e-2 if nsplit == 1 else 2e-4
+    assert (got - ref).abs().max().item() < tol
