@@ -1,0 +1,157 @@
+"""Headline benchmark: captions/s of the ViT-B/16 + 6-layer decoder greedy path (224x224,
+max_len=30) on N MI355X, data-parallel over images (BASELINE.json `metric`, configs[1] at N=1,
+configs[3] shape at N=8 with 256 images per GPU).
+
+A step = one pass of the hot path over one batch of synthetic images already resident in HBM:
+ViT encoder -> 29 KV-cached greedy decode steps -> (N>1) one RCCL all-gather of the int32 ids ->
+the reference's batch-global stop rule.  Launch as
+  python bench.py [--gpus 1 --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel's algorithmic rate measured
+with HIP events around each of its launches inside the timed region; `cpu_baseline` times the
+CPU oracle (fp32 restatement of the reference algorithm, full-prefix recompute) on the host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from image_caption_amd import _lib, parallel  # noqa: E402
+from image_caption_amd import weights as W  # noqa: E402
+from image_caption_amd.engine import Engine, apply_stop_rule  # noqa: E402
+
+METRIC = "captions/sec (224×224, max_len=30, greedy) at 1/2/4/8 MI355X vs CPU ref"
+PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA, MI355X_MICROARCH.md chip table
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(seconds: float, batch: int, max_len: int) -> dict:
+    """Oracle (port of the reference algorithm, fp32, full-prefix recompute) on host cores."""
+    from oracle import captioner as O
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = W.to_torch(W.vit_state_dict(0))
+    imgs = torch.from_numpy(W.synthetic_images(batch, seed=99))
+    O.greedy_search(sd, imgs, W.START_TOKEN, W.END_TOKEN, max_len)  # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.greedy_search(sd, imgs, W.START_TOKEN, W.END_TOKEN, max_len)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(n * batch / el, 3), "unit": "captions/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/captioner.py greedy_search fp32, {n} call(s) x {batch} images, max_len={max_len}, "
+                      f"{el:.1f} s on {threads} host threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--max-len", type=int, default=30)
+    ap.add_argument("--precision", default="bf16x2", choices=sorted(_lib.PRECISIONS))
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, ws, local = parallel.init()
+    if ws != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    sd = W.to_torch(W.vit_state_dict(0))
+    eng = Engine(sd, "vit", {}, precision=args.precision, device=dev)
+    B = args.batch
+    total = B * ws
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=1 + rank)).to(dev)
+    L = args.max_len
+
+    def step():
+        mem = eng.encode(imgs)
+        ids, _ = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L)
+        if ws > 1:
+            ids = parallel.gather_rows(ids, total)
+        return apply_stop_rule(ids.long(), W.END_TOKEN)
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+
+    eng.profile(True)
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    prof = [eng.profile_read(c) for c in (_lib.PROF_GEMM_128, _lib.PROF_GEMM_64, _lib.PROF_ENC_ATTN,
+                                          _lib.PROF_CROSS_ATTN)]
+    eng.profile(False)
+    value = total * args.steps / el
+    if rank == 0:
+        step_ms = el / args.steps * 1e3
+        dom = max(prof, key=lambda p: p["ms"])
+        avg_ms = dom["ms"] / max(dom["launches"], 1)
+        for p in prof:
+            log(f"  {p['kernel']:34s} launches {p['launches']:6d}  {p['ms'] / args.steps:9.3f} ms/step  "
+                f"{p['flops'] / max(p['ms'], 1e-9) / 1e9:9.1f} TFLOP/s alg  "
+                f"{p['bytes'] / max(p['ms'], 1e-9) / 1e6:9.1f} GB/s operand")
+        if "attn" in dom["kernel"] and "cross" in dom["kernel"]:
+            achieved = dom["bytes"] / dom["launches"] / (avg_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None}
+        else:
+            achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None}
+        roof.update({"kernel": dom["kernel"], "launches_per_step": dom["launches"] // args.steps,
+                     "avg_launch_us": round(avg_ms * 1e3, 2),
+                     "share_of_step": round(dom["ms"] / args.steps / step_ms, 3)})
+        cpu = None
+        if ws == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds, args.cpu_batch, L)
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "captions/s", "n_gpus": ws, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic images N(0,1) + seeded random-init weights",
+            "config": {"workload": "vit_b16 encoder + 6-layer decoder, greedy, 224x224, max_len=30",
+                       "per_gpu_batch": B, "global_batch": total, "max_len": L, "precision": args.precision,
+                       "decode_steps": L - 1, "output_len": int(out.shape[1]), "parallelism": f"dp{ws}"},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -151,10 +151,14 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
+int gemm_tile_class(const GemmArgs& g) {
+  const long big_tiles = (long)((g.M + 127) / 128) * (g.N / 128) * g.batch;
+  return (g.N % 128 == 0 && big_tiles >= 512) ? PROF_GEMM_128 : PROF_GEMM_64;
+}
+
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
   if (g.K % BK != 0 || g.N % 64 != 0 || (g.nsplit != 1 && g.nsplit != 2)) return hipErrorInvalidValue;
-  const long big_tiles = (long)((g.M + 127) / 128) * (g.N / 128) * g.batch;
-  if (g.N % 128 == 0 && big_tiles >= 512) return run<128, 128, 64, 64>(g, s);
+  if (gemm_tile_class(g) == PROF_GEMM_128) return run<128, 128, 64, 64>(g, s);
   return run<64, 64, 32, 32>(g, s);
 }

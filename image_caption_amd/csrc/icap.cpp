@@ -105,11 +105,48 @@ struct icap_handle {
   // grid
   float* enc_pe = nullptr;
   std::vector<EncLayer> enc;
+  // live kernel timing (icap_profile_*): HIP events bracket each launch of the hot kernels
+  struct ProfRec {
+    int cls;
+    double flops, bytes;
+    hipEvent_t a, b;
+  };
+  bool prof_on = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<ProfRec> prof;
+  hipEvent_t ev() {
+    if (ev_used == ev_pool.size()) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      ev_pool.push_back(e);
+    }
+    return ev_pool[ev_used++];
+  }
+  template <class F>
+  void timed(int cls, double flops, double bytes, hipStream_t s, F&& launch) {
+    if (!prof_on) {
+      launch();
+      return;
+    }
+    ProfRec r{cls, flops, bytes, ev(), ev()};
+    HIPCHK(hipEventRecord(r.a, s));
+    launch();
+    HIPCHK(hipEventRecord(r.b, s));
+    prof.push_back(r);
+  }
+  void run_gemm(const GemmArgs& g, hipStream_t s) {
+    const double flops = 2.0 * g.M * g.N * g.K * g.batch;  // algorithmic (one plane)
+    const double bytes = 2.0 * g.batch * ((double)g.M * g.K * g.nsplit + (double)g.N * g.K);
+    timed(gemm_tile_class(g), flops, bytes, s, [&] { HIPCHK(launch_gemm(g, s)); });
+  }
+
   // workspaces
   DevBuf e_x, e_a, e_qkv, e_h, e_patch;  // encoder
   DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin;  // decoder
 
   ~icap_handle() {
+    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_x, &d_a, &d_qkv, &d_q, &d_qt, &d_c, &d_o, &d_h,
                       &d_kv, &d_fin})
@@ -154,7 +191,14 @@ struct icap_handle {
     g.C = C; g.ldc = ldc; g.c_lo = c_lo;
     g.M = M; g.N = W.N; g.K = W.K; g.nsplit = ns; g.c_planes = ns;
     g.epi = epi; g.out = out;
-    HIPCHK(launch_gemm(g, s));
+    run_gemm(g, s);
+  }
+  void attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, bf16_t* out, long out_ld, long out_lo,
+                 hipStream_t s) {
+    const double flops = 4.0 * B * H * (double)N * N * 64;
+    const double bytes = 2.0 * ns * B * (double)N * H * 64 * 4;
+    timed(PROF_ENC_ATTN, flops, bytes, s,
+          [&] { HIPCHK(launch_enc_attention(qkv, ld, lo, B, N, H, 0.125f, out, out_ld, out_lo, ns, s)); });
   }
 };
 
@@ -232,7 +276,7 @@ void enc_layer_postln(icap_handle* h, const EncLayer& L, int B, int N, float* x,
   const int D = h->d.d_model, F = h->d.dim_ff, M = B * N;
   const long aL = (long)M * D, qL = (long)M * 3 * D, hL = (long)M * F;
   h->gemm(a, D, aL, L.qkv, M, qkv, 3 * D, qL, EPI_NONE, OUT_SPLIT, s);
-  HIPCHK(launch_enc_attention(qkv, 3 * D, qL, B, N, D / 64, 0.125f, a, D, aL, h->ns, s));
+  h->attention(qkv, 3 * D, qL, B, N, D / 64, a, D, aL, s);
   h->gemm(a, D, aL, L.out, M, x, D, 0, EPI_NONE, OUT_F32_RESID, s);
   HIPCHK(launch_layernorm(x, D, M, D, 0, 0, 0, L.n1.w, L.n1.b, 1e-5f, x, D, a, D, aL, h->ns, s));
   h->gemm(a, D, aL, L.lin1, M, hb, F, hL, EPI_RELU, OUT_SPLIT, s);
@@ -266,13 +310,13 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
     ga.epi = EPI_NONE; ga.out = OUT_F32;
     ga.rm_group = np; ga.rm_stride = T; ga.rm_off = 1;
     ga.addend = h->pos; ga.add_ld = V; ga.add_group = np; ga.add_off = 1;
-    HIPCHK(launch_gemm(ga, s));
+    h->run_gemm(ga, s);
   }
   HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
   for (const VitLayer& L : h->vit) {
     HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
     h->gemm(a, V, aL, L.qkv, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s);
-    HIPCHK(launch_enc_attention(qkv, 3 * V, qL, B, T, d.vit_heads, 0.125f, a, V, aL, ns, s));
+    h->attention(qkv, 3 * V, qL, B, T, d.vit_heads, a, V, aL, s);
     h->gemm(a, V, aL, L.out, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s);
     HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
     h->gemm(a, V, aL, L.mlp0, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);
@@ -303,7 +347,7 @@ void encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, 
     ga.M = M; ga.N = D; ga.K = C; ga.nsplit = ns;
     ga.epi = EPI_NONE; ga.out = OUT_F32;
     ga.addend = h->enc_pe; ga.add_ld = D; ga.add_group = N; ga.add_off = 0;
-    HIPCHK(launch_gemm(ga, s));
+    h->run_gemm(ga, s);
   }
   // activation planes of x for the first encoder layer's QKV GEMM
   HIPCHK(launch_split_f32(memory, (long)M * D, a, (long)M * D, ns, s));
@@ -362,9 +406,11 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       g.C = b.qt; g.ldc = (long)H * D; g.c_batch = D;
       g.M = rows; g.N = D; g.K = 64; g.nsplit = ns; g.batch = H;
       g.epi = EPI_NONE; g.out = OUT_F32;
-      HIPCHK(launch_gemm(g, s));
+      h->run_gemm(g, s);
     }
-    HIPCHK(launch_cross_attn_absorbed(b.qt, mem, rows, n_new, S, H, D, 0.125f, b.c, b.cL, ns, s));
+    h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 4.0 * (double)(rows / n_new) * S * D, s, [&] {
+      HIPCHK(launch_cross_attn_absorbed(b.qt, mem, rows, n_new, S, H, D, 0.125f, b.c, b.cL, ns, s));
+    });
     {
       GemmArgs g = gemm_args();  // o[:, h*64:(h+1)*64] = c_h · Wv_h^T + bv_h
       g.A = b.c; g.lda = (long)H * D; g.a_batch = D; g.a_lo = b.cL;
@@ -373,7 +419,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       g.C = b.o; g.ldc = D; g.c_batch = 64; g.c_lo = b.aL;
       g.M = rows; g.N = 64; g.K = D; g.nsplit = ns; g.batch = H; g.c_planes = ns;
       g.epi = EPI_NONE; g.out = OUT_SPLIT;
-      HIPCHK(launch_gemm(g, s));
+      h->run_gemm(g, s);
     }
     h->gemm(b.o, D, b.aL, L.ca_out, rows, b.x, D, 0, EPI_NONE, OUT_F32_RESID, s);
     HIPCHK(launch_layernorm(b.x, D, rows, D, 0, 0, 0, L.n2.w, L.n2.b, 1e-5f, b.x, D, b.a, D, b.aL, ns, s));
@@ -510,6 +556,38 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
     h->d_fin.ensure((size_t)rows * 4);  // scratch ids
     ha.ids = h->d_fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
     HIPCHK(launch_head(ha, s));
+  });
+}
+
+int icap_profile_enable(icap_handle* h, int enable) {
+  return guarded([&] {
+    REQUIRE(h, "null handle");
+    h->prof_on = enable != 0;
+    h->prof.clear();
+    h->ev_used = 0;
+  });
+}
+
+int icap_profile_read(icap_handle* h, int kernel_class, double* total_ms, long* launches, double* flops,
+                      double* bytes) {
+  return guarded([&] {
+    REQUIRE(h && total_ms && launches && flops && bytes, "bad arguments");
+    double t = 0, f = 0, b = 0;
+    long n = 0;
+    for (const auto& r : h->prof) {
+      if (r.cls != kernel_class) continue;
+      HIPCHK(hipEventSynchronize(r.b));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, r.a, r.b));
+      t += ms;
+      f += r.flops;
+      b += r.bytes;
+      ++n;
+    }
+    *total_ms = t;
+    *launches = n;
+    *flops = f;
+    *bytes = b;
   });
 }
 

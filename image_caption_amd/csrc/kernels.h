@@ -23,6 +23,9 @@ struct GemmArgs {
 };
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
+// Which gemm_bf16_kernel instantiation launch_gemm picks (PROF_GEMM_128 / PROF_GEMM_64).
+int gemm_tile_class(const GemmArgs& g);
+enum { PROF_GEMM_128 = 0, PROF_GEMM_64 = 1, PROF_ENC_ATTN = 2, PROF_CROSS_ATTN = 3 };
 
 // LayerNorm over rows of D fp32 values; optional fp32 output (may alias input) and
 // bf16 hi(/lo) planes.  Input row r is read from (r / in_group) * in_stride + in_off + r % in_group.

@@ -209,3 +209,17 @@ class Engine:
                                             int(bool(causal)), logits.data_ptr(), stream_ptr(self.device)),
               "icap_decoder_forward")
         return logits
+
+    # ------------------------------------------------------------------ live kernel timing
+    def profile(self, enable: bool) -> None:
+        check(self.lib.icap_profile_enable(self.handle, int(bool(enable))), "icap_profile_enable")
+
+    def profile_read(self, kernel_class: int) -> dict:
+        """Device time of every recorded launch of one kernel class (HIP events on the launch
+        stream), with the launches' algorithmic flops and operand bytes."""
+        t, n = ctypes.c_double(), ctypes.c_long()
+        f, b = ctypes.c_double(), ctypes.c_double()
+        check(self.lib.icap_profile_read(self.handle, kernel_class, ctypes.byref(t), ctypes.byref(n),
+                                         ctypes.byref(f), ctypes.byref(b)), "icap_profile_read")
+        return {"kernel": _lib.PROF_NAMES[kernel_class], "ms": t.value, "launches": n.value,
+                "flops": f.value, "bytes": b.value}

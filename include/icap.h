@@ -110,6 +110,18 @@ int icap_decode_sample(icap_handle* h, const float* memory, int B, int S, int ma
 int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const float* memory, int S,
                          int causal, float* logits, void* stream);
 
+/* ---- live kernel timing (bench.py roofline) ---- */
+#define ICAP_PROF_GEMM_128 0   /* gemm_bf16_kernel<128,128,64,64> (encoder GEMMs)      */
+#define ICAP_PROF_GEMM_64 1    /* gemm_bf16_kernel<64,64,32,32>  (decode-step GEMMs)    */
+#define ICAP_PROF_ENC_ATTN 2   /* enc_attention_kernel                                  */
+#define ICAP_PROF_CROSS_ATTN 3 /* cross_attn_absorbed_kernel                            */
+/* Enable (1) / disable (0) HIP-event bracketing of every hot-kernel launch; clears records. */
+int icap_profile_enable(icap_handle* h, int enable);
+/* Sum over recorded launches of one class: device ms, launch count, algorithmic flops and bytes
+ * (flops count one activation plane; bytes are the operand bytes the launches must read). */
+int icap_profile_read(icap_handle* h, int kernel_class, double* total_ms, long* launches, double* flops,
+                      double* bytes);
+
 /* ---- op-level entry points (kernel parity tests) ---- */
 /* C = epi(A·W^T + bias); A = nsplit bf16 planes (plane stride a_lo); W (N,K) bf16.
  * epi: 0 none, 1 GELU(erf), 2 ReLU.  out: 0 fp32, 1 bf16, 2 split bf16 planes, 3 fp32 +=. */

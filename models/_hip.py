@@ -1,0 +1,77 @@
+"""Routing between the nn.Module surface and the HIP engine (image_caption_amd.engine).
+
+Rule: a call takes the HIP path when its tensors are on a GPU, autograd is off,
+the module is in eval mode and the call is expressible by the engine (generate/greedy; decoder
+forward with no mask or the causal mask and no padding masks; encoder forward).  Training calls
+(grad on, dropout on, padding masks) keep the module's own PyTorch semantics - those are not the
+hot path.  On a GPU the HIP path has no silent fallback: if libicap.so cannot load, the call
+raises.  `backend="torch"` in the model config forces the PyTorch modules, `backend="hip"`
+forbids them.
+"""
+from __future__ import annotations
+
+import weakref
+from typing import Optional
+
+import torch
+
+BACKENDS = ("auto", "hip", "torch")
+
+
+def attach_owner(child: torch.nn.Module, owner: torch.nn.Module) -> None:
+    object.__setattr__(child, "_hip_owner", weakref.ref(owner))
+
+
+def owner_of(child: torch.nn.Module) -> Optional[torch.nn.Module]:
+    ref = getattr(child, "_hip_owner", None)
+    return ref() if ref is not None else None
+
+
+def is_causal_mask(mask: torch.Tensor, T: int) -> bool:
+    """Same test as torch's _detect_is_causal_mask: equal to the standard causal float mask."""
+    if mask is None or mask.dim() != 2 or mask.shape != (T, T):
+        return False
+    ref = torch.triu(torch.full((T, T), float("-inf"), device=mask.device, dtype=mask.dtype), diagonal=1)
+    if mask.dtype == torch.bool:
+        return bool(torch.equal(mask, ref.isinf()))
+    return bool(torch.equal(mask, ref))
+
+
+class HipRouted:
+    """Mixin for the top-level captioning models (engine cache + routing decision)."""
+
+    _hip_kind = "vit"
+
+    def _hip_setup(self, backend: str = "auto", precision: str = "bf16x2") -> None:
+        if backend not in BACKENDS:
+            raise ValueError(f"backend must be one of {BACKENDS}")
+        object.__setattr__(self, "hip_backend", backend)
+        object.__setattr__(self, "hip_precision", precision)
+        object.__setattr__(self, "_hip_cache", None)
+
+    def use_hip(self, x: torch.Tensor, *, grad_ok: bool = False) -> bool:
+        if self.hip_backend == "torch":
+            return False
+        on_gpu = x.is_cuda
+        if self.hip_backend == "hip" and not on_gpu:
+            raise RuntimeError("backend='hip' needs GPU tensors")
+        if not on_gpu:
+            return False
+        if self.training or (torch.is_grad_enabled() and not grad_ok):
+            if self.hip_backend == "hip":
+                raise RuntimeError("backend='hip' serves eval-mode, no-grad calls only")
+            return False
+        return True
+
+    def hip_engine(self, device: torch.device):
+        from image_caption_amd.engine import Engine
+
+        tensors = [t for t in self.state_dict().values() if torch.is_tensor(t)]
+        key = (str(device), self.hip_precision, tuple((t.data_ptr(), t._version) for t in tensors))
+        cache = self._hip_cache
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        eng = Engine(self.state_dict(), self._hip_kind, {"d_model": self.d_model},
+                     precision=self.hip_precision, device=device)
+        object.__setattr__(self, "_hip_cache", (key, eng))
+        return eng

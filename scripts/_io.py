@@ -1,0 +1,75 @@
+"""Image preprocessing and checkpoint loading shared by the drop-in inference scripts.
+
+torchvision is absent here, so the transforms of the reference scripts are restated on PIL +
+numpy with torchvision's semantics for PIL inputs:
+  * Resize(256) + CenterCrop(224)  (scripts/inference_vit_transformer.py:75-80)
+  * Resize((224, 224))            (scripts/inference_grid_transformer.py:43-47, scripts/inference.py:47-53)
+  * ToTensor + Normalize(ImageNet mean/std)
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import torch
+
+MEAN = np.array([0.485, 0.456, 0.406], dtype=np.float32)
+STD = np.array([0.229, 0.224, 0.225], dtype=np.float32)
+
+
+def _pil():
+    from PIL import Image
+
+    return Image
+
+
+def resize_shorter(img, size: int):
+    w, h = img.size
+    if w <= h:
+        nw, nh = size, int(size * h / w)
+    else:
+        nw, nh = int(size * w / h), size
+    return img.resize((nw, nh), _pil().BILINEAR)
+
+
+def center_crop(img, size: int):
+    w, h = img.size
+    top = int(round((h - size) / 2.0))
+    left = int(round((w - size) / 2.0))
+    return img.crop((left, top, left + size, top + size))
+
+
+def to_normalized_tensor(img) -> torch.Tensor:
+    a = np.asarray(img.convert("RGB"), dtype=np.float32) / 255.0
+    a = (a - MEAN) / STD
+    return torch.from_numpy(np.ascontiguousarray(a.transpose(2, 0, 1)))
+
+
+def preprocess(image_path: str, mode: str = "crop", image_size: int = 224) -> torch.Tensor:
+    """(3,H,W) normalised tensor; mode "crop" = Resize(256)+CenterCrop, "square" = Resize((s,s))."""
+    img = _pil().open(image_path).convert("RGB")
+    if mode == "crop":
+        img = center_crop(resize_shorter(img, 256), image_size)
+    else:
+        img = img.resize((image_size, image_size), _pil().BILINEAR)
+    return to_normalized_tensor(img)
+
+
+def load_checkpoint(path: str, device):
+    """torch.load with weights_only=True (no unpickling of arbitrary objects)."""
+    try:
+        return torch.load(path, map_location=device, weights_only=True)
+    except Exception as e:
+        raise RuntimeError(f"{path}: cannot be loaded with weights_only=True ({e}); re-save it as a plain "
+                           "{'model_state_dict': ..., 'config': {...}} dict of tensors and primitives") from e
+
+
+def load_vocab(path: str) -> dict:
+    with open(path, "r", encoding="utf-8") as f:
+        return json.load(f)
+
+
+def default_vocab_path() -> str:
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return os.path.join(here, "data", "vocab.json")

@@ -1,0 +1,166 @@
+"""HIP path vs the reference-generated goldens and the CPU oracle, through the C-ABI and through
+the drop-in nn.Module surface.  Tolerances: bf16x2 (default) mode - token ids identical, logits
+within 1e-3 (SURVEY/BASELINE north star); bf16 mode - ids identical wherever the reference
+top-2 margin exceeds 0.2, logits within 0.1."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from image_caption_amd import weights as W
+from oracle import captioner as O
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gold(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+@pytest.fixture(scope="module")
+def vit_sd():
+    return W.to_torch(W.vit_state_dict(0))
+
+
+@pytest.fixture(scope="module")
+def vit_engine(vit_sd, cuda):
+    from image_caption_amd.engine import Engine
+
+    return Engine(vit_sd, "vit", {}, device=cuda)
+
+
+def _first_diverge(a, b):
+    d = np.nonzero((a != b).any(0))[0]
+    return int(d[0]) if len(d) else a.shape[1]
+
+
+def test_vit_golden_ids_and_logits(vit_engine, cuda):
+    g = gold("vit_b4.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    mem = vit_engine.encode(imgs)
+    assert np.abs(mem[:, :4, :16].cpu().numpy() - g["memory_head"]).max() < 1e-3
+    ids = vit_engine.greedy(mem, W.START_TOKEN, W.END_TOKEN, 30).cpu().numpy()
+    assert ids.dtype == np.int64 and np.array_equal(ids, g["ids"])
+    tf = vit_engine.decoder_forward(torch.from_numpy(g["ids"][:, :-1]).to(cuda), mem, causal=True)
+    assert np.abs(tf.cpu().numpy() - g["logits_tf"]).max() < 1e-3
+
+
+def test_decoder_forward_golden(vit_engine, cuda):
+    from tests.golden.make_golden import decoder_ops_memory
+
+    g = gold("decoder_ops.npz")
+    tgt = torch.from_numpy(g["tgt"]).to(cuda)
+    mem = torch.from_numpy(decoder_ops_memory()).to(cuda)
+    for causal, key in ((True, "logits_causal"), (False, "logits_nomask")):
+        out = vit_engine.decoder_forward(tgt, mem, causal=causal).cpu().numpy()
+        assert np.abs(out - g[key]).max() < 1e-3, key
+
+
+def test_sampled_decode_golden(vit_engine, cuda):
+    from utils.scst_loss import sample_stop_length
+
+    g = gold("sample_b4.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    mem = vit_engine.encode(imgs)
+    ids, lp = vit_engine.sample(mem, torch.from_numpy(g["uniforms"]).to(cuda), W.START_TOKEN, W.END_TOKEN, 30)
+    L = sample_stop_length(ids.long(), W.END_TOKEN)
+    assert np.array_equal(ids[:, :L].cpu().numpy(), g["ids"])
+    assert np.abs(lp[:, : L - 1].cpu().numpy() - g["log_probs"]).max() < 1e-3
+
+
+def test_dropin_model_generate_runs_hip(cuda, vit_sd):
+    from image_caption_amd import _lib
+    from models.vit_transformer_model import build_model
+
+    g = gold("vit_b4.npz")
+    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False})
+    m.load_state_dict(vit_sd)
+    m = m.to(cuda)
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    ids = m.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=30)
+    assert _lib._LIB is not None and m._hip_cache is not None  # the HIP engine served the call
+    assert ids.is_cuda and ids.dtype == torch.long
+    assert np.array_equal(ids.cpu().numpy(), g["ids"])
+    # scripts/inference.py loop: unmasked full-prefix decoder on HIP
+    from scripts.inference import generate_caption  # noqa: F401  (import check)
+
+    nm = gold("nomask_b1.npz")["ids"].tolist()
+    with torch.no_grad():
+        feats = m.encoder(imgs[:1])
+        inputs = torch.tensor([[W.START_TOKEN]], device=cuda)
+        got = []
+        for _ in range(20):
+            pid = int(m.decoder(inputs, feats)[:, -1, :].max(1)[1].item())
+            if pid == W.END_TOKEN:
+                break
+            got.append(pid)
+            inputs = torch.cat([inputs, torch.tensor([[pid]], device=cuda)], dim=1)
+    assert got == nm
+
+
+def test_grid_golden(cuda):
+    from models.grid_transformer_model import build_model
+
+    g = gold("grid_b4.npz")
+    m = build_model(W.VOCAB_SIZE, {"pretrained_cnn": False})
+    m.load_state_dict(W.to_torch(W.grid_state_dict(0)))
+    m = m.to(cuda).eval()
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    with torch.no_grad():
+        mem = m.encoder(imgs)
+    assert np.allclose(mem.double().sum(dim=(1, 2)).cpu().numpy(), g["memory_sum"], rtol=1e-4, atol=0.5)
+    ids = m.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=30)
+    assert np.array_equal(ids.cpu().numpy(), g["ids"])
+
+
+def test_batch_independence_and_determinism_at_b256(vit_engine, cuda, vit_sd):
+    """Full bench size: images are independent (a 256-batch reproduces 8 images decoded alone),
+    the decode is bitwise deterministic, and 8 sampled rows match the CPU oracle."""
+    imgs = torch.from_numpy(W.synthetic_images(256, seed=1)).to(cuda)
+    mem = vit_engine.encode(imgs)
+    a, _ = vit_engine.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, 30)
+    b, _ = vit_engine.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, 30)
+    assert torch.equal(a, b)
+    pick = torch.tensor([0, 37, 64, 101, 128, 177, 200, 255])
+    alone, _ = vit_engine.greedy_raw(vit_engine.encode(imgs[pick.to(cuda)]), W.START_TOKEN, W.END_TOKEN, 30)
+    assert torch.equal(alone, a[pick.to(cuda)])
+    ref_mem = O.vit_encode(vit_sd, imgs[pick.to(cuda)].cpu())
+    assert (mem[pick.to(cuda)].cpu() - ref_mem).abs().max().item() < 1e-3
+    ref = O.greedy_from_memory(vit_sd, ref_mem, W.START_TOKEN, W.END_TOKEN, 30)
+    assert np.array_equal(a[pick.to(cuda)].long().cpu().numpy()[:, : ref.shape[1]], ref.numpy())
+
+
+def test_bf16_mode_margin_gated(cuda, vit_sd):
+    from image_caption_amd.engine import Engine
+
+    g = gold("vit_b4.npz")
+    eng = Engine(vit_sd, "vit", {}, precision="bf16", device=cuda)
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    mem = eng.encode(imgs)
+    tf = eng.decoder_forward(torch.from_numpy(g["ids"][:, :-1]).to(cuda), mem, causal=True).cpu().numpy()
+    assert np.abs(tf - g["logits_tf"]).max() < 0.1
+    ids = eng.greedy(mem, W.START_TOKEN, W.END_TOKEN, 30).cpu().numpy()
+    # identical up to the first step whose reference margin is within the bf16 error band
+    for r in range(4):
+        close = np.nonzero(g["margins"][r] < 0.2)[0]
+        upto = (int(close[0]) if len(close) else 29) + 1
+        assert np.array_equal(ids[r, :upto], g["ids"][r, :upto])
+
+
+def test_scst_step_on_gpu(cuda, vit_sd):
+    from models.vit_transformer_model import build_model
+    from utils.scst_loss import SCSTLoss
+
+    vocab = {f"w{i}": i for i in range(W.VOCAB_SIZE)}
+    vocab.update({"<pad>": 0, "<unk>": 106, "<start>": 107, "<end>": 108})
+    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False})
+    m.load_state_dict(vit_sd)
+    m = m.to(cuda)
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    u = torch.from_numpy(gold("sample_b4.npz")["uniforms"]).to(cuda)
+    refs = [["w1 w2 w3"], ["w4 w5"], ["w6"], ["w7 w8 w9 w10"]]
+    with torch.no_grad():
+        loss, info = SCSTLoss()(m, imgs, refs, vocab, cuda, max_len=30, uniforms=u)
+    assert torch.isfinite(loss) and set(info) == {"sample_reward", "greedy_reward", "advantage"}

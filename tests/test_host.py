@@ -1,0 +1,174 @@
+"""Host-side logic on CPU: drop-in modules (PyTorch path) vs the oracle, the C-ABI library's
+exports, stop rules, CIDEr-D, preprocessing, and the data-parallel gather over gloo (world 2)."""
+import os
+import re
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from image_caption_amd import weights as W
+from image_caption_amd.engine import apply_stop_rule
+from oracle import captioner as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+
+def test_header_symbols_exported():
+    from image_caption_amd import _lib
+
+    decl = re.findall(r"\b(icap_\w+)\s*\(", open(os.path.join(ROOT, "include", "icap.h")).read())
+    assert len(set(decl)) >= 14
+    lib = _lib.load()
+    for name in set(decl):
+        assert hasattr(lib, name), name
+    assert set(decl) == set(_lib.SIGNATURES), set(decl) ^ set(_lib.SIGNATURES)
+    assert lib.icap_abi_version() == _lib.ABI_VERSION
+
+
+def test_library_refuses_without_gpu_inputs():
+    from image_caption_amd import _lib
+
+    lib = _lib.load()
+    assert lib.icap_encode_vit(None, None, 1, None, None) != 0
+    assert b"bad arguments" in lib.icap_last_error()
+
+
+def test_dropin_vit_model_state_dict_and_greedy():
+    from models.vit_transformer_model import build_model
+
+    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False})
+    sd = W.to_torch(W.vit_state_dict(0))
+    m.load_state_dict(sd, strict=True)
+    assert set(m.state_dict()) == set(sd)
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=9))
+    ids = m.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=10)
+    assert not m.training
+    assert torch.equal(ids, O.greedy_search(sd, imgs, W.START_TOKEN, W.END_TOKEN, 10))
+    with pytest.raises(ValueError):
+        m.generate(imgs, W.START_TOKEN, W.END_TOKEN, method="nope")
+
+
+def test_dropin_grid_model_state_dict():
+    from models.grid_transformer_model import build_model
+
+    m = build_model(W.VOCAB_SIZE, {"pretrained_cnn": False})
+    sd = W.to_torch(W.grid_state_dict(0))
+    m.load_state_dict(sd, strict=True)
+    assert set(m.state_dict()) == set(sd)
+
+
+def test_forced_hip_backend_refuses_cpu():
+    from models.vit_transformer_model import build_model
+
+    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False, "backend": "hip"})
+    with pytest.raises(RuntimeError):
+        m.generate(torch.zeros(1, 3, 224, 224), W.START_TOKEN, W.END_TOKEN, max_len=3)
+
+
+def test_stop_rules():
+    E = W.END_TOKEN
+    ids = torch.tensor([[107, 5, E, E, 7], [107, E, 3, E, 9]])
+    assert apply_stop_rule(ids, E).shape[1] == 4  # first column where every row is <end>: col 3
+    assert apply_stop_rule(torch.tensor([[107, 1, 2]]), E).shape[1] == 3
+    from utils.scst_loss import masked_token_logp, sample_stop_length
+
+    assert sample_stop_length(ids, E) == 3  # every row has emitted <end> by column 2
+    logits = torch.zeros(2, 4, W.VOCAB_SIZE)
+    lp = masked_token_logp(logits, ids, E)
+    assert lp[0, :2].ne(0).all() and lp[0, 2:].eq(0).all() and lp[1, 0].ne(0) and lp[1, 1:].eq(0).all()
+
+
+def test_cider_ids_match_string_restatement():
+    from image_caption_amd.cider import cider_d
+    from oracle.cider_ref import compute_score
+
+    rng = np.random.Generator(np.random.PCG64(5))
+    hyps, refs = [], []
+    for i in range(40):
+        hyps.append(list(rng.integers(1, 12, size=rng.integers(0, 9))))
+        refs.append([list(rng.integers(1, 12, size=rng.integers(1, 10))) for _ in range(rng.integers(1, 3))])
+    s = lambda t: " ".join(f"w{x}" for x in t)
+    m1, per1 = cider_d(hyps, refs)
+    m2, per2 = compute_score({i: [s(r) for r in rs] for i, rs in enumerate(refs)}, {i: [s(h)] for i, h in enumerate(hyps)})
+    assert np.allclose(per1, per2, rtol=1e-12, atol=1e-12) and abs(m1 - m2) < 1e-12
+    # identical caption and reference scores > 0; disjoint scores 0
+    assert cider_d([[1, 2, 3], [4]], [[[1, 2, 3]], [[5]]])[1][1] == 0.0
+
+
+def test_preprocess_matches_manual():
+    from PIL import Image
+
+    from scripts._io import MEAN, STD, center_crop, resize_shorter, to_normalized_tensor
+
+    a = (np.arange(300 * 400 * 3) % 251).astype(np.uint8).reshape(300, 400, 3)
+    img = Image.fromarray(a)
+    r = resize_shorter(img, 256)
+    assert r.size == (341, 256)
+    c = center_crop(r, 224)
+    assert c.size == (224, 224)
+    t = to_normalized_tensor(c)
+    ref = (np.asarray(c, dtype=np.float32) / 255.0 - MEAN) / STD
+    assert np.allclose(t.numpy(), ref.transpose(2, 0, 1))
+
+
+def test_shard_bounds():
+    from image_caption_amd.parallel import shard_bounds
+
+    for total in (0, 1, 7, 256, 2048, 1023):
+        for ws in (1, 2, 3, 8):
+            spans = [shard_bounds(total, ws, r) for r in range(ws)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(ws - 1))
+            assert max(e - s for s, e in spans) - min(e - s for s, e in spans) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, ws, port, total, q):
+    import torch.distributed as dist
+
+    from image_caption_amd import parallel
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    parallel.init("gloo")
+    sd = W.to_torch(W.vit_state_dict(0))
+    mem_all = torch.from_numpy(np.random.Generator(np.random.PCG64(3)).standard_normal((total, 20, 512)).astype(np.float32))
+    s, e = parallel.shard_bounds(total, ws, rank)
+    ids = O.greedy_from_memory(sd, mem_all[s:e], W.START_TOKEN, W.END_TOKEN, 6)
+    full = torch.full((e - s, 6), W.END_TOKEN, dtype=torch.int32)
+    full[:, : ids.shape[1]] = ids.int()
+    g = parallel.gather_rows(full, total)
+    if rank == 0:
+        q.put(apply_stop_rule(g.long(), W.END_TOKEN).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_gather_matches_single_process():
+    total, ws = 5, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, ws, port, total, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sd = W.to_torch(W.vit_state_dict(0))
+    mem_all = torch.from_numpy(np.random.Generator(np.random.PCG64(3)).standard_normal((total, 20, 512)).astype(np.float32))
+    ref = O.greedy_from_memory(sd, mem_all, W.START_TOKEN, W.END_TOKEN, 6)
+    assert np.array_equal(got, ref.numpy())

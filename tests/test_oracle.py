@@ -1,0 +1,163 @@
+"""Pin the CPU oracle (oracle/captioner.py) against the reference-generated golden fixtures and
+against independent implementations of the third-party trunks (HF transformers ViT / ResNet)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from image_caption_amd import weights as W
+from oracle import captioner as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+
+def gold(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+@pytest.fixture(scope="module")
+def vit_sd():
+    return W.to_torch(W.vit_state_dict(0))
+
+
+@pytest.fixture(scope="module")
+def grid_sd():
+    return W.to_torch(W.grid_state_dict(0))
+
+
+def test_vit_greedy_matches_reference(vit_sd):
+    g = gold("vit_b4.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=int(g["image_seed"])))
+    mem = O.vit_encode(vit_sd, imgs)
+    assert np.allclose(mem[:, :4, :16].numpy(), g["memory_head"], atol=2e-5)
+    assert np.allclose(mem.double().sum(dim=(1, 2)).numpy(), g["memory_sum"], rtol=1e-5, atol=1e-2)
+    ids = O.greedy_from_memory(vit_sd, mem, W.START_TOKEN, W.END_TOKEN, int(g["max_len"]))
+    assert np.array_equal(ids.numpy(), g["ids"])
+    tf = O.teacher_forced_logits(vit_sd, mem, ids)
+    assert np.abs(tf.numpy() - g["logits_tf"]).max() < 1e-4
+
+
+def test_grid_greedy_matches_reference(grid_sd):
+    g = gold("grid_b4.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=int(g["image_seed"])))
+    mem = O.grid_encode(grid_sd, imgs)
+    assert np.allclose(mem.double().sum(dim=(1, 2)).numpy(), g["memory_sum"], rtol=1e-5, atol=1e-2)
+    ids = O.greedy_from_memory(grid_sd, mem, W.START_TOKEN, W.END_TOKEN, int(g["max_len"]))
+    assert np.array_equal(ids.numpy(), g["ids"])
+    assert np.abs(O.teacher_forced_logits(grid_sd, mem, ids).numpy() - g["logits_tf"]).max() < 1e-4
+
+
+def test_decoder_forward_causal_and_unmasked(vit_sd):
+    from tests.golden.make_golden import decoder_ops_memory
+
+    g = gold("decoder_ops.npz")
+    tgt = torch.from_numpy(g["tgt"])
+    mem = torch.from_numpy(decoder_ops_memory())
+    assert np.abs(O.decoder_forward(vit_sd, tgt, mem, causal=True).numpy() - g["logits_causal"]).max() < 1e-4
+    assert np.abs(O.decoder_forward(vit_sd, tgt, mem, causal=False).numpy() - g["logits_nomask"]).max() < 1e-4
+
+
+def test_inference_py_loop(vit_sd):
+    g = gold("nomask_b1.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0))
+    mem = O.vit_encode(vit_sd, imgs)[:1]
+    assert O.inference_py_generate(vit_sd, mem, W.START_TOKEN, W.END_TOKEN, 20) == g["ids"].tolist()
+
+
+def test_sampled_decode_with_fixed_uniforms(vit_sd):
+    g = gold("sample_b4.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0))
+    mem = O.vit_encode(vit_sd, imgs)
+    ids, lp = O.sample_with_log_probs(vit_sd, mem, torch.from_numpy(g["uniforms"]), W.START_TOKEN, W.END_TOKEN, 30)
+    assert np.array_equal(ids.numpy(), g["ids"])
+    assert np.abs(lp.numpy() - g["log_probs"]).max() < 1e-4
+
+
+def test_vit_trunk_vs_hf_transformers(vit_sd):
+    """torchvision ViT-B/16 restatement vs HF ViTModel (independent implementation)."""
+    tr = pytest.importorskip("transformers")
+    cfg = tr.ViTConfig(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072,
+                       hidden_act="gelu", layer_norm_eps=1e-6, image_size=224, patch_size=16, qkv_bias=True,
+                       hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    hf = tr.ViTModel(cfg, add_pooling_layer=False).eval()
+    keys = set(hf.state_dict())
+    P = "encoder.vit."
+    m = {"embeddings.cls_token": vit_sd[P + "class_token"],
+         "embeddings.position_embeddings": vit_sd[P + "encoder.pos_embedding"],
+         "embeddings.patch_embeddings.projection.weight": vit_sd[P + "conv_proj.weight"],
+         "embeddings.patch_embeddings.projection.bias": vit_sd[P + "conv_proj.bias"],
+         "layernorm.weight": vit_sd[P + "encoder.ln.weight"], "layernorm.bias": vit_sd[P + "encoder.ln.bias"]}
+    new_names = "layers.0.attention.q_proj.weight" in keys
+    for i in range(12):
+        L = P + f"encoder.layers.encoder_layer_{i}."
+        w, b = vit_sd[L + "self_attention.in_proj_weight"], vit_sd[L + "self_attention.in_proj_bias"]
+        if new_names:
+            H = f"layers.{i}."
+            names = {"q": "attention.q_proj", "k": "attention.k_proj", "v": "attention.v_proj",
+                     "o": "attention.o_proj", "fc1": "mlp.fc1", "fc2": "mlp.fc2"}
+        else:
+            H = f"encoder.layer.{i}."
+            names = {"q": "attention.attention.query", "k": "attention.attention.key",
+                     "v": "attention.attention.value", "o": "attention.output.dense",
+                     "fc1": "intermediate.dense", "fc2": "output.dense"}
+        for j, n in enumerate("qkv"):
+            m[H + names[n] + ".weight"] = w[j * 768:(j + 1) * 768]
+            m[H + names[n] + ".bias"] = b[j * 768:(j + 1) * 768]
+        m[H + names["o"] + ".weight"] = vit_sd[L + "self_attention.out_proj.weight"]
+        m[H + names["o"] + ".bias"] = vit_sd[L + "self_attention.out_proj.bias"]
+        m[H + names["fc1"] + ".weight"] = vit_sd[L + "mlp.0.weight"]
+        m[H + names["fc1"] + ".bias"] = vit_sd[L + "mlp.0.bias"]
+        m[H + names["fc2"] + ".weight"] = vit_sd[L + "mlp.3.weight"]
+        m[H + names["fc2"] + ".bias"] = vit_sd[L + "mlp.3.bias"]
+        for a, bn in (("ln_1", "layernorm_before"), ("ln_2", "layernorm_after")):
+            m[H + bn + ".weight"] = vit_sd[L + a + ".weight"]
+            m[H + bn + ".bias"] = vit_sd[L + a + ".bias"]
+    hf.load_state_dict(m, strict=True)
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=4))
+    with torch.no_grad():
+        h = hf(pixel_values=imgs).last_hidden_state[:, 1:]
+        ref = O.linear(h, vit_sd["encoder.projection.weight"], vit_sd["encoder.projection.bias"])
+    assert (O.vit_encode(vit_sd, imgs) - ref).abs().max().item() < 2e-4
+
+
+def test_resnet_trunk_vs_hf_transformers(grid_sd):
+    tr = pytest.importorskip("transformers")
+    cfg = tr.ResNetConfig(depths=[3, 4, 23, 3], hidden_sizes=[256, 512, 1024, 2048], layer_type="bottleneck",
+                          embedding_size=64, downsample_in_first_stage=False)
+    hf = tr.ResNetModel(cfg).eval()
+    P = "encoder.cnn."
+    m = {}
+
+    def conv_bn(dst, conv, bn):
+        m[dst + "convolution.weight"] = grid_sd[conv + ".weight"]
+        for k in ("weight", "bias", "running_mean", "running_var", "num_batches_tracked"):
+            m[dst + "normalization." + k] = grid_sd[bn + "." + k]
+
+    conv_bn("embedder.embedder.", P + "0", P + "1")
+    for s, n in enumerate((3, 4, 23, 3)):
+        for b in range(n):
+            src, dst = P + f"{4 + s}.{b}.", f"encoder.stages.{s}.layers.{b}."
+            if b == 0:
+                conv_bn(dst + "shortcut.", src + "downsample.0", src + "downsample.1")
+            for j in range(3):
+                conv_bn(dst + f"layer.{j}.", src + f"conv{j + 1}", src + f"bn{j + 1}")
+    missing, unexpected = hf.load_state_dict(m, strict=False)
+    assert not unexpected and all("num_batches" in k for k in missing)
+    imgs = torch.from_numpy(W.synthetic_images(1, seed=4))
+    with torch.no_grad():
+        ref = hf(pixel_values=imgs).last_hidden_state
+        got = O.resnet101_trunk(grid_sd, imgs)
+    assert (got - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item())
+
+
+def test_generator_is_deterministic_and_bf16_exact():
+    a = W.vit_state_dict(3)
+    b = W.vit_state_dict(3)
+    for k in a:
+        assert np.array_equal(a[k], b[k])
+    w = torch.from_numpy(a["decoder.fc_out.weight"])
+    assert torch.equal(w, w.to(torch.bfloat16).float())
+    x = np.random.Generator(np.random.PCG64(0)).standard_normal(10000).astype(np.float32)
+    assert np.array_equal(W.round_to_bf16(x), torch.from_numpy(x).to(torch.bfloat16).float().numpy())

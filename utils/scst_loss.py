@@ -1,0 +1,154 @@
+"""Drop-in `utils/scst_loss.py` (reference: utils/scst_loss.py): self-critical sequence training.
+
+SCSTLoss.forward = sample captions with their log-probs, greedy baseline via model.generate,
+CIDEr-D rewards, advantage = r(sample) - r(greedy), loss = -mean(advantage * sum(log p)).
+
+Changes on the hot path:
+  * sampling runs as one batched HIP decode (icap_decode_sample): fp32 fc_out + softmax and an
+    inverse-CDF draw on uniforms that are INJECTED (default torch.rand on the images' device),
+    replacing torch.multinomial, so CPU and GPU consume identical randomness; the sampler runs
+    without dropout (the reference samples in train mode with dropout 0.1 active, :161);
+  * when autograd is on, the sampled sequence's log-probs are recomputed teacher-forced through
+    the PyTorch decoder (train mode) so the REINFORCE loss has a gradient;
+  * CIDEr-D is image_caption_amd.cider on token ids (pycocoevalcap is absent; parity unpinned).
+BLEU / combined rewards and MixedLoss are training-only and not provided.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from image_caption_amd import cider as _cider
+
+
+def _split(s: str, word2idx: Optional[dict]) -> List:
+    words = s.split()
+    return [word2idx.get(w, w) for w in words] if word2idx else words
+
+
+class CiderRewardCalculator:
+    """compute_reward(predictions: list[str], references: list[list[str]]) -> list[float]
+    (scst_loss:20-54).  Strings are split on whitespace; with `vocab` given, words map to ids."""
+
+    def __init__(self, vocab: Optional[dict] = None):
+        self.word2idx = vocab
+
+    def compute_reward(self, predictions, references):
+        hyps = [_split(p, self.word2idx) for p in predictions]
+        refs = [[_split(r, self.word2idx) for r in (rs if isinstance(rs, list) else [rs])] for rs in references]
+        try:
+            return list(_cider.cider_d(hyps, refs)[1])
+        except Exception as e:  # the reference returns zero rewards on scorer failure (:52-54)
+            print(f"CIDEr failed: {e}")
+            return [0.0] * len(predictions)
+
+    def compute_reward_ids(self, hyp_ids: Sequence[Sequence[int]], ref_ids: Sequence[Sequence[Sequence[int]]]):
+        return list(_cider.cider_d(hyp_ids, ref_ids)[1])
+
+
+def sample_stop_length(ids: torch.Tensor, end_token: int) -> int:
+    """Columns the reference keeps: it breaks right after the step at which every sequence has
+    emitted <end> at least once (scst_loss:246-249)."""
+    fin = (ids[:, 1:] == end_token).cummax(dim=1).values.all(dim=0)
+    if bool(fin.any()):
+        return int(torch.nonzero(fin)[0, 0]) + 2
+    return ids.shape[1]
+
+
+def masked_token_logp(logits: torch.Tensor, ids: torch.Tensor, end_token: int) -> torch.Tensor:
+    """log p(ids[:, t+1] | prefix) with steps after a sequence's first <end> zeroed (:236-239)."""
+    lp = F.log_softmax(logits, dim=-1).gather(2, ids[:, 1:].unsqueeze(2)).squeeze(2)
+    ended = (ids[:, 1:] == end_token).long().cumsum(dim=1)
+    finished_before = torch.cat([torch.zeros_like(ended[:, :1]), ended[:, :-1]], dim=1) > 0
+    return lp.masked_fill(finished_before, 0.0)
+
+
+class SCSTLoss(nn.Module):
+    def __init__(self, reward_type="cider", cider_weight=1.0, bleu_weight=0.0):
+        super().__init__()
+        if reward_type != "cider":
+            raise NotImplementedError("only the CIDEr reward is on the hot path")
+        self.reward_calculator = CiderRewardCalculator()
+
+    def forward(self, model, images, references, vocab, device, sample_method="sample", max_len=50,
+                uniforms: Optional[torch.Tensor] = None):
+        start, end, pad = vocab["<start>"], vocab["<end>"], vocab["<pad>"]
+        self.reward_calculator.word2idx = vocab
+        model.train()
+        sample_ids, sample_log_probs = self._sample_with_log_probs(model, images, start, end, max_len, device,
+                                                                   uniforms)
+        with torch.no_grad():
+            greedy_ids = model.generate(images, start, end, max_len, method="greedy")
+        refs = [[_split(r, vocab) for r in (rs if isinstance(rs, list) else [rs])] for rs in references]
+        s_r = self.reward_calculator.compute_reward_ids(
+            [_cider.caption_ids(r, start, end, pad) for r in sample_ids.tolist()], refs)
+        g_r = self.reward_calculator.compute_reward_ids(
+            [_cider.caption_ids(r, start, end, pad) for r in greedy_ids.tolist()], refs)
+        s_r = torch.tensor(s_r, device=device, dtype=torch.float)
+        g_r = torch.tensor(g_r, device=device, dtype=torch.float)
+        adv = s_r - g_r
+        loss = -(adv * sample_log_probs.sum(dim=1)).mean()
+        return loss, {"sample_reward": s_r.mean().item(), "greedy_reward": g_r.mean().item(),
+                      "advantage": adv.mean().item()}
+
+    def _sample_with_log_probs(self, model, images, start_token, end_token, max_len, device,
+                               uniforms: Optional[torch.Tensor] = None):
+        """-> (ids (B, L) int64, log_probs (B, L-1)), L per the reference stop rule."""
+        B = images.size(0)
+        if uniforms is None:
+            uniforms = torch.rand(max_len - 1, B, device=images.device)
+        if images.is_cuda and getattr(model, "hip_backend", "torch") != "torch":
+            eng = model.hip_engine(images.device)
+            with torch.no_grad():
+                enc_in = model.encoder.cnn(images.float()) if getattr(model, "_hip_kind", "") == "grid" else images
+                mem = eng.encode(enc_in)
+                ids32, logp = eng.sample(mem, uniforms, start_token, end_token, max_len)
+            ids = ids32.long()
+            L = sample_stop_length(ids, end_token)
+            ids, logp = ids[:, :L], logp[:, : L - 1]
+            if torch.is_grad_enabled():
+                memory = model.encoder(images)
+                mask = model.decoder.generate_square_subsequent_mask(L - 1, images.device)
+                logits = model.decoder(ids[:, :-1], memory, tgt_mask=mask)
+                logp = masked_token_logp(logits, ids, end_token)
+            return ids, logp
+        return self._sample_torch(model, images, start_token, end_token, max_len, uniforms)
+
+    @staticmethod
+    def _sample_torch(model, images, start_token, end_token, max_len, uniforms):
+        """PyTorch loop of the reference (:210-254) with the same inverse-CDF draw."""
+        B = images.size(0)
+        memory = model.encoder(images)
+        generated = torch.full((B, 1), start_token, dtype=torch.long, device=images.device)
+        finished = torch.zeros(B, dtype=torch.bool, device=images.device)
+        out = []
+        for step in range(max_len - 1):
+            mask = model.decoder.generate_square_subsequent_mask(generated.size(1), images.device)
+            logits = model.decoder(generated, memory, tgt_mask=mask)[:, -1, :]
+            probs = F.softmax(logits, dim=-1)
+            cdf = probs.cumsum(-1)
+            nxt = (cdf <= uniforms[step].unsqueeze(-1) * cdf[:, -1:]).sum(-1).clamp_max(logits.shape[-1] - 1)
+            lp = F.log_softmax(logits, dim=-1).gather(1, nxt.unsqueeze(1)).squeeze(1)
+            out.append(lp.masked_fill(finished, 0.0))
+            generated = torch.cat([generated, nxt.unsqueeze(1)], dim=1)
+            finished = finished | (nxt == end_token)
+            if bool(finished.all()):
+                break
+        return generated, torch.stack(out, dim=1)
+
+    def _decode_captions(self, caption_ids, idx2word, end_token, pad_token, start_token):
+        from models._common import decode_ids
+
+        return decode_ids(caption_ids.cpu(), idx2word, end_token, pad_token, start_token)
+
+
+def get_reference_captions(caption_ids, vocab):
+    """Reference id rows -> [[caption string]] per image (scst_loss:328-354)."""
+    from models._common import decode_ids
+
+    idx2word = {i: w for w, i in vocab.items()}
+    caps = decode_ids(caption_ids, idx2word, vocab["<end>"], vocab["<pad>"], vocab["<start>"])
+    return [[c] for c in caps]
