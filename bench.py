@@ -112,8 +112,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    prof = [eng.profile_read(c) for c in (_lib.PROF_GEMM_128, _lib.PROF_GEMM_64, _lib.PROF_ENC_ATTN,
-                                          _lib.PROF_CROSS_ATTN)]
+    prof = [eng.profile_read(c) for c in sorted(_lib.PROF_NAMES)]
     eng.profile(False)
     value = total * args.steps / el
     if rank == 0:

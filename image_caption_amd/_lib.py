@@ -18,9 +18,10 @@ ABI_VERSION = 1
 KIND_VIT, KIND_GRID = 0, 1
 PREC_BF16, PREC_BF16X2 = 1, 2
 PRECISIONS = {"bf16": PREC_BF16, "bf16x2": PREC_BF16X2}
-PROF_GEMM_128, PROF_GEMM_64, PROF_ENC_ATTN, PROF_CROSS_ATTN = 0, 1, 2, 3
+PROF_GEMM_128, PROF_GEMM_64, PROF_ENC_ATTN, PROF_CROSS_ATTN, PROF_GEMM_WAVE, PROF_GEMM_256 = 0, 1, 2, 3, 4, 5
 PROF_NAMES = {PROF_GEMM_128: "gemm_bf16_kernel<128,128,64,64>", PROF_GEMM_64: "gemm_bf16_kernel<64,64,32,32>",
-              PROF_ENC_ATTN: "enc_attention_kernel", PROF_CROSS_ATTN: "cross_attn_absorbed_kernel"}
+              PROF_ENC_ATTN: "enc_attention_kernel", PROF_CROSS_ATTN: "cross_attn_absorbed_kernel",
+              PROF_GEMM_WAVE: "gemm_dec_kernel", PROF_GEMM_256: "gemm_256_kernel"}
 
 
 class LnW(ctypes.Structure):
@@ -79,6 +80,7 @@ SIGNATURES = {
                                    c_void_p, c_void_p]),
     "icap_decoder_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                      c_void_p]),
+    "icap_set_graphs": (c_int, [c_void_p, c_int]),
     "icap_profile_enable": (c_int, [c_void_p, c_int]),
     "icap_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(c_long),
                                   POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),

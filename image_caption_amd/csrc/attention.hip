@@ -379,3 +379,202 @@ hipError_t launch_cross_attn_absorbed(const float* qt, const float* mem, int row
                      scale, out, lo, nsplit);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Cross-attention, key-absorbed form on MFMA (flash-style over 32-key chunks).
+// One 4-wave block per query row; wave w owns d in [128w, 128w + 128) of the 512-wide memory.
+//   scores  S^T[s][h] = sum_d mem[s][d] * qt[h][d]         (A = memory rows, B = q~^T, 8 heads in 16)
+//           partial over each wave's d range, summed through LDS, x 1/8, online softmax per head
+//           (head = lane & 15, so the row statistics are lane-local + 2 xor-shuffles)
+//   context C^T[d][h] += sum_s mem^T[d][s] * P^T[s][h]      (A = mem^T via ds_read_b64_tr_b16,
+//           B = the score accumulators themselves, k order permuted consistently)
+// memory and q~ arrive as bf16 planes (hi, lo); every product uses hi.hi + lo.hi + hi.lo.
+// LDS: two 32-key chunks x planes x 32 KiB (global_load_lds, 16-byte chunk c of key row k stored
+// at chunk c ^ (k & 15): the 16 key rows of a ds_read_b128 group hit 16 different banks).
+namespace {
+
+template <int NS>
+__global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __restrict__ qt, long qt_lo,
+                                                              const bf16_t* __restrict__ mem, long mem_lo,
+                                                              int rows_per_image, int S, float scale,
+                                                              bf16_t* out, long out_lo) {
+  constexpr int DM = 512, H = 8, CK = 32;        // model width, heads, keys per chunk
+  constexpr int PLANE = CK * DM * 2;             // 32 KiB per plane per chunk
+  constexpr int BUF = NS * PLANE;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = (float*)(smem + 2 * BUF);         // [4 waves][2 tiles][4 regs][64 lanes]
+  const int r = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const bf16_t* mb = mem + (long)(r / rows_per_image) * S * DM;
+  const int nchunks = (S + CK - 1) / CK;
+
+  // q~ fragments (B operand of the scores): head fr (zero for fr >= 8), d = 128w + 32ks + 8fq + j
+  bf16x8 qh[4], ql[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const long off = (long)r * H * DM + fr * DM + wave * 128 + ks * 32 + fq * 8;
+    if (fr < H) {
+      qh[ks] = *(const bf16x8*)(qt + off);
+      if (NS == 2) ql[ks] = *(const bf16x8*)(qt + qt_lo + off);
+    } else {
+      qh[ks] = (bf16x8){};
+      ql[ks] = (bf16x8){};
+    }
+  }
+
+  // chunk staging: instruction i (of 16 per wave) covers key row (wave*4 + i/4)... per plane 32 rows
+  // x 1 KiB; lane writes 16 B at lane-linear position; source chunk pre-swizzled.
+  auto stage = [&](int c, int buf) {
+#pragma unroll
+    for (int pl = 0; pl < NS; ++pl) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int key = wave * 8 + i;                       // 8 rows per wave per plane
+        const int g = min(c * CK + key, S - 1);
+        const int cs = lane ^ (key & 15);                  // 64 chunks of 16 B per 1 KiB row
+        const bf16_t* src = mb + (pl ? mem_lo : 0) + (long)g * DM + cs * 8;
+        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
+                                         (LDS_AS void*)(smem + buf * BUF + pl * PLANE + key * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const int q4 = fr >> 2, p4 = fr & 3;
+
+  stage(0, 0);
+  for (int c = 0; c < nchunks; ++c) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (c + 1 < nchunks) stage(c + 1, (c + 1) & 1);
+    const char* cb = smem + (c & 1) * BUF;
+    // partial scores over this wave's d range
+    f32x4 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      const int key = kt * 16 + fr;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int ch = (wave * 128 + ks * 32 + fq * 8) >> 3;
+        const int off = key * 1024 + ((ch ^ (key & 15)) << 4);
+        const bf16x8 mh = *(const bf16x8*)(cb + off);
+        a = mfma16(mh, qh[ks], a);
+        if (NS == 2) {
+          const bf16x8 ml = *(const bf16x8*)(cb + PLANE + off);
+          a = mfma16(ml, qh[ks], a);
+          a = mfma16(mh, ql[ks], a);
+        }
+      }
+      s[kt] = a;
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[((wave * 2 + kt) * 4 + j) * 64 + lane] = s[kt][j];
+    __syncthreads();
+    // total scores (every wave), scale, mask, online softmax per head (= lane & 15)
+    float cmax = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v += red[((w * 2 + kt) * 4 + j) * 64 + lane];
+        const int key = c * CK + kt * 16 + fq * 4 + j;
+        v = key < S ? v * scale : -INFINITY;
+        s[kt][j] = v;
+        cmax = fmaxf(cmax, v);
+      }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    const float m_new = fmaxf(m_run, cmax);
+    const float alpha = __expf(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = __expf(s[kt][j] - m_new);
+        s[kt][j] = e;
+        psum += e;
+      }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    // P^T as the B operand (k = key, permuted): element j < 4 -> key 4fq + j, j >= 4 -> 16 + 4fq + j - 4
+    bf16x8 ph, pl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ph[j] = (__bf16)s[0][j];
+      ph[4 + j] = (__bf16)s[1][j];
+      if (NS == 2) {
+        pl[j] = (__bf16)(s[0][j] - (float)ph[j]);
+        pl[4 + j] = (__bf16)(s[1][j] - (float)ph[4 + j]);
+      }
+    }
+    // context: C^T[d][h] for this wave's 8 d-tiles; A = mem^T via transposed LDS reads
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      acc[dt] *= alpha;
+      const int d = wave * 128 + dt * 16 + 4 * p4;       // this lane's 4 d values in the tr block
+      const int k0 = 4 * fq + q4, k1 = k0 + 16;
+      const int o0 = k0 * 1024 + ((((d >> 3) ^ (k0 & 15))) << 4) + (d & 7) * 2;
+      const int o1 = k1 * 1024 + ((((d >> 3) ^ (k1 & 15))) << 4) + (d & 7) * 2;
+      const bf16x8 vh = tr_pair(cb + o0, cb + o1);
+      acc[dt] = mfma16(vh, ph, acc[dt]);
+      if (NS == 2) {
+        const bf16x8 vl = tr_pair(cb + PLANE + o0, cb + PLANE + o1);
+        acc[dt] = mfma16(vl, ph, acc[dt]);
+        acc[dt] = mfma16(vh, pl, acc[dt]);
+      }
+    }
+  }
+  // C^T layout: lane holds head fr, d = 16dt + 4fq + r (4 consecutive d) -> 8-byte plane stores
+  if (fr < H) {
+    const float inv = 1.f / l_run;
+    bf16_t* dst = out + (long)r * H * DM + fr * DM + wave * 128;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      bf16_t hv[4], lv[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) split_bf(acc[dt][rr] * inv, hv[rr], lv[rr]);
+      const int d = dt * 16 + 4 * fq;
+      *(u32x2*)(dst + d) = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+      if (NS == 2)
+        *(u32x2*)(dst + out_lo + d) =
+            (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* mem, long mem_lo, int rows,
+                                  int rows_per_image, int S, float scale, bf16_t* out, long out_lo, int nsplit,
+                                  hipStream_t s) {
+  if (S <= 0 || rows <= 0 || (nsplit != 1 && nsplit != 2)) return hipErrorInvalidValue;
+  const int lds = 2 * nsplit * 32 * 512 * 2 + 4 * 2 * 4 * 64 * 4;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)cross_attn_mfma_kernel<2>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * 32 * 512 * 2 + 8192);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)cross_attn_mfma_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * 32 * 512 * 2 + 8192);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  if (nsplit == 2)
+    hipLaunchKernelGGL(cross_attn_mfma_kernel<2>, dim3(rows), dim3(256), lds, s, qt, qt_lo, mem, mem_lo,
+                       rows_per_image, S, scale, out, out_lo);
+  else
+    hipLaunchKernelGGL(cross_attn_mfma_kernel<1>, dim3(rows), dim3(256), lds, s, qt, qt_lo, mem, mem_lo,
+                       rows_per_image, S, scale, out, out_lo);
+  return hipGetLastError();
+}

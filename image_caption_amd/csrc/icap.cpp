@@ -45,11 +45,14 @@ int guarded(F&& f) {
   return 1;
 }
 
+int g_ws_generation = 0;  // bumped on every workspace (re)allocation: invalidates captured graphs
+
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
   void ensure(size_t bytes) {
     if (bytes <= n) return;
+    ++g_ws_generation;
     if (p) HIPCHK(hipFree(p));
     p = nullptr;
     n = 0;
@@ -91,8 +94,28 @@ struct DecLayer {
 
 }  // namespace
 
+// Captured decode loop (hipGraph): all max_len-1 steps x ~80 kernels replayed with one launch.
+struct DecodeGraph {
+  int B = 0, S = 0, L = 0, mode = -1, start = -1, end = -1, gen = -1;
+  bool logits = false;
+  int calls = 0;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  DevBuf mem, ids, lg, uni, lp;
+  void reset() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    exec = nullptr;
+    graph = nullptr;
+    calls = 0;
+  }
+};
+
 struct icap_handle {
   icap_model_desc d{};
+  bool use_graphs = true;
+  hipStream_t cap_stream = nullptr;
+  DecodeGraph dg;
   int ns = 2;  // activation planes (1 = bf16, 2 = hi/lo)
   std::vector<void*> owned;
   // decoder
@@ -143,13 +166,16 @@ struct icap_handle {
 
   // workspaces
   DevBuf e_x, e_a, e_qkv, e_h, e_patch;  // encoder
-  DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin;  // decoder
+  DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin, d_part;  // decoder
 
   ~icap_handle() {
+    dg.reset();
+    for (DevBuf* b : {&dg.mem, &dg.ids, &dg.lg, &dg.uni, &dg.lp}) b->release();
+    if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_x, &d_a, &d_qkv, &d_q, &d_qt, &d_c, &d_o, &d_h,
-                      &d_kv, &d_fin})
+                      &d_kv, &d_fin, &d_part})
       b->release();
   }
 
@@ -192,6 +218,21 @@ struct icap_handle {
     g.M = M; g.N = W.N; g.K = W.K; g.nsplit = ns; g.c_planes = ns;
     g.epi = epi; g.out = out;
     run_gemm(g, s);
+  }
+  // decode-step GEMM (wave tiles, optional split-K into fp32 partial slabs)
+  void wgemm(const bf16_t* A, long lda, long a_lo, const bf16_t* W, long ldw, const float* bias, int M, int N, int K,
+             void* C, long ldc, long c_lo, int epi, int out, int tile, int ksplit, long part_stride, hipStream_t s,
+             int batch = 1, long a_batch = 0, long w_batch = 0, long bias_batch = 0, long c_batch = 0) {
+    WaveGemmArgs g = wave_args();
+    g.A = A; g.lda = lda; g.a_lo = a_lo; g.a_batch = a_batch;
+    g.W = W; g.ldw = ldw; g.w_batch = w_batch;
+    g.bias = bias; g.bias_batch = bias_batch;
+    g.C = C; g.ldc = ldc; g.c_lo = c_lo; g.c_batch = c_batch; g.c_planes = ns;
+    g.M = M; g.N = N; g.K = K; g.nsplit = ns; g.batch = batch; g.ksplit = ksplit; g.part_stride = part_stride;
+    g.epi = epi; g.out = out; g.tile = tile;
+    const double flops = 2.0 * M * N * K * batch;
+    const double bytes = 2.0 * batch * ((double)M * K * ns + (double)N * K);
+    timed(PROF_GEMM_WAVE, flops, bytes, s, [&] { HIPCHK(launch_gemm_dec(g, s)); });
   }
   void attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, bf16_t* out, long out_ld, long out_lo,
                  hipStream_t s) {
@@ -355,8 +396,10 @@ void encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, 
     enc_layer_postln(h, L, B, N, memory, a, h->e_qkv.as<bf16_t>(), h->e_h.as<bf16_t>(), s);
 }
 
+constexpr int MAX_KSPLIT = 8;
+
 struct DecodeBufs {
-  float *x, *qkv, *qt, *kc, *vc;
+  float *x, *qkv, *qt, *kc, *vc, *part;
   bf16_t *a, *q, *c, *o, *hb;
   long aL, qL, cL, hL;
 };
@@ -373,65 +416,67 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax) {
   h->d_o.ensure((size_t)rows * D * 2 * ns);
   h->d_h.ensure((size_t)rows * d.dim_ff * 2 * ns);
   h->d_kv.ensure((size_t)2 * d.n_dec_layers * B * H * Lmax * 64 * 4);
+  h->d_part.ensure((size_t)MAX_KSPLIT * rows * D * 4);
   DecodeBufs b;
   b.x = h->d_x.as<float>(); b.a = h->d_a.as<bf16_t>(); b.qkv = h->d_qkv.as<float>();
   b.q = h->d_q.as<bf16_t>(); b.qt = h->d_qt.as<float>(); b.c = h->d_c.as<bf16_t>();
   b.o = h->d_o.as<bf16_t>(); b.hb = h->d_h.as<bf16_t>();
   b.kc = h->d_kv.as<float>();
+  b.part = h->d_part.as<float>();
   b.vc = b.kc + (size_t)d.n_dec_layers * B * H * Lmax * 64;
   b.aL = (long)rows * D; b.qL = (long)rows * D; b.cL = (long)rows * H * D; b.hL = (long)rows * d.dim_ff;
   return b;
 }
 
 // One pass of all decoder layers over `rows` query rows (n_new per image, positions t0..t0+n_new).
+// Post-LN layer (torch TransformerDecoderLayer.forward, transformer.py:1144-1153):
+//   x = LN1(x + SA(x)); x = LN2(x + CA(x, mem)); x = LN3(x + W2 relu(W1 x)).
+// GEMMs are wave-tile decode GEMMs; the three N=512 residual GEMMs split K into fp32 partial
+// slabs that the residual-LayerNorm kernel reduces together with bias + residual.
 void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int Lmax, int causal,
                     const float* mem, int S, hipStream_t s) {
   const icap_model_desc& d = h->d;
   const int D = d.d_model, H = d.nhead, F = d.dim_ff, rows = B * n_new, ns = h->ns;
   const size_t kv_layer = (size_t)B * H * Lmax * 64;
+  const long PS = (long)rows * D;  // partial slab stride
+  const int KS_D = 4, KS_F = 8;    // split-K of the K=512 and K=dim_ff residual GEMMs
   for (int l = 0; l < d.n_dec_layers; ++l) {
     const DecLayer& L = h->dec[l];
-    // self-attention block: x = LN1(x + SA(x))
-    h->gemm(b.a, D, b.aL, L.sa_qkv, rows, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, s);
+    // self-attention block
+    h->wgemm(b.a, D, b.aL, L.sa_qkv.w, D, L.sa_qkv.b, rows, 3 * D, D, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, WAVE_2x2,
+             1, 0, s);
     HIPCHK(launch_dec_self_attn(b.qkv, B, n_new, t0, H, b.kc + l * kv_layer, b.vc + l * kv_layer, Lmax, causal,
                                 0.125f, b.o, b.aL, ns, s));
-    h->gemm(b.o, D, b.aL, L.sa_out, rows, b.x, D, 0, EPI_NONE, OUT_F32_RESID, s);
-    HIPCHK(launch_layernorm(b.x, D, rows, D, 0, 0, 0, L.n1.w, L.n1.b, 1e-5f, b.x, D, b.a, D, b.aL, ns, s));
-    // cross-attention block (key-absorbed): x = LN2(x + CA(x, mem))
-    h->gemm(b.a, D, b.aL, L.ca_q, rows, b.q, D, b.qL, EPI_NONE, OUT_SPLIT, s);
-    {
-      GemmArgs g = gemm_args();  // qt[:, h*D:(h+1)*D] = q[:, h*64:(h+1)*64] · Wk_h
-      g.A = b.q; g.lda = D; g.a_batch = 64; g.a_lo = b.qL;
-      g.W = L.ca_kT; g.ldw = 64; g.w_batch = (long)D * 64;
-      g.C = b.qt; g.ldc = (long)H * D; g.c_batch = D;
-      g.M = rows; g.N = D; g.K = 64; g.nsplit = ns; g.batch = H;
-      g.epi = EPI_NONE; g.out = OUT_F32;
-      h->run_gemm(g, s);
-    }
+    h->wgemm(b.o, D, b.aL, L.sa_out.w, D, nullptr, rows, D, D, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_D,
+             PS, s);
+    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_D, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
+                                     ns, s));
+    // cross-attention block (key-absorbed)
+    h->wgemm(b.a, D, b.aL, L.ca_q.w, D, L.ca_q.b, rows, D, D, b.q, D, b.qL, EPI_NONE, OUT_SPLIT, WAVE_1x2, 1, 0, s);
+    // qt[:, h*D:(h+1)*D] = q[:, h*64:(h+1)*64] . Wk_h
+    h->wgemm(b.q, D, b.qL, L.ca_kT, 64, nullptr, rows, D, 64, b.qt, (long)H * D, 0, EPI_NONE, OUT_F32, WAVE_2x2, 1,
+             0, s, H, 64, (long)D * 64, 0, D);
     h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 4.0 * (double)(rows / n_new) * S * D, s, [&] {
       HIPCHK(launch_cross_attn_absorbed(b.qt, mem, rows, n_new, S, H, D, 0.125f, b.c, b.cL, ns, s));
     });
-    {
-      GemmArgs g = gemm_args();  // o[:, h*64:(h+1)*64] = c_h · Wv_h^T + bv_h
-      g.A = b.c; g.lda = (long)H * D; g.a_batch = D; g.a_lo = b.cL;
-      g.W = L.ca_v; g.ldw = D; g.w_batch = 64L * D;
-      g.bias = L.ca_vb; g.bias_batch = 64;
-      g.C = b.o; g.ldc = D; g.c_batch = 64; g.c_lo = b.aL;
-      g.M = rows; g.N = 64; g.K = D; g.nsplit = ns; g.batch = H; g.c_planes = ns;
-      g.epi = EPI_NONE; g.out = OUT_SPLIT;
-      h->run_gemm(g, s);
-    }
-    h->gemm(b.o, D, b.aL, L.ca_out, rows, b.x, D, 0, EPI_NONE, OUT_F32_RESID, s);
-    HIPCHK(launch_layernorm(b.x, D, rows, D, 0, 0, 0, L.n2.w, L.n2.b, 1e-5f, b.x, D, b.a, D, b.aL, ns, s));
-    // feed-forward block: x = LN3(x + W2 relu(W1 x))
-    h->gemm(b.a, D, b.aL, L.lin1, rows, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, s);
-    h->gemm(b.hb, F, b.hL, L.lin2, rows, b.x, D, 0, EPI_NONE, OUT_F32_RESID, s);
-    HIPCHK(launch_layernorm(b.x, D, rows, D, 0, 0, 0, L.n3.w, L.n3.b, 1e-5f, b.x, D, b.a, D, b.aL, ns, s));
+    // o[:, h*64:(h+1)*64] = c_h . Wv_h^T + bv_h
+    h->wgemm(b.c, (long)H * D, b.cL, L.ca_v, D, L.ca_vb, rows, 64, D, b.o, D, b.aL, EPI_NONE, OUT_SPLIT, WAVE_1x1, 1,
+             0, s, H, D, 64L * D, 64, 64);
+    h->wgemm(b.o, D, b.aL, L.ca_out.w, D, nullptr, rows, D, D, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_D,
+             PS, s);
+    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_D, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL,
+                                     ns, s));
+    // feed-forward block
+    h->wgemm(b.a, D, b.aL, L.lin1.w, D, L.lin1.b, rows, F, D, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, WAVE_2x2, 1, 0, s);
+    h->wgemm(b.hb, F, b.hL, L.lin2.w, F, nullptr, rows, D, F, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_F, PS,
+             s);
+    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_F, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a, b.aL,
+                                     ns, s));
   }
 }
 
-void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
-                 float* step_logits, const float* uniforms, float* logp, hipStream_t s) {
+void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
+                       float* step_logits, const float* uniforms, float* logp, hipStream_t s) {
   const icap_model_desc& d = h->d;
   REQUIRE(B > 0 && max_len >= 1, "bad batch / max_len");
   REQUIRE(max_len <= d.pe_len, "max_len exceeds the positional-encoding table (PositionalEncoding max_len)");
@@ -463,6 +508,68 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     }
     HIPCHK(launch_head(ha, s));
   }
+}
+
+// Graph path: the first call with a new (B, S, max_len, mode) runs eagerly (allocates the
+// workspace, sets kernel attributes); the second captures the whole loop on a private stream into
+// a hipGraph over handle-owned in/out buffers; later calls copy memory in, replay, copy ids out.
+void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
+                 float* step_logits, const float* uniforms, float* logp, hipStream_t s) {
+  DecodeGraph& g = h->dg;
+  const int mode = uniforms ? 1 : 0;
+  const bool wl = step_logits != nullptr;
+  if (!h->use_graphs) {
+    decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s);
+    return;
+  }
+  if (g.B != B || g.S != S || g.L != max_len || g.mode != mode || g.logits != wl || g.start != start ||
+      g.end != end || (g.exec && g.gen != g_ws_generation)) {
+    g.reset();
+    g.B = B; g.S = S; g.L = max_len; g.mode = mode; g.logits = wl; g.start = start; g.end = end;
+  }
+  if (!g.exec && g.calls++ == 0) {
+    decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s);
+    return;
+  }
+  const size_t mem_bytes = (size_t)B * S * h->d.d_model * 4;
+  const size_t lg_bytes = (size_t)(max_len - 1) * B * h->d.vocab * 4;
+  if (!g.exec) {
+    g.mem.ensure(mem_bytes);
+    g.ids.ensure((size_t)B * max_len * 4);
+    if (wl) g.lg.ensure(lg_bytes);
+    if (mode) {
+      g.uni.ensure((size_t)(max_len - 1) * B * 4);
+      g.lp.ensure((size_t)B * (max_len - 1) * 4);
+    }
+    dec_bufs(h, B, B, max_len);  // make sure nothing allocates during capture
+    if (mode) h->d_fin.ensure((size_t)B);
+    if (!h->cap_stream) HIPCHK(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamSynchronize(s));
+    const bool prof = h->prof_on;
+    h->prof_on = false;
+    HIPCHK(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+    try {
+      decode_loop_eager(h, g.mem.as<float>(), B, S, max_len, start, end, g.ids.as<int32_t>(),
+                        wl ? g.lg.as<float>() : nullptr, mode ? g.uni.as<float>() : nullptr,
+                        mode ? g.lp.as<float>() : nullptr, h->cap_stream);
+    } catch (...) {
+      hipGraph_t dead = nullptr;
+      (void)hipStreamEndCapture(h->cap_stream, &dead);
+      if (dead) (void)hipGraphDestroy(dead);
+      h->prof_on = prof;
+      throw;
+    }
+    HIPCHK(hipStreamEndCapture(h->cap_stream, &g.graph));
+    HIPCHK(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
+    h->prof_on = prof;
+    g.gen = g_ws_generation;
+  }
+  HIPCHK(hipMemcpyAsync(g.mem.p, mem, mem_bytes, hipMemcpyDeviceToDevice, s));
+  if (mode) HIPCHK(hipMemcpyAsync(g.uni.p, uniforms, (size_t)(max_len - 1) * B * 4, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipGraphLaunch(g.exec, s));
+  HIPCHK(hipMemcpyAsync(ids, g.ids.p, (size_t)B * max_len * 4, hipMemcpyDeviceToDevice, s));
+  if (wl) HIPCHK(hipMemcpyAsync(step_logits, g.lg.p, lg_bytes, hipMemcpyDeviceToDevice, s));
+  if (mode) HIPCHK(hipMemcpyAsync(logp, g.lp.p, (size_t)B * (max_len - 1) * 4, hipMemcpyDeviceToDevice, s));
 }
 
 }  // namespace
@@ -556,6 +663,14 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
     h->d_fin.ensure((size_t)rows * 4);  // scratch ids
     ha.ids = h->d_fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
     HIPCHK(launch_head(ha, s));
+  });
+}
+
+int icap_set_graphs(icap_handle* h, int enable) {
+  return guarded([&] {
+    REQUIRE(h, "null handle");
+    h->use_graphs = enable != 0;
+    h->dg.reset();
   });
 }
 

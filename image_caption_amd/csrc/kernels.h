@@ -7,7 +7,7 @@ typedef uint16_t bf16_t;
 
 // Epilogue / output selectors shared by kernels and the host dispatcher.
 enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RELU = 2 };
-enum { OUT_F32 = 0, OUT_BF16 = 1, OUT_SPLIT = 2, OUT_F32_RESID = 3 };
+enum { OUT_F32 = 0, OUT_BF16 = 1, OUT_SPLIT = 2, OUT_F32_RESID = 3, OUT_PARTIAL = 4 };
 
 // C[b] (+)= epi(A[b] · W[b]^T + bias[b] + addend) with A given as `nsplit` bf16 planes
 // (plane p of row r at A + p*a_lo + r*lda); W is [N][K] bf16 (nn.Linear layout).
@@ -23,9 +23,33 @@ struct GemmArgs {
 };
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
-// Which gemm_bf16_kernel instantiation launch_gemm picks (PROF_GEMM_128 / PROF_GEMM_64).
+// Which kernel launch_gemm picks (PROF_GEMM_256 / PROF_GEMM_128 / PROF_GEMM_64).
 int gemm_tile_class(const GemmArgs& g);
-enum { PROF_GEMM_128 = 0, PROF_GEMM_64 = 1, PROF_ENC_ATTN = 2, PROF_CROSS_ATTN = 3 };
+// 256 x 256-tile, 8-wave encoder GEMM (batch 1, N % 256 == 0).
+hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s);
+enum { PROF_GEMM_128 = 0, PROF_GEMM_64 = 1, PROF_ENC_ATTN = 2, PROF_CROSS_ATTN = 3, PROF_GEMM_WAVE = 4, PROF_GEMM_256 = 5 };
+
+// Decode-step GEMM: each wave streams a (16 TM) x (16 TN) tile's operands into registers (no LDS);
+// block = 4 waves along N.  ksplit > 1 with out = OUT_PARTIAL writes fp32 partial slabs
+// C[split * part_stride + row * ldc + col] (bias is then the consumer's job).
+enum { WAVE_2x2 = 0, WAVE_1x2 = 1, WAVE_1x1 = 2, WAVE_2x1 = 3 };
+struct WaveGemmArgs {
+  const bf16_t* A; long lda; long a_batch; long a_lo;
+  const bf16_t* W; long ldw; long w_batch;
+  const float* bias; long bias_batch;
+  void* C; long ldc; long c_batch; long c_lo; int c_planes;
+  int M, N, K, nsplit, batch, ksplit;
+  long part_stride;
+  int epi, out, tile;
+};
+inline WaveGemmArgs wave_args() {
+  WaveGemmArgs g{};
+  g.batch = 1; g.nsplit = 1; g.c_planes = 2; g.ksplit = 1; g.tile = WAVE_2x2;
+  return g;
+}
+hipError_t launch_gemm_wave(const WaveGemmArgs& g, hipStream_t s);
+// Same contract, 32 x 32 block tiles with the whole K' range (<= 1024 per split) DMA'd to LDS first.
+hipError_t launch_gemm_dec(const WaveGemmArgs& g, hipStream_t s);
 
 // LayerNorm over rows of D fp32 values; optional fp32 output (may alias input) and
 // bf16 hi(/lo) planes.  Input row r is read from (r / in_group) * in_stride + in_off + r % in_group.
@@ -34,6 +58,10 @@ hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_gr
                             long ld_f32, bf16_t* out_bf, long ld_bf, long bf_lo, int nsplit,
                             hipStream_t s);
 
+// x = LN(x + sum_{s<nparts} parts[s*part_stride + row*D + col] + bias) in place (fp32), plus planes.
+hipError_t launch_residual_layernorm(float* x, int rows, int D, const float* parts, int nparts, long part_stride,
+                                    const float* bias, const float* w, const float* b, float eps, bf16_t* out_bf,
+                                    long bf_lo, int nsplit, hipStream_t s);
 hipError_t launch_im2col_patches(const float* img, int B, int C, int HW, int P, bf16_t* out, long lo,
                                  int nsplit, hipStream_t s);
 hipError_t launch_cls_rows(const float* cls, const float* pos, float* x, int B, int tokens, int D,
@@ -59,6 +87,10 @@ hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int 
 hipError_t launch_cross_attn_absorbed(const float* qt, const float* mem, int rows, int rows_per_image,
                                       int S, int H, int Dm, float scale, bf16_t* out, long lo, int nsplit,
                                       hipStream_t s);
+// Same contract on MFMA: q~ and memory as bf16 planes (plane strides qt_lo / mem_lo), H = 8, Dm = 512.
+hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* mem, long mem_lo, int rows,
+                                  int rows_per_image, int S, float scale, bf16_t* out, long out_lo, int nsplit,
+                                  hipStream_t s);
 // fc_out + argmax (greedy) or inverse-CDF sample; writes ids[r*ld_ids + col], optional logits, and
 // (if emb != null) the next step's embedded token into x/a.
 struct HeadArgs {

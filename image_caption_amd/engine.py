@@ -210,6 +210,10 @@ class Engine:
               "icap_decoder_forward")
         return logits
 
+    def set_graphs(self, enable: bool) -> None:
+        """hipGraph replay of the decode loop (default on)."""
+        check(self.lib.icap_set_graphs(self.handle, int(bool(enable))), "icap_set_graphs")
+
     # ------------------------------------------------------------------ live kernel timing
     def profile(self, enable: bool) -> None:
         check(self.lib.icap_profile_enable(self.handle, int(bool(enable))), "icap_profile_enable")

@@ -110,11 +110,19 @@ int icap_decode_sample(icap_handle* h, const float* memory, int B, int S, int ma
 int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const float* memory, int S,
                          int causal, float* logits, void* stream);
 
+/* Enable (1, default) / disable (0) hipGraph capture of the decode loop: the first decode call
+ * with a new (B, S, max_len, mode) runs eagerly, the next captures ~80 kernels x (max_len-1)
+ * steps into one graph that later calls replay (kernel timing via icap_profile_* is recorded on
+ * the eager calls only). */
+int icap_set_graphs(icap_handle* h, int enable);
+
 /* ---- live kernel timing (bench.py roofline) ---- */
 #define ICAP_PROF_GEMM_128 0   /* gemm_bf16_kernel<128,128,64,64> (encoder GEMMs)      */
 #define ICAP_PROF_GEMM_64 1    /* gemm_bf16_kernel<64,64,32,32>  (decode-step GEMMs)    */
 #define ICAP_PROF_ENC_ATTN 2   /* enc_attention_kernel                                  */
 #define ICAP_PROF_CROSS_ATTN 3 /* cross_attn_absorbed_kernel                            */
+#define ICAP_PROF_GEMM_WAVE 4  /* gemm_dec_kernel (decode-step GEMMs, whole K' range DMA'd to LDS) */
+#define ICAP_PROF_GEMM_256 5   /* gemm_256_kernel (encoder GEMMs, 256 x 256 tiles)      */
 /* Enable (1) / disable (0) HIP-event bracketing of every hot-kernel launch; clears records. */
 int icap_profile_enable(icap_handle* h, int enable);
 /* Sum over recorded launches of one class: device ms, launch count, algorithmic flops and bytes

@@ -26,7 +26,7 @@ def value(p: torch.Tensor, nsplit: int) -> torch.Tensor:
     return p.double() if nsplit == 1 else p[0].double() + p[1].double()
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (64, 64, 64), (8192, 1024, 768), (50, 512, 2048)])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (64, 64, 64), (8192, 1024, 768), (50, 512, 2048), (16484, 1024, 512)])
 @pytest.mark.parametrize("nsplit", [1, 2])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_gemm(cuda, M, N, K, nsplit, epi):

@@ -164,3 +164,23 @@ def test_scst_step_on_gpu(cuda, vit_sd):
     with torch.no_grad():
         loss, info = SCSTLoss()(m, imgs, refs, vocab, cuda, max_len=30, uniforms=u)
     assert torch.isfinite(loss) and set(info) == {"sample_reward", "greedy_reward", "advantage"}
+
+
+def test_decode_graph_replay_matches_eager(vit_engine, cuda):
+    imgs = torch.from_numpy(W.synthetic_images(8, seed=21)).to(cuda)
+    mem = vit_engine.encode(imgs)
+    vit_engine.set_graphs(False)
+    ref_ids, ref_lg = vit_engine.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, 30, want_logits=True)
+    u = torch.rand(29, 8, device=cuda)
+    ref_s = vit_engine.sample(mem, u, W.START_TOKEN, W.END_TOKEN, 30)
+    vit_engine.set_graphs(True)
+    for _ in range(3):  # eager, capture + replay, replay
+        ids, lg = vit_engine.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, 30, want_logits=True)
+        assert torch.equal(ids, ref_ids) and torch.equal(lg, ref_lg)
+    for _ in range(3):
+        sid, slp = vit_engine.sample(mem, u, W.START_TOKEN, W.END_TOKEN, 30)
+        assert torch.equal(sid, ref_s[0]) and torch.equal(slp, ref_s[1])
+    # a different batch in between must not reuse the captured buffers
+    other = vit_engine.encode(imgs[:3])
+    a, _ = vit_engine.greedy_raw(other, W.START_TOKEN, W.END_TOKEN, 30)
+    assert torch.equal(a, ref_ids[:3])
