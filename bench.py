@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graphs", action="store_true", help="launch the decode loop eagerly (no hipGraph)")
     args = ap.parse_args()
 
     rank, ws, local = parallel.init()
@@ -80,6 +81,8 @@ def main():
 
     sd = W.to_torch(W.vit_state_dict(0))
     eng = Engine(sd, "vit", {}, precision=args.precision, device=dev)
+    if args.no_graphs:
+        eng.set_graphs(False)
     B = args.batch
     total = B * ws
     imgs = torch.from_numpy(W.synthetic_images(B, seed=1 + rank)).to(dev)

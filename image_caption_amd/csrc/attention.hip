@@ -382,37 +382,41 @@ hipError_t launch_cross_attn_absorbed(const float* qt, const float* mem, int row
 
 // ---------------------------------------------------------------------------------------------
 // Cross-attention, key-absorbed form on MFMA (flash-style over 32-key chunks).
-// One 4-wave block per query row; wave w owns d in [128w, 128w + 128) of the 512-wide memory.
-//   scores  S^T[s][h] = sum_d mem[s][d] * qt[h][d]         (A = memory rows, B = q~^T, 8 heads in 16)
-//           partial over each wave's d range, summed through LDS, x 1/8, online softmax per head
-//           (head = lane & 15, so the row statistics are lane-local + 2 xor-shuffles)
-//   context C^T[d][h] += sum_s mem^T[d][s] * P^T[s][h]      (A = mem^T via ds_read_b64_tr_b16,
-//           B = the score accumulators themselves, k order permuted consistently)
+// One 16-wave block per query row (LDS-DMA ingest scales with issuing waves, ~6 GB/s each).
+//   scores  S^T[s][h] = sum_d mem[s][d] * qt[h][d]       (A = memory rows, B = q~^T, 8 heads in 16)
+//           wave w: key tile w & 1, d range [64 (w >> 1), +64); the 8 d-partials are summed in two
+//           levels through LDS; x 1/8; online softmax per head (head = lane & 15, lane-local stats)
+//   context C^T[d][h] += sum_s mem^T[d][s] * P^T[s][h]    (A = mem^T via ds_read_b64_tr_b16,
+//           B = the score accumulators themselves; wave w owns d in [32w, 32w + 32))
 // memory and q~ arrive as bf16 planes (hi, lo); every product uses hi.hi + lo.hi + hi.lo.
-// LDS: two 32-key chunks x planes x 32 KiB (global_load_lds, 16-byte chunk c of key row k stored
-// at chunk c ^ (k & 15): the 16 key rows of a ds_read_b128 group hit 16 different banks).
+// LDS: two 32-key chunk buffers x planes x 32 KiB, both in flight from the start (chunk c + 2 is
+// issued once chunk c has been consumed); 16-byte chunk c of key row k stored at c ^ (k & 15), so the
+// 16 key rows of a ds_read_b128 group hit 16 different banks.
 namespace {
 
 template <int NS>
-__global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __restrict__ qt, long qt_lo,
-                                                              const bf16_t* __restrict__ mem, long mem_lo,
-                                                              int rows_per_image, int S, float scale,
-                                                              bf16_t* out, long out_lo) {
+__global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __restrict__ qt, long qt_lo,
+                                                               const bf16_t* __restrict__ mem, long mem_lo,
+                                                               int rows_per_image, int S, float scale,
+                                                               bf16_t* out, long out_lo) {
   constexpr int DM = 512, H = 8, CK = 32;        // model width, heads, keys per chunk
   constexpr int PLANE = CK * DM * 2;             // 32 KiB per plane per chunk
   constexpr int BUF = NS * PLANE;
+  constexpr int PER_CHUNK = 2 * NS;              // LDS-DMA instructions per wave per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = (float*)(smem + 2 * BUF);         // [4 waves][2 tiles][4 regs][64 lanes]
+  float* red = (float*)(smem + 2 * BUF);         // [8 d-groups][2 tiles][4 regs][64 lanes]
+  float* tot = red + 8 * 512;                    // [2 tiles][4 regs][64 lanes]
   const int r = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
+  const int skt = wave & 1, sdg = wave >> 1;     // score role: key tile, d-group
   const bf16_t* mb = mem + (long)(r / rows_per_image) * S * DM;
   const int nchunks = (S + CK - 1) / CK;
 
-  // q~ fragments (B operand of the scores): head fr (zero for fr >= 8), d = 128w + 32ks + 8fq + j
-  bf16x8 qh[4], ql[4];
+  // q~ fragments (B operand of the scores): head fr (zero for fr >= 8), d = 64 sdg + 32 ks + 8 fq + j
+  bf16x8 qh[2], ql[2];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const long off = (long)r * H * DM + fr * DM + wave * 128 + ks * 32 + fq * 8;
+  for (int ks = 0; ks < 2; ++ks) {
+    const long off = (long)r * H * DM + fr * DM + sdg * 64 + ks * 32 + fq * 8;
     if (fr < H) {
       qh[ks] = *(const bf16x8*)(qt + off);
       if (NS == 2) ql[ks] = *(const bf16x8*)(qt + qt_lo + off);
@@ -422,16 +426,16 @@ __global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __re
     }
   }
 
-  // chunk staging: instruction i (of 16 per wave) covers key row (wave*4 + i/4)... per plane 32 rows
-  // x 1 KiB; lane writes 16 B at lane-linear position; source chunk pre-swizzled.
+  // chunk staging: wave w loads key rows 2w, 2w + 1 of every plane (1 KiB per instruction);
+  // lane-linear LDS destination, source 16-B chunk pre-swizzled.
   auto stage = [&](int c, int buf) {
 #pragma unroll
     for (int pl = 0; pl < NS; ++pl) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int key = wave * 8 + i;                       // 8 rows per wave per plane
+      for (int i = 0; i < 2; ++i) {
+        const int key = wave * 2 + i;
         const int g = min(c * CK + key, S - 1);
-        const int cs = lane ^ (key & 15);                  // 64 chunks of 16 B per 1 KiB row
+        const int cs = lane ^ (key & 15);
         const bf16_t* src = mb + (pl ? mem_lo : 0) + (long)g * DM + cs * 8;
         __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
                                          (LDS_AS void*)(smem + buf * BUF + pl * PLANE + key * 1024), 16, 0, 0);
@@ -439,27 +443,25 @@ __global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __re
     }
   };
 
-  f32x4 acc[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[2];
+  acc[0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  acc[1] = acc[0];
   float m_run = -INFINITY, l_run = 0.f;
   const int q4 = fr >> 2, p4 = fr & 3;
 
   stage(0, 0);
+  if (nchunks > 1) stage(1, 1);
   for (int c = 0; c < nchunks; ++c) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (c + 1 < nchunks) stage(c + 1, (c + 1) & 1);
+    if (c + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_CHUNK) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     const char* cb = smem + (c & 1) * BUF;
-    // partial scores over this wave's d range
-    f32x4 s[2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    {  // partial scores: key tile skt, d-group sdg
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
-      const int key = kt * 16 + fr;
+      const int key = skt * 16 + fr;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int ch = (wave * 128 + ks * 32 + fq * 8) >> 3;
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = (sdg * 64 + ks * 32 + fq * 8) >> 3;
         const int off = key * 1024 + ((ch ^ (key & 15)) << 4);
         const bf16x8 mh = *(const bf16x8*)(cb + off);
         a = mfma16(mh, qh[ks], a);
@@ -469,24 +471,26 @@ __global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __re
           a = mfma16(mh, ql[ks], a);
         }
       }
-      s[kt] = a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[((sdg * 2 + skt) * 4 + j) * 64 + lane] = a[j];
     }
+    __syncthreads();
+    if (threadIdx.x < 512) {
+      float v = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) red[((wave * 2 + kt) * 4 + j) * 64 + lane] = s[kt][j];
+      for (int g = 0; g < 8; ++g) v += red[g * 512 + threadIdx.x];
+      tot[threadIdx.x] = v;
+    }
     __syncthreads();
     // total scores (every wave), scale, mask, online softmax per head (= lane & 15)
+    f32x4 s[2];
     float cmax = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) v += red[((w * 2 + kt) * 4 + j) * 64 + lane];
         const int key = c * CK + kt * 16 + fq * 4 + j;
-        v = key < S ? v * scale : -INFINITY;
+        const float v = key < S ? tot[(kt * 4 + j) * 64 + lane] * scale : -INFINITY;
         s[kt][j] = v;
         cmax = fmaxf(cmax, v);
       }
@@ -518,11 +522,11 @@ __global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __re
         pl[4 + j] = (__bf16)(s[1][j] - (float)ph[4 + j]);
       }
     }
-    // context: C^T[d][h] for this wave's 8 d-tiles; A = mem^T via transposed LDS reads
+    // context: C^T[d][h] for this wave's 2 d-tiles; A = mem^T via transposed LDS reads
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
+    for (int dt = 0; dt < 2; ++dt) {
       acc[dt] *= alpha;
-      const int d = wave * 128 + dt * 16 + 4 * p4;       // this lane's 4 d values in the tr block
+      const int d = wave * 32 + dt * 16 + 4 * p4;        // this lane's 4 d values in the tr block
       const int k0 = 4 * fq + q4, k1 = k0 + 16;
       const int o0 = k0 * 1024 + ((((d >> 3) ^ (k0 & 15))) << 4) + (d & 7) * 2;
       const int o1 = k1 * 1024 + ((((d >> 3) ^ (k1 & 15))) << 4) + (d & 7) * 2;
@@ -534,13 +538,17 @@ __global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __re
         acc[dt] = mfma16(vh, pl, acc[dt]);
       }
     }
+    if (c + 2 < nchunks) {
+      __syncthreads();  // every wave is done with buffer c & 1
+      stage(c + 2, c & 1);
+    }
   }
   // C^T layout: lane holds head fr, d = 16dt + 4fq + r (4 consecutive d) -> 8-byte plane stores
   if (fr < H) {
     const float inv = 1.f / l_run;
-    bf16_t* dst = out + (long)r * H * DM + fr * DM + wave * 128;
+    bf16_t* dst = out + (long)r * H * DM + fr * DM + wave * 32;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
+    for (int dt = 0; dt < 2; ++dt) {
       bf16_t hv[4], lv[4];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) split_bf(acc[dt][rr] * inv, hv[rr], lv[rr]);
@@ -553,28 +561,30 @@ __global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __re
   }
 }
 
+constexpr int XA_RED_BYTES = (8 * 512 + 512) * 4;
+
 }  // namespace
 
 hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* mem, long mem_lo, int rows,
                                   int rows_per_image, int S, float scale, bf16_t* out, long out_lo, int nsplit,
                                   hipStream_t s) {
   if (S <= 0 || rows <= 0 || (nsplit != 1 && nsplit != 2)) return hipErrorInvalidValue;
-  const int lds = 2 * nsplit * 32 * 512 * 2 + 4 * 2 * 4 * 64 * 4;
+  const int lds = 2 * nsplit * 32 * 512 * 2 + XA_RED_BYTES;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)cross_attn_mfma_kernel<2>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * 32 * 512 * 2 + 8192);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * 32 * 512 * 2 + XA_RED_BYTES);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)cross_attn_mfma_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * 32 * 512 * 2 + 8192);
+                              2 * 32 * 512 * 2 + XA_RED_BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
   if (nsplit == 2)
-    hipLaunchKernelGGL(cross_attn_mfma_kernel<2>, dim3(rows), dim3(256), lds, s, qt, qt_lo, mem, mem_lo,
+    hipLaunchKernelGGL(cross_attn_mfma_kernel<2>, dim3(rows), dim3(1024), lds, s, qt, qt_lo, mem, mem_lo,
                        rows_per_image, S, scale, out, out_lo);
   else
-    hipLaunchKernelGGL(cross_attn_mfma_kernel<1>, dim3(rows), dim3(256), lds, s, qt, qt_lo, mem, mem_lo,
+    hipLaunchKernelGGL(cross_attn_mfma_kernel<1>, dim3(rows), dim3(1024), lds, s, qt, qt_lo, mem, mem_lo,
                        rows_per_image, S, scale, out, out_lo);
   return hipGetLastError();
 }

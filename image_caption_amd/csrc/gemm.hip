@@ -314,46 +314,62 @@ hipError_t launch_gemm_wave(const WaveGemmArgs& g, hipStream_t s) {
 // covers 16 rows x 64 B (lane l -> row l >> 2, 16-byte chunk l & 3).
 namespace {
 
-constexpr int DEC_MAX_KSTEPS = 32;  // 32 k-steps x 32 = K' 1024 -> 128 KiB of LDS
+constexpr int DEC_MAX_KSTEPS = 16;  // per split: 16 k-steps x 32 = K 512 -> (ns + 1) x 32 KiB of LDS
+constexpr int DEC_RED_BYTES = 16 * 64 * 16;  // cross-wave reduction: 16 waves x 64 lanes x f32x4
 
-__global__ __launch_bounds__(256) void gemm_dec_kernel(WaveGemmArgs p) {
+// 16 waves: wave w computes output quadrant (w & 3) over the k-steps ks == (w >> 2) mod 4, so every
+// wave has loads to issue (LDS-DMA ingest scales with the number of issuing waves: ~6 GB/s each)
+// and the 4 partial quadrants are summed through LDS before the epilogue.  Per k-step the LDS holds
+// ns activation-plane slices and ONE weight slice (shared by the planes), each 32 rows x 64 B with
+// 16-B chunk c of row r stored at c ^ ((r >> 2) & 3) (conflict-free 16-lane fragment reads).
+__global__ __launch_bounds__(1024) void gemm_dec_kernel(WaveGemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32;
   const int batch = blockIdx.z / p.ksplit, split = blockIdx.z % p.ksplit;
   const bf16_t* A = p.A + (long)batch * p.a_batch;
   const bf16_t* W = p.W + (long)batch * p.w_batch;
-  const int ks_total = p.nsplit * p.K / 32, nks = ks_total / p.ksplit, kbeg = split * nks;
+  const int ns = p.nsplit, nops = ns + 1, step_bytes = nops * 2048;
+  const int nks = p.K / 32 / p.ksplit, kbeg = split * nks;
 
-  // staging: instruction q in [0, 4 * nks): k-step q >> 2, operand (q >> 1) & 1, row half q & 1
-  const int lrow = lane >> 2, lchunk = lane & 3;
-  for (int q = wave; q < 4 * nks; q += 4) {
-    const int ks = q >> 2, opnd = (q >> 1) & 1, half = q & 1;
+  // staging: instruction q in [0, 2 * nops * nks): k-step q / (2 nops), operand, row half
+  const int lrow = lane >> 2, lchunk = (lane & 3) ^ ((lrow >> 2) & 3);
+  const int nq = 2 * nops * nks;
+  for (int q = wave; q < nq; q += 16) {
+    const int ks = q / (2 * nops), rem = q - ks * 2 * nops, opnd = rem >> 1, half = rem & 1;
     const int kg = (kbeg + ks) * 32 + lchunk * 8;
     const int r = half * 16 + lrow;
-    const bf16_t* src;
-    if (opnd == 0) {
-      const int plane = kg / p.K, kin = kg - plane * p.K;
-      src = A + plane * p.a_lo + (long)min(m0 + r, p.M - 1) * p.lda + kin;
-    } else {
-      src = W + (long)min(n0 + r, p.N - 1) * p.ldw + (kg % p.K);
-    }
+    const bf16_t* src = opnd < ns ? A + opnd * p.a_lo + (long)min(m0 + r, p.M - 1) * p.lda + kg
+                                  : W + (long)min(n0 + r, p.N - 1) * p.ldw + kg;
     __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
-                                     (LDS_AS void*)(smem + ks * 4096 + opnd * 2048 + half * 1024), 16, 0, 0);
+                                     (LDS_AS void*)(smem + ks * step_bytes + opnd * 2048 + half * 1024), 16, 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  const int qm = wave >> 1, qn = wave & 1;  // this wave's 16 x 16 quadrant
+  const int quad = wave & 3, kgrp = wave >> 2;
+  const int qm = quad >> 1, qn = quad & 1;
   const int fr = lane & 15, fq = lane >> 4;
+  const int sw = (fq ^ ((fr >> 2) & 3)) * 16;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const char* pa = smem + (qm * 16 + fr) * 64 + fq * 16;
-  const char* pb = smem + 2048 + (qn * 16 + fr) * 64 + fq * 16;
-  for (int ks = 0; ks < nks; ++ks) {
-    const bf16x8 a = *(const bf16x8*)(pa + ks * 4096);
-    const bf16x8 b = *(const bf16x8*)(pb + ks * 4096);
+  const char* pa = smem + (qm * 16 + fr) * 64 + sw;
+  const char* pb = smem + ns * 2048 + (qn * 16 + fr) * 64 + sw;
+  for (int ks = kgrp; ks < nks; ks += 4) {
+    const bf16x8 b = *(const bf16x8*)(pb + ks * step_bytes);
+    const bf16x8 a = *(const bf16x8*)(pa + ks * step_bytes);
     acc = mfma16(a, b, acc);
+    if (ns == 2) {
+      const bf16x8 al = *(const bf16x8*)(pa + 2048 + ks * step_bytes);
+      acc = mfma16(al, b, acc);
+    }
   }
+  __syncthreads();  // staging area is reused for the reduction
+  f32x4* red = (f32x4*)smem;
+  if (kgrp) red[(kgrp * 4 + quad) * 64 + lane] = acc;
+  __syncthreads();
+  if (kgrp) return;
+#pragma unroll
+  for (int g = 1; g < 4; ++g) acc += red[(g * 4 + quad) * 64 + lane];
 
   const int col = n0 + qn * 16 + fr;
   if (col >= p.N) return;
@@ -390,21 +406,127 @@ __global__ __launch_bounds__(256) void gemm_dec_kernel(WaveGemmArgs p) {
 hipError_t launch_gemm_dec(const WaveGemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0 || g.ksplit < 1 || g.N % 16) return hipErrorInvalidValue;
   if (g.K % 32 || (g.nsplit != 1 && g.nsplit != 2)) return hipErrorInvalidValue;
-  const int steps = g.nsplit * g.K / 32;
+  const int steps = g.K / 32;
   if (steps % g.ksplit || steps / g.ksplit > DEC_MAX_KSTEPS) return hipErrorInvalidValue;
   if (g.out == OUT_PARTIAL && g.part_stride <= 0) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)gemm_dec_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             DEC_MAX_KSTEPS * 4096);
+                                             DEC_MAX_KSTEPS * 3 * 2048);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int lds = steps / g.ksplit * 4096;
+  const int lds = std::max(steps / g.ksplit * (g.nsplit + 1) * 2048, DEC_RED_BYTES);
   dim3 grid((g.N + 31) / 32, (g.M + 31) / 32, g.batch * g.ksplit);
-  hipLaunchKernelGGL(gemm_dec_kernel, grid, dim3(256), lds, s, g);
+  hipLaunchKernelGGL(gemm_dec_kernel, grid, dim3(1024), lds, s, g);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Epilogue of the 256 x 256 encoder GEMMs.  The MFMA computed the transposed tile (W as the A
+// operand), so lane l holds output row m = mb + i*16 + (l & 15) and FOUR consecutive columns
+// n = nb + j*16 + 4*(l >> 4) + r: every store is a 16-byte (fp32) or 8-byte (bf16 plane) vector.
+// Every runtime condition is hoisted out of the element loops and the loads are issued in batches
+// (4 bias vectors; 8 residual vectors per column group), so a block waits a handful of memory
+// latencies instead of one per element (a per-element "load or not" branch makes hipcc wait
+// vmcnt(0) after each load).  Rows >= M load from row M - 1 and are not stored.
+namespace {
+
+template <int TM, int TN>
+__device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM][TN], int mb, int nb, int fr,
+                                             int fq) {
+  const int M = p.M;
+  if (p.bias) {
+    f32x4 bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bv[j] = *(const f32x4*)(p.bias + nb + j * 16 + 4 * fq);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += bv[j];
+  }
+  if (p.addend) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      f32x4 ad[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = min(mb + i * 16 + fr, M - 1);
+        ad[i] = *(const f32x4*)(p.addend + (long)((row % p.add_group) + p.add_off) * p.add_ld + nb + j * 16 + 4 * fq);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[i][j] += ad[i];
+    }
+  }
+  if (p.epi == EPI_GELU) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = gelu_erf_fast(acc[i][j][r]);
+  } else if (p.epi == EPI_RELU) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaxf(acc[i][j][r], 0.f);
+  }
+  int orow[TM];  // element offset of the row (launch_gemm_256 guarantees < 2^31); -1: row >= M
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = mb + i * 16 + fr;
+    const int mc = min(m, M - 1);
+    orow[i] = (int)((p.rm_group ? (long)(mc / p.rm_group) * p.rm_stride + p.rm_off + mc % p.rm_group : (long)mc) *
+                    p.ldc);
+    if (m >= M) orow[i] = -1 - orow[i];
+  }
+
+  if (p.out == OUT_F32) {
+    float* C = (float*)p.C;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        if (orow[i] >= 0) *(f32x4*)(C + orow[i] + nb + j * 16 + 4 * fq) = acc[i][j];
+  } else if (p.out == OUT_F32_RESID) {
+    float* C = (float*)p.C;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i0 = 0; i0 < TM; i0 += 4) {
+        f32x4 c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ro = orow[i0 + i] < 0 ? -1 - orow[i0 + i] : orow[i0 + i];
+          c[i] = *(const f32x4*)(C + ro + nb + j * 16 + 4 * fq);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (orow[i0 + i] >= 0) *(f32x4*)(C + orow[i0 + i] + nb + j * 16 + 4 * fq) = c[i] + acc[i0 + i][j];
+      }
+  } else {
+    bf16_t* C = (bf16_t*)p.C;
+    const bool lo_plane = p.out == OUT_SPLIT && p.c_planes == 2;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (orow[i] < 0) continue;
+        const long o = orow[i] + nb + j * 16 + 4 * fq;
+        bf16_t h[4], l[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) split_bf(acc[i][j][r], h[r], l[r]);
+        *(u32x2*)(C + o) = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+        if (lo_plane)
+          *(u32x2*)(C + o + p.c_lo) =
+              (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
+      }
+  }
+}
+
+}  // namespace
 
 // ---------------------------------------------------------------------------------------------
 // Encoder GEMM, 256 x 256 block tile, 8 waves (2 x 4, each 128 x 64 = 8 x 4 MFMA 16x16 tiles).
@@ -419,14 +541,15 @@ hipError_t launch_gemm_dec(const WaveGemmArgs& g, hipStream_t s) {
 // share their A rows in that XCD's L2.
 namespace {
 
-template <int NS>
-__global__ __launch_bounds__(512) void gemm_256_kernel(GemmArgs p) {
-  constexpr int BM = 256, BN = 256, WM = 128, WN = 64, TM = WM / 16, TN = WN / 16;
+template <int NS, int NW, bool NOMFMA = false>
+__global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
+  constexpr int WGM = NW / 4;                       // wave grid WGM x 4
+  constexpr int BM = 256, BN = 256, WM = BM / WGM, WN = 64, TM = WM / 16, TN = WN / 16;
   constexpr int KS = 32;                            // k per stage (one MFMA k-step)
   constexpr int OPB = BM * KS * 2;                  // 16 KiB per operand tile per stage
   constexpr int STAGE = (NS + 1) * OPB;             // A planes + W share one stage
   constexpr int NSTAGE = NS == 2 ? 3 : 4;           // 144 / 128 KiB of LDS
-  constexpr int IPW = OPB / 1024 / 8;               // 1 KiB DMA instructions per wave per operand (2)
+  constexpr int IPW = OPB / 1024 / NW;              // 1 KiB DMA instructions per wave per operand
   constexpr int PER_STAGE = IPW * (NS + 1);         // DMA instructions per wave per stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -500,70 +623,164 @@ __global__ __launch_bounds__(512) void gemm_256_kernel(GemmArgs p) {
       for (int i = 0; i < TM; ++i) {
         const bf16x8 af = *(const bf16x8*)(s0 + pl * OPB + (wm * WM + i * 16) * 64 + foff);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af, acc[i][j]);  // D = W·A^T
-      }
-  }
-
-  // epilogue.  The MFMA computed the transposed tile (W as the A operand), so lane l holds
-  // output row m = i*16 + (l & 15) and FOUR consecutive output columns n = j*16 + 4*(l >> 4) + r:
-  // every store is a 16-byte (fp32) or 8-byte (bf16 plane) vector.
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + 4 * fq;
-    const f32x4 bv = p.bias ? *(const f32x4*)(p.bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * WM + i * 16 + fr;
-      f32x4 v = acc[i][j] + bv;
-      if (p.addend) {
-        const int row = min(m, M - 1);
-        v += *(const f32x4*)(p.addend + (long)((row % p.add_group) + p.add_off) * p.add_ld + n);
-      }
-      if (p.epi == EPI_GELU) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = 0.5f * v[r] * (1.f + erff(v[r] * 0.70710678118654752f));
-      } else if (p.epi == EPI_RELU) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      }
-      acc[i][j] = v;
-    }
-  }
-  auto out_index = [&](int i, int j, long& o) -> bool {
-    const int m = m0 + wm * WM + i * 16 + fr;
-    const long orow = p.rm_group ? (long)(m / p.rm_group) * p.rm_stride + p.rm_off + m % p.rm_group : (long)m;
-    o = orow * p.ldc + n0 + wn * WN + j * 16 + 4 * fq;
-    return m < M;
-  };
-  if (p.out == OUT_F32 || p.out == OUT_F32_RESID) {
-    float* C = (float*)p.C;
-    const bool add = p.out == OUT_F32_RESID;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        long o;
-        if (out_index(i, j, o)) *(f32x4*)(C + o) = add ? *(const f32x4*)(C + o) + acc[i][j] : acc[i][j];
-      }
-  } else {
-    bf16_t* C = (bf16_t*)p.C;
-    const bool lo_plane = p.out == OUT_SPLIT && p.c_planes == 2;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        long o;
-        if (out_index(i, j, o)) {
-          bf16_t h[4], l[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) split_bf(acc[i][j][r], h[r], l[r]);
-          *(u32x2*)(C + o) = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
-          if (lo_plane)
-            *(u32x2*)(C + o + p.c_lo) =
-                (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
+        for (int j = 0; j < TN; ++j) {
+          if (NOMFMA) {  // measurement variant: staging pipeline only (keeps the fragment reads live)
+            asm volatile("" ::"v"(af), "v"(bfr[j]));
+          } else {
+            acc[i][j] = mfma16(bfr[j], af, acc[i][j]);  // D = W·A^T
+          }
         }
       }
   }
+
+  epilogue_256<TM, TN>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// Encoder GEMM, 8-phase schedule (cdna_hip_programming.md "The 256^2 8-phase template").
+// 256 x 256 block tile, BK = 64, 8 waves as 2 (M) x 4 (N), wave tile 128 x 64 = 8 x 4 MFMA tiles,
+// computed as four 64 x 32 quadrants, one per phase:
+//   phase: ds_read the quadrant's register subtile -> issue ONE half-tile of LDS-DMA prefetch ->
+//          [last phase of a K-tile: counted vmcnt] -> s_barrier -> lgkmcnt(0) -> setprio(1),
+//          16 MFMA, setprio(0) -> s_barrier
+// LDS (128 KiB): 2 K-tile buffers x {A, W} x 2 k-halves x 256 rows x 64 B; 16-B chunk c of row r at
+// c ^ (((r >> 3) & 1) << 1) (pre-swizzled on the DMA source, conflict-free 16-row fragment reads).
+// Half-tiles (16 KiB, 2 DMA instructions per wave) are the operand rows of ONE quadrant, loaded in
+// the order of their last read in a K-tile (A qm=0 @ phase 0, W qn=1 @ 1, A qm=1 @ 2, W qn=0 @ 3): load j
+// (= 4 t + x) is issued in phase j - 7, one phase after the lgkmcnt(0)+barrier that retired the
+// previous reads of its buffer, and every K-tile is retired by a vmcnt(6) (3 half-tiles left in
+// flight) in the last phase of the K-tile before it.  bf16x2: the activation planes are further
+// K-tiles (K' = nsplit K; the W k-tile is re-staged per plane from L2).
+namespace {
+
+template <bool ROW128>
+__global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs p) {
+  constexpr int BM = 256, BK = 64, KH = 16384, BUF = 65536;  // k-half region, buffer bytes
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nbn = p.N / BM, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bm = wg / nbn, bn = wg - bm * nbn;
+  const int m0 = bm * BM, n0 = bn * BM;
+  const int M = p.M, K = p.K;
+  const int ktp = K / BK, nk = p.nsplit * ktp, nloads = 4 * nk;
+
+  // DMA geometry: a half-tile is the part of the K-tile ONE phase's quadrant reads, so its last
+  // read falls in one phase: A half q = rows {64 q .. 64 q + 63} of both wave rows (wr = 0, 1),
+  // W half q = rows {64 wc + 32 q .. + 31} of all four wave columns.  Wave w DMAs 16 of those rows
+  // per k-half (one 1 KiB instruction each); the LDS image stays row-major [k-half][256 rows][64 B].
+  // ROW128: LDS image [256 rows][128 B] per operand (both k-halves in one row), one DMA instruction
+  // = 8 rows x a full 128-B line, chunk c of row r at c ^ ((r >> 1) & 7); otherwise [k-half][rows][64 B]
+  // with 16 rows x 64 B per instruction, chunk c at c ^ (((r >> 3) & 1) << 1).
+  const int lchunk = (lane & 3) ^ ((((lane >> 2) >> 3) & 1) << 1);  // 64-B rows: row bit 3 == (lane >> 2) bit 3
+  const int a_row0 = (wave >> 2) * 128 + (wave & 3) * 16;          // + 64 q
+  const int w_row0 = (wave >> 1) * 64 + (wave & 1) * 16;            // + 32 q
+  auto issue = [&](int j) {  // half-tile load j -> K-tile j / 4, half x = j % 4 (A q0, W q1, A q1, W q0)
+    const int t = j >> 2, x = j & 3;
+    const bool isA = !(x & 1);
+    const int q = (x == 1 || x == 2) ? 1 : 0;
+    const int plane = t / ktp, k0 = (t - plane * ktp) * BK;
+    const int rbase = isA ? a_row0 + 64 * q : w_row0 + 32 * q;  // this wave's 16 rows
+    char* dst = smem + (t & 1) * BUF + (isA ? 0 : 2 * KH) + rbase * (ROW128 ? 128 : 64);
+    if (ROW128) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int row = rbase + g * 8 + (lane >> 3);                 // rbase is 16-aligned
+        const int c128 = (lane & 7) ^ ((row >> 1) & 7);
+        const bf16_t* src = isA ? p.A + plane * p.a_lo + (long)min(m0 + row, M - 1) * p.lda + k0 + c128 * 8
+                                : p.W + (long)(n0 + row) * p.ldw + k0 + c128 * 8;
+        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)(dst + g * 1024), 16, 0, 0);
+      }
+    } else {
+      const int row = rbase + (lane >> 2);
+      const bf16_t* src = isA ? p.A + plane * p.a_lo + (long)min(m0 + row, M - 1) * p.lda + k0 + lchunk * 8
+                              : p.W + (long)(n0 + row) * p.ldw + k0 + lchunk * 8;
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)dst, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(src + 32), (LDS_AS void*)(dst + KH), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 ra[4][2], rb[2][2];  // register subtiles: A [m-tile][k-half], W [n-tile][k-half]
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // fragment (row r = 16-aligned base + fr, k-chunk kh * 4 + fq) byte offsets within an operand image
+  const int fsw = (fq ^ (((fr >> 3) & 1) << 1)) << 4;  // row bit 3 == fr bit 3 (tile rows are 16-aligned)
+  auto foff = [&](int rbase, int kh) -> int {
+    if (ROW128) return (rbase + fr) * 128 + (((kh * 4 + fq) ^ ((fr >> 1) & 7)) << 4);
+    return kh * KH + (rbase + fr) * 64 + fsw;
+  };
+  auto read_a = [&](const char* buf, int qm) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) ra[i][kh] = *(const bf16x8*)(buf + foff(wr * 128 + qm * 64 + i * 16, kh));
+  };
+  auto read_b = [&](const char* buf, int qn) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) rb[j][kh] = *(const bf16x8*)(buf + 2 * KH + foff(wc * 64 + qn * 32 + j * 16, kh));
+  };
+  auto mfma_q = [&](int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm * 4 + i][qn * 2 + j] = mfma16(rb[j][kh], ra[i][kh], acc[qm * 4 + i][qn * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: loads 0..6 in flight, K-tile 0 retired
+  for (int j = 0; j < 7 && j < nloads; ++j) issue(j);
+  if (nloads > 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int qm = ph >> 1, qn = (ph == 1 || ph == 2) ? 1 : 0;
+      if (ph == 0) {
+        read_b(buf, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(buf, 0);
+      } else if (ph == 2) {
+        read_a(buf, 1);
+      } else {
+        read_b(buf, qn);
+      }
+      const int j = 4 * t + ph + 7;
+      if (j < nloads) issue(j);
+      if (ph == 3) {
+        // retire K-tile t + 1: loads beyond 4t + 7 that are already issued may stay in flight
+        const int ahead = min(nloads, 4 * t + 11) - (4 * t + 8);
+        if (ahead >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if (ahead == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_q(qm, qn);
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+
+  epilogue_256<8, 4>(p, acc, m0 + wr * 128, n0 + wc * 64, fr, fq);
 }
 
 }  // namespace
@@ -571,20 +788,41 @@ __global__ __launch_bounds__(512) void gemm_256_kernel(GemmArgs p) {
 hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N % 256 || g.K % 32 || g.batch != 1 || (g.nsplit != 1 && g.nsplit != 2))
     return hipErrorInvalidValue;
+  const long last_row = g.rm_group ? (long)((g.M - 1) / g.rm_group) * g.rm_stride + g.rm_off + g.rm_group : g.M;
+  if (last_row * g.ldc >= (1L << 31)) return hipErrorInvalidValue;  // epilogue uses 32-bit row offsets
   constexpr int lds2 = 3 * 3 * 256 * 32 * 2, lds1 = 4 * 2 * 256 * 32 * 2;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e =
-        hipFuncSetAttribute((const void*)gemm_256_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)gemm_256_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
+  static int nw = 0;
+  if (!nw) {
+    const char* v = getenv("ICAP_GEMM256_WAVES");  // experiment knob: 8, 16, or 0 = 8-phase kernel
+    nw = v ? atoi(v) : 16;
+    if (nw != 8 && nw != 16 && nw != 1 && nw != 2 && nw != 160) nw = 16;
+    for (const void* f : {(const void*)gemm_8ph_kernel<false>, (const void*)gemm_8ph_kernel<true>})
+      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 131072) != hipSuccess)
+        return hipErrorInvalidValue;
+    hipError_t e = hipSuccess;
+    for (const void* f : {(const void*)gemm_256_kernel<2, 8>, (const void*)gemm_256_kernel<2, 16>,
+                          (const void*)gemm_256_kernel<2, 16, true>})
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
+    for (const void* f : {(const void*)gemm_256_kernel<1, 8>, (const void*)gemm_256_kernel<1, 16>})
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
     if (e != hipSuccess) return e;
-    attr = true;
   }
   const int nwg = (g.N / 256) * ((g.M + 255) / 256);
-  if (g.nsplit == 2)
-    hipLaunchKernelGGL(gemm_256_kernel<2>, dim3(nwg), dim3(512), lds2, s, g);
-  else
-    hipLaunchKernelGGL(gemm_256_kernel<1>, dim3(nwg), dim3(512), lds1, s, g);
+  if ((nw == 1 || nw == 2) && g.K % 64 == 0) {
+    if (nw == 2) hipLaunchKernelGGL(gemm_8ph_kernel<true>, dim3(nwg), dim3(512), 131072, s, g);
+    else hipLaunchKernelGGL(gemm_8ph_kernel<false>, dim3(nwg), dim3(512), 131072, s, g);
+    return hipGetLastError();
+  }
+  if (nw == 160 && g.nsplit == 2) {
+    hipLaunchKernelGGL((gemm_256_kernel<2, 16, true>), dim3(nwg), dim3(1024), lds2, s, g);
+    return hipGetLastError();
+  }
+  if (g.nsplit == 2) {
+    if (nw == 16) hipLaunchKernelGGL((gemm_256_kernel<2, 16>), dim3(nwg), dim3(1024), lds2, s, g);
+    else hipLaunchKernelGGL((gemm_256_kernel<2, 8>), dim3(nwg), dim3(512), lds2, s, g);
+  } else {
+    if (nw == 16) hipLaunchKernelGGL((gemm_256_kernel<1, 16>), dim3(nwg), dim3(1024), lds1, s, g);
+    else hipLaunchKernelGGL((gemm_256_kernel<1, 8>), dim3(nwg), dim3(512), lds1, s, g);
+  }
   return hipGetLastError();
 }

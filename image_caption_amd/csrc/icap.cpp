@@ -101,7 +101,7 @@ struct DecodeGraph {
   int calls = 0;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
-  DevBuf mem, ids, lg, uni, lp;
+  DevBuf ids, lg, uni, lp;
   void reset() {
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -166,15 +166,15 @@ struct icap_handle {
 
   // workspaces
   DevBuf e_x, e_a, e_qkv, e_h, e_patch;  // encoder
-  DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin, d_part;  // decoder
+  DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin, d_part, d_memp;  // decoder
 
   ~icap_handle() {
     dg.reset();
-    for (DevBuf* b : {&dg.mem, &dg.ids, &dg.lg, &dg.uni, &dg.lp}) b->release();
+    for (DevBuf* b : {&dg.ids, &dg.lg, &dg.uni, &dg.lp}) b->release();
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_x, &d_a, &d_qkv, &d_q, &d_qt, &d_c, &d_o, &d_h,
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_x, &d_a, &d_qkv, &d_q, &d_qt, &d_c, &d_o, &d_h, &d_memp,
                       &d_kv, &d_fin, &d_part})
       b->release();
   }
@@ -399,19 +399,20 @@ void encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, 
 constexpr int MAX_KSPLIT = 8;
 
 struct DecodeBufs {
-  float *x, *qkv, *qt, *kc, *vc, *part;
-  bf16_t *a, *q, *c, *o, *hb;
-  long aL, qL, cL, hL;
+  float *x, *qkv, *kc, *vc, *part;
+  bf16_t *a, *q, *qt, *c, *o, *hb, *memp;
+  long aL, qL, cL, hL, memL;
 };
 
-DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax) {
+DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S) {
   const icap_model_desc& d = h->d;
   const int D = d.d_model, ns = h->ns, H = d.nhead;
   h->d_x.ensure((size_t)rows * D * 4);
   h->d_a.ensure((size_t)rows * D * 2 * ns);
   h->d_qkv.ensure((size_t)rows * 3 * D * 4);
   h->d_q.ensure((size_t)rows * D * 2 * ns);
-  h->d_qt.ensure((size_t)rows * H * D * 4);
+  h->d_qt.ensure((size_t)rows * H * D * 2 * ns);
+  h->d_memp.ensure((size_t)B * S * D * 2 * ns);
   h->d_c.ensure((size_t)rows * H * D * 2 * ns);
   h->d_o.ensure((size_t)rows * D * 2 * ns);
   h->d_h.ensure((size_t)rows * d.dim_ff * 2 * ns);
@@ -419,11 +420,12 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax) {
   h->d_part.ensure((size_t)MAX_KSPLIT * rows * D * 4);
   DecodeBufs b;
   b.x = h->d_x.as<float>(); b.a = h->d_a.as<bf16_t>(); b.qkv = h->d_qkv.as<float>();
-  b.q = h->d_q.as<bf16_t>(); b.qt = h->d_qt.as<float>(); b.c = h->d_c.as<bf16_t>();
+  b.q = h->d_q.as<bf16_t>(); b.qt = h->d_qt.as<bf16_t>(); b.c = h->d_c.as<bf16_t>();
   b.o = h->d_o.as<bf16_t>(); b.hb = h->d_h.as<bf16_t>();
   b.kc = h->d_kv.as<float>();
   b.part = h->d_part.as<float>();
   b.vc = b.kc + (size_t)d.n_dec_layers * B * H * Lmax * 64;
+  b.memp = h->d_memp.as<bf16_t>(); b.memL = (long)B * S * D;
   b.aL = (long)rows * D; b.qL = (long)rows * D; b.cL = (long)rows * H * D; b.hL = (long)rows * d.dim_ff;
   return b;
 }
@@ -434,7 +436,7 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax) {
 // GEMMs are wave-tile decode GEMMs; the three N=512 residual GEMMs split K into fp32 partial
 // slabs that the residual-LayerNorm kernel reduces together with bias + residual.
 void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int Lmax, int causal,
-                    const float* mem, int S, hipStream_t s) {
+                    int S, hipStream_t s) {
   const icap_model_desc& d = h->d;
   const int D = d.d_model, H = d.nhead, F = d.dim_ff, rows = B * n_new, ns = h->ns;
   const size_t kv_layer = (size_t)B * H * Lmax * 64;
@@ -453,11 +455,11 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
                                      ns, s));
     // cross-attention block (key-absorbed)
     h->wgemm(b.a, D, b.aL, L.ca_q.w, D, L.ca_q.b, rows, D, D, b.q, D, b.qL, EPI_NONE, OUT_SPLIT, WAVE_1x2, 1, 0, s);
-    // qt[:, h*D:(h+1)*D] = q[:, h*64:(h+1)*64] . Wk_h
-    h->wgemm(b.q, D, b.qL, L.ca_kT, 64, nullptr, rows, D, 64, b.qt, (long)H * D, 0, EPI_NONE, OUT_F32, WAVE_2x2, 1,
-             0, s, H, 64, (long)D * 64, 0, D);
-    h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 4.0 * (double)(rows / n_new) * S * D, s, [&] {
-      HIPCHK(launch_cross_attn_absorbed(b.qt, mem, rows, n_new, S, H, D, 0.125f, b.c, b.cL, ns, s));
+    // qt[:, h*D:(h+1)*D] = q[:, h*64:(h+1)*64] . Wk_h   (bf16 planes: the scores' MFMA operand)
+    h->wgemm(b.q, D, b.qL, L.ca_kT, 64, nullptr, rows, D, 64, b.qt, (long)H * D, b.cL, EPI_NONE, OUT_SPLIT, WAVE_2x2,
+             1, 0, s, H, 64, (long)D * 64, 0, D);
+    h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * ns * (double)(rows / n_new) * S * D, s, [&] {
+      HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, n_new, S, 0.125f, b.c, b.cL, ns, s));
     });
     // o[:, h*64:(h+1)*64] = c_h . Wv_h^T + bv_h
     h->wgemm(b.c, (long)H * D, b.cL, L.ca_v, D, L.ca_vb, rows, 64, D, b.o, D, b.aL, EPI_NONE, OUT_SPLIT, WAVE_1x1, 1,
@@ -482,8 +484,9 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   REQUIRE(max_len <= d.pe_len, "max_len exceeds the positional-encoding table (PositionalEncoding max_len)");
   REQUIRE(S > 0 && S <= 256, "memory length must be in [1, 256]");
   const int D = d.d_model;
-  DecodeBufs b = dec_bufs(h, B, B, max_len);
-  const float scale = std::sqrt((float)D) == 0 ? 0.f : (float)std::sqrt((double)D);
+  DecodeBufs b = dec_bufs(h, B, B, max_len, S);
+  const float scale = (float)std::sqrt((double)D);
+  if (mem) HIPCHK(launch_split_f32(mem, b.memL, b.memp, b.memL, h->ns, s));
   HIPCHK(launch_fill_col(ids, B, max_len, 0, start, s));
   HIPCHK(launch_embed(nullptr, 0, start, B, 1, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
   uint8_t* fin = nullptr;
@@ -493,7 +496,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
     HIPCHK(hipMemsetAsync(fin, 0, B, s));
   }
   for (int t = 0; t + 1 < max_len; ++t) {
-    decoder_layers(h, b, B, 1, t, max_len, 1, mem, S, s);
+    decoder_layers(h, b, B, 1, t, max_len, 1, S, s);
     HeadArgs ha{};
     ha.x = b.x; ha.rows = B; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = d.vocab;
     ha.logits = step_logits ? step_logits + (size_t)t * B * d.vocab : nullptr;
@@ -531,17 +534,15 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s);
     return;
   }
-  const size_t mem_bytes = (size_t)B * S * h->d.d_model * 4;
   const size_t lg_bytes = (size_t)(max_len - 1) * B * h->d.vocab * 4;
   if (!g.exec) {
-    g.mem.ensure(mem_bytes);
     g.ids.ensure((size_t)B * max_len * 4);
     if (wl) g.lg.ensure(lg_bytes);
     if (mode) {
       g.uni.ensure((size_t)(max_len - 1) * B * 4);
       g.lp.ensure((size_t)B * (max_len - 1) * 4);
     }
-    dec_bufs(h, B, B, max_len);  // make sure nothing allocates during capture
+    dec_bufs(h, B, B, max_len, S);  // make sure nothing allocates during capture
     if (mode) h->d_fin.ensure((size_t)B);
     if (!h->cap_stream) HIPCHK(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(hipStreamSynchronize(s));
@@ -549,7 +550,7 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     h->prof_on = false;
     HIPCHK(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
     try {
-      decode_loop_eager(h, g.mem.as<float>(), B, S, max_len, start, end, g.ids.as<int32_t>(),
+      decode_loop_eager(h, nullptr, B, S, max_len, start, end, g.ids.as<int32_t>(),
                         wl ? g.lg.as<float>() : nullptr, mode ? g.uni.as<float>() : nullptr,
                         mode ? g.lp.as<float>() : nullptr, h->cap_stream);
     } catch (...) {
@@ -564,7 +565,8 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     h->prof_on = prof;
     g.gen = g_ws_generation;
   }
-  HIPCHK(hipMemcpyAsync(g.mem.p, mem, mem_bytes, hipMemcpyDeviceToDevice, s));
+  DecodeBufs b = dec_bufs(h, B, B, max_len, S);  // no allocation: sized at capture
+  HIPCHK(launch_split_f32(mem, b.memL, b.memp, b.memL, h->ns, s));
   if (mode) HIPCHK(hipMemcpyAsync(g.uni.p, uniforms, (size_t)(max_len - 1) * B * 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipGraphLaunch(g.exec, s));
   HIPCHK(hipMemcpyAsync(ids, g.ids.p, (size_t)B * max_len * 4, hipMemcpyDeviceToDevice, s));
@@ -653,10 +655,11 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
     REQUIRE(S > 0 && S <= 256, "memory length must be in [1, 256]");
     hipStream_t s = (hipStream_t)stream;
     const int D = h->d.d_model, rows = B * T;
-    DecodeBufs b = dec_bufs(h, rows, B, T);
+    DecodeBufs b = dec_bufs(h, rows, B, T, S);
+    HIPCHK(launch_split_f32(memory, b.memL, b.memp, b.memL, h->ns, s));
     const float scale = (float)std::sqrt((double)D);
     HIPCHK(launch_embed(tgt, T, 0, rows, T, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
-    decoder_layers(h, b, B, T, 0, T, causal, memory, S, s);
+    decoder_layers(h, b, B, T, 0, T, causal, S, s);
     HeadArgs ha{};
     ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = h->d.vocab;
     ha.logits = logits; ha.ld_logits = h->d.vocab;

@@ -67,55 +67,61 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 
 // Post-LN residual block tail: x = LN(x + sum_s parts[s] + bias) in place, plus bf16 planes of
 // the result.  Reduces the split-K partial slabs of the preceding decode GEMM (no atomics).
-template <int PER>
-__global__ __launch_bounds__(256) void residual_layernorm_kernel(float* __restrict__ x, int rows,
-                                                                 const float* __restrict__ parts, int nparts,
-                                                                 long part_stride, const float* __restrict__ bias,
-                                                                 const float* __restrict__ w,
-                                                                 const float* __restrict__ b, float eps,
-                                                                 bf16_t* out_bf, long bf_lo, int nsplit) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  constexpr int D = PER * 64;
+// x = LN(x + sum_s parts[s] + bias) in place, plus the bf16 planes of the result.  One block of
+// D / 4 threads per row (each thread owns 4 consecutive columns), so a decode step's few hundred
+// rows spread over every CU and each lane issues all its loads (x, bias, up to 8 partial slabs) at
+// once: the kernel costs one memory latency, not one per slab.
+constexpr int RLN_MAX_PARTS = 8;
+
+template <int NT>
+__global__ __launch_bounds__(NT) void residual_layernorm_kernel(float* __restrict__ x, int rows,
+                                                                const float* __restrict__ parts, int nparts,
+                                                                long part_stride, const float* __restrict__ bias,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ b, float eps,
+                                                                bf16_t* out_bf, long bf_lo, int nsplit) {
+  constexpr int D = NT * 4, NW = NT / 64;
+  __shared__ float red[2][NW];
+  const int row = blockIdx.x, col = threadIdx.x * 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* xr = x + (long)row * D;
-  float v[PER];
+  f32x4 pp[RLN_MAX_PARTS];
 #pragma unroll
-  for (int c = 0; c < PER / 4; ++c) {
-    const int col = c * 256 + lane * 4;
-    f32x4 t = *(const f32x4*)(xr + col);
-    const f32x4 bb = *(const f32x4*)(bias + col);
-    for (int s = 0; s < nparts; ++s) {
-      const f32x4 pp = *(const f32x4*)(parts + s * part_stride + (long)row * D + col);
-      t[0] += pp[0]; t[1] += pp[1]; t[2] += pp[2]; t[3] += pp[3];
-    }
-    v[c * 4 + 0] = t[0] + bb[0]; v[c * 4 + 1] = t[1] + bb[1]; v[c * 4 + 2] = t[2] + bb[2]; v[c * 4 + 3] = t[3] + bb[3];
+  for (int s = 0; s < RLN_MAX_PARTS; ++s)
+    pp[s] = s < nparts ? *(const f32x4*)(parts + s * part_stride + (long)row * D + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 v = *(const f32x4*)(xr + col);
+  const f32x4 bb = bias ? *(const f32x4*)(bias + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  const f32x4 wv = *(const f32x4*)(w + col), bv = *(const f32x4*)(b + col);
+  v += bb;
+#pragma unroll
+  for (int s = 0; s < RLN_MAX_PARTS; ++s) v += pp[s];
+  float sm = wave_sum(v[0] + v[1] + v[2] + v[3]);
+  if (lane == 0) red[0][wave] = sm;
+  __syncthreads();
+  sm = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) sm += red[0][i];
+  const float mean = sm / (float)D;
+  f32x4 d = v - mean;
+  float q = wave_sum(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]);
+  if (lane == 0) red[1][wave] = q;
+  __syncthreads();
+  q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) q += red[1][i];
+  const float rstd = 1.0f / sqrtf(q / (float)D + eps);
+  f32x4 y;
+  bf16_t h[4], l[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    y[k] = d[k] * rstd * wv[k] + bv[k];
+    split_bf(y[k], h[k], l[k]);
   }
-  float sm = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) sm += v[i];
-  const float mean = wave_sum(sm) / (float)D;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) { const float d = v[i] - mean; q += d * d; }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
-#pragma unroll
-  for (int c = 0; c < PER / 4; ++c) {
-    const int col = c * 256 + lane * 4;
-    const f32x4 wv = *(const f32x4*)(w + col), bv = *(const f32x4*)(b + col);
-    f32x4 y;
-    bf16_t h[4], l[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      y[k] = (v[c * 4 + k] - mean) * rstd * wv[k] + bv[k];
-      split_bf(y[k], h[k], l[k]);
-    }
-    *(f32x4*)(xr + col) = y;
-    bf16_t* o = out_bf + (long)row * D + col;
-    *(u32x2*)o = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
-    if (nsplit == 2)
-      *(u32x2*)(o + bf_lo) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
-  }
+  *(f32x4*)(xr + col) = y;
+  bf16_t* o = out_bf + (long)row * D + col;
+  *(u32x2*)o = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+  if (nsplit == 2)
+    *(u32x2*)(o + bf_lo) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
 }
 
 // img (B,C,HW,HW) -> rows (B*np, C*P*P) in (c, kh, kw) order == torchvision conv_proj weight order.
@@ -234,12 +240,13 @@ hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_gr
 hipError_t launch_residual_layernorm(float* x, int rows, int D, const float* parts, int nparts, long part_stride,
                                     const float* bias, const float* w, const float* b, float eps, bf16_t* out_bf,
                                     long bf_lo, int nsplit, hipStream_t s) {
-  dim3 grid((rows + 3) / 4);
+  if (nparts < 0 || nparts > RLN_MAX_PARTS || rows <= 0) return hipErrorInvalidValue;
+  dim3 grid(rows);
   if (D == 512)
-    hipLaunchKernelGGL(residual_layernorm_kernel<8>, grid, dim3(256), 0, s, x, rows, parts, nparts, part_stride,
+    hipLaunchKernelGGL(residual_layernorm_kernel<128>, grid, dim3(128), 0, s, x, rows, parts, nparts, part_stride,
                        bias, w, b, eps, out_bf, bf_lo, nsplit);
   else if (D == 768)
-    hipLaunchKernelGGL(residual_layernorm_kernel<12>, grid, dim3(256), 0, s, x, rows, parts, nparts, part_stride,
+    hipLaunchKernelGGL(residual_layernorm_kernel<192>, grid, dim3(192), 0, s, x, rows, parts, nparts, part_stride,
                        bias, w, b, eps, out_bf, bf_lo, nsplit);
   else
     return hipErrorInvalidValue;

@@ -6,7 +6,7 @@ from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-name = lambda r: r["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[:48]
+name = lambda r: r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:48]
 dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
 tot = defaultdict(float)
 cnt = defaultdict(int)
