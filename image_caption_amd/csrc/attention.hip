@@ -39,8 +39,8 @@ __device__ __forceinline__ bf16x8 tr_pair(const char* p0, const char* p1) {
   return __builtin_bit_cast(bf16x8, c);
 }
 
-template <int NKT, bool SPLIT>
-__global__ __launch_bounds__(256) void enc_attention_kernel(const bf16_t* __restrict__ qkv, long ld, long lo,
+template <int NKT, bool SPLIT, int NW>
+__global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __restrict__ qkv, long ld, long lo,
                                                             int N, int H, float scale, bf16_t* out,
                                                             long out_ld, long out_lo) {
   constexpr int NP = NKT * 16;           // padded keys (multiple of 32)
@@ -55,40 +55,40 @@ __global__ __launch_bounds__(256) void enc_attention_kernel(const bf16_t* __rest
   const int D = H * 64;
   const bf16_t* base = qkv + (long)b * N * ld;
 
-  // stage K and V (zero-padded rows >= N); K swizzled for row-fragment reads, V plain for tr reads
-  for (int c = tid; c < NP * 8; c += 256) {
-    const int row = c >> 3, ch = c & 7;
-    u32x4 kh = {0, 0, 0, 0}, vh = kh, kl = kh, vl = kh;
-    if (row < N) {
-      const bf16_t* src = base + (long)row * ld + h * 64 + ch * 8;
-      kh = *(const u32x4*)(src + D);
-      vh = *(const u32x4*)(src + 2 * D);
-      if (SPLIT) {
-        kl = *(const u32x4*)(src + lo + D);
-        vl = *(const u32x4*)(src + lo + 2 * D);
-      }
-    }
-    const int ko = row * 128 + ((ch ^ (row & 7)) << 4), vo = row * 128 + ch * 16;
-    *(u32x4*)(Kh + ko) = kh;
-    *(u32x4*)(Vh + vo) = vh;
-    if (SPLIT) {
-      *(u32x4*)(Kl + ko) = kl;
-      *(u32x4*)(Vl + vo) = vl;
-    }
-  }
-  __syncthreads();
-
+  // stage K and V by LDS-DMA, one instruction = 8 rows x 128 B (full lines), lane-linear image:
+  // K chunk c of row r stored at c ^ (r & 7) (pre-swizzled on the source; conflict-free row-fragment
+  // reads), V plain for the transposed reads.  Rows >= N repeat row N - 1: their scores are masked to
+  // -inf and their V rows meet p = 0.  All waves issue (LDS-DMA ingest scales with issuing waves).
   const int fr = lane & 15, g = lane >> 4;
   const int nqt = (N + 15) / 16;
-  for (int qt = wave; qt < nqt; qt += 4) {
+  bf16x8 qh[2], ql[2];
+  auto load_q = [&](int qt) {
     const int q = min(qt * 16 + fr, N - 1);
-    bf16x8 qh[2], ql[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16_t* src = base + (long)q * ld + h * 64 + ks * 32 + g * 8;
       qh[ks] = *(const bf16x8*)src;
       if (SPLIT) ql[ks] = *(const bf16x8*)(src + lo);
     }
+  };
+  if (wave < nqt) load_q(wave);
+  {
+    constexpr int PER_MAT = NP / 8, NMAT = SPLIT ? 4 : 2;
+    const int lrow = lane >> 3, lch = lane & 7;
+    for (int ins = wave; ins < NMAT * PER_MAT; ins += NW) {
+      const int mat = ins / PER_MAT, row = (ins - mat * PER_MAT) * 8 + lrow;  // mat: Kh, Vh, Kl, Vl
+      const bool isK = !(mat & 1);
+      const int ch = isK ? lch ^ (row & 7) : lch;
+      const bf16_t* src = base + (mat >= 2 ? lo : 0) + (long)min(row, N - 1) * ld + (isK ? D : 2 * D) + h * 64 + ch * 8;
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
+                                       (LDS_AS void*)(smem + mat * MAT + (ins - mat * PER_MAT) * 1024), 16, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int qt = wave; qt < nqt; qt += NW) {
+    if (qt != wave) load_q(qt);
     f32x4 s[NKT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
@@ -334,15 +334,17 @@ __global__ __launch_bounds__(512) void cross_attn_absorbed_kernel(const float* _
 template <int NKT, bool SPLIT>
 hipError_t run_enc(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale, bf16_t* out,
                    long out_ld, long out_lo, hipStream_t s) {
+  // 4 waves: the split-precision score tile needs > 256 VGPRs (8 waves per block spill)
+  constexpr int NW = 4;
   const int lds = NKT * 16 * 128 * (SPLIT ? 4 : 2);
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_kernel<NKT, SPLIT>,
+    const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_kernel<NKT, SPLIT, NW>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((enc_attention_kernel<NKT, SPLIT>), dim3(H, B), dim3(256), lds, s, qkv, ld, lo, N, H,
+  hipLaunchKernelGGL((enc_attention_kernel<NKT, SPLIT, NW>), dim3(H, B), dim3(NW * 64), lds, s, qkv, ld, lo, N, H,
                      scale, out, out_ld, out_lo);
   return hipGetLastError();
 }

@@ -293,6 +293,7 @@ hipError_t launch_gemm_wave(const WaveGemmArgs& g, hipStream_t s) {
   const int D = per % 4 == 0 ? 4 : (per % 2 == 0 ? 2 : 0);
   if (D == 0) return hipErrorInvalidValue;
   if (g.out == OUT_PARTIAL && g.part_stride <= 0) return hipErrorInvalidValue;
+  if (g.N % 4) return hipErrorInvalidValue;  // 4 consecutive output columns per lane
   switch (g.tile) {
     case WAVE_2x2: return run_wave<2, 2, 4>(g, s, D);
     case WAVE_1x2: return run_wave<1, 2, 4>(g, s, D);
@@ -322,7 +323,9 @@ constexpr int DEC_RED_BYTES = 16 * 64 * 16;  // cross-wave reduction: 16 waves x
 // and the 4 partial quadrants are summed through LDS before the epilogue.  Per k-step the LDS holds
 // ns activation-plane slices and ONE weight slice (shared by the planes), each 32 rows x 64 B with
 // 16-B chunk c of row r stored at c ^ ((r >> 2) & 3) (conflict-free 16-lane fragment reads).
-__global__ __launch_bounds__(1024) void gemm_dec_kernel(WaveGemmArgs p) {
+template <int NWV>
+__global__ __launch_bounds__(NWV * 64) void gemm_dec_kernel(WaveGemmArgs p) {
+  constexpr int KGRPS = NWV / 4;  // k-step groups (waves per output quadrant)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32;
@@ -335,7 +338,7 @@ __global__ __launch_bounds__(1024) void gemm_dec_kernel(WaveGemmArgs p) {
   // staging: instruction q in [0, 2 * nops * nks): k-step q / (2 nops), operand, row half
   const int lrow = lane >> 2, lchunk = (lane & 3) ^ ((lrow >> 2) & 3);
   const int nq = 2 * nops * nks;
-  for (int q = wave; q < nq; q += 16) {
+  for (int q = wave; q < nq; q += NWV) {
     const int ks = q / (2 * nops), rem = q - ks * 2 * nops, opnd = rem >> 1, half = rem & 1;
     const int kg = (kbeg + ks) * 32 + lchunk * 8;
     const int r = half * 16 + lrow;
@@ -347,57 +350,62 @@ __global__ __launch_bounds__(1024) void gemm_dec_kernel(WaveGemmArgs p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  const int quad = wave & 3, kgrp = wave >> 2;
+  const int quad = wave & 3, kgrp = wave >> 2;  // kgrp < KGRPS
   const int qm = quad >> 1, qn = quad & 1;
   const int fr = lane & 15, fq = lane >> 4;
   const int sw = (fq ^ ((fr >> 2) & 3)) * 16;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const char* pa = smem + (qm * 16 + fr) * 64 + sw;
   const char* pb = smem + ns * 2048 + (qn * 16 + fr) * 64 + sw;
-  for (int ks = kgrp; ks < nks; ks += 4) {
+  // W as the first operand: lane holds output row m = fr, four consecutive columns n = 4 fq + r
+  for (int ks = kgrp; ks < nks; ks += KGRPS) {
     const bf16x8 b = *(const bf16x8*)(pb + ks * step_bytes);
     const bf16x8 a = *(const bf16x8*)(pa + ks * step_bytes);
-    acc = mfma16(a, b, acc);
+    acc = mfma16(b, a, acc);
     if (ns == 2) {
       const bf16x8 al = *(const bf16x8*)(pa + 2048 + ks * step_bytes);
-      acc = mfma16(al, b, acc);
+      acc = mfma16(b, al, acc);
     }
   }
-  __syncthreads();  // staging area is reused for the reduction
-  f32x4* red = (f32x4*)smem;
-  if (kgrp) red[(kgrp * 4 + quad) * 64 + lane] = acc;
-  __syncthreads();
-  if (kgrp) return;
+  if (KGRPS > 1) {
+    __syncthreads();  // staging area is reused for the reduction
+    f32x4* red = (f32x4*)smem;
+    if (kgrp) red[(kgrp * 4 + quad) * 64 + lane] = acc;
+    __syncthreads();
+    if (kgrp == 0) {
 #pragma unroll
-  for (int g = 1; g < 4; ++g) acc += red[(g * 4 + quad) * 64 + lane];
+      for (int g = 1; g < KGRPS; ++g) acc += red[(g * 4 + quad) * 64 + lane];
+    }
+  }
 
-  const int col = n0 + qn * 16 + fr;
-  if (col >= p.N) return;
-  const float bv = (p.bias && p.ksplit == 1) ? p.bias[(long)batch * p.bias_batch + col] : 0.f;
+  const int row = m0 + qm * 16 + fr;
+  const int col = n0 + qn * 16 + 4 * fq;
+  if (KGRPS > 1 && kgrp) return;
+  if (row >= p.M || col >= p.N) return;
+  f32x4 v = acc;
+  if (p.bias && p.ksplit == 1) v += *(const f32x4*)(p.bias + (long)batch * p.bias_batch + col);
+  if (p.epi == EPI_GELU) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = m0 + qm * 16 + fq * 4 + r;
-    if (row >= p.M) continue;
-    float v = acc[r] + bv;
-    const long o = (long)batch * p.c_batch + (long)row * p.ldc + col;
-    if (p.out == OUT_PARTIAL) {
-      ((float*)p.C)[(long)split * p.part_stride + o] = v;
-      continue;
-    }
-    if (p.epi == EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-    else if (p.epi == EPI_RELU) v = fmaxf(v, 0.f);
-    if (p.out == OUT_F32) {
-      ((float*)p.C)[o] = v;
-    } else if (p.out == OUT_F32_RESID) {
-      ((float*)p.C)[o] += v;
-    } else if (p.out == OUT_BF16) {
-      ((bf16_t*)p.C)[o] = f2bf(v);
-    } else {
-      bf16_t hi, lo;
-      split_bf(v, hi, lo);
-      ((bf16_t*)p.C)[o] = hi;
-      if (p.c_planes == 2) ((bf16_t*)p.C)[o + p.c_lo] = lo;
-    }
+    for (int r = 0; r < 4; ++r) v[r] = gelu_erf_fast(v[r]);
+  } else if (p.epi == EPI_RELU) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+  }
+  const long o = (long)batch * p.c_batch + (long)row * p.ldc + col;
+  if (p.out == OUT_PARTIAL) {
+    *(f32x4*)((float*)p.C + (long)split * p.part_stride + o) = v;
+  } else if (p.out == OUT_F32) {
+    *(f32x4*)((float*)p.C + o) = v;
+  } else if (p.out == OUT_F32_RESID) {
+    *(f32x4*)((float*)p.C + o) += v;
+  } else {
+    bf16_t h[4], l[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) split_bf(v[r], h[r], l[r]);
+    bf16_t* C = (bf16_t*)p.C;
+    *(u32x2*)(C + o) = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+    if (p.out == OUT_SPLIT && p.c_planes == 2)
+      *(u32x2*)(C + o + p.c_lo) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
   }
 }
 
@@ -409,16 +417,25 @@ hipError_t launch_gemm_dec(const WaveGemmArgs& g, hipStream_t s) {
   const int steps = g.K / 32;
   if (steps % g.ksplit || steps / g.ksplit > DEC_MAX_KSTEPS) return hipErrorInvalidValue;
   if (g.out == OUT_PARTIAL && g.part_stride <= 0) return hipErrorInvalidValue;
+  if (g.N % 4) return hipErrorInvalidValue;  // 4 consecutive output columns per lane
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)gemm_dec_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             DEC_MAX_KSTEPS * 3 * 2048);
-    if (e != hipSuccess) return e;
+    for (const void* f : {(const void*)gemm_dec_kernel<4>, (const void*)gemm_dec_kernel<16>}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, DEC_MAX_KSTEPS * 3 * 2048);
+      if (e != hipSuccess) return e;
+    }
     attr = true;
   }
-  const int lds = std::max(steps / g.ksplit * (g.nsplit + 1) * 2048, DEC_RED_BYTES);
+  // few k-steps per block: 4 waves (one per quadrant, no reduction, up to 8 blocks per CU);
+  // otherwise 16 waves so that enough waves issue the LDS-DMA of the larger slice
+  const int nks = steps / g.ksplit;
   dim3 grid((g.N + 31) / 32, (g.M + 31) / 32, g.batch * g.ksplit);
-  hipLaunchKernelGGL(gemm_dec_kernel, grid, dim3(1024), lds, s, g);
+  if (nks <= 4) {
+    hipLaunchKernelGGL(gemm_dec_kernel<4>, grid, dim3(256), nks * (g.nsplit + 1) * 2048, s, g);
+  } else {
+    const int lds = std::max(nks * (g.nsplit + 1) * 2048, DEC_RED_BYTES);
+    hipLaunchKernelGGL(gemm_dec_kernel<16>, grid, dim3(1024), lds, s, g);
+  }
   return hipGetLastError();
 }
 
