@@ -8,8 +8,15 @@ the reference's batch-global stop rule.  Launch as
   python bench.py [--gpus 1 --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel's algorithmic rate measured
-with HIP events around each of its launches inside the timed region; `cpu_baseline` times the
-CPU oracle (fp32 restatement of the reference algorithm, full-prefix recompute) on the host.
+with HIP events around each of its launches inside the timed region; its `traffic` is the HBM-side
+bytes per launch of that kernel from the committed rocprofv3 PMC summary (tools/pmc_bench.sh:
+FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction) when one exists for it; `cpu_baseline` times
+the CPU oracle (fp32 restatement of the reference algorithm, full-prefix recompute) on the host.
+`--model grid` measures config 3 (ResNet-101 trunk through PyTorch/MIOpen fp32 as in the drop-in
+model, then the HIP encoder tail and decode loop); `--mode scst` measures config 5's reward step
+(encode once, HIP sample on injected uniforms + HIP greedy baseline from the same memory, all-gather
+of both id sets, CIDEr-D over the GLOBAL batch on rank 0).  Neither is the
+headline line.
 """
 from __future__ import annotations
 
@@ -32,6 +39,20 @@ from image_caption_amd.engine import Engine, apply_stop_rule  # noqa: E402
 METRIC = "captions/sec (224×224, max_len=30, greedy) at 1/2/4/8 MI355X vs CPU ref"
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA, MI355X_MICROARCH.md chip table
 PEAK_HBM_GBS = 8000.0
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+
+
+def pmc_traffic(kernel: str):
+    """Per-launch HBM-side bytes of `kernel` from the committed PMC summary, or None."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            table = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for name, row in table.items():
+        if name.split("<")[0] == kernel:
+            return int(row["traffic_bytes"])
+    return None
 
 
 def log(*a):
@@ -71,6 +92,8 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graphs", action="store_true", help="launch the decode loop eagerly (no hipGraph)")
+    ap.add_argument("--model", default="vit", choices=["vit", "grid"])
+    ap.add_argument("--mode", default="greedy", choices=["greedy", "scst"])
     args = ap.parse_args()
 
     rank, ws, local = parallel.init()
@@ -79,8 +102,15 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    sd = W.to_torch(W.vit_state_dict(0))
-    eng = Engine(sd, "vit", {}, precision=args.precision, device=dev)
+    sd = W.to_torch(W.vit_state_dict(0) if args.model == "vit" else W.grid_state_dict(0))
+    eng = Engine(sd, args.model, {}, precision=args.precision, device=dev)
+    trunk = None
+    if args.model == "grid":
+        from models.grid_transformer_model import GridFeatureEncoder
+
+        genc = GridFeatureEncoder(pretrained_cnn=False)
+        genc.load_state_dict({k[len("encoder."):]: v for k, v in sd.items() if k.startswith("encoder.")})
+        trunk = genc.cnn.to(dev).eval()
     if args.no_graphs:
         eng.set_graphs(False)
     B = args.batch
@@ -88,12 +118,43 @@ def main():
     imgs = torch.from_numpy(W.synthetic_images(B, seed=1 + rank)).to(dev)
     L = args.max_len
 
+    def encode():
+        if trunk is not None:
+            with torch.no_grad():
+                return eng.encode(trunk(imgs))
+        return eng.encode(imgs)
+
     def step():
-        mem = eng.encode(imgs)
+        mem = encode()
         ids, _ = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L)
         if ws > 1:
             ids = parallel.gather_rows(ids, total)
         return apply_stop_rule(ids.long(), W.END_TOKEN)
+
+    if args.mode == "scst":
+        from image_caption_amd import cider
+        from utils.scst_loss import sample_stop_length
+
+        gen = torch.Generator(device="cpu").manual_seed(5)
+        # one synthetic reference caption (5-12 tokens) per image of the global batch
+        refs = [[torch.randint(1, 100, (int(torch.randint(5, 13, (1,), generator=gen)),), generator=gen).tolist()]
+                for _ in range(total)]
+        uni = torch.rand(L - 1, B, generator=gen).to(dev)
+
+        def step():  # noqa: F811
+            mem = encode()
+            sid, _ = eng.sample(mem, uni, W.START_TOKEN, W.END_TOKEN, L)
+            gid, _ = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L)
+            if ws > 1:
+                sid, gid = parallel.gather_rows(sid, total), parallel.gather_rows(gid, total)
+            sid, gid = sid.long(), apply_stop_rule(gid.long(), W.END_TOKEN)
+            sid = sid[:, : sample_stop_length(sid, W.END_TOKEN)]
+            if rank == 0:
+                cap = lambda r: cider.caption_ids(r, W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN)
+                s_r = cider.cider_d([cap(r) for r in sid.tolist()], refs)[1]
+                g_r = cider.cider_d([cap(r) for r in gid.tolist()], refs)[1]
+                return torch.tensor(s_r) - torch.tensor(g_r)
+            return gid
 
     for _ in range(args.warmup):
         out = step()
@@ -129,24 +190,32 @@ def main():
         if "attn" in dom["kernel"] and "cross" in dom["kernel"]:
             achieved = dom["bytes"] / dom["launches"] / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None}
+                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(dom["kernel"])}
         else:
             achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
             roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None}
+                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(dom["kernel"])}
         roof.update({"kernel": dom["kernel"], "launches_per_step": dom["launches"] // args.steps,
                      "avg_launch_us": round(avg_ms * 1e3, 2),
                      "share_of_step": round(dom["ms"] / args.steps / step_ms, 3)})
         cpu = None
-        if ws == 1 and not args.no_cpu_baseline:
+        if roof["traffic"] is not None:
+            roof["traffic_unit"] = "bytes/launch (HBM-side, rocprofv3 PMC, profiles/r01/pmc_traffic.json)"
+        if ws == 1 and not args.no_cpu_baseline and args.model == "vit":
             cpu = cpu_baseline(args.cpu_seconds, args.cpu_batch, L)
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "captions/s", "n_gpus": ws, "steps": args.steps,
+            "metric": METRIC if args.mode == "greedy" else "images/sec, SCST reward step (sample + greedy + CIDEr-D)",
+            "value": round(value, 2), "unit": "captions/s" if args.mode == "greedy" else "images/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic images N(0,1) + seeded random-init weights",
-            "config": {"workload": "vit_b16 encoder + 6-layer decoder, greedy, 224x224, max_len=30",
+            "config": {"workload": ("vit_b16 encoder + 6-layer decoder, greedy, 224x224, max_len=30" if args.model == "vit"
+                                    else "grid resnet101 (torch/MIOpen fp32) + 6-layer encoder + 6-layer decoder, "
+                                         "greedy, 224x224, max_len=30")
+                       + ("; SCST reward step: sample + greedy + CIDEr-D (global batch)" if args.mode == "scst"
+                          else ""),
                        "per_gpu_batch": B, "global_batch": total, "max_len": L, "precision": args.precision,
-                       "decode_steps": L - 1, "output_len": int(out.shape[1]), "parallelism": f"dp{ws}"},
+                       "decode_steps": L - 1, "output_len": int(out.shape[1]) if args.mode == "greedy" else None,
+                       "parallelism": f"dp{ws}"},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -115,7 +115,7 @@ struct icap_handle {
   icap_model_desc d{};
   bool use_graphs = true;
   hipStream_t cap_stream = nullptr;
-  DecodeGraph dg;
+  DecodeGraph dg[2];  // one captured loop per mode (0 greedy, 1 sample): SCST alternates them
   int ns = 2;  // activation planes (1 = bf16, 2 = hi/lo)
   std::vector<void*> owned;
   // decoder
@@ -169,8 +169,10 @@ struct icap_handle {
   DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin, d_part, d_memp;  // decoder
 
   ~icap_handle() {
-    dg.reset();
-    for (DevBuf* b : {&dg.ids, &dg.lg, &dg.uni, &dg.lp}) b->release();
+    for (DecodeGraph& g : dg) {
+      g.reset();
+      for (DevBuf* b : {&g.ids, &g.lg, &g.uni, &g.lp}) b->release();
+    }
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
@@ -518,8 +520,8 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
 // a hipGraph over handle-owned in/out buffers; later calls copy memory in, replay, copy ids out.
 void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
                  float* step_logits, const float* uniforms, float* logp, hipStream_t s) {
-  DecodeGraph& g = h->dg;
   const int mode = uniforms ? 1 : 0;
+  DecodeGraph& g = h->dg[mode];
   const bool wl = step_logits != nullptr;
   if (!h->use_graphs) {
     decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s);
@@ -673,7 +675,7 @@ int icap_set_graphs(icap_handle* h, int enable) {
   return guarded([&] {
     REQUIRE(h, "null handle");
     h->use_graphs = enable != 0;
-    h->dg.reset();
+    for (DecodeGraph& g : h->dg) g.reset();
   });
 }
 
