@@ -440,6 +440,128 @@ hipError_t launch_gemm_dec(const WaveGemmArgs& g, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Chained per-head GEMMs (launch_chain_dec): block = (128 output columns, 32 rows, head).
+// Everything it needs is DMA'd to LDS up front (X 32 x 512 planes, W1_h 64 x 512, W2 chunk
+// 128 x 64: 152 KiB for bf16x2) by all 16 waves, one wait.  Phase 1: Y (32 x 64) over K = 512,
+// 8 output tiles x 2 k-groups, reduced through LDS, + b1, split into bf16 planes written back to
+// LDS in the MFMA operand layout.  Phase 2: O (32 x 128) = Y W2^T, one 16 x 16 tile per wave.
+// Layouts as gemm_dec_kernel: per k-step rows of 64 B, chunk c of row r at c ^ ((r >> 2) & 3).
+namespace {
+
+__global__ __launch_bounds__(1024) void chain_dec_kernel(ChainArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 128, m0 = blockIdx.y * 32, h = blockIdx.z;
+  const int ns = p.nsplit;
+  // LDS map (bytes): X [16 ks][ns][32 rows][64 B] | W1 [16 ks][64 rows][64 B] | W2 [2 ks][128][64 B]
+  const int XS = ns * 2048;  // X bytes per k-step
+  char* sx = smem;
+  char* sw1 = smem + 16 * XS;
+  char* sw2 = sw1 + 16 * 4096;
+  const bf16_t* X = p.X + (long)h * p.x_hstride;
+  const bf16_t* W1 = p.W1 + (long)h * 64 * 512;
+  const bf16_t* W2 = p.W2 + (long)h * p.w2_hstride;
+  const int lrow = lane >> 2, lchunk = (lane & 3) ^ ((lrow >> 2) & 3);
+  // DMA: X 16 ks x ns x 2 halves, W1 16 ks x 4 quarters, W2 2 ks x 8 eighths (1 KiB each)
+  const int nx = 16 * ns * 2, nw1 = 64, nq = nx + nw1 + 16;
+  for (int q = wave; q < nq; q += 16) {
+    const bf16_t* src;
+    char* dst;
+    if (q < nx) {
+      const int ks = q / (2 * ns), rem = q - ks * 2 * ns, pl = rem >> 1, half = rem & 1;
+      const int r = half * 16 + lrow;
+      src = X + pl * p.x_lo + (long)min(m0 + r, p.M - 1) * p.ldx + ks * 32 + lchunk * 8;
+      dst = sx + ks * XS + pl * 2048 + half * 1024;
+    } else if (q < nx + nw1) {
+      const int i = q - nx, ks = i >> 2, qu = i & 3;
+      src = W1 + (long)(qu * 16 + lrow) * 512 + ks * 32 + lchunk * 8;
+      dst = sw1 + ks * 4096 + qu * 1024;
+    } else {
+      const int i = q - nx - nw1, ks = i >> 3, e = i & 7;
+      src = W2 + (long)(n0 + e * 16 + lrow) * p.ldw2 + ks * 32 + lchunk * 8;
+      dst = sw2 + ks * 8192 + e * 1024;
+    }
+    __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)dst, 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sw = (fq ^ ((fr >> 2) & 3)) * 16;
+  // phase 1: wave -> tile (tm = t >> 2: rows, tn = t & 3: Y columns) and k-group kg (ks parity)
+  const int t1 = wave & 7, kg = wave >> 3, tm = t1 >> 2, tn = t1 & 3;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int ks = kg; ks < 16; ks += 2) {
+    const bf16x8 b = *(const bf16x8*)(sw1 + ks * 4096 + (tn * 16 + fr) * 64 + sw);
+    const char* xa = sx + ks * XS + (tm * 16 + fr) * 64 + sw;
+    acc = mfma16(b, *(const bf16x8*)xa, acc);  // lane: row fr, Y columns 4 fq + r
+    if (ns == 2) acc = mfma16(b, *(const bf16x8*)(xa + 2048), acc);
+  }
+  __syncthreads();  // X / W1 no longer read: reuse the X area
+  f32x4* red = (f32x4*)smem;
+  if (kg) red[t1 * 64 + lane] = acc;
+  __syncthreads();
+  char* sy = smem + 8 * 1024 * 2;  // Y planes [2 ks][ns][32 rows][64 B], after the reduction area
+  if (!kg) {
+    acc += red[t1 * 64 + lane];
+    const int col = tn * 16 + 4 * fq;  // Y column within the head (0..63)
+    acc += *(const f32x4*)(p.b1 + h * 64 + col);
+    bf16_t hv[4], lv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) split_bf(acc[r], hv[r], lv[r]);
+    const int m = tm * 16 + fr, ks = col >> 5, c = (col & 31) >> 3;
+    char* dst = sy + ks * XS + m * 64 + ((c ^ ((m >> 2) & 3)) << 4) + (col & 7) * 2;
+    *(u32x2*)dst = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+    if (ns == 2)
+      *(u32x2*)(dst + 2048) =
+          (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+  }
+  __syncthreads();
+  // phase 2: wave -> output tile (rows tm2 = wave >> 3, columns tn2 = wave & 7), K = 64
+  const int tm2 = wave >> 3, tn2 = wave & 7;
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const bf16x8 b = *(const bf16x8*)(sw2 + ks * 8192 + (tn2 * 16 + fr) * 64 + sw);
+    const char* ya = sy + ks * XS + (tm2 * 16 + fr) * 64 + sw;
+    o = mfma16(b, *(const bf16x8*)ya, o);
+    if (ns == 2) o = mfma16(b, *(const bf16x8*)(ya + 2048), o);
+  }
+  const int row = m0 + tm2 * 16 + fr;
+  if (row >= p.M) return;
+  const int col = n0 + tn2 * 16 + 4 * fq;
+  if (p.out == OUT_PARTIAL) {
+    *(f32x4*)((float*)p.C + (long)h * p.part_stride + (long)row * p.ldc + col) = o;
+  } else {
+    bf16_t hv[4], lv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) split_bf(o[r], hv[r], lv[r]);
+    bf16_t* dst = (bf16_t*)p.C + (long)row * p.ldc + (long)h * p.c_hstride + col;
+    *(u32x2*)dst = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+    if (ns == 2)
+      *(u32x2*)(dst + p.c_lo) =
+          (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+  }
+}
+
+}  // namespace
+
+hipError_t launch_chain_dec(const ChainArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N2 % 128 || a.H <= 0 || (a.nsplit != 1 && a.nsplit != 2)) return hipErrorInvalidValue;
+  if (a.out != OUT_PARTIAL && a.out != OUT_SPLIT) return hipErrorInvalidValue;
+  const int lds = 16 * a.nsplit * 2048 + 16 * 4096 + 2 * 8192;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)chain_dec_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             16 * 2 * 2048 + 16 * 4096 + 2 * 8192);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(chain_dec_kernel, dim3(a.N2 / 128, (a.M + 31) / 32, a.H), dim3(1024), lds, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Epilogue of the 256 x 256 encoder GEMMs.  The MFMA computed the transposed tile (W as the A
 // operand), so lane l holds output row m = mb + i*16 + (l & 15) and FOUR consecutive columns
 // n = nb + j*16 + 4*(l >> 4) + r: every store is a 16-byte (fp32) or 8-byte (bf16 plane) vector.

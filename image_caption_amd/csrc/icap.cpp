@@ -236,6 +236,11 @@ struct icap_handle {
     const double bytes = 2.0 * batch * ((double)M * K * ns + (double)N * K);
     timed(PROF_GEMM_WAVE, flops, bytes, s, [&] { HIPCHK(launch_gemm_dec(g, s)); });
   }
+  void chain(const ChainArgs& a, hipStream_t s) {
+    const double flops = 2.0 * a.M * a.H * (64.0 * 512 + (double)a.N2 * 64);
+    const double bytes = 2.0 * a.H * ((double)a.M * 512 * ns + 64.0 * 512 + (double)a.N2 * 64);
+    timed(PROF_GEMM_WAVE, flops, bytes, s, [&] { HIPCHK(launch_chain_dec(a, s)); });
+  }
   void attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, bf16_t* out, long out_ld, long out_lo,
                  hipStream_t s) {
     const double flops = 4.0 * B * H * (double)N * N * 64;
@@ -456,20 +461,32 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
     HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_D, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
                                      ns, s));
     // cross-attention block (key-absorbed)
-    h->wgemm(b.a, D, b.aL, L.ca_q.w, D, L.ca_q.b, rows, D, D, b.q, D, b.qL, EPI_NONE, OUT_SPLIT, WAVE_1x2, 1, 0, s);
-    // qt[:, h*D:(h+1)*D] = q[:, h*64:(h+1)*64] . Wk_h   (bf16 planes: the scores' MFMA operand)
-    h->wgemm(b.q, D, b.qL, L.ca_kT, 64, nullptr, rows, D, 64, b.qt, (long)H * D, b.cL, EPI_NONE, OUT_SPLIT, WAVE_2x2,
-             1, 0, s, H, 64, (long)D * 64, 0, D);
+    // per head, one launch: q_h = a Wq_h^T + bq_h, then qt[:, h*D:(h+1)*D] = q_h Wk_h (bf16 planes)
+    {
+      ChainArgs c{};
+      c.X = b.a; c.ldx = D; c.x_lo = b.aL; c.x_hstride = 0;
+      c.W1 = L.ca_q.w; c.b1 = L.ca_q.b;
+      c.W2 = L.ca_kT; c.ldw2 = 64; c.w2_hstride = (long)D * 64;
+      c.C = b.qt; c.ldc = (long)H * D; c.c_lo = b.cL; c.c_hstride = D;
+      c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_SPLIT;
+      h->chain(c, s);
+    }
     h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * ns * (double)(rows / n_new) * S * D, s, [&] {
       HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, n_new, S, 0.125f, b.c, b.cL, ns, s));
     });
-    // o[:, h*64:(h+1)*64] = c_h . Wv_h^T + bv_h
-    h->wgemm(b.c, (long)H * D, b.cL, L.ca_v, D, L.ca_vb, rows, 64, D, b.o, D, b.aL, EPI_NONE, OUT_SPLIT, WAVE_1x1, 1,
-             0, s, H, D, 64L * D, 64, 64);
-    h->wgemm(b.o, D, b.aL, L.ca_out.w, D, nullptr, rows, D, D, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_D,
-             PS, s);
-    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_D, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL,
-                                     ns, s));
+    // per head, one launch: o_h = c_h Wv_h^T + bv_h, then slab h = o_h Wo[:, h*64:(h+1)*64]^T; the
+    // residual LN sums the H slabs (the output projection as a split-K over heads)
+    {
+      ChainArgs c{};
+      c.X = b.c; c.ldx = (long)H * D; c.x_lo = b.cL; c.x_hstride = D;
+      c.W1 = L.ca_v; c.b1 = L.ca_vb;
+      c.W2 = L.ca_out.w; c.ldw2 = D; c.w2_hstride = 64;
+      c.C = b.part; c.ldc = D; c.part_stride = PS;
+      c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_PARTIAL;
+      h->chain(c, s);
+    }
+    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL, ns,
+                                     s));
     // feed-forward block
     h->wgemm(b.a, D, b.aL, L.lin1.w, D, L.lin1.b, rows, F, D, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, WAVE_2x2, 1, 0, s);
     h->wgemm(b.hb, F, b.hL, L.lin2.w, F, nullptr, rows, D, F, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_F, PS,

@@ -51,6 +51,20 @@ hipError_t launch_gemm_wave(const WaveGemmArgs& g, hipStream_t s);
 // Same contract, 32 x 32 block tiles with the whole K' range (<= 1024 per split) DMA'd to LDS first.
 hipError_t launch_gemm_dec(const WaveGemmArgs& g, hipStream_t s);
 
+// Two chained per-head GEMMs in one launch (decoder cross-attention block), for each head h:
+//   Y_h = X_h W1_h^T + b1_h      X_h: rows x 512 (bf16 planes), W1_h: rows [64h, 64h + 64) of W1 [.][512]
+//   O_h = Y_h W2_h^T             W2_h: N2 x 64 at W2 + h * w2_hstride, row stride ldw2
+// out = OUT_SPLIT: planes of O_h at C + row * ldc + h * c_hstride (+ c_lo for the lo plane);
+// out = OUT_PARTIAL: fp32 O_h into slab h at C + h * part_stride + row * ldc.
+struct ChainArgs {
+  const bf16_t* X; long ldx; long x_lo; long x_hstride;
+  const bf16_t* W1; const float* b1;
+  const bf16_t* W2; long ldw2; long w2_hstride;
+  void* C; long ldc; long c_lo; long c_hstride; long part_stride;
+  int M, N2, H, nsplit, out;
+};
+hipError_t launch_chain_dec(const ChainArgs& a, hipStream_t s);
+
 // LayerNorm over rows of D fp32 values; optional fp32 output (may alias input) and
 // bf16 hi(/lo) planes.  Input row r is read from (r / in_group) * in_stride + in_off + r % in_group.
 hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_group, long in_stride,
