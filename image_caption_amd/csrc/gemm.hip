@@ -680,7 +680,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
 // share their A rows in that XCD's L2.
 namespace {
 
-template <int NS, int NW, bool NOMFMA = false>
+template <int NS, int NW, int NOMFMA = 0>  // measurement variants: 1 = no MFMA, 2 = staging ring only
 __global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
   constexpr int WGM = NW / 4;                       // wave grid WGM x 4
   constexpr int BM = 256, BN = 256, WM = BM / WGM, WN = 64, TM = WM / 16, TN = WN / 16;
@@ -753,6 +753,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
     // refill the buffer read in iteration kt-1 (every wave has passed this barrier)
     if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
     const char* s0 = smem + (kt % NSTAGE) * STAGE;
+    if (NOMFMA == 2) continue;
     bf16x8 bfr[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + NS * OPB + (wn * WN + j * 16) * 64 + foff);
@@ -934,34 +935,36 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
   if (!nw) {
     const char* v = getenv("ICAP_GEMM256_WAVES");  // experiment knob: 8, 16, or 0 = 8-phase kernel
     nw = v ? atoi(v) : 16;
-    if (nw != 8 && nw != 16 && nw != 1 && nw != 2 && nw != 160) nw = 16;
+    if (nw != 8 && nw != 16 && nw != 1 && nw != 2 && nw != 160 && nw != 161) nw = 16;
     for (const void* f : {(const void*)gemm_8ph_kernel<false>, (const void*)gemm_8ph_kernel<true>})
       if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 131072) != hipSuccess)
         return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     for (const void* f : {(const void*)gemm_256_kernel<2, 8>, (const void*)gemm_256_kernel<2, 16>,
-                          (const void*)gemm_256_kernel<2, 16, true>})
+                          (const void*)gemm_256_kernel<2, 16, 1>, (const void*)gemm_256_kernel<2, 16, 2>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
     for (const void* f : {(const void*)gemm_256_kernel<1, 8>, (const void*)gemm_256_kernel<1, 16>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
     if (e != hipSuccess) return e;
   }
   const int nwg = (g.N / 256) * ((g.M + 255) / 256);
+  const GemmArgs& g2 = g;
   if ((nw == 1 || nw == 2) && g.K % 64 == 0) {
     if (nw == 2) hipLaunchKernelGGL(gemm_8ph_kernel<true>, dim3(nwg), dim3(512), 131072, s, g);
     else hipLaunchKernelGGL(gemm_8ph_kernel<false>, dim3(nwg), dim3(512), 131072, s, g);
     return hipGetLastError();
   }
-  if (nw == 160 && g.nsplit == 2) {
-    hipLaunchKernelGGL((gemm_256_kernel<2, 16, true>), dim3(nwg), dim3(1024), lds2, s, g);
+  if ((nw == 160 || nw == 161) && g.nsplit == 2) {
+    if (nw == 160) hipLaunchKernelGGL((gemm_256_kernel<2, 16, 1>), dim3(nwg), dim3(1024), lds2, s, g2);
+    else hipLaunchKernelGGL((gemm_256_kernel<2, 16, 2>), dim3(nwg), dim3(1024), lds2, s, g2);
     return hipGetLastError();
   }
   if (g.nsplit == 2) {
-    if (nw == 16) hipLaunchKernelGGL((gemm_256_kernel<2, 16>), dim3(nwg), dim3(1024), lds2, s, g);
-    else hipLaunchKernelGGL((gemm_256_kernel<2, 8>), dim3(nwg), dim3(512), lds2, s, g);
+    if (nw == 16) hipLaunchKernelGGL((gemm_256_kernel<2, 16>), dim3(nwg), dim3(1024), lds2, s, g2);
+    else hipLaunchKernelGGL((gemm_256_kernel<2, 8>), dim3(nwg), dim3(512), lds2, s, g2);
   } else {
-    if (nw == 16) hipLaunchKernelGGL((gemm_256_kernel<1, 16>), dim3(nwg), dim3(1024), lds1, s, g);
-    else hipLaunchKernelGGL((gemm_256_kernel<1, 8>), dim3(nwg), dim3(512), lds1, s, g);
+    if (nw == 16) hipLaunchKernelGGL((gemm_256_kernel<1, 16>), dim3(nwg), dim3(1024), lds1, s, g2);
+    else hipLaunchKernelGGL((gemm_256_kernel<1, 8>), dim3(nwg), dim3(512), lds1, s, g2);
   }
   return hipGetLastError();
 }

@@ -11,7 +11,7 @@ iters = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 name = sys.argv[2] if len(sys.argv) > 2 else "mlp3"
 ns = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 n, k, epi, out = SHAPES[name]
-m = 256 * 197
+m = int(os.environ.get("GEMM_M", 256 * 197))
 A = torch.randn(ns, m, k, device=dev).to(torch.bfloat16)
 W = (torch.randn(n, k, device=dev) / k ** 0.5).to(torch.bfloat16)
 b = torch.randn(n, device=dev)

@@ -10,6 +10,7 @@ i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU" \
            "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "TCC_REQ_sum TCC_EA0_RDREQ_sum TA_BUSY_avr TCP_TOTAL_CACHE_ACCESSES_sum" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 tools/gemm_one.py 3 $SHAPE $NS > $OUT/p$i.log 2>&1

@@ -13,16 +13,16 @@
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
 
-__global__ __launch_bounds__(256) void ingest(const char* __restrict__ src, long src_bytes, int blk_bytes, int inflight,
-                                              int mode, int* sink) {
+__global__ __launch_bounds__(1024) void ingest(const char* __restrict__ src, long src_bytes, int blk_bytes, int inflight,
+                                               int mode, int* sink) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   const long base = ((long)blockIdx.x * 7919 * 1024) & (src_bytes - 1);
   const long b0 = base & ~1023L;
-  const int per_group = inflight / 4096;  // instructions per wave per group (4 waves x 1 KiB each)
+  const int per_group = inflight / (1024 * nwv);  // instructions per wave per group
   for (int g0 = 0; g0 < blk_bytes; g0 += inflight) {
     for (int i = 0; i < per_group; ++i) {
-      const int ins = (g0 / 1024) + i * 4 + wave;  // global instruction index (1 KiB each)
+      const int ins = (g0 / 1024) + i * nwv + wave;  // global instruction index (1 KiB each)
       long off;
       if (mode == 0) off = (long)ins * 1024 + lane * 16;
       else if (mode == 1) {  // 16 rows x 64 B: rows of 1 KiB pitch, column block = ins % 16
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void ingest(const char* __restrict__ src, long
       }
       if (mode == 3) continue;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ((b0 + off) & (src_bytes - 1))),
-                                       (__attribute__((address_space(3))) void*)(lds + ((i * 4 + wave) * 1024) % (128 * 1024)),
+                                       (__attribute__((address_space(3))) void*)(lds + ((i * nwv + wave) * 1024) % (128 * 1024)),
                                        16, 0, 0);
     }
     if (mode == 3) {
@@ -68,23 +68,24 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  printf("%-6s %-5s %-9s %-6s %-6s %10s %12s\n", "src", "mode", "inflight", "grid", "blkKB", "us", "GB/s/CU");
-  for (int blk : {1024 * 1024})
-  for (long sb : {512L << 10, 64L << 20})
-    for (int mode : {0, 3})
+  printf("%-8s %-5s %-9s %-6s %-6s %10s %12s\n", "src", "waves", "inflight", "grid", "blocks/CU", "us", "GB/s/CU");
+  const int blk = 1024 * 1024;
+  for (long sb : {4L << 20, 64L << 20})
+    for (int nwv : {4, 16})
       for (int infl : {32768, 65536})
-        for (int grid : {256, 512, 1024, 2048}) {
+        for (int grid : {256, 512, 1024}) {
+          if (nwv == 16 && grid > 512) continue;
           const int lds = infl;
           for (int rep = 0; rep < 2; ++rep) {
             CK(hipEventRecord(a));
-            hipLaunchKernelGGL(ingest, dim3(grid), dim3(256), lds, 0, src, sb, blk, infl, mode, sink);
+            hipLaunchKernelGGL(ingest, dim3(grid), dim3(nwv * 64), lds, 0, src, sb, blk, infl, 1, sink);
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
           }
           float ms;
           CK(hipEventElapsedTime(&ms, a, b));
           const double per_cu = (double)grid * blk / 256 / (ms * 1e-3) / 1e9;
-          printf("%-6ld %-5d %-9d %-6d %-6d %10.2f %12.1f\n", sb >> 10, mode, infl, grid, blk >> 10, ms * 1e3, per_cu);
+          printf("%-8ld %-5d %-9d %-6d %-6d %10.2f %12.1f\n", sb >> 10, nwv, infl, grid, grid / 256, ms * 1e3, per_cu);
         }
   return 0;
 }
