@@ -15,8 +15,9 @@ the CPU oracle (fp32 restatement of the reference algorithm, full-prefix recompu
 `--model grid` measures config 3 (ResNet-101 trunk through PyTorch/MIOpen fp32 as in the drop-in
 model, then the HIP encoder tail and decode loop); `--mode scst` measures config 5's reward step
 (encode once, HIP sample on injected uniforms + HIP greedy baseline from the same memory, all-gather
-of both id sets, CIDEr-D over the GLOBAL batch on rank 0).  Neither is the
-headline line.
+of both id sets, CIDEr-D over the GLOBAL batch on rank 0); `--mode beam`
+measures the batched beam search (§8(f)1: encode + icap_decode_beam, every image at once).  None of
+these is the headline line.
 """
 from __future__ import annotations
 
@@ -93,7 +94,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graphs", action="store_true", help="launch the decode loop eagerly (no hipGraph)")
     ap.add_argument("--model", default="vit", choices=["vit", "grid"])
-    ap.add_argument("--mode", default="greedy", choices=["greedy", "scst"])
+    ap.add_argument("--mode", default="greedy", choices=["greedy", "scst", "beam"])
+    ap.add_argument("--beam", type=int, default=5, help="beam width of --mode beam")
     args = ap.parse_args()
 
     rank, ws, local = parallel.init()
@@ -130,6 +132,14 @@ def main():
         if ws > 1:
             ids = parallel.gather_rows(ids, total)
         return apply_stop_rule(ids.long(), W.END_TOKEN)
+
+    if args.mode == "beam":
+        def step():  # noqa: F811
+            mem = encode()
+            ids, lens = eng.beam(mem, W.START_TOKEN, W.END_TOKEN, L, args.beam, grid_variant=args.model == "grid")
+            if ws > 1:
+                ids = parallel.gather_rows(ids, total)
+            return ids
 
     if args.mode == "scst":
         from image_caption_amd import cider
@@ -204,15 +214,16 @@ def main():
         if ws == 1 and not args.no_cpu_baseline and args.model == "vit":
             cpu = cpu_baseline(args.cpu_seconds, args.cpu_batch, L)
         line = {
-            "metric": METRIC if args.mode == "greedy" else "images/sec, SCST reward step (sample + greedy + CIDEr-D)",
-            "value": round(value, 2), "unit": "captions/s" if args.mode == "greedy" else "images/s", "n_gpus": ws, "steps": args.steps,
+            "metric": {"greedy": METRIC, "scst": "images/sec, SCST reward step (sample + greedy + CIDEr-D)",
+                       "beam": f"captions/sec, beam search (beam {args.beam}, max_len={L})"}[args.mode],
+            "value": round(value, 2), "unit": "images/s" if args.mode == "scst" else "captions/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic images N(0,1) + seeded random-init weights",
             "config": {"workload": ("vit_b16 encoder + 6-layer decoder, greedy, 224x224, max_len=30" if args.model == "vit"
                                     else "grid resnet101 (torch/MIOpen fp32) + 6-layer encoder + 6-layer decoder, "
                                          "greedy, 224x224, max_len=30")
-                       + ("; SCST reward step: sample + greedy + CIDEr-D (global batch)" if args.mode == "scst"
-                          else ""),
+                       + {"greedy": "", "scst": "; SCST reward step: sample + greedy + CIDEr-D (global batch)",
+                          "beam": f"; beam search, beam {args.beam}"}[args.mode],
                        "per_gpu_batch": B, "global_batch": total, "max_len": L, "precision": args.precision,
                        "decode_steps": L - 1, "output_len": int(out.shape[1]) if args.mode == "greedy" else None,
                        "parallelism": f"dp{ws}"},

@@ -20,7 +20,7 @@ PREC_BF16, PREC_BF16X2 = 1, 2
 PRECISIONS = {"bf16": PREC_BF16, "bf16x2": PREC_BF16X2}
 PROF_GEMM_128, PROF_GEMM_64, PROF_ENC_ATTN, PROF_CROSS_ATTN, PROF_GEMM_WAVE, PROF_GEMM_256 = 0, 1, 2, 3, 4, 5
 PROF_NAMES = {PROF_GEMM_128: "gemm_bf16_kernel<128,128,64,64>", PROF_GEMM_64: "gemm_bf16_kernel<64,64,32,32>",
-              PROF_ENC_ATTN: "enc_attention_kernel", PROF_CROSS_ATTN: "cross_attn_absorbed_kernel",
+              PROF_ENC_ATTN: "enc_attention_kernel", PROF_CROSS_ATTN: "cross_attn_mfma_kernel",
               PROF_GEMM_WAVE: "gemm_dec_kernel", PROF_GEMM_256: "gemm_256_kernel"}
 
 
@@ -78,6 +78,8 @@ SIGNATURES = {
                                    c_void_p]),
     "icap_decode_sample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
+    "icap_decode_beam": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                 c_void_p, c_void_p]),
     "icap_decoder_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                      c_void_p]),
     "icap_set_graphs": (c_int, [c_void_p, c_int]),

@@ -12,11 +12,11 @@
 // dec_self_attn: one decode step's causal self-attention over an fp32 KV cache (t <= max_len
 //   keys, one wave per (image, head), exact fp32 VALU math).
 //
-// cross_attn_absorbed: decoder cross-attention with the key projection absorbed into the query,
+// cross_attn_mfma: decoder cross-attention with the key projection absorbed into the query,
 //   score_h(s) = (q_h · Wk_h) · mem_s / sqrt(hd) (the q·bk term is constant over s and cancels
 //   in the softmax), context c_h = sum_s p_h(s) mem_s; the caller applies Wv_h and bv (sum p = 1).
-//   Memory (B,S,512) fp32 is read directly - it stays resident in the 256 MiB Infinity Cache
-//   across the 6 layers x 29 steps instead of 6 per-layer K/V projections.
+//   The memory is read once per layer-step (as bf16 hi/lo planes) instead of 6 per-layer K/V
+//   projections.
 #include "common.h"
 #include "kernels.h"
 
@@ -183,9 +183,12 @@ __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __
 
 // ---------------------------------------------------------------------------------------------
 // qkv rows: (b * n_new + i) with [q | k | v] of width 3D.  Cache kc/vc: [B][H][Lmax][64] fp32.
+// anc (optional, beam search): anc[b * Lmax + j] = the cache row holding this row's key/value of
+// position j < t0 (its ancestor at step j); without it the row's own cache is read.
 __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restrict__ qkv, int n_new, int t0,
                                                            int H, float* kc, float* vc, int Lmax, int causal,
-                                                           float scale, bf16_t* out, long lo, int nsplit) {
+                                                           float scale, bf16_t* out, long lo, int nsplit,
+                                                           const int32_t* __restrict__ anc) {
   __shared__ float sq[64];
   __shared__ float sp[512];
   const int h = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
@@ -209,7 +212,10 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restri
       const int key = k0 + lane;
       float sc = -INFINITY;
       if (key < nkeys) {
-        const float* kv = key < t0 ? kcb + (long)key * 64 : rows + (key - t0) * ld + D + h * 64;
+        const float* kv;
+        if (key >= t0) kv = rows + (key - t0) * ld + D + h * 64;
+        else if (anc) kv = kc + ((long)anc[(long)b * Lmax + key] * H + h) * Lmax * 64 + (long)key * 64;
+        else kv = kcb + (long)key * 64;
         float acc = 0.f;
 #pragma unroll 16
         for (int d = 0; d < 64; ++d) acc = fmaf(sq[d], kv[d], acc);
@@ -232,102 +238,13 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restri
     __syncthreads();
     float acc = 0.f;
     for (int key = 0; key < nkeys; ++key) {
-      const float* vv = key < t0 ? vcb + (long)key * 64 : rows + (key - t0) * ld + 2 * D + h * 64;
+      const float* vv;
+      if (key >= t0) vv = rows + (key - t0) * ld + 2 * D + h * 64;
+      else if (anc) vv = vc + ((long)anc[(long)b * Lmax + key] * H + h) * Lmax * 64 + (long)key * 64;
+      else vv = vcb + (long)key * 64;
       acc = fmaf(sp[key], vv[lane], acc);
     }
     st_planes(out, ((long)b * n_new + i) * D + h * 64 + lane, lo, nsplit, acc / l);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// One workgroup (512 threads) per query row r; image = r / rows_per_image.
-// qt: [rows][H*Dm] fp32, mem: [images][S][Dm] fp32, out planes: [rows][H*Dm].
-constexpr int XH = 8;  // heads (d_model 512 / 64)
-__global__ __launch_bounds__(512) void cross_attn_absorbed_kernel(const float* __restrict__ qt,
-                                                                  const float* __restrict__ mem, int rows_per_image,
-                                                                  int S, int Dm, float scale, bf16_t* out, long lo,
-                                                                  int nsplit) {
-  extern __shared__ __attribute__((aligned(16))) float xs[];
-  float* sq = xs;                 // [Dm][XH]
-  float* sp = xs + Dm * XH;       // [256][XH] scores / probs
-  float* part = sp + 256 * XH;    // [256][XH] partial sums of the second d-half
-  const int r = blockIdx.x, tid = threadIdx.x;
-  const float* qrow = qt + (long)r * XH * Dm;
-  const float* mb = mem + (long)(r / rows_per_image) * S * Dm;
-  for (int i = tid; i < XH * Dm; i += 512) {
-    const int h = i / Dm, d = i % Dm;
-    sq[d * XH + h] = qrow[i];
-  }
-  __syncthreads();
-  // scores: thread (s, half) dots over half of d
-  {
-    const int s = tid & 255, half = tid >> 8;
-    float acc[XH];
-#pragma unroll
-    for (int h = 0; h < XH; ++h) acc[h] = 0.f;
-    if (s < S) {
-      const float* mr = mb + (long)s * Dm;
-      const int d0 = half * (Dm / 2), d1 = d0 + Dm / 2;
-      for (int d = d0; d < d1; d += 4) {
-        const f32x4 mv = *(const f32x4*)(mr + d);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const f32x4 qa = *(const f32x4*)(sq + (d + k) * XH);
-          const f32x4 qb = *(const f32x4*)(sq + (d + k) * XH + 4);
-          acc[0] = fmaf(qa[0], mv[k], acc[0]); acc[1] = fmaf(qa[1], mv[k], acc[1]);
-          acc[2] = fmaf(qa[2], mv[k], acc[2]); acc[3] = fmaf(qa[3], mv[k], acc[3]);
-          acc[4] = fmaf(qb[0], mv[k], acc[4]); acc[5] = fmaf(qb[1], mv[k], acc[5]);
-          acc[6] = fmaf(qb[2], mv[k], acc[6]); acc[7] = fmaf(qb[3], mv[k], acc[7]);
-        }
-      }
-      float* dst = (half ? part : sp) + s * XH;
-#pragma unroll
-      for (int h = 0; h < XH; ++h) dst[h] = acc[h];
-    }
-  }
-  __syncthreads();
-  // softmax per head: wave w handles head w (8 waves, 8 heads)
-  {
-    const int w = tid >> 6, lane = tid & 63;
-    float v[4];
-    float m = -INFINITY;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int s = c * 64 + lane;
-      v[c] = s < S ? (sp[s * XH + w] + part[s * XH + w]) * scale : -INFINITY;
-      m = fmaxf(m, v[c]);
-    }
-    m = wave_max(m);
-    float l = 0.f;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      v[c] = (c * 64 + lane) < S ? __expf(v[c] - m) : 0.f;
-      l += v[c];
-    }
-    l = wave_sum(l);
-    const float inv = 1.f / l;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int s = c * 64 + lane;
-      if (s < S) sp[s * XH + w] = v[c] * inv;
-    }
-  }
-  __syncthreads();
-  // context: thread owns column d, all heads
-  for (int d = tid; d < Dm; d += 512) {
-    float acc[XH];
-#pragma unroll
-    for (int h = 0; h < XH; ++h) acc[h] = 0.f;
-    for (int s = 0; s < S; ++s) {
-      const float mv = mb[(long)s * Dm + d];
-      const f32x4 pa = *(const f32x4*)(sp + s * XH), pb = *(const f32x4*)(sp + s * XH + 4);
-      acc[0] = fmaf(pa[0], mv, acc[0]); acc[1] = fmaf(pa[1], mv, acc[1]);
-      acc[2] = fmaf(pa[2], mv, acc[2]); acc[3] = fmaf(pa[3], mv, acc[3]);
-      acc[4] = fmaf(pb[0], mv, acc[4]); acc[5] = fmaf(pb[1], mv, acc[5]);
-      acc[6] = fmaf(pb[2], mv, acc[6]); acc[7] = fmaf(pb[3], mv, acc[7]);
-    }
-#pragma unroll
-    for (int h = 0; h < XH; ++h) st_planes(out, (long)r * XH * Dm + h * Dm + d, lo, nsplit, acc[h]);
   }
 }
 
@@ -366,21 +283,14 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
 }
 
 hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int H, float* kc, float* vc, int Lmax,
-                                int causal, float scale, bf16_t* out, long lo, int nsplit, hipStream_t s) {
-  if (t0 + n_new > Lmax || t0 + n_new > 512) return hipErrorInvalidValue;
+                                int causal, float scale, bf16_t* out, long lo, int nsplit, hipStream_t s,
+                                const int32_t* anc) {
+  if (t0 + n_new > Lmax || t0 + n_new > 512 || (anc && n_new != 1)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(dec_self_attn_kernel, dim3(H, B), dim3(64), 0, s, qkv, n_new, t0, H, kc, vc, Lmax, causal,
-                     scale, out, lo, nsplit);
+                     scale, out, lo, nsplit, anc);
   return hipGetLastError();
 }
 
-hipError_t launch_cross_attn_absorbed(const float* qt, const float* mem, int rows, int rows_per_image, int S, int H,
-                                      int Dm, float scale, bf16_t* out, long lo, int nsplit, hipStream_t s) {
-  if (H != XH || S > 256 || Dm % 8) return hipErrorInvalidValue;
-  const int lds = (Dm * XH + 2 * 256 * XH) * 4;
-  hipLaunchKernelGGL(cross_attn_absorbed_kernel, dim3(rows), dim3(512), lds, s, qt, mem, rows_per_image, S, Dm,
-                     scale, out, lo, nsplit);
-  return hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------------------------
 // Cross-attention, key-absorbed form on MFMA (flash-style over 32-key chunks).

@@ -166,7 +166,7 @@ struct icap_handle {
 
   // workspaces
   DevBuf e_x, e_a, e_qkv, e_h, e_patch;  // encoder
-  DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin, d_part, d_memp;  // decoder
+  DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin, d_part, d_memp, d_beam;  // decoder
 
   ~icap_handle() {
     for (DecodeGraph& g : dg) {
@@ -176,7 +176,7 @@ struct icap_handle {
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_x, &d_a, &d_qkv, &d_q, &d_qt, &d_c, &d_o, &d_h, &d_memp,
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_x, &d_a, &d_qkv, &d_q, &d_qt, &d_c, &d_o, &d_h, &d_memp, &d_beam,
                       &d_kv, &d_fin, &d_part})
       b->release();
   }
@@ -411,7 +411,9 @@ struct DecodeBufs {
   long aL, qL, cL, hL, memL;
 };
 
-DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S) {
+// rows: decoder rows per pass; B: memory images; kv_rows: KV-cache rows (default B; B*K for beams)
+DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_rows = 0) {
+  if (kv_rows <= 0) kv_rows = B;
   const icap_model_desc& d = h->d;
   const int D = d.d_model, ns = h->ns, H = d.nhead;
   h->d_x.ensure((size_t)rows * D * 4);
@@ -423,7 +425,7 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S) {
   h->d_c.ensure((size_t)rows * H * D * 2 * ns);
   h->d_o.ensure((size_t)rows * D * 2 * ns);
   h->d_h.ensure((size_t)rows * d.dim_ff * 2 * ns);
-  h->d_kv.ensure((size_t)2 * d.n_dec_layers * B * H * Lmax * 64 * 4);
+  h->d_kv.ensure((size_t)2 * d.n_dec_layers * kv_rows * H * Lmax * 64 * 4);
   h->d_part.ensure((size_t)MAX_KSPLIT * rows * D * 4);
   DecodeBufs b;
   b.x = h->d_x.as<float>(); b.a = h->d_a.as<bf16_t>(); b.qkv = h->d_qkv.as<float>();
@@ -431,7 +433,7 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S) {
   b.o = h->d_o.as<bf16_t>(); b.hb = h->d_h.as<bf16_t>();
   b.kc = h->d_kv.as<float>();
   b.part = h->d_part.as<float>();
-  b.vc = b.kc + (size_t)d.n_dec_layers * B * H * Lmax * 64;
+  b.vc = b.kc + (size_t)d.n_dec_layers * kv_rows * H * Lmax * 64;
   b.memp = h->d_memp.as<bf16_t>(); b.memL = (long)B * S * D;
   b.aL = (long)rows * D; b.qL = (long)rows * D; b.cL = (long)rows * H * D; b.hL = (long)rows * d.dim_ff;
   return b;
@@ -442,10 +444,13 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S) {
 //   x = LN1(x + SA(x)); x = LN2(x + CA(x, mem)); x = LN3(x + W2 relu(W1 x)).
 // GEMMs are wave-tile decode GEMMs; the three N=512 residual GEMMs split K into fp32 partial
 // slabs that the residual-LayerNorm kernel reduces together with bias + residual.
+// B here counts KV rows (sequences); mem_rpi = decoder rows per memory image (default n_new; the
+// beam slots of an image for beam search); anc = beam ancestry table for the self-attention.
 void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int Lmax, int causal,
-                    int S, hipStream_t s) {
+                    int S, hipStream_t s, const int32_t* anc = nullptr, int mem_rpi = 0) {
   const icap_model_desc& d = h->d;
   const int D = d.d_model, H = d.nhead, F = d.dim_ff, rows = B * n_new, ns = h->ns;
+  if (mem_rpi <= 0) mem_rpi = n_new;
   const size_t kv_layer = (size_t)B * H * Lmax * 64;
   const long PS = (long)rows * D;  // partial slab stride
   const int KS_D = 4, KS_F = 8;    // split-K of the K=512 and K=dim_ff residual GEMMs
@@ -455,7 +460,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
     h->wgemm(b.a, D, b.aL, L.sa_qkv.w, D, L.sa_qkv.b, rows, 3 * D, D, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, WAVE_2x2,
              1, 0, s);
     HIPCHK(launch_dec_self_attn(b.qkv, B, n_new, t0, H, b.kc + l * kv_layer, b.vc + l * kv_layer, Lmax, causal,
-                                0.125f, b.o, b.aL, ns, s));
+                                0.125f, b.o, b.aL, ns, s, anc));
     h->wgemm(b.o, D, b.aL, L.sa_out.w, D, nullptr, rows, D, D, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_D,
              PS, s);
     HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_D, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
@@ -472,7 +477,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       h->chain(c, s);
     }
     h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * ns * (double)(rows / n_new) * S * D, s, [&] {
-      HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, n_new, S, 0.125f, b.c, b.cL, ns, s));
+      HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, mem_rpi, S, 0.125f, b.c, b.cL, ns, s));
     });
     // per head, one launch: o_h = c_h Wv_h^T + bv_h, then slab h = o_h Wo[:, h*64:(h+1)*64]^T; the
     // residual LN sums the H slabs (the output projection as a split-K over heads)
@@ -593,6 +598,58 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
   if (mode) HIPCHK(hipMemcpyAsync(logp, g.lp.p, (size_t)B * (max_len - 1) * 4, hipMemcpyDeviceToDevice, s));
 }
 
+// Batched beam search (models/vit_transformer_model.py:327-420, grid:253-322): B images x K beam
+// slots as B*K decoder rows; per step the rows' logits go to beam_select (beam.hip), which keeps
+// the per-image state (live beam count, scores, token histories, ancestry of the KV rows, the best
+// completed sequence).  Images that stopped keep being decoded (their rows are ignored) so every
+// launch has a fixed shape.
+void decode_beam(icap_handle* h, const float* mem, int B, int S, int max_len, int K, int grid_variant, int start,
+                 int end, int32_t* ids, int32_t* lens, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  REQUIRE(B > 0 && max_len >= 2 && K >= 1 && K <= 15, "bad batch / max_len / beam size (1..15)");
+  REQUIRE(max_len <= d.pe_len, "max_len exceeds the positional-encoding table (PositionalEncoding max_len)");
+  REQUIRE(S > 0 && S <= 256, "memory length must be in [1, 256]");
+  const int D = d.d_model, rows = B * K, V = d.vocab;
+  DecodeBufs b = dec_bufs(h, rows, B, max_len, S, rows);
+  // beam state, carved from one buffer: seq[2] + anc[2] (rows x L ints), best_seq (B x L),
+  // scores[2] (rows), kcur / done / ncomp / best_len (B ints), best_score (B), logits (rows x V)
+  const size_t RL = (size_t)rows * max_len, BL = (size_t)B * max_len;
+  const size_t n_i = 4 * RL + BL + 4 * (size_t)B, n_f = 2 * (size_t)rows + B + (size_t)rows * V;
+  h->d_beam.ensure((n_i + n_f) * 4 + 64);
+  int32_t* base = h->d_beam.as<int32_t>();
+  int32_t* seq[2] = {base, base + RL};
+  int32_t* anc[2] = {base + 2 * RL, base + 3 * RL};
+  int32_t* best_seq = base + 4 * RL;
+  int* kcur = base + 4 * RL + BL;
+  int* done = kcur + B;
+  int* ncomp = done + B;
+  int* best_len = ncomp + B;
+  float* fb = (float*)(best_len + B);
+  float* sc[2] = {fb, fb + rows};
+  float* best_score = fb + 2 * rows;
+  float* logits = best_score + B;
+  HIPCHK(launch_split_f32(mem, b.memL, b.memp, b.memL, h->ns, s));
+  HIPCHK(launch_beam_init(B, K, start, max_len, seq[0], seq[1], anc[0], anc[1], sc[0], kcur, done, ncomp, best_score,
+                          best_len, s));
+  const float scale = (float)std::sqrt((double)D);
+  int cur = 0;
+  for (int t = 0; t + 1 < max_len; ++t) {
+    HIPCHK(launch_embed(seq[cur] + t, max_len, 0, rows, 1, t, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
+    decoder_layers(h, b, rows, 1, t, max_len, 1, S, s, t > 0 ? anc[cur] : nullptr, K);
+    HeadArgs ha{};
+    ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = V;
+    ha.logits = logits; ha.ld_logits = V;
+    h->d_fin.ensure((size_t)rows * 4);  // scratch argmax ids
+    ha.ids = h->d_fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
+    HIPCHK(launch_head(ha, s));
+    HIPCHK(launch_beam_select(logits, V, B, K, t, max_len, grid_variant, end, seq[cur], seq[cur ^ 1], anc[cur],
+                              anc[cur ^ 1], sc[cur], sc[cur ^ 1], kcur, done, ncomp, best_score, best_seq, best_len,
+                              s));
+    cur ^= 1;
+  }
+  HIPCHK(launch_beam_finalize(B, K, max_len, seq[cur], sc[cur], kcur, ncomp, best_seq, best_len, ids, lens, s));
+}
+
 }  // namespace
 
 // ================================================================================== C ABI
@@ -662,6 +719,15 @@ int icap_decode_sample(icap_handle* h, const float* memory, int B, int S, int ma
   return guarded([&] {
     REQUIRE(h && memory && ids && uniforms && logp, "bad arguments");
     decode_loop(h, memory, B, S, max_len, start_token, end_token, ids, nullptr, uniforms, logp,
+                (hipStream_t)stream);
+  });
+}
+
+int icap_decode_beam(icap_handle* h, const float* memory, int B, int S, int max_len, int beam_size, int grid_variant,
+                     int start_token, int end_token, int32_t* ids, int32_t* lengths, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && memory && ids && lengths, "bad arguments");
+    decode_beam(h, memory, B, S, max_len, beam_size, grid_variant != 0, start_token, end_token, ids, lengths,
                 (hipStream_t)stream);
   });
 }

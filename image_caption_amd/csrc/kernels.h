@@ -96,15 +96,23 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
 // Decoder self-attention with fp32 KV cache; n_new query rows per image starting at t0.
 hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int H, float* kc, float* vc,
                                 int Lmax, int causal, float scale, bf16_t* out, long lo, int nsplit,
-                                hipStream_t s);
-// Cross-attention in the key-absorbed form: qt rows hold q_h·Wk_h (H × Dm); mem (images,S,Dm) fp32.
-hipError_t launch_cross_attn_absorbed(const float* qt, const float* mem, int rows, int rows_per_image,
-                                      int S, int H, int Dm, float scale, bf16_t* out, long lo, int nsplit,
-                                      hipStream_t s);
-// Same contract on MFMA: q~ and memory as bf16 planes (plane strides qt_lo / mem_lo), H = 8, Dm = 512.
+                                hipStream_t s, const int32_t* anc = nullptr);
+// Cross-attention in the key-absorbed form on MFMA: rows hold q~_h = q_h·Wk_h (8 heads x 512) as bf16
+// planes (plane stride qt_lo); memory (images, S, 512) as bf16 planes (mem_lo); context planes out.
 hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* mem, long mem_lo, int rows,
                                   int rows_per_image, int S, float scale, bf16_t* out, long out_lo, int nsplit,
                                   hipStream_t s);
+// Batched beam search (beam.hip): state init, per-step selection, final pick.
+hipError_t launch_beam_init(int B, int K, int start, int Lmax, int32_t* seq_a, int32_t* seq_b, int32_t* anc_a,
+                            int32_t* anc_b, float* scores, int* kcur, int* done, int* ncomp, float* best_score,
+                            int* best_len, hipStream_t s);
+hipError_t launch_beam_select(const float* logits, int V, int B, int K, int t, int Lmax, int grid_variant, int end_tok,
+                              const int32_t* seq_c, int32_t* seq_n, const int32_t* anc_c, int32_t* anc_n,
+                              const float* sc_c, float* sc_n, int* kcur, int* done, int* ncomp, float* best_score,
+                              int32_t* best_seq, int* best_len, hipStream_t s);
+hipError_t launch_beam_finalize(int B, int K, int Lmax, const int32_t* seq, const float* scores, const int* kcur,
+                                const int* ncomp, const int32_t* best_seq, const int* best_len, int32_t* ids,
+                                int32_t* lens, hipStream_t s);
 // fc_out + argmax (greedy) or inverse-CDF sample; writes ids[r*ld_ids + col], optional logits, and
 // (if emb != null) the next step's embedded token into x/a.
 struct HeadArgs {

@@ -200,6 +200,18 @@ class Engine:
               "icap_decode_sample")
         return ids, logp
 
+    def beam(self, memory: torch.Tensor, start: int, end: int, max_len: int, beam_size: int,
+             grid_variant: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Beam search for every image at once: ids (B,max_len) int32 zero-padded, lengths (B) int32."""
+        mem = memory.to(device=self.device, dtype=torch.float32).contiguous()
+        B, S = mem.shape[0], mem.shape[1]
+        ids = torch.empty(B, max_len, device=self.device, dtype=torch.int32)
+        lens = torch.empty(B, device=self.device, dtype=torch.int32)
+        check(self.lib.icap_decode_beam(self.handle, mem.data_ptr(), B, S, max_len, int(beam_size),
+                                        int(bool(grid_variant)), int(start), int(end), ids.data_ptr(),
+                                        lens.data_ptr(), stream_ptr(self.device)), "icap_decode_beam")
+        return ids, lens
+
     def decoder_forward(self, tgt: torch.Tensor, memory: torch.Tensor, causal: bool) -> torch.Tensor:
         t = tgt.to(device=self.device, dtype=torch.int32).contiguous()
         mem = memory.to(device=self.device, dtype=torch.float32).contiguous()

@@ -97,6 +97,16 @@ int icap_encode_grid_tail(icap_handle* h, const float* feats, int B, float* memo
 int icap_decode_greedy(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
                        int end_token, int32_t* ids, float* step_logits, void* stream);
 
+/* Batched beam search, beam_size K in [1, 15]: every image runs the reference's per-image beam
+ * search (log-softmax scores, top-K over beam x vocab, finished beams collected and pruned so the
+ * live beam count shrinks); grid_variant != 0 selects the Grid model's stop tests (completed >= live
+ * beams, or no live beam) instead of the ViT's (every live beam ended).  ids (B,max_len) int32 =
+ * the chosen sequence (start token first) zero-padded, lengths (B) int32 its token count.
+ * Replaces: _beam_search, models/vit_transformer_model.py:327-420 (grid:253-322), run for all
+ * images at once as B*K rows of the KV-cached decoder. */
+int icap_decode_beam(icap_handle* h, const float* memory, int B, int S, int max_len, int beam_size, int grid_variant,
+                     int start_token, int end_token, int32_t* ids, int32_t* lengths, void* stream);
+
 /* Sampled decode with injected uniforms (max_len-1,B) in [0,1): ids (B,max_len) int32 and
  * log-probs (B,max_len-1) fp32, zeroed after a sample has emitted end (masked_fill semantics).
  * Replaces: SCSTLoss._sample_with_log_probs, utils/scst_loss.py:202-254 (torch.multinomial ->

@@ -91,6 +91,15 @@ def beam_search(model, images, start_token, end_token, max_len, beam_size, grid_
     """`_beam_search` (vit:327-420 / grid:253-322): one image at a time, log-softmax scores,
     pruning of finished beams (the live beam count shrinks).  The two reference variants differ
     in their stop tests, selected by `grid_variant`."""
+    if getattr(model, "use_hip", None) is not None and not model.training and model.use_hip(images):
+        # every image at once on the GPU (icap_decode_beam: B*K rows of the KV-cached decoder), then
+        # the reference's per-image results concatenated as it does (vit:335-341)
+        with torch.no_grad():
+            memory = model.encoder(images)
+            ids, lens = model.hip_engine(images.device).beam(memory, start_token, end_token, max_len, beam_size,
+                                                             grid_variant)
+        ids, lens = ids.long(), lens.tolist()
+        return torch.cat([ids[i:i + 1, :lens[i]] for i in range(ids.shape[0])], dim=0)
     if images.size(0) != 1:
         return torch.cat([beam_search(model, images[i:i + 1], start_token, end_token, max_len, beam_size,
                                       grid_variant) for i in range(images.size(0))], dim=0)

@@ -233,6 +233,53 @@ def inference_py_generate(sd, memory: Tensor, start: int, end: int, max_len: int
     return out_ids
 
 
+def beam_from_memory(sd, memory: Tensor, start: int, end: int, max_len: int, beam_size: int,
+                     grid_variant: bool = False, return_margins: bool = False):
+    """`_beam_search` for ONE image (memory (1,S,d)), full-prefix recompute each step:
+    vit:327-420 (stop when every live beam ended) or grid:253-322 (stop when the completed count
+    reaches the live beam count, or no live beam is left).  Returns the chosen sequence (1,L)
+    int64; with return_margins also the smallest gap, over all steps, between the k-th selected
+    candidate score and the best rejected one (how far the selection is from a tie)."""
+    V = sd["decoder.fc_out.weight"].shape[0]
+    with torch.no_grad():
+        mem = memory.expand(beam_size, -1, -1)
+        seqs = torch.full((beam_size, 1), start, dtype=torch.long)
+        scores = torch.zeros(beam_size)
+        done, done_scores = [], []
+        margin = float("inf")
+        for step in range(max_len - 1):
+            if grid_variant and seqs.size(0) == 0:
+                break
+            logp = torch.log_softmax(decoder_forward(sd, seqs, mem, causal=True)[:, -1, :], dim=-1)
+            cand = logp[0] if step == 0 else (scores.unsqueeze(1) + logp).view(-1)
+            top = cand.topk(min(beam_size + 1, cand.numel()))
+            if top.values.numel() > beam_size:
+                margin = min(margin, float(top.values[beam_size - 1] - top.values[beam_size]))
+            top_s, top_i = top.values[:beam_size], top.indices[:beam_size]
+            if step == 0:
+                seqs = torch.cat([seqs[0:1].expand(beam_size, -1), top_i.unsqueeze(1)], dim=1)
+            else:
+                seqs = torch.cat([seqs[top_i // V], (top_i % V).unsqueeze(1)], dim=1)
+            scores = top_s
+            ended = seqs[:, -1] == end
+            if bool(ended.any()):
+                for i in ended.nonzero(as_tuple=True)[0]:
+                    done.append(seqs[i])
+                    done_scores.append(scores[i])
+                if grid_variant:
+                    if len(done) >= beam_size:
+                        break
+                elif bool(ended.all()):
+                    break
+                keep = ~ended
+                seqs, scores, mem = seqs[keep], scores[keep], mem[keep]
+                if grid_variant and seqs.size(0) == 0:
+                    break
+                beam_size = seqs.size(0)
+        out = (done[int(torch.tensor(done_scores).argmax())] if done else seqs[scores.argmax()]).unsqueeze(0)
+    return (out, margin) if return_margins else out
+
+
 def inverse_cdf_sample(logits: Tensor, u: Tensor) -> Tuple[Tensor, Tensor]:
     """Categorical sample from softmax(logits) with injected uniforms u in [0,1):
     first index whose inclusive prefix sum of probabilities exceeds u * total."""

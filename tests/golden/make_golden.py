@@ -19,7 +19,8 @@ What is restated because its module cannot import here:
     around the reference decoder module, with torch.multinomial replaced by inverse-CDF sampling
     on fixed uniforms.
 
-Usage: python tests/golden/make_golden.py   (writes tests/golden/*.npz, ~1 min on 8 cores)
+Usage: python tests/golden/make_golden.py [beam_vit]   (writes tests/golden/*.npz, ~2 min on 8 cores;
+       with beam_vit only the beam-search fixture)
 """
 from __future__ import annotations
 
@@ -38,6 +39,7 @@ sys.path.insert(0, ROOT)
 from image_caption_amd import weights as W  # noqa: E402
 
 REF = "/root/reference"
+END_BIAS = 1.4  # <end> logit offset of the beam-search fixtures (makes beams finish early)
 
 
 def load_ref_vit_module():
@@ -89,11 +91,47 @@ def top2(logits):
     return (t[..., 0] - t[..., 1]).numpy()
 
 
+def make_beam(ref, sd, imgs, out):
+    # (vi) beam search through the reference's OWN ViTTransformerCaptioning._beam_search (vit:327-420),
+    # one image per call as the reference loops: default weights (beam 3, images 0-1, no beam ever
+    # ends) and the same weights with the <end> logit raised by END_BIAS (beam 5, images 0-3: beams
+    # finish, are collected and pruned).  The oracle's selection margin is stored with each case.
+    from oracle import captioner as O
+
+    cases = [(0.0, 3, i) for i in range(2)] + [(END_BIAS, 5, i) for i in range(4)]
+    rows, lens, margins = [], [], []
+    for delta, k, i in cases:
+        sdb = dict(sd)
+        fb = sdb["decoder.fc_out.bias"].clone()
+        fb[W.END_TOKEN] += delta
+        sdb["decoder.fc_out.bias"] = fb
+        mb = ref_vit_model(ref, sdb)
+        with torch.no_grad():
+            seq = mb.generate(imgs[i:i + 1], W.START_TOKEN, W.END_TOKEN, max_len=30, method="beam_search")
+            if k != 5:  # generate() fixes beam_size=5 for the ViT model (vit:292); other widths go direct
+                seq = mb._beam_search(imgs[i:i + 1], W.START_TOKEN, W.END_TOKEN, 30, k)
+            _, margin = O.beam_from_memory(sdb, mb.encoder(imgs[i:i + 1]), W.START_TOKEN, W.END_TOKEN, 30, k,
+                                           False, return_margins=True)
+        row = np.full(30, -1, dtype=np.int64)
+        row[: seq.shape[1]] = seq[0].numpy()
+        rows.append(row)
+        lens.append(seq.shape[1])
+        margins.append(margin)
+    np.savez_compressed(os.path.join(HERE, "beam_vit.npz"), end_bias=np.array([c[0] for c in cases]),
+                        beam=np.array([c[1] for c in cases]), image=np.array([c[2] for c in cases]),
+                        ids=np.stack(rows), lengths=np.array(lens), margins=np.array(margins))
+    out["beam_vit"] = (len(cases),)
+
+
 def main():
     torch.manual_seed(0)
     torch.set_num_threads(os.cpu_count() or 8)
     ref = load_ref_vit_module()
     out = {}
+    if sys.argv[1:] == ["beam_vit"]:  # regenerate only the beam fixture
+        make_beam(ref, W.to_torch(W.vit_state_dict(0)), torch.from_numpy(W.synthetic_images(4, seed=0)), out)
+        print(out)
+        return
 
     # (i)/(ii) ViT config-1: B=4, greedy max_len=30 through the reference generate()
     sd = W.to_torch(W.vit_state_dict(0))
@@ -175,6 +213,7 @@ def main():
                         ids=gids.numpy(), memory_sum=gmem.double().sum(dim=(1, 2)).numpy(),
                         memory_head=gmem[:, :4, :16].numpy(), logits_tf=gtf.numpy(), margins=top2(gtf))
     out["grid_b4"] = gids.shape
+    make_beam(ref, sd, imgs, out)
     for k, v in out.items():
         print(k, tuple(v) if hasattr(v, "__len__") else v)
 

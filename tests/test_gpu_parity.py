@@ -184,3 +184,66 @@ def test_decode_graph_replay_matches_eager(vit_engine, cuda):
     other = vit_engine.encode(imgs[:3])
     a, _ = vit_engine.greedy_raw(other, W.START_TOKEN, W.END_TOKEN, 30)
     assert torch.equal(a, ref_ids[:3])
+
+
+def _biased(sd, delta):
+    out = dict(sd)
+    b = out["decoder.fc_out.bias"].clone()
+    b[W.END_TOKEN] += float(delta)
+    out["decoder.fc_out.bias"] = b
+    return out
+
+
+def test_beam_search_golden_and_batching(cuda, vit_sd):
+    """icap_decode_beam: reference beam-search ids (fixtures of vit:327-420) for every image of the
+    batch at once; exact wherever the reference's selection margin exceeds 1e-4 (bf16x2 logits are
+    within ~3e-5).  Batched rows must equal one-image runs (ancestry / slot bookkeeping)."""
+    from image_caption_amd.engine import Engine
+
+    g = gold("beam_vit.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    for delta, k in sorted({(float(d), int(b)) for d, b in zip(g["end_bias"], g["beam"])}):
+        eng = Engine(_biased(vit_sd, delta), "vit", {}, device=cuda)
+        mem = eng.encode(imgs)
+        ids, lens = eng.beam(mem, W.START_TOKEN, W.END_TOKEN, 30, k)
+        ids, lens = ids.cpu().numpy(), lens.cpu().numpy()
+        for d, kk, i, row, n, mg in zip(g["end_bias"], g["beam"], g["image"], g["ids"], g["lengths"], g["margins"]):
+            if float(d) != delta or int(kk) != k or mg <= 1e-4:
+                continue
+            assert lens[i] == n and np.array_equal(ids[i, :n], row[:n]), (delta, k, i)
+            assert (ids[i, n:] == 0).all()
+        for i in range(4):  # one image alone == its row of the batch
+            one, ln = eng.beam(mem[i:i + 1], W.START_TOKEN, W.END_TOKEN, 30, k)
+            assert int(ln[0]) == lens[i] and np.array_equal(one[0].cpu().numpy(), ids[i])
+
+
+def test_beam_search_grid_variant_vs_oracle(cuda, vit_sd):
+    """Grid stop tests (grid:253-322) on the same decoder: GPU vs the oracle restatement."""
+    from image_caption_amd.engine import Engine
+
+    sd = _biased(vit_sd, 1.6)
+    eng = Engine(sd, "vit", {}, device=cuda)
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=3)).to(cuda)
+    mem = eng.encode(imgs)
+    ids, lens = eng.beam(mem, W.START_TOKEN, W.END_TOKEN, 20, 4, grid_variant=True)
+    for i in range(4):
+        ref, margin = O.beam_from_memory(sd, mem[i:i + 1].cpu(), W.START_TOKEN, W.END_TOKEN, 20, 4, True,
+                                         return_margins=True)
+        if margin > 1e-4:
+            n = ref.shape[1]
+            assert int(lens[i]) == n and np.array_equal(ids[i, :n].cpu().numpy(), ref[0].numpy()), i
+
+
+def test_dropin_beam_search_runs_hip(cuda, vit_sd):
+    from models.vit_transformer_model import build_model
+
+    g = gold("beam_vit.npz")
+    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False})
+    m.load_state_dict(_biased(vit_sd, 1.4))
+    m = m.to(cuda)
+    imgs = torch.from_numpy(W.synthetic_images(1, seed=0)).to(cuda)  # image 0 of the fixtures
+    out = m.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=30, method="beam_search")
+    assert m._hip_cache is not None and out.is_cuda and out.dtype == torch.long
+    sel = [j for j in range(len(g["image"])) if g["image"][j] == 0 and g["beam"][j] == 5][0]
+    n = int(g["lengths"][sel])
+    assert out.shape == (1, n) and np.array_equal(out[0].cpu().numpy(), g["ids"][sel][:n])

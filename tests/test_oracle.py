@@ -161,3 +161,18 @@ def test_generator_is_deterministic_and_bf16_exact():
     assert torch.equal(w, w.to(torch.bfloat16).float())
     x = np.random.Generator(np.random.PCG64(0)).standard_normal(10000).astype(np.float32)
     assert np.array_equal(W.round_to_bf16(x), torch.from_numpy(x).to(torch.bfloat16).float().numpy())
+
+
+def test_beam_search_matches_reference(vit_sd):
+    """oracle.beam_from_memory (restated vit:327-420 loop) vs the reference's own _beam_search."""
+    g = gold("beam_vit.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0))
+    with torch.no_grad():
+        mem = O.vit_encode(vit_sd, imgs)
+    for delta, k, i, row, n in zip(g["end_bias"], g["beam"], g["image"], g["ids"], g["lengths"]):
+        sd = dict(vit_sd)
+        b = sd["decoder.fc_out.bias"].clone()
+        b[W.END_TOKEN] += float(delta)
+        sd["decoder.fc_out.bias"] = b
+        got = O.beam_from_memory(sd, mem[i:i + 1], W.START_TOKEN, W.END_TOKEN, 30, int(k))
+        assert got.shape[1] == n and np.array_equal(got[0].numpy(), row[:n])
