@@ -89,80 +89,101 @@ __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __
 
   for (int qt = wave; qt < nqt; qt += NW) {
     if (qt != wave) load_q(qt);
-    f32x4 s[NKT];
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const int row = kt * 16 + fr;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int off = row * 128 + (((ks * 4 + g) ^ (row & 7)) << 4);
-        const bf16x8 kh = *(const bf16x8*)(Kh + off);
-        acc = mfma16(kh, qh[ks], acc);
-        if (SPLIT) {
-          const bf16x8 kl = *(const bf16x8*)(Kl + off);
-          acc = mfma16(kl, qh[ks], acc);
-          acc = mfma16(kh, ql[ks], acc);
-        }
-      }
-      s[kt] = acc;
-    }
-    // softmax over keys for query (lane & 15): key of s[kt][r] = 16 kt + 4 g + r
-    float m = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kt * 16 + g * 4 + r;
-        const float v = key < N ? s[kt][r] * scale : -INFINITY;
-        s[kt][r] = v;
-        m = fmaxf(m, v);
-      }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    float l = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = __expf(s[kt][r] - m);
-        s[kt][r] = e;
-        l += e;
-      }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = 1.f / l;
-
-    // O^T[d][q] = sum_k V^T[d][k] P^T[k][q]
+    // keys in chunks of CH tiles (an even count: the P.V MFMA takes 32 keys = 2 tiles) with an
+    // online softmax, so only CH score tiles are live (16 waves per block fit in 128 VGPRs)
+    constexpr int CH = 4;
+    float m = -INFINITY, l = 0.f;  // running max / per-lane partial sum for query (lane & 15)
     f32x4 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int q4 = fr >> 2, p4 = fr & 3;
+#pragma unroll 1
+    for (int c0 = 0; c0 < NKT; c0 += CH) {  // rolled: unrolled chunks get interleaved and spill
+      constexpr int CMAX = CH;
+      const int nt = NKT - c0 < CH ? NKT - c0 : CH;
+      f32x4 s[CMAX];
 #pragma unroll
-    for (int i = 0; i < NKT / 2; ++i) {
-      bf16x8 ph, pl;
+      for (int u = 0; u < CMAX; ++u) {
+        if (u >= nt) break;
+        const int kt = c0 + u;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const int row = kt * 16 + fr;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        ph[j] = (__bf16)s[2 * i][j];
-        ph[4 + j] = (__bf16)s[2 * i + 1][j];
-        if (SPLIT) {
-          pl[j] = (__bf16)(s[2 * i][j] - (float)ph[j]);
-          pl[4 + j] = (__bf16)(s[2 * i + 1][j] - (float)ph[4 + j]);
+        for (int ks = 0; ks < 2; ++ks) {
+          const int off = row * 128 + (((ks * 4 + g) ^ (row & 7)) << 4);
+          const bf16x8 kh = *(const bf16x8*)(Kh + off);
+          acc = mfma16(kh, qh[ks], acc);
+          if (SPLIT) {
+            const bf16x8 kl = *(const bf16x8*)(Kl + off);
+            acc = mfma16(kl, qh[ks], acc);
+            acc = mfma16(kh, ql[ks], acc);
+          }
+        }
+        s[u] = acc;
+      }
+      // key of s[u][r] = 16 (c0 + u) + 4 g + r
+      float cm = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < CMAX; ++u) {
+        if (u >= nt) break;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = (c0 + u) * 16 + g * 4 + r;
+          const float v = key < N ? s[u][r] * scale : -INFINITY;
+          s[u][r] = v;
+          cm = fmaxf(cm, v);
         }
       }
-      const int key0 = 32 * i + 4 * g + q4;
+      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      const float m_new = fmaxf(m, cm);
+      if (m_new == -INFINITY) continue;  // every key of this chunk is padding (uniform per query)
+      const float alpha = __expf(m - m_new);
+      m = m_new;
+      l *= alpha;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int off0 = key0 * 128 + (dt * 16 + 4 * p4) * 2, off1 = off0 + 16 * 128;
-        const bf16x8 vh = tr_pair(Vh + off0, Vh + off1);
-        o[dt] = mfma16(vh, ph, o[dt]);
-        if (SPLIT) {
-          const bf16x8 vl = tr_pair(Vl + off0, Vl + off1);
-          o[dt] = mfma16(vl, ph, o[dt]);
-          o[dt] = mfma16(vh, pl, o[dt]);
+      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+#pragma unroll
+      for (int u = 0; u < CMAX; ++u) {
+        if (u >= nt) break;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __expf(s[u][r] - m_new);
+          s[u][r] = e;
+          l += e;
+        }
+      }
+      // O^T[d][q] += sum_k V^T[d][k] P^T[k][q], 32 keys (2 tiles) per MFMA
+#pragma unroll
+      for (int u = 0; u < CMAX; u += 2) {
+        if (u >= nt) break;
+        bf16x8 ph, pl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ph[j] = (__bf16)s[u][j];
+          ph[4 + j] = (__bf16)s[u + 1][j];
+          if (SPLIT) {
+            pl[j] = (__bf16)(s[u][j] - (float)ph[j]);
+            pl[4 + j] = (__bf16)(s[u + 1][j] - (float)ph[4 + j]);
+          }
+        }
+        const int key0 = 16 * (c0 + u) + 4 * g + q4;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int off0 = key0 * 128 + (dt * 16 + 4 * p4) * 2, off1 = off0 + 16 * 128;
+          const bf16x8 vh = tr_pair(Vh + off0, Vh + off1);
+          o[dt] = mfma16(vh, ph, o[dt]);
+          if (SPLIT) {
+            const bf16x8 vl = tr_pair(Vl + off0, Vl + off1);
+            o[dt] = mfma16(vl, ph, o[dt]);
+            o[dt] = mfma16(vh, pl, o[dt]);
+          }
         }
       }
     }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
     const int qq = qt * 16 + fr;
     if (qq < N) {
       bf16_t* dst = out + ((long)b * N + qq) * out_ld + h * 64;
@@ -251,8 +272,9 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restri
 template <int NKT, bool SPLIT>
 hipError_t run_enc(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale, bf16_t* out,
                    long out_ld, long out_lo, hipStream_t s) {
-  // 4 waves: the split-precision score tile needs > 256 VGPRs (8 waves per block spill)
-  constexpr int NW = 4;
+  // one wave per 16-query tile (ViT: 13 of 16 busy; grid: 4); the chunked softmax keeps the
+  // score tiles to 4, which fits 128 VGPRs
+  constexpr int NW = NKT > 4 ? 16 : 4;
   const int lds = NKT * 16 * 128 * (SPLIT ? 4 : 2);
   static bool attr = false;
   if (!attr) {

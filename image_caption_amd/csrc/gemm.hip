@@ -715,6 +715,20 @@ __global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
   auto stage = [&](int kt, int buf) {
     const int kin = kt * KS;
     char* s0 = smem + buf * STAGE;
+    if (NOMFMA == 3) {  // measurement: same bytes per stage as full 128-B lines (A as [M][2K], W as row pairs)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (wave * 2 + i) * 8 + (lane >> 3);
+        const bf16_t* src = p.A + (long)min(m0 + row, M - 1) * 2 * p.lda + kt * 64 + (lane & 7) * 8;
+        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)(s0 + (wave * 2 + i) * 1024), 16,
+                                         0, 0);
+      }
+      const int pair = wave * 8 + (lane >> 3);
+      const bf16_t* wsrc = p.W + (long)((n0 >> 1) + pair) * 2 * p.ldw + kt * 64 + (lane & 7) * 8;
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)wsrc, (LDS_AS void*)(s0 + 2 * OPB + wave * 1024), 16,
+                                       0, 0);
+      return;
+    }
 #pragma unroll
     for (int pl = 0; pl < NS; ++pl) {
       const bf16_t* Ab = a_base + pl * p.a_lo + kin;
@@ -753,7 +767,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
     // refill the buffer read in iteration kt-1 (every wave has passed this barrier)
     if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
     const char* s0 = smem + (kt % NSTAGE) * STAGE;
-    if (NOMFMA == 2) continue;
+    if (NOMFMA >= 2) continue;
     bf16x8 bfr[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + NS * OPB + (wn * WN + j * 16) * 64 + foff);
@@ -935,13 +949,14 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
   if (!nw) {
     const char* v = getenv("ICAP_GEMM256_WAVES");  // experiment knob: 8, 16, or 0 = 8-phase kernel
     nw = v ? atoi(v) : 16;
-    if (nw != 8 && nw != 16 && nw != 1 && nw != 2 && nw != 160 && nw != 161) nw = 16;
+    if (nw != 8 && nw != 16 && nw != 1 && nw != 2 && nw != 160 && nw != 161 && nw != 162) nw = 16;
     for (const void* f : {(const void*)gemm_8ph_kernel<false>, (const void*)gemm_8ph_kernel<true>})
       if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 131072) != hipSuccess)
         return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     for (const void* f : {(const void*)gemm_256_kernel<2, 8>, (const void*)gemm_256_kernel<2, 16>,
-                          (const void*)gemm_256_kernel<2, 16, 1>, (const void*)gemm_256_kernel<2, 16, 2>})
+                          (const void*)gemm_256_kernel<2, 16, 1>, (const void*)gemm_256_kernel<2, 16, 2>,
+                          (const void*)gemm_256_kernel<2, 16, 3>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
     for (const void* f : {(const void*)gemm_256_kernel<1, 8>, (const void*)gemm_256_kernel<1, 16>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
@@ -954,9 +969,10 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
     else hipLaunchKernelGGL(gemm_8ph_kernel<false>, dim3(nwg), dim3(512), 131072, s, g);
     return hipGetLastError();
   }
-  if ((nw == 160 || nw == 161) && g.nsplit == 2) {
+  if ((nw == 160 || nw == 161 || nw == 162) && g.nsplit == 2) {
     if (nw == 160) hipLaunchKernelGGL((gemm_256_kernel<2, 16, 1>), dim3(nwg), dim3(1024), lds2, s, g2);
-    else hipLaunchKernelGGL((gemm_256_kernel<2, 16, 2>), dim3(nwg), dim3(1024), lds2, s, g2);
+    else if (nw == 161) hipLaunchKernelGGL((gemm_256_kernel<2, 16, 2>), dim3(nwg), dim3(1024), lds2, s, g2);
+    else hipLaunchKernelGGL((gemm_256_kernel<2, 16, 3>), dim3(nwg), dim3(1024), lds2, s, g2);
     return hipGetLastError();
   }
   if (g.nsplit == 2) {

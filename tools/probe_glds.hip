@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <algorithm>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -68,24 +69,24 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  printf("%-8s %-5s %-9s %-6s %-6s %10s %12s\n", "src", "waves", "inflight", "grid", "blocks/CU", "us", "GB/s/CU");
+  printf("%-8s %-5s %-5s %-9s %-6s %10s %12s\n", "srcKB", "mode", "waves", "inflight", "grid", "us", "GB/s/CU");
   const int blk = 1024 * 1024;
   for (long sb : {4L << 20, 64L << 20})
-    for (int nwv : {4, 16})
-      for (int infl : {32768, 65536})
-        for (int grid : {256, 512, 1024}) {
-          if (nwv == 16 && grid > 512) continue;
-          const int lds = infl;
-          for (int rep = 0; rep < 2; ++rep) {
-            CK(hipEventRecord(a));
-            hipLaunchKernelGGL(ingest, dim3(grid), dim3(nwv * 64), lds, 0, src, sb, blk, infl, 1, sink);
-            CK(hipEventRecord(b));
-            CK(hipEventSynchronize(b));
+    for (int mode : {0, 1, 2})
+      for (int nwv : {16})
+        for (int infl : {65536})
+          for (int grid : {32, 256, 512}) {
+            const int lds = infl;
+            for (int rep = 0; rep < 2; ++rep) {
+              CK(hipEventRecord(a));
+              hipLaunchKernelGGL(ingest, dim3(grid), dim3(nwv * 64), lds, 0, src, sb, blk, infl, mode, sink);
+              CK(hipEventRecord(b));
+              CK(hipEventSynchronize(b));
+            }
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            const double per_cu = (double)grid * blk / std::min(grid, 256) / (ms * 1e-3) / 1e9;
+            printf("%-8ld %-5d %-5d %-9d %-6d %10.2f %12.1f\n", sb >> 10, mode, nwv, infl, grid, ms * 1e3, per_cu);
           }
-          float ms;
-          CK(hipEventElapsedTime(&ms, a, b));
-          const double per_cu = (double)grid * blk / 256 / (ms * 1e-3) / 1e9;
-          printf("%-8ld %-5d %-9d %-6d %-6d %10.2f %12.1f\n", sb >> 10, nwv, infl, grid, grid / 256, ms * 1e3, per_cu);
-        }
   return 0;
 }
