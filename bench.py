@@ -12,8 +12,8 @@ with HIP events around each of its launches inside the timed region; its `traffi
 bytes per launch of that kernel from the committed rocprofv3 PMC summary (tools/pmc_bench.sh:
 FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction) when one exists for it; `cpu_baseline` times
 the CPU oracle (fp32 restatement of the reference algorithm, full-prefix recompute) on the host.
-`--model grid` measures config 3 (ResNet-101 trunk through PyTorch/MIOpen fp32 as in the drop-in
-model, then the HIP encoder tail and decode loop); `--mode scst` measures config 5's reward step
+`--model grid` measures config 3 (ResNet-101 trunk as HIP MFMA GEMMs over NHWC planes, then the
+HIP encoder tail and decode loop; `--torch-trunk` runs the trunk through PyTorch/MIOpen fp32 instead); `--mode scst` measures config 5's reward step
 (encode once, HIP sample on injected uniforms + HIP greedy baseline from the same memory, all-gather
 of both id sets, CIDEr-D over the GLOBAL batch on rank 0); `--mode beam`
 measures the batched beam search (§8(f)1: encode + icap_decode_beam, every image at once).  None of
@@ -94,6 +94,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graphs", action="store_true", help="launch the decode loop eagerly (no hipGraph)")
     ap.add_argument("--model", default="vit", choices=["vit", "grid"])
+    ap.add_argument("--torch-trunk", action="store_true", help="grid: ResNet trunk via PyTorch/MIOpen fp32")
     ap.add_argument("--mode", default="greedy", choices=["greedy", "scst", "beam"])
     ap.add_argument("--beam", type=int, default=5, help="beam width of --mode beam")
     args = ap.parse_args()
@@ -107,7 +108,7 @@ def main():
     sd = W.to_torch(W.vit_state_dict(0) if args.model == "vit" else W.grid_state_dict(0))
     eng = Engine(sd, args.model, {}, precision=args.precision, device=dev)
     trunk = None
-    if args.model == "grid":
+    if args.model == "grid" and args.torch_trunk:
         from models.grid_transformer_model import GridFeatureEncoder
 
         genc = GridFeatureEncoder(pretrained_cnn=False)
@@ -220,8 +221,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic images N(0,1) + seeded random-init weights",
             "config": {"workload": ("vit_b16 encoder + 6-layer decoder, greedy, 224x224, max_len=30" if args.model == "vit"
-                                    else "grid resnet101 (torch/MIOpen fp32) + 6-layer encoder + 6-layer decoder, "
-                                         "greedy, 224x224, max_len=30")
+                                    else f"grid resnet101 ({'torch/MIOpen fp32' if args.torch_trunk else 'HIP'}) "
+                                         "+ 6-layer encoder + 6-layer decoder, greedy, 224x224, max_len=30")
                        + {"greedy": "", "scst": "; SCST reward step: sample + greedy + CIDEr-D (global batch)",
                           "beam": f"; beam search, beam {args.beam}"}[args.mode],
                        "per_gpu_batch": B, "global_batch": total, "max_len": L, "precision": args.precision,

@@ -13,7 +13,7 @@ from pathlib import Path
 import torch  # noqa: F401  (load torch's HIP runtime before libicap)
 
 LIB_PATH = Path(__file__).resolve().parent / "libicap.so"
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 KIND_VIT, KIND_GRID = 0, 1
 PREC_BF16, PREC_BF16X2 = 1, 2
@@ -47,6 +47,11 @@ class DecLayerW(ctypes.Structure):
                 ("lin2_w", c_void_p), ("lin2_b", c_void_p), ("norm1", LnW), ("norm2", LnW), ("norm3", LnW)]
 
 
+class ConvBnW(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("bn_w", c_void_p), ("bn_b", c_void_p), ("bn_mean", c_void_p),
+                ("bn_var", c_void_p), ("cout", c_int), ("cin", c_int), ("k", c_int), ("stride", c_int)]
+
+
 class ModelDesc(ctypes.Structure):
     _fields_ = [
         ("kind", c_int), ("precision", c_int),
@@ -63,6 +68,8 @@ class ModelDesc(ctypes.Structure):
         ("cnn_dim", c_int), ("grid_tokens", c_int), ("n_enc_layers", c_int),
         ("enc_pe", c_void_p),
         ("enc_layers", POINTER(EncLayerW)),
+        ("n_trunk", c_int), ("trunk_blocks", c_int * 4),
+        ("trunk", POINTER(ConvBnW)),
     ]
 
 
@@ -74,6 +81,7 @@ SIGNATURES = {
     "icap_destroy": (c_int, [c_void_p]),
     "icap_encode_vit": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "icap_encode_grid_tail": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "icap_encode_grid": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "icap_decode_greedy": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_void_p]),
     "icap_decode_sample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,

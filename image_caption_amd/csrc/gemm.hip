@@ -111,14 +111,19 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn * WN + j * 16 + fr;
     const float bv = bias ? bias[col] : 0.f;
+    const float sv = p.scale ? p.scale[col] : 1.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm * WM + i * 16 + fq * 4 + r;
         if (row >= M) continue;
-        float v = acc[i][j][r] + bv;
+        float v = acc[i][j][r] * sv + bv;
         if (p.addend) v += p.addend[(long)((row % p.add_group) + p.add_off) * p.add_ld + col];
+        if (p.res) {
+          const long ro = (long)row * p.res_ld + col;
+          v += bf2f(p.res[ro]) + bf2f(p.res[ro + p.res_lo]);
+        }
         if (p.epi == EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
         else if (p.epi == EPI_RELU) v = fmaxf(v, 0.f);
         const long orow = p.rm_group ? (long)(row / p.rm_group) * p.rm_stride + p.rm_off + row % p.rm_group
@@ -575,6 +580,15 @@ template <int TM, int TN>
 __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM][TN], int mb, int nb, int fr,
                                              int fq) {
   const int M = p.M;
+  if (p.scale) {
+    f32x4 sv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) sv[j] = *(const f32x4*)(p.scale + nb + j * 16 + 4 * fq);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] *= sv[j];
+  }
   if (p.bias) {
     f32x4 bv[TN];
 #pragma unroll
@@ -595,6 +609,25 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[i][j] += ad[i];
+    }
+  }
+  if (p.res) {  // residual from bf16 planes (hi + lo), 4 consecutive columns = 8 B per plane
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      u32x2 rh[TM], rl[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const long ro = (long)min(mb + i * 16 + fr, M - 1) * p.res_ld + nb + j * 16 + 4 * fq;
+        rh[i] = *(const u32x2*)(p.res + ro);
+        rl[i] = *(const u32x2*)(p.res + ro + p.res_lo);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t wh = rh[i][r >> 1] >> ((r & 1) * 16), wl = rl[i][r >> 1] >> ((r & 1) * 16);
+          acc[i][j][r] += bf2f((bf16_t)(wh & 0xffff)) + bf2f((bf16_t)(wl & 0xffff));
+        }
     }
   }
   if (p.epi == EPI_GELU) {

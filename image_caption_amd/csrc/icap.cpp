@@ -84,6 +84,11 @@ struct EncLayer {
   Lin qkv, out, lin1, lin2;
   LN n1, n2;
 };
+struct Conv {  // packed Conv2d + eval BatchNorm: bf16 W [cout][Kp] in (kh, kw, c) order, fp32 scale/shift
+  bf16_t* w = nullptr;
+  float *scale = nullptr, *shift = nullptr;
+  int cout = 0, cin = 0, k = 1, stride = 1, Kp = 0;
+};
 struct DecLayer {
   Lin sa_qkv, sa_out, ca_q, ca_out, lin1, lin2;
   bf16_t* ca_kT = nullptr;  // [H][d_model][64]: W_k,h^T for the key absorption
@@ -128,6 +133,7 @@ struct icap_handle {
   // grid
   float* enc_pe = nullptr;
   std::vector<EncLayer> enc;
+  std::vector<Conv> trunk;  // stem, then per bottleneck block [downsample] conv1 conv2 conv3
   // live kernel timing (icap_profile_*): HIP events bracket each launch of the hot kernels
   struct ProfRec {
     int cls;
@@ -166,6 +172,7 @@ struct icap_handle {
 
   // workspaces
   DevBuf e_x, e_a, e_qkv, e_h, e_patch;  // encoder
+  DevBuf t_x, t_y, t_1, t_2, t_r, t_col;  // ResNet trunk (NHWC planes)
   DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin, d_part, d_memp, d_beam;  // decoder
 
   ~icap_handle() {
@@ -176,6 +183,7 @@ struct icap_handle {
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
+    for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col}) b->release();
     for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_x, &d_a, &d_qkv, &d_q, &d_qt, &d_c, &d_o, &d_h, &d_memp, &d_beam,
                       &d_kv, &d_fin, &d_part})
       b->release();
@@ -208,6 +216,19 @@ struct icap_handle {
     return l;
   }
   LN ln(const icap_ln_w& p, int D, hipStream_t s) { return LN{own_f32(p.w, D, s), own_f32(p.b, D, s)}; }
+  Conv pack_conv(const icap_conv_bn_w& c, hipStream_t s) {
+    REQUIRE(c.w && c.bn_w && c.bn_b && c.bn_mean && c.bn_var, "missing trunk parameter pointer");
+    REQUIRE(c.cout % 64 == 0 && c.k % 2 == 1 && (c.stride == 1 || c.stride == 2), "unsupported trunk conv");
+    Conv o;
+    o.cout = c.cout; o.cin = c.cin; o.k = c.k; o.stride = c.stride;
+    o.Kp = (c.cin * c.k * c.k + 63) / 64 * 64;
+    o.w = (bf16_t*)alloc((size_t)o.cout * o.Kp * 2);
+    HIPCHK(launch_pack_conv(c.w, c.cout, c.cin, c.k, o.Kp, o.w, s));
+    o.scale = (float*)alloc((size_t)c.cout * 4);
+    o.shift = (float*)alloc((size_t)c.cout * 4);
+    HIPCHK(launch_bn_fold(c.bn_w, c.bn_b, c.bn_mean, c.bn_var, c.cout, 1e-5f, o.scale, o.shift, s));
+    return o;
+  }
 
   // ---------------------------------------------------------------- GEMM helper
   void gemm(const bf16_t* A, long lda, long a_lo, const Lin& W, int M, void* C, long ldc, long c_lo, int epi,
@@ -301,6 +322,14 @@ void pack(icap_handle* h, hipStream_t s) {
     h->proj = h->lin(d.proj_w, d.proj_b, D, V, s);
   } else if (d.kind == ICAP_KIND_GRID) {
     h->proj = h->lin(d.proj_w, d.proj_b, D, d.cnn_dim, s);
+    if (d.n_trunk) {
+      int n = 1;
+      for (int st = 0; st < 4; ++st) n += 3 * d.trunk_blocks[st] + (d.trunk_blocks[st] > 0);
+      REQUIRE(d.trunk && d.n_trunk == n, "trunk conv count does not match trunk_blocks");
+      REQUIRE(d.trunk[0].k == 7 && d.trunk[0].stride == 2 && d.trunk[0].cin == 3, "trunk stem must be 7x7/2 on RGB");
+      for (int i = 0; i < n; ++i) h->trunk.push_back(h->pack_conv(d.trunk[i], s));
+      REQUIRE(h->trunk.back().cout == d.cnn_dim, "trunk output channels != projection input");
+    }
     h->enc_pe = h->own_f32(d.enc_pe, (size_t)d.grid_tokens * D, s);
     for (int i = 0; i < d.n_enc_layers; ++i) {
       const icap_enc_layer_w& L = d.enc_layers[i];
@@ -376,17 +405,15 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   h->gemm(a, V, a2L, h->proj, B * np, memory, Dm, 0, EPI_NONE, OUT_F32, s);
 }
 
-void encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, hipStream_t s) {
+// Grid tail over trunk features given as row planes [B*49][C] (row = b*49 + h*7 + w, i.e. the
+// flatten(2).permute(0, 2, 1) order of grid:100-101): 1x1 projection + PE, 6 post-LN layers.
+void encode_grid_rows(icap_handle* h, const bf16_t* rows, long rL, int B, float* memory, hipStream_t s) {
   const icap_model_desc& d = h->d;
   const int D = d.d_model, N = d.grid_tokens, M = B * N, C = d.cnn_dim, ns = h->ns;
-  h->e_patch.ensure((size_t)M * C * 2 * ns);
   h->e_a.ensure((size_t)M * D * 2 * ns);
   h->e_qkv.ensure((size_t)M * 3 * D * 2 * ns);
   h->e_h.ensure((size_t)M * d.dim_ff * 2 * ns);
-  bf16_t* rows = h->e_patch.as<bf16_t>();
   bf16_t* a = h->e_a.as<bf16_t>();
-  const long rL = (long)M * C;
-  HIPCHK(launch_nchw_to_rows(feats, B, C, N, rows, rL, ns, s));
   {  // 1x1 conv projection + positional encoding
     GemmArgs ga = gemm_args();
     ga.A = rows; ga.lda = C; ga.a_lo = rL;
@@ -401,6 +428,118 @@ void encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, 
   HIPCHK(launch_split_f32(memory, (long)M * D, a, (long)M * D, ns, s));
   for (const EncLayer& L : h->enc)
     enc_layer_postln(h, L, B, N, memory, a, h->e_qkv.as<bf16_t>(), h->e_h.as<bf16_t>(), s);
+}
+
+void encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  const int N = d.grid_tokens, M = B * N, C = d.cnn_dim, ns = h->ns;
+  h->e_patch.ensure((size_t)M * C * 2 * ns);
+  bf16_t* rows = h->e_patch.as<bf16_t>();
+  const long rL = (long)M * C;
+  HIPCHK(launch_nchw_to_rows(feats, B, C, N, rows, rL, ns, s));
+  encode_grid_rows(h, rows, rL, B, memory, s);
+}
+
+// One trunk convolution as a GEMM: rows = output pixels (NHWC), out = 2 bf16 planes of
+// epi(acc * bn_scale + bn_shift (+ residual planes)).  A is `ns` planes with row stride a_ld.
+void trunk_conv(icap_handle* h, const Conv& c, const bf16_t* A, long a_ld, long a_lo, int M, bf16_t* out, long out_lo,
+                bool relu, const bf16_t* res, long res_lo, hipStream_t s) {
+  GemmArgs g = gemm_args();
+  g.A = A; g.lda = a_ld; g.a_lo = a_lo;
+  g.W = c.w; g.ldw = c.Kp;
+  g.bias = c.shift; g.scale = c.scale;
+  g.C = out; g.ldc = c.cout; g.c_lo = out_lo; g.c_planes = 2;
+  g.M = M; g.N = c.cout; g.K = c.Kp; g.nsplit = h->ns;
+  g.epi = relu ? EPI_RELU : EPI_NONE; g.out = OUT_SPLIT;
+  g.res = res; g.res_ld = c.cout; g.res_lo = res_lo;
+  h->run_gemm(g, s);
+}
+
+// ResNet-101 trunk (torchvision Bottleneck, stride on the 3x3) on NHWC bf16 planes, then the tail.
+// Images go through in chunks of TRUNK_CHUNK so the stem GEMM grid and the workspaces stay bounded.
+constexpr int TRUNK_CHUNK = 256;
+
+void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  REQUIRE(!h->trunk.empty(), "handle was created without the ResNet trunk (n_trunk = 0)");
+  REQUIRE(d.grid_tokens == 49, "the trunk path expects 224x224 images -> 7x7 grids");
+  const int ns = h->ns, HW = 224;
+  const int H1 = (HW - 1) / 2 + 1, H2 = (H1 - 1) / 2 + 1;  // 112 (stem), 56 (max-pool)
+  const long act_per_img = [&] {  // largest NHWC activation of one image (elements of one plane)
+    long m = (long)H1 * H1 * h->trunk[0].cout;
+    int hw = H2;
+    size_t ci = 1;
+    for (int st = 0; st < 4; ++st)
+      for (int j = 0; j < d.trunk_blocks[st]; ++j) {
+        if (j == 0) ++ci;
+        const Conv& c1 = h->trunk[ci];
+        m = std::max(m, (long)hw * hw * std::max(c1.cin, c1.cout));
+        if (j == 0 && h->trunk[ci + 1].stride == 2) hw = (hw - 1) / 2 + 1;
+        m = std::max(m, (long)hw * hw * h->trunk[ci + 2].cout);
+        ci += 3;
+      }
+    return m;
+  }();
+  const long col_per_img = [&] {  // largest GEMM A gather (stem / 3x3 im2col, stride-2 subsample)
+    long m = (long)H1 * H1 * h->trunk[0].Kp;
+    int hw = H2;
+    size_t ci = 1;
+    for (int st = 0; st < 4; ++st)
+      for (int j = 0; j < d.trunk_blocks[st]; ++j) {
+        const bool ds = j == 0;
+        if (ds) ++ci;
+        const Conv& c2 = h->trunk[ci + 1];
+        const int oh = c2.stride == 2 ? (hw - 1) / 2 + 1 : hw;
+        m = std::max(m, (long)oh * oh * c2.Kp);
+        if (ds) m = std::max(m, (long)oh * oh * h->trunk[ci - 1].cin);
+        hw = oh;
+        ci += 3;
+      }
+    return m;
+  }();
+  const int bc_max = std::min(B, TRUNK_CHUNK);
+  const long aL = act_per_img * bc_max, cL = col_per_img * bc_max;
+  for (DevBuf* b : {&h->t_x, &h->t_y, &h->t_1, &h->t_2, &h->t_r}) b->ensure((size_t)aL * 2 * 2);
+  h->t_col.ensure((size_t)cL * 2 * ns);
+  bf16_t *X = h->t_x.as<bf16_t>(), *Y = h->t_y.as<bf16_t>(), *T1 = h->t_1.as<bf16_t>(), *T2 = h->t_2.as<bf16_t>(),
+         *R = h->t_r.as<bf16_t>(), *col = h->t_col.as<bf16_t>();
+  for (int b0 = 0; b0 < B; b0 += bc_max) {
+    const int bc = std::min(bc_max, B - b0);
+    const Conv& stem = h->trunk[0];
+    HIPCHK(launch_stem_im2col(img + (size_t)b0 * 3 * HW * HW, bc, HW, H1, stem.Kp, col, cL, ns, s));
+    trunk_conv(h, stem, col, stem.Kp, cL, bc * H1 * H1, T1, aL, true, nullptr, 0, s);
+    HIPCHK(launch_maxpool3s2(T1, aL, bc, H1, H1, stem.cout, H2, H2, X, aL, ns, s));
+    int hw = H2;
+    size_t ci = 1;
+    for (int st = 0; st < 4; ++st)
+      for (int j = 0; j < d.trunk_blocks[st]; ++j) {
+        const Conv* ds = j == 0 ? &h->trunk[ci++] : nullptr;
+        const Conv &c1 = h->trunk[ci], &c2 = h->trunk[ci + 1], &c3 = h->trunk[ci + 2];
+        ci += 3;
+        const int oh = c2.stride == 2 ? (hw - 1) / 2 + 1 : hw;
+        const int Min = bc * hw * hw, Mout = bc * oh * oh;
+        const bf16_t* res = X;
+        if (ds) {  // identity branch: 1x1 conv (stride = the block's) + BN, no ReLU
+          const bf16_t* dsA = X;
+          long dsL = aL;
+          if (ds->stride == 2) {
+            HIPCHK(launch_subsample2(X, aL, bc, hw, hw, ds->cin, col, cL, ns, s));
+            dsA = col;
+            dsL = cL;
+          }
+          trunk_conv(h, *ds, dsA, ds->cin, dsL, Mout, R, aL, false, nullptr, 0, s);
+          res = R;
+        }
+        trunk_conv(h, c1, X, c1.cin, aL, Min, T1, aL, true, nullptr, 0, s);
+        HIPCHK(launch_im2col3(T1, aL, bc, hw, hw, c1.cout, c2.stride, oh, oh, col, cL, ns, s));
+        trunk_conv(h, c2, col, c2.Kp, cL, Mout, T2, aL, true, nullptr, 0, s);
+        trunk_conv(h, c3, T2, c3.cin, aL, Mout, Y, aL, true, res, aL, s);
+        std::swap(X, Y);
+        hw = oh;
+      }
+    REQUIRE(hw * hw == d.grid_tokens, "trunk output grid != grid_tokens");
+    encode_grid_rows(h, X, aL, bc, memory + (size_t)b0 * d.grid_tokens * d.d_model, s);
+  }
 }
 
 constexpr int MAX_KSPLIT = 8;
@@ -702,6 +841,14 @@ int icap_encode_grid_tail(icap_handle* h, const float* feats, int B, float* memo
     REQUIRE(h && feats && memory && B > 0, "bad arguments");
     REQUIRE(h->d.kind == ICAP_KIND_GRID, "handle is not a Grid model");
     encode_grid_tail(h, feats, B, memory, (hipStream_t)stream);
+  });
+}
+
+int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && images && memory && B > 0, "bad arguments");
+    REQUIRE(h->d.kind == ICAP_KIND_GRID, "icap_encode_grid on a non-Grid model");
+    encode_grid(h, images, B, memory, (hipStream_t)stream);
   });
 }
 

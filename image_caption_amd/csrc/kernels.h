@@ -20,6 +20,9 @@ struct GemmArgs {
   int epi, out;
   int rm_group; long rm_stride; long rm_off;          // output row remap (0 = identity)
   const float* addend; long add_ld; int add_group; int add_off;
+  // convolution epilogue (ResNet trunk): v = acc * scale[n] + bias[n] (+ res planes) before the
+  // activation; res = bf16 hi plane at res[row * res_ld + n], lo plane at + res_lo
+  const float* scale; const bf16_t* res; long res_ld; long res_lo;
 };
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
@@ -83,6 +86,18 @@ hipError_t launch_cls_rows(const float* cls, const float* pos, float* x, int B, 
 hipError_t launch_nchw_to_rows(const float* feats, int B, int C, int S, bf16_t* out, long lo, int nsplit,
                                hipStream_t s);
 // x[r] = emb[tok] * scale + pe[t0 + r % T], tok = tok_ptr[(r / T) * tok_ld + r % T] (or fixed_tok if null)
+// ResNet trunk (trunk.hip): gathers into GEMM A operands (NHWC bf16 planes), max-pool, packing
+hipError_t launch_stem_im2col(const float* img, int B, int HW, int OH, int Kp, bf16_t* out, long lo, int nsplit,
+                              hipStream_t s);
+hipError_t launch_im2col3(const bf16_t* x, long xlo, int B, int H, int W, int C, int stride, int OH, int OW,
+                          bf16_t* out, long lo, int nsplit, hipStream_t s);
+hipError_t launch_subsample2(const bf16_t* x, long xlo, int B, int H, int W, int C, bf16_t* out, long lo, int nsplit,
+                             hipStream_t s);
+hipError_t launch_maxpool3s2(const bf16_t* x, long xlo, int B, int H, int W, int C, int OH, int OW, bf16_t* out,
+                             long lo, int nsplit, hipStream_t s);
+hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int Kp, bf16_t* out, hipStream_t s);
+hipError_t launch_bn_fold(const float* g, const float* b, const float* mean, const float* var, int C, float eps,
+                          float* scale, float* shift, hipStream_t s);
 hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0, const float* emb,
                         const float* pe, int D, float scale, float* x, bf16_t* a, long lo, int nsplit, hipStream_t s);
 hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hipStream_t s);

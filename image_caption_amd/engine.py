@@ -15,7 +15,7 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import (DecLayerW, EncLayerW, LnW, MhaW, ModelDesc, VitLayerW, check, stream_ptr)
+from ._lib import (ConvBnW, DecLayerW, EncLayerW, LnW, MhaW, ModelDesc, VitLayerW, check, stream_ptr)
 
 DEFAULT_PRECISION = "bf16x2"
 
@@ -27,6 +27,35 @@ def _ln(sd, p):
 def _mha(sd, p):
     return MhaW(sd[p + ".in_proj_weight"].data_ptr(), sd[p + ".in_proj_bias"].data_ptr(),
                 sd[p + ".out_proj.weight"].data_ptr(), sd[p + ".out_proj.bias"].data_ptr())
+
+
+def _conv_bn(sd, conv, bn, stride):
+    w = sd[conv + ".weight"]
+    return ConvBnW(w.data_ptr(), sd[bn + ".weight"].data_ptr(), sd[bn + ".bias"].data_ptr(),
+                   sd[bn + ".running_mean"].data_ptr(), sd[bn + ".running_var"].data_ptr(),
+                   w.shape[0], w.shape[1], w.shape[2], stride)
+
+
+def trunk_convs(sd, prefix="encoder.cnn."):
+    """The ResNet trunk of a GridFeatureEncoder state_dict (cnn = resnet children[:-2]: 0 conv1,
+    1 bn1, 4..7 layer1..4) in icap_model_desc order, with the blocks per stage.  None if absent."""
+    if prefix + "0.weight" not in sd:
+        return None
+    convs = [_conv_bn(sd, prefix + "0", prefix + "1", 2)]
+    blocks = []
+    for st in range(4):
+        n = 0
+        while f"{prefix}{4 + st}.{n}.conv1.weight" in sd:
+            p = f"{prefix}{4 + st}.{n}"
+            stride = 2 if (st > 0 and n == 0) else 1
+            if n == 0:
+                convs.append(_conv_bn(sd, p + ".downsample.0", p + ".downsample.1", stride))
+            convs.append(_conv_bn(sd, p + ".conv1", p + ".bn1", 1))
+            convs.append(_conv_bn(sd, p + ".conv2", p + ".bn2", stride))
+            convs.append(_conv_bn(sd, p + ".conv3", p + ".bn3", 1))
+            n += 1
+        blocks.append(n)
+    return convs, blocks
 
 
 def apply_stop_rule(ids: torch.Tensor, end_token: int) -> torch.Tensor:
@@ -52,6 +81,7 @@ class Engine:
             raise _lib.IcapError("the HIP engine needs a GPU device")
         self.device = device
         self.kind = kind
+        self.has_trunk = False
         self.precision = precision
         sd = {k: v.detach().to(device=device, dtype=torch.float32).contiguous()
               for k, v in state_dict.items() if torch.is_floating_point(v)}
@@ -131,6 +161,15 @@ class Engine:
             desc.n_enc_layers = n_enc
             desc.enc_pe = sd["encoder.pos_encoder.pe"].data_ptr()
             desc.enc_layers = ctypes.cast(el, ctypes.POINTER(EncLayerW))
+            trunk = trunk_convs(sd)
+            if trunk is not None:
+                convs, blocks = trunk
+                tw = (ConvBnW * len(convs))(*convs)
+                keep.append(tw)
+                desc.n_trunk = len(convs)
+                desc.trunk_blocks[:] = blocks
+                desc.trunk = ctypes.cast(tw, ctypes.POINTER(ConvBnW))
+            self.has_trunk = trunk is not None
             self.mem_tokens = 49
         else:
             raise ValueError(f"unknown model kind {kind!r}")
@@ -151,7 +190,8 @@ class Engine:
 
     # ------------------------------------------------------------------ encoders
     def encode(self, images: torch.Tensor) -> torch.Tensor:
-        """ViT: images (B,3,224,224) -> memory (B,196,d).  Grid: trunk features (B,2048,7,7)."""
+        """ViT: images (B,3,224,224) -> memory (B,196,d).  Grid: images (B,3,224,224) through the HIP
+        ResNet trunk, or trunk features (B,2048,7,7) through the tail only."""
         x = images.to(device=self.device, dtype=torch.float32).contiguous()
         B = x.shape[0]
         mem = torch.empty(B, self.mem_tokens, self.d_model, device=self.device, dtype=torch.float32)
@@ -160,9 +200,14 @@ class Engine:
                 raise ValueError(f"expected (B,3,224,224) images, got {tuple(x.shape)}")
             check(self.lib.icap_encode_vit(self.handle, x.data_ptr(), B, mem.data_ptr(), stream_ptr(self.device)),
                   "icap_encode_vit")
+        elif tuple(x.shape[1:]) == (3, 224, 224):
+            if not self.has_trunk:
+                raise _lib.IcapError("this Grid engine was built without the encoder.cnn weights")
+            check(self.lib.icap_encode_grid(self.handle, x.data_ptr(), B, mem.data_ptr(), stream_ptr(self.device)),
+                  "icap_encode_grid")
         else:
             if x.dim() != 4 or x.shape[2] * x.shape[3] != self.mem_tokens:
-                raise ValueError(f"expected (B,C,7,7) trunk features, got {tuple(x.shape)}")
+                raise ValueError(f"expected (B,3,224,224) images or (B,C,7,7) trunk features, got {tuple(x.shape)}")
             check(self.lib.icap_encode_grid_tail(self.handle, x.data_ptr(), B, mem.data_ptr(),
                                                  stream_ptr(self.device)), "icap_encode_grid_tail")
         return mem

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define ICAP_ABI_VERSION 1
+#define ICAP_ABI_VERSION 2
 
 #define ICAP_KIND_VIT 0   /* ViTTransformerCaptioning  (models/vit_transformer_model.py:185)  */
 #define ICAP_KIND_GRID 1  /* GridTransformerCaptioning (models/grid_transformer_model.py:161) */
@@ -55,6 +55,12 @@ typedef struct { /* nn.TransformerDecoderLayer (post-LN, ReLU): decoder.transfor
   icap_ln_w norm1, norm2, norm3;
 } icap_dec_layer_w;
 
+typedef struct { /* Conv2d(bias=False) + eval BatchNorm2d of the torchvision ResNet-101 trunk */
+  const float* w;                                  /* (cout, cin, k, k)                            */
+  const float *bn_w, *bn_b, *bn_mean, *bn_var;     /* (cout) each; eps 1e-5                         */
+  int cout, cin, k, stride;                        /* padding = k / 2                               */
+} icap_conv_bn_w;
+
 typedef struct {
   int kind, precision;
   /* decoder (TransformerDecoder, vit:103-182) */
@@ -71,6 +77,12 @@ typedef struct {
   int cnn_dim, grid_tokens, n_enc_layers;
   const float* enc_pe;
   const icap_enc_layer_w* enc_layers;
+  /* Grid ResNet-101 trunk (GridFeatureEncoder.cnn = resnet101 children[:-2], grid:51), optional
+   * (n_trunk = 0: only icap_encode_grid_tail is available).  Order: stem conv1+bn1 (7x7/2), then
+   * for each stage s and bottleneck block j: [downsample.0+.1 when j == 0], conv1+bn1 (1x1),
+   * conv2+bn2 (3x3, the stage stride on j == 0), conv3+bn3 (1x1); trunk_blocks = blocks per stage. */
+  int n_trunk, trunk_blocks[4];
+  const icap_conv_bn_w* trunk;
 } icap_model_desc;
 
 int icap_abi_version(void);
@@ -89,6 +101,11 @@ int icap_encode_vit(icap_handle* h, const float* images, int B, float* memory, v
 /* ResNet trunk features (B,cnn_dim,7,7) fp32 -> memory (B,49,d_model) fp32.
  * Replaces: GridFeatureEncoder.forward after self.cnn, models/grid_transformer_model.py:97-108. */
 int icap_encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, void* stream);
+
+/* images (B,3,224,224) fp32 normalised -> memory (B,49,d_model) fp32: the ResNet-101 trunk as
+ * MFMA GEMMs over NHWC activation planes (BatchNorm folded into the epilogue), then the tail.
+ * Replaces: GridFeatureEncoder.forward, models/grid_transformer_model.py:86-108 (self.cnn included). */
+int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, void* stream);
 
 /* Greedy decode of max_len-1 steps with a KV cache: ids (B,max_len) int32, column 0 = start.
  * step_logits (max_len-1,B,vocab) fp32 is optional (NULL to skip).  The reference's batch-global

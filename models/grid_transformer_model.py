@@ -1,9 +1,9 @@
 """Drop-in `models.grid_transformer_model` (reference: models/grid_transformer_model.py).
 
 ResNet-101 grid features -> 1x1 conv -> sinusoidal PE -> 6 post-LN Transformer encoder layers ->
-the shared Transformer decoder.  On the HIP path the ResNet-101 trunk still runs as PyTorch-ROCm
-(MIOpen) convolutions in fp32 - SURVEY.md §8(f)3 schedules its HIP port - and everything after
-it (projection, PE, encoder layers, decoder, greedy loop) runs in libicap.so.
+the shared Transformer decoder.  On the HIP path everything runs in libicap.so: the ResNet-101
+trunk as MFMA GEMMs over NHWC activation planes (BatchNorm folded into the GEMM epilogue,
+SURVEY.md §8(f)3), then projection, PE, encoder layers, decoder and the decode loops.
 """
 from __future__ import annotations
 
@@ -49,9 +49,11 @@ class GridFeatureEncoder(nn.Module):
     def forward(self, images):
         owner = owner_of(self)
         if owner is not None and not self.training and owner.use_hip(images):
-            with torch.no_grad():
-                feats = self.cnn(images.float())  # PyTorch-ROCm trunk (MIOpen), fp32
-            return owner.hip_engine(images.device).encode(feats)
+            eng = owner.hip_engine(images.device)
+            if tuple(images.shape[1:]) == (3, 224, 224):
+                return eng.encode(images)  # HIP trunk + tail
+            with torch.no_grad():  # other image sizes: torch trunk, HIP tail
+                return eng.encode(self.cnn(images.float()))
         x = self.projection(self.cnn(images))
         x = x.flatten(2).permute(0, 2, 1)
         return self.transformer_encoder(self.pos_encoder(x))

@@ -111,8 +111,33 @@ def test_grid_golden(cuda):
     with torch.no_grad():
         mem = m.encoder(imgs)
     assert np.allclose(mem.double().sum(dim=(1, 2)).cpu().numpy(), g["memory_sum"], rtol=1e-4, atol=0.5)
+    assert np.abs(mem[:, :4, :16].cpu().numpy() - g["memory_head"]).max() < 1e-3
     ids = m.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=30)
     assert np.array_equal(ids.cpu().numpy(), g["ids"])
+    eng = m.hip_engine(imgs.device)
+    assert eng.has_trunk  # images went through the HIP ResNet trunk, not torch
+    tf = eng.decoder_forward(torch.from_numpy(g["ids"][:, :-1]).to(cuda), mem, causal=True)
+    assert np.abs(tf.cpu().numpy() - g["logits_tf"]).max() < 1e-3
+
+
+def test_grid_trunk_vs_oracle_across_chunks(cuda):
+    """HIP ResNet-101 trunk + tail at B=260 (two trunk chunks: 256 + 4 images) against the CPU
+    oracle (oracle/captioner.py resnet101_trunk + grid_encode_tail) on images either side of the
+    chunk seam, and the features-only entry (icap_encode_grid_tail) on the oracle's trunk output."""
+    from image_caption_amd.engine import Engine
+
+    sd = W.to_torch(W.grid_state_dict(0))
+    eng = Engine(sd, "grid", {}, device=cuda)
+    imgs = torch.from_numpy(W.synthetic_images(260, seed=2)).to(cuda)
+    mem = eng.encode(imgs)
+    pick = torch.tensor([0, 131, 255, 256, 259])
+    sub = imgs[pick.to(cuda)].cpu()
+    with torch.no_grad():
+        feats = O.resnet101_trunk(sd, sub)
+        ref = O.grid_encode_tail(sd, feats)
+    assert (mem[pick.to(cuda)].cpu() - ref).abs().max().item() < 1e-3
+    tail = eng.encode(feats.to(cuda))
+    assert (tail.cpu() - ref).abs().max().item() < 1e-3
 
 
 def test_batch_independence_and_determinism_at_b256(vit_engine, cuda, vit_sd):
