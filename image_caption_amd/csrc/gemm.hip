@@ -19,7 +19,29 @@ namespace {
 
 constexpr int BK = 64;
 
-template <int BM, int BN, int WM, int WN>
+// Implicit-GEMM convolution rows (GemmArgs::cv): a staging lane's output pixel, fixed for the K loop.
+struct ConvRow {
+  int pb, oy, ox;  // input pixel index of the window origin (stride applied), its y and x
+};
+__device__ __forceinline__ ConvRow conv_row(const GemmArgs& p, int gr) {
+  const int b = gr / p.cv_OHW, rem = gr - b * p.cv_OHW, oh = rem / p.cv_OW, ow = rem - oh * p.cv_OW;
+  const int oy = oh * p.cv_stride, ox = ow * p.cv_stride;
+  return {(b * p.cv_H + oy) * p.cv_W + ox, oy, ox};
+}
+// Source of the 16-byte chunk at k (8 consecutive k, one tap) of row r; base = A + plane offset.
+template <int CONV>
+__device__ __forceinline__ const bf16_t* conv_src(const GemmArgs& p, const bf16_t* base, const ConvRow& r, int k) {
+  if (CONV == 2)  // stem: kernel row kh = k / 32 of the bordered NHWC4 image, 8 pixels x 4 channels
+    return base + (long)(r.pb + (k >> 5) * p.cv_W) * 4 + (k & 31);
+  const int tap = k >> p.cv_cshift, c = k & ((1 << p.cv_cshift) - 1);
+  const int kh = (tap * 11) >> 5, kw = tap - 3 * kh;  // tap / 3, tap % 3 for tap < 9
+  const int iy = r.oy + kh - 1, ix = r.ox + kw - 1;
+  const bool ok = (unsigned)iy < (unsigned)p.cv_H && (unsigned)ix < (unsigned)p.cv_W;
+  const bf16_t* src = base + ((long)(r.pb + (kh - 1) * p.cv_W + kw - 1) << p.cv_cshift) + c;
+  return ok ? src : p.cv_zero;
+}
+
+template <int BM, int BN, int WM, int WN, int CONV = 0>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
   constexpr int WAVES_N = BN / WN;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -38,11 +60,17 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
   const int nk = p.nsplit * K / BK;
 
   long a_off[IA], b_off[IB];
+  ConvRow cr[CONV ? IA : 1];
 #pragma unroll
   for (int i = 0; i < IA; ++i) {
     int idx = (wave * IA + i) * 64 + lane, row = idx >> 3, cs = idx & 7;
     int gr = min(m0 + row, M - 1);
-    a_off[i] = (long)gr * p.lda + ((cs ^ (row & 7)) << 3);
+    if (CONV) {
+      cr[i] = conv_row(p, gr);
+      a_off[i] = (cs ^ (row & 7)) << 3;  // k offset of the lane's chunk
+    } else {
+      a_off[i] = (long)gr * p.lda + ((cs ^ (row & 7)) << 3);
+    }
   }
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
@@ -58,9 +86,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < IA; ++i)
-      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(Ab + a_off[i]),
-                                       (LDS_AS void*)(sa + (wave * IA + i) * 1024), 16, 0, 0);
+    for (int i = 0; i < IA; ++i) {
+      const bf16_t* src = CONV ? conv_src<CONV>(p, A + plane * p.a_lo, cr[CONV ? i : 0], kin + (int)a_off[i])
+                               : Ab + a_off[i];
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)(sa + (wave * IA + i) * 1024), 16,
+                                       0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < IB; ++i)
       __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(Wb + b_off[i]),
@@ -150,7 +181,10 @@ template <int BM, int BN, int WM, int WN>
 hipError_t run(const GemmArgs& g, hipStream_t s) {
   constexpr int lds = 2 * (BM + BN) * BK * 2;
   dim3 grid(g.N / BN, (g.M + BM - 1) / BM, g.batch);
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN>), grid, dim3(256), lds, s, g);
+  if (grid.y > 65535) return hipErrorInvalidValue;
+  if (g.cv == 1) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), lds, s, g);
+  else if (g.cv == 2) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, 2>), grid, dim3(256), lds, s, g);
+  else hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN>), grid, dim3(256), lds, s, g);
   return hipGetLastError();
 }
 
@@ -166,6 +200,8 @@ int gemm_tile_class(const GemmArgs& g) {
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
   if (g.K % BK != 0 || g.N % 64 != 0 || (g.nsplit != 1 && g.nsplit != 2)) return hipErrorInvalidValue;
+  if (g.cv && (g.batch != 1 || !g.cv_zero || (g.cv == 1 && g.cv_cshift < 6) || g.cv_OHW <= 0 || g.cv_OW <= 0))
+    return hipErrorInvalidValue;
   const int cls = gemm_tile_class(g);
   if (cls == PROF_GEMM_256) return launch_gemm_256(g, s);
   if (cls == PROF_GEMM_128) return run<128, 128, 64, 64>(g, s);
@@ -713,7 +749,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
 // share their A rows in that XCD's L2.
 namespace {
 
-template <int NS, int NW, int NOMFMA = 0>  // measurement variants: 1 = no MFMA, 2 = staging ring only
+template <int NS, int NW, int NOMFMA = 0, int CONV = 0>  // measurement variants: 1 = no MFMA, 2 = staging only
 __global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
   constexpr int WGM = NW / 4;                       // wave grid WGM x 4
   constexpr int BM = 256, BN = 256, WM = BM / WGM, WN = 64, TM = WM / 16, TN = WN / 16;
@@ -745,6 +781,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
   const bf16_t* b_base = p.W + (long)min(n0 + srow, p.N - 1) * p.ldw + schunk * 8;
   const long a_step = 16 * p.lda, b_step = 16 * p.ldw;
   const bool a_tail = m0 + BM > M;
+  ConvRow cr[CONV ? IPW : 1];
+  if (CONV)
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) cr[i] = conv_row(p, min(m0 + srow + i * 16, M - 1));
   auto stage = [&](int kt, int buf) {
     const int kin = kt * KS;
     char* s0 = smem + buf * STAGE;
@@ -768,7 +808,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
 #pragma unroll
       for (int i = 0; i < IPW; ++i) {
         const bf16_t* src = Ab + i * a_step;
-        if (a_tail && m0 + srow + i * 16 >= M) src = Ab + (long)(M - 1 - m0 - srow) * p.lda;
+        if (CONV) src = conv_src<CONV>(p, p.A + pl * p.a_lo, cr[CONV ? i : 0], kin + schunk * 8);
+        else if (a_tail && m0 + srow + i * 16 >= M) src = Ab + (long)(M - 1 - m0 - srow) * p.lda;
         __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
                                          (LDS_AS void*)(s0 + pl * OPB + (wave * IPW + i) * 1024), 16, 0, 0);
       }
@@ -989,14 +1030,21 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
     hipError_t e = hipSuccess;
     for (const void* f : {(const void*)gemm_256_kernel<2, 8>, (const void*)gemm_256_kernel<2, 16>,
                           (const void*)gemm_256_kernel<2, 16, 1>, (const void*)gemm_256_kernel<2, 16, 2>,
-                          (const void*)gemm_256_kernel<2, 16, 3>})
+                          (const void*)gemm_256_kernel<2, 16, 3>, (const void*)gemm_256_kernel<2, 16, 0, 1>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
-    for (const void* f : {(const void*)gemm_256_kernel<1, 8>, (const void*)gemm_256_kernel<1, 16>})
+    for (const void* f : {(const void*)gemm_256_kernel<1, 8>, (const void*)gemm_256_kernel<1, 16>,
+                          (const void*)gemm_256_kernel<1, 16, 0, 1>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
     if (e != hipSuccess) return e;
   }
   const int nwg = (g.N / 256) * ((g.M + 255) / 256);
   const GemmArgs& g2 = g;
+  if (g.cv) {  // implicit-GEMM 3x3 convolution
+    if (g.cv != 1) return hipErrorInvalidValue;
+    if (g.nsplit == 2) hipLaunchKernelGGL((gemm_256_kernel<2, 16, 0, 1>), dim3(nwg), dim3(1024), lds2, s, g2);
+    else hipLaunchKernelGGL((gemm_256_kernel<1, 16, 0, 1>), dim3(nwg), dim3(1024), lds1, s, g2);
+    return hipGetLastError();
+  }
   if ((nw == 1 || nw == 2) && g.K % 64 == 0) {
     if (nw == 2) hipLaunchKernelGGL(gemm_8ph_kernel<true>, dim3(nwg), dim3(512), 131072, s, g);
     else hipLaunchKernelGGL(gemm_8ph_kernel<false>, dim3(nwg), dim3(512), 131072, s, g);

@@ -134,6 +134,7 @@ struct icap_handle {
   float* enc_pe = nullptr;
   std::vector<EncLayer> enc;
   std::vector<Conv> trunk;  // stem, then per bottleneck block [downsample] conv1 conv2 conv3
+  bf16_t* zero = nullptr;   // 256 zero bytes: the implicit-GEMM source of out-of-image taps
   // live kernel timing (icap_profile_*): HIP events bracket each launch of the hot kernels
   struct ProfRec {
     int cls;
@@ -221,9 +222,15 @@ struct icap_handle {
     REQUIRE(c.cout % 64 == 0 && c.k % 2 == 1 && (c.stride == 1 || c.stride == 2), "unsupported trunk conv");
     Conv o;
     o.cout = c.cout; o.cin = c.cin; o.k = c.k; o.stride = c.stride;
-    o.Kp = (c.cin * c.k * c.k + 63) / 64 * 64;
+    // k order = the implicit-GEMM gather order: (kh, kw, c); the 7x7 stem as 7 rows of 8 taps x 4
+    // channels (one 64-B NHWC4 row segment per 32-deep k-step), padded to 8 rows for BK = 64
+    const bool stem = c.k == 7;
+    REQUIRE(stem ? c.cin <= 4 : (c.k == 1 || (c.k == 3 && (c.cin & (c.cin - 1)) == 0 && c.cin >= 64)),
+            "unsupported trunk conv shape");
+    const int cp = stem ? 4 : c.cin, kwp = stem ? 8 : c.k;
+    o.Kp = stem ? 8 * 8 * 4 : (c.cin * c.k * c.k + 63) / 64 * 64;
     o.w = (bf16_t*)alloc((size_t)o.cout * o.Kp * 2);
-    HIPCHK(launch_pack_conv(c.w, c.cout, c.cin, c.k, o.Kp, o.w, s));
+    HIPCHK(launch_pack_conv(c.w, c.cout, c.cin, c.k, cp, kwp, o.Kp, o.w, s));
     o.scale = (float*)alloc((size_t)c.cout * 4);
     o.shift = (float*)alloc((size_t)c.cout * 4);
     HIPCHK(launch_bn_fold(c.bn_w, c.bn_b, c.bn_mean, c.bn_var, c.cout, 1e-5f, o.scale, o.shift, s));
@@ -328,6 +335,8 @@ void pack(icap_handle* h, hipStream_t s) {
       REQUIRE(d.trunk && d.n_trunk == n, "trunk conv count does not match trunk_blocks");
       REQUIRE(d.trunk[0].k == 7 && d.trunk[0].stride == 2 && d.trunk[0].cin == 3, "trunk stem must be 7x7/2 on RGB");
       for (int i = 0; i < n; ++i) h->trunk.push_back(h->pack_conv(d.trunk[i], s));
+      h->zero = (bf16_t*)h->alloc(256);
+      HIPCHK(hipMemsetAsync(h->zero, 0, 256, s));
       REQUIRE(h->trunk.back().cout == d.cnn_dim, "trunk output channels != projection input");
     }
     h->enc_pe = h->own_f32(d.enc_pe, (size_t)d.grid_tokens * D, s);
@@ -442,9 +451,19 @@ void encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, 
 
 // One trunk convolution as a GEMM: rows = output pixels (NHWC), out = 2 bf16 planes of
 // epi(acc * bn_scale + bn_shift (+ residual planes)).  A is `ns` planes with row stride a_ld.
+struct ConvGeom {  // implicit-GEMM input geometry (GemmArgs::cv); cv = 0: A is a plain [M][K] matrix
+  int cv = 0, H = 0, W = 0, C = 0, OW = 0, OH = 0;
+};
+
 void trunk_conv(icap_handle* h, const Conv& c, const bf16_t* A, long a_ld, long a_lo, int M, bf16_t* out, long out_lo,
-                bool relu, const bf16_t* res, long res_lo, hipStream_t s) {
+                bool relu, const bf16_t* res, long res_lo, hipStream_t s, const ConvGeom& cg = ConvGeom()) {
   GemmArgs g = gemm_args();
+  if (cg.cv) {
+    g.cv = cg.cv; g.cv_H = cg.H; g.cv_W = cg.W; g.cv_OW = cg.OW; g.cv_OHW = cg.OH * cg.OW;
+    g.cv_stride = cg.cv == 2 ? 2 : c.stride; g.cv_zero = h->zero;
+    g.cv_cshift = 0;
+    while ((1 << g.cv_cshift) < cg.C) ++g.cv_cshift;
+  }
   g.A = A; g.lda = a_ld; g.a_lo = a_lo;
   g.W = c.w; g.ldw = c.Kp;
   g.bias = c.shift; g.scale = c.scale;
@@ -480,8 +499,10 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
       }
     return m;
   }();
-  const long col_per_img = [&] {  // largest GEMM A gather (stem / 3x3 im2col, stride-2 subsample)
-    long m = (long)H1 * H1 * h->trunk[0].Kp;
+  constexpr int BORDER = 3;
+  const int HP = HW + 2 * BORDER;                     // the stem's bordered NHWC4 image
+  const long col_per_img = [&] {  // stem image / stride-2 subsample of a downsample's input
+    long m = (long)HP * HP * 4;
     int hw = H2;
     size_t ci = 1;
     for (int st = 0; st < 4; ++st)
@@ -490,7 +511,6 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
         if (ds) ++ci;
         const Conv& c2 = h->trunk[ci + 1];
         const int oh = c2.stride == 2 ? (hw - 1) / 2 + 1 : hw;
-        m = std::max(m, (long)oh * oh * c2.Kp);
         if (ds) m = std::max(m, (long)oh * oh * h->trunk[ci - 1].cin);
         hw = oh;
         ci += 3;
@@ -506,8 +526,10 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
   for (int b0 = 0; b0 < B; b0 += bc_max) {
     const int bc = std::min(bc_max, B - b0);
     const Conv& stem = h->trunk[0];
-    HIPCHK(launch_stem_im2col(img + (size_t)b0 * 3 * HW * HW, bc, HW, H1, stem.Kp, col, cL, ns, s));
-    trunk_conv(h, stem, col, stem.Kp, cL, bc * H1 * H1, T1, aL, true, nullptr, 0, s);
+    HIPCHK(launch_image_nhwc4(img + (size_t)b0 * 3 * HW * HW, bc, HW, BORDER, col, cL, ns, s));
+    ConvGeom sg;
+    sg.cv = 2; sg.H = HP; sg.W = HP; sg.C = 4; sg.OH = H1; sg.OW = H1;
+    trunk_conv(h, stem, col, 0, cL, bc * H1 * H1, T1, aL, true, nullptr, 0, s, sg);
     HIPCHK(launch_maxpool3s2(T1, aL, bc, H1, H1, stem.cout, H2, H2, X, aL, ns, s));
     int hw = H2;
     size_t ci = 1;
@@ -531,8 +553,9 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
           res = R;
         }
         trunk_conv(h, c1, X, c1.cin, aL, Min, T1, aL, true, nullptr, 0, s);
-        HIPCHK(launch_im2col3(T1, aL, bc, hw, hw, c1.cout, c2.stride, oh, oh, col, cL, ns, s));
-        trunk_conv(h, c2, col, c2.Kp, cL, Mout, T2, aL, true, nullptr, 0, s);
+        ConvGeom g3;  // 3x3 conv2 read straight from T1 (implicit GEMM)
+        g3.cv = 1; g3.H = hw; g3.W = hw; g3.C = c1.cout; g3.OH = oh; g3.OW = oh;
+        trunk_conv(h, c2, T1, 0, aL, Mout, T2, aL, true, nullptr, 0, s, g3);
         trunk_conv(h, c3, T2, c3.cin, aL, Mout, Y, aL, true, res, aL, s);
         std::swap(X, Y);
         hw = oh;

@@ -23,6 +23,12 @@ struct GemmArgs {
   // convolution epilogue (ResNet trunk): v = acc * scale[n] + bias[n] (+ res planes) before the
   // activation; res = bf16 hi plane at res[row * res_ld + n], lo plane at + res_lo
   const float* scale; const bf16_t* res; long res_ld; long res_lo;
+  // implicit-GEMM convolution (A is not materialised; rows = output pixels (b, oh, ow)):
+  //   cv = 1: 3x3 / pad 1 / stride cv_stride over NHWC planes A [B][cv_H][cv_W][C], C = 1 << cv_cshift
+  //           (>= 64), k = (kh*3 + kw)*C + c; taps outside the image read cv_zero (>= 16 zero bytes)
+  //   cv = 2: 7x7 / stride 2 stem over a zero-bordered NHWC4 image A [B][cv_H][cv_W][4] (border 3),
+  //           k = (kh*8 + kw)*4 + c, i.e. one 32-deep k-step = one kernel row = 64 contiguous bytes
+  int cv, cv_H, cv_W, cv_cshift, cv_OW, cv_OHW, cv_stride; const bf16_t* cv_zero;
 };
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
@@ -87,15 +93,16 @@ hipError_t launch_nchw_to_rows(const float* feats, int B, int C, int S, bf16_t* 
                                hipStream_t s);
 // x[r] = emb[tok] * scale + pe[t0 + r % T], tok = tok_ptr[(r / T) * tok_ld + r % T] (or fixed_tok if null)
 // ResNet trunk (trunk.hip): gathers into GEMM A operands (NHWC bf16 planes), max-pool, packing
-hipError_t launch_stem_im2col(const float* img, int B, int HW, int OH, int Kp, bf16_t* out, long lo, int nsplit,
-                              hipStream_t s);
-hipError_t launch_im2col3(const bf16_t* x, long xlo, int B, int H, int W, int C, int stride, int OH, int OW,
-                          bf16_t* out, long lo, int nsplit, hipStream_t s);
 hipError_t launch_subsample2(const bf16_t* x, long xlo, int B, int H, int W, int C, bf16_t* out, long lo, int nsplit,
                              hipStream_t s);
 hipError_t launch_maxpool3s2(const bf16_t* x, long xlo, int B, int H, int W, int C, int OH, int OW, bf16_t* out,
                              long lo, int nsplit, hipStream_t s);
-hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int Kp, bf16_t* out, hipStream_t s);
+// [Cout][Kp] bf16 with k = (kh*kwp + kw)*cp + c (cp >= cin, kwp >= k; padding taps/channels are 0)
+hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int cp, int kwp, int Kp, bf16_t* out,
+                            hipStream_t s);
+// (B,3,HW,HW) fp32 -> zero-bordered NHWC4 planes [B][HW+2*border][HW+2*border][4] (channel 3 = 0)
+hipError_t launch_image_nhwc4(const float* img, int B, int HW, int border, bf16_t* out, long lo, int nsplit,
+                              hipStream_t s);
 hipError_t launch_bn_fold(const float* g, const float* b, const float* mean, const float* var, int C, float eps,
                           float* scale, float* shift, hipStream_t s);
 hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0, const float* emb,

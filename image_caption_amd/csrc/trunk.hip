@@ -1,59 +1,14 @@
 // ResNet-101 trunk helpers (GridFeatureEncoder.cnn, grid:51 = torchvision resnet101 children[:-2]).
 // Activations are NHWC bf16 hi/lo planes ([B][H][W][C], lo plane at +lo); every convolution is an
-// MFMA GEMM over rows = output pixels (gemm.hip, BatchNorm as the fp32 scale/shift epilogue, the
-// residual added from planes before the ReLU).  These kernels produce the GEMM A operands that are
-// not the activation itself: the 7x7/2 stem patches from the NCHW fp32 image, the 3x3 patches
-// (stride 1 or 2, pad 1) in (kh, kw, c) order = the packed weight order, the stride-2 subsample
-// of a 1x1 downsample, and the 3x3/2 max-pool.
+// MFMA GEMM over rows = output pixels (gemm.hip: the 3x3 and 7x7 convolutions as implicit GEMMs
+// that gather their A tiles straight from the activation, BatchNorm as the fp32 scale/shift
+// epilogue, the residual added from planes before the ReLU).  Here: the stem's input layout (the
+// NCHW fp32 image as a zero-bordered NHWC4 plane pair), the stride-2 subsample feeding a 1x1
+// downsample, the 3x3/2 max-pool, and the weight/BatchNorm packing.
 #include "common.h"
 #include "kernels.h"
 
 namespace {
-
-// img (B,3,224,224) fp32 -> rows (B*112*112) x Kp, k = (kh*7 + kw)*3 + c for k < 147, 0 beyond
-__global__ void stem_im2col_kernel(const float* __restrict__ img, int B, int HW, int OH, int Kp, bf16_t* out, long lo,
-                                   int nsplit) {
-  const long total = (long)B * OH * OH * Kp;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int k = (int)(i % Kp);
-    const long r = i / Kp;
-    const int ow = (int)(r % OH), oh = (int)((r / OH) % OH), b = (int)(r / ((long)OH * OH));
-    float v = 0.f;
-    if (k < 147) {
-      const int c = k % 3, kw = (k / 3) % 7, kh = k / 21;
-      const int y = oh * 2 - 3 + kh, x = ow * 2 - 3 + kw;
-      if (y >= 0 && y < HW && x >= 0 && x < HW) v = img[(((long)b * 3 + c) * HW + y) * HW + x];
-    }
-    bf16_t hv, lv;
-    split_bf(v, hv, lv);
-    out[i] = hv;
-    if (nsplit == 2) out[i + lo] = lv;
-  }
-}
-
-// planes [B][H][W][C] -> rows (B*OH*OW) x 9C, k = (kh*3 + kw)*C + c; 8 channels per thread
-__global__ void im2col3_kernel(const bf16_t* __restrict__ x, long xlo, int B, int H, int W, int C, int stride, int OH,
-                               int OW, bf16_t* out, long lo, int nsplit) {
-  const int C8 = C / 8;
-  const long total = (long)B * OH * OW * 9 * C8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i % C8);
-    const long t = i / C8;
-    const int tap = (int)(t % 9);
-    const long r = t / 9;
-    const int ow = (int)(r % OW), oh = (int)((r / OW) % OH), b = (int)(r / ((long)OH * OW));
-    const int y = oh * stride - 1 + tap / 3, xx = ow * stride - 1 + tap % 3;
-    u32x4 h = {0, 0, 0, 0}, l = {0, 0, 0, 0};
-    if (y >= 0 && y < H && xx >= 0 && xx < W) {
-      const long src = (((long)b * H + y) * W + xx) * C + c8 * 8;
-      h = *(const u32x4*)(x + src);
-      if (nsplit == 2) l = *(const u32x4*)(x + src + xlo);
-    }
-    const long dst = r * 9 * C + (long)tap * C + c8 * 8;
-    *(u32x4*)(out + dst) = h;
-    if (nsplit == 2) *(u32x4*)(out + dst + lo) = l;
-  }
-}
 
 // planes [B][H][W][C] -> [B][H/2][W/2][C] (every other pixel: the 1x1 stride-2 downsample input)
 __global__ void subsample2_kernel(const bf16_t* __restrict__ x, long xlo, int B, int H, int W, int C, bf16_t* out,
@@ -71,53 +26,55 @@ __global__ void subsample2_kernel(const bf16_t* __restrict__ x, long xlo, int B,
   }
 }
 
-// 3x3 / stride 2 / pad 1 max-pool on planes (the value is hi + lo; -inf padding like torch)
+// 3x3 / stride 2 / pad 1 max-pool on planes (the value is hi + lo; -inf padding like torch);
+// 8 channels per thread, 16-byte loads of each plane
 __global__ void maxpool3s2_kernel(const bf16_t* __restrict__ x, long xlo, int B, int H, int W, int C, int OH, int OW,
                                   bf16_t* out, long lo, int nsplit) {
-  const long total = (long)B * OH * OW * C;
+  const int C8 = C / 8;
+  const long total = (long)B * OH * OW * C8;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long r = i / C;
+    const int c8 = (int)(i % C8);
+    const long r = i / C8;
     const int ow = (int)(r % OW), oh = (int)((r / OW) % OH), b = (int)(r / ((long)OH * OW));
-    float m = -INFINITY;
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
     for (int dy = 0; dy < 3; ++dy) {
       const int y = oh * 2 - 1 + dy;
       if (y < 0 || y >= H) continue;
       for (int dx = 0; dx < 3; ++dx) {
         const int xx = ow * 2 - 1 + dx;
         if (xx < 0 || xx >= W) continue;
-        const long src = (((long)b * H + y) * W + xx) * C + c;
-        float v = bf2f(x[src]);
-        if (nsplit == 2) v += bf2f(x[src + xlo]);
-        m = fmaxf(m, v);
+        const long src = (((long)b * H + y) * W + xx) * C + c8 * 8;
+        const u32x4 hv = *(const u32x4*)(x + src);
+        u32x4 lv = {0, 0, 0, 0};
+        if (nsplit == 2) lv = *(const u32x4*)(x + src + xlo);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t hw = hv[e >> 1], lw = lv[e >> 1];
+          const float v = __uint_as_float((e & 1 ? hw >> 16 : hw & 0xffffu) << 16) +
+                          __uint_as_float((e & 1 ? lw >> 16 : lw & 0xffffu) << 16);
+          m[e] = fmaxf(m[e], v);
+        }
       }
     }
-    bf16_t hv, lv;
-    split_bf(m, hv, lv);
-    out[i] = hv;
-    if (nsplit == 2) out[i + lo] = lv;
+    u32x4 ho, lo4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bf16_t h0, l0, h1, l1;
+      split_bf(m[2 * e], h0, l0);
+      split_bf(m[2 * e + 1], h1, l1);
+      ho[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      lo4[e] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+    }
+    *(u32x4*)(out + r * C + c8 * 8) = ho;
+    if (nsplit == 2) *(u32x4*)(out + r * C + c8 * 8 + lo) = lo4;
   }
 }
 
 int grid_for(long n) { return (int)std::min<long>((n + 255) / 256, 65536); }
 
 }  // namespace
-
-hipError_t launch_stem_im2col(const float* img, int B, int HW, int OH, int Kp, bf16_t* out, long lo, int nsplit,
-                              hipStream_t s) {
-  if (Kp < 147 || Kp % 32) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(stem_im2col_kernel, dim3(grid_for((long)B * OH * OH * Kp)), dim3(256), 0, s, img, B, HW, OH,
-                     Kp, out, lo, nsplit);
-  return hipGetLastError();
-}
-
-hipError_t launch_im2col3(const bf16_t* x, long xlo, int B, int H, int W, int C, int stride, int OH, int OW,
-                          bf16_t* out, long lo, int nsplit, hipStream_t s) {
-  if (C % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(im2col3_kernel, dim3(grid_for((long)B * OH * OW * 9 * (C / 8))), dim3(256), 0, s, x, xlo, B, H,
-                     W, C, stride, OH, OW, out, lo, nsplit);
-  return hipGetLastError();
-}
 
 hipError_t launch_subsample2(const bf16_t* x, long xlo, int B, int H, int W, int C, bf16_t* out, long lo, int nsplit,
                              hipStream_t s) {
@@ -129,26 +86,49 @@ hipError_t launch_subsample2(const bf16_t* x, long xlo, int B, int H, int W, int
 
 hipError_t launch_maxpool3s2(const bf16_t* x, long xlo, int B, int H, int W, int C, int OH, int OW, bf16_t* out,
                              long lo, int nsplit, hipStream_t s) {
-  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid_for((long)B * OH * OW * C)), dim3(256), 0, s, x, xlo, B, H, W, C,
-                     OH, OW, out, lo, nsplit);
+  if (C % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid_for((long)B * OH * OW * (C / 8))), dim3(256), 0, s, x, xlo, B, H,
+                     W, C, OH, OW, out, lo, nsplit);
   return hipGetLastError();
 }
 
 namespace {
 
-// torch conv weight [Cout][Cin][kh][kw] fp32 -> [Cout][Kp] bf16 in (kh, kw, c) order, zero for k >= K
-__global__ void pack_conv_kernel(const float* __restrict__ w, int cout, int cin, int k, int Kp, bf16_t* out) {
+// torch conv weight [Cout][Cin][kh][kw] fp32 -> [Cout][Kp] bf16, k = (kh*kwp + kw)*cp + c, 0 on padding
+__global__ void pack_conv_kernel(const float* __restrict__ w, int cout, int cin, int k, int cp, int kwp, int Kp,
+                                 bf16_t* out) {
   const long total = (long)cout * Kp;
-  const int K = cin * k * k;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int kk = (int)(i % Kp);
     const long o = i / Kp;
+    const int c = kk % cp, tap = kk / cp, kh = tap / kwp, kw = tap % kwp;
     float v = 0.f;
-    if (kk < K) {
-      const int c = kk % cin, tap = kk / cin, kh = tap / k, kw = tap % k;
-      v = w[((o * cin + c) * k + kh) * k + kw];
-    }
+    if (c < cin && kw < k && kh < k) v = w[((o * cin + c) * k + kh) * k + kw];
     out[i] = f2bf(v);
+  }
+}
+
+// (B,3,HW,HW) fp32 -> [B][HP][HP][4] planes, HP = HW + 2*border, zero border and channel 3
+__global__ void image_nhwc4_kernel(const float* __restrict__ img, int B, int HW, int border, bf16_t* out, long lo,
+                                   int nsplit) {
+  const int HP = HW + 2 * border;
+  const long total = (long)B * HP * HP;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(i % HP) - border, y = (int)((i / HP) % HP) - border;
+    const long b = i / ((long)HP * HP);
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (y >= 0 && y < HW && x >= 0 && x < HW)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = img[((b * 3 + c) * HW + y) * HW + x];
+    bf16_t h[4], l[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) split_bf(v[c], h[c], l[c]);
+    u32x2 hv = {(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+    *(u32x2*)(out + i * 4) = hv;
+    if (nsplit == 2) {
+      u32x2 lv = {(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
+      *(u32x2*)(out + i * 4 + lo) = lv;
+    }
   }
 }
 
@@ -164,9 +144,19 @@ __global__ void bn_fold_kernel(const float* g, const float* b, const float* mean
 
 }  // namespace
 
-hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int Kp, bf16_t* out, hipStream_t s) {
-  if (Kp < cin * k * k) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pack_conv_kernel, dim3(grid_for((long)cout * Kp)), dim3(256), 0, s, w, cout, cin, k, Kp, out);
+hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int cp, int kwp, int Kp, bf16_t* out,
+                            hipStream_t s) {
+  if (cp < cin || kwp < k || Kp < k * kwp * cp) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_conv_kernel, dim3(grid_for((long)cout * Kp)), dim3(256), 0, s, w, cout, cin, k, cp, kwp,
+                     Kp, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_image_nhwc4(const float* img, int B, int HW, int border, bf16_t* out, long lo, int nsplit,
+                              hipStream_t s) {
+  const long HP = HW + 2 * border;
+  hipLaunchKernelGGL(image_nhwc4_kernel, dim3(grid_for(B * HP * HP)), dim3(256), 0, s, img, B, HW, border, out, lo,
+                     nsplit);
   return hipGetLastError();
 }
 
