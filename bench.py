@@ -43,8 +43,11 @@ PEAK_HBM_GBS = 8000.0
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
 
 
-def pmc_traffic(kernel: str):
-    """Per-launch HBM-side bytes of `kernel` from the committed PMC summary, or None."""
+def pmc_traffic(kernel: str, headline: bool = True):
+    """Per-launch HBM-side bytes of `kernel` from the committed PMC summary (collected on the
+    headline workload: ViT greedy, tools/pmc_bench.sh), or None for any other workload."""
+    if not headline:
+        return None
     try:
         with open(TRAFFIC_JSON) as f:
             table = json.load(f)
@@ -193,6 +196,7 @@ def main():
     if rank == 0:
         step_ms = el / args.steps * 1e3
         dom = max(prof, key=lambda p: p["ms"])
+        headline = args.model == "vit" and args.mode == "greedy"  # the PMC summary's workload
         avg_ms = dom["ms"] / max(dom["launches"], 1)
         for p in prof:
             log(f"  {p['kernel']:34s} launches {p['launches']:6d}  {p['ms'] / args.steps:9.3f} ms/step  "
@@ -201,11 +205,11 @@ def main():
         if "attn" in dom["kernel"] and "cross" in dom["kernel"]:
             achieved = dom["bytes"] / dom["launches"] / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(dom["kernel"])}
+                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(dom["kernel"], headline)}
         else:
             achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
             roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(dom["kernel"])}
+                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(dom["kernel"], headline)}
         roof.update({"kernel": dom["kernel"], "launches_per_step": dom["launches"] // args.steps,
                      "avg_launch_us": round(avg_ms * 1e3, 2),
                      "share_of_step": round(dom["ms"] / args.steps / step_ms, 3)})

@@ -82,6 +82,7 @@ SIGNATURES = {
     "icap_encode_vit": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "icap_encode_grid_tail": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "icap_encode_grid": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "icap_preprocess": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "icap_decode_greedy": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_void_p]),
     "icap_decode_sample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,

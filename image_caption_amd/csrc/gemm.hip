@@ -191,10 +191,23 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 int gemm_tile_class(const GemmArgs& g) {
+  static int force = -1;  // measurement knob for the trunk convolutions (GEMMs with a BN scale)
+  if (force < 0) {
+    const char* v = getenv("ICAP_CONV_CLASS");
+    force = v ? atoi(v) : 0;
+  }
+  if (force && g.scale) {
+    if (force == 256 && g.N % 256 == 0 && g.batch == 1) return PROF_GEMM_256;
+    if (force == 128 && g.N % 128 == 0) return PROF_GEMM_128;
+    if (force == 64) return PROF_GEMM_64;
+  }
+  // 256 x 256 tiles whenever N allows and there are >= 96 of them (trunk sweep, profiles/r01
+  // v6_trunk_class_sweep.txt: even 98-196 tiles beat 4x as many 128 x 128 tiles); 128 x 128 only for
+  // N >= 256 (at N = 128 the 64 x 64 kernel is faster)
   const long huge_tiles = (long)((g.M + 255) / 256) * (g.N / 256) * g.batch;
-  if (g.N % 256 == 0 && g.batch == 1 && huge_tiles >= 256) return PROF_GEMM_256;
+  if (g.N % 256 == 0 && g.batch == 1 && huge_tiles >= 96) return PROF_GEMM_256;
   const long big_tiles = (long)((g.M + 127) / 128) * (g.N / 128) * g.batch;
-  return (g.N % 128 == 0 && big_tiles >= 512) ? PROF_GEMM_128 : PROF_GEMM_64;
+  return (g.N % 128 == 0 && g.N >= 256 && big_tiles >= 512) ? PROF_GEMM_128 : PROF_GEMM_64;
 }
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {

@@ -875,6 +875,14 @@ int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, 
   });
 }
 
+int icap_preprocess(const uint8_t* pixels, const int64_t* offsets, const int32_t* geom, int B, int S, int max_rows,
+                    uint8_t* tmp, float* out, void* stream) {
+  return guarded([&] {
+    REQUIRE(pixels && offsets && geom && tmp && out && B > 0 && S > 0 && max_rows > 0, "bad arguments");
+    HIPCHK(launch_preprocess(pixels, offsets, geom, B, S, max_rows, tmp, out, (hipStream_t)stream));
+  });
+}
+
 int icap_decode_greedy(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
                        int end_token, int32_t* ids, float* step_logits, void* stream) {
   return guarded([&] {

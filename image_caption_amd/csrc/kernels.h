@@ -98,6 +98,9 @@ hipError_t launch_subsample2(const bf16_t* x, long xlo, int B, int H, int W, int
 hipError_t launch_maxpool3s2(const bf16_t* x, long xlo, int B, int H, int W, int C, int OH, int OW, bf16_t* out,
                              long lo, int nsplit, hipStream_t s);
 // [Cout][Kp] bf16 with k = (kh*kwp + kw)*cp + c (cp >= cin, kwp >= k; padding taps/channels are 0)
+// On-GPU eval preprocessing (preprocess.hip): uint8 RGB images -> normalised (B,3,S,S) fp32
+hipError_t launch_preprocess(const uint8_t* px, const int64_t* offs, const int32_t* geom, int B, int S, int max_rows,
+                             uint8_t* tmp, float* out, hipStream_t s);
 hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int cp, int kwp, int Kp, bf16_t* out,
                             hipStream_t s);
 // (B,3,HW,HW) fp32 -> zero-bordered NHWC4 planes [B][HW+2*border][HW+2*border][4] (channel 3 = 0)

@@ -56,6 +56,22 @@ def preprocess(image_path: str, mode: str = "crop", image_size: int = 224) -> to
     return to_normalized_tensor(img)
 
 
+def decode_rgb(image_path: str) -> np.ndarray:
+    """Image.open(path).convert('RGB') as an (H, W, 3) uint8 array."""
+    return np.asarray(_pil().open(image_path).convert("RGB"))
+
+
+def preprocess_to_device(image_paths, mode: str, device, image_size: int = 224) -> torch.Tensor:
+    """(B,3,S,S) batch on `device`: decode on the host, then on a GPU the whole batch is resized,
+    cropped and normalised by the HIP kernels (image_caption_amd.preprocess, bit-identical to the
+    PIL path of preprocess() above); on the CPU that PIL path itself."""
+    if torch.device(device).type == "cuda":
+        from image_caption_amd.preprocess import preprocess_batch
+
+        return preprocess_batch([decode_rgb(p) for p in image_paths], mode, image_size, device)
+    return torch.stack([preprocess(p, mode, image_size) for p in image_paths])
+
+
 def load_checkpoint(path: str, device):
     """torch.load with weights_only=True (no unpickling of arbitrary objects)."""
     try:

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from models.grid_transformer_model import build_model  # noqa: E402
 from models._common import decode_ids  # noqa: E402
-from scripts._io import default_vocab_path, load_checkpoint, load_vocab, preprocess  # noqa: E402
+from scripts._io import default_vocab_path, load_checkpoint, load_vocab, preprocess, preprocess_to_device  # noqa: E402
 
 
 def load_model(checkpoint_path, device="cuda"):
@@ -32,7 +32,7 @@ def preprocess_image(image_path, image_size=224):
 
 
 def generate_caption(model, image_path, vocab, device="cuda", method="greedy", max_len=50, beam_size=5):
-    image = preprocess_image(image_path).to(device)
+    image = preprocess_to_device([image_path], "square", device)
     with torch.no_grad():
         ids = model.generate(image, start_token=vocab["<start>"], end_token=vocab["<end>"], max_len=max_len,
                              method=method, beam_size=beam_size)

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from models.vit_transformer_model import build_model  # noqa: E402
 from models._common import decode_ids  # noqa: E402
-from scripts._io import default_vocab_path, load_checkpoint, load_vocab, preprocess  # noqa: E402
+from scripts._io import default_vocab_path, load_checkpoint, load_vocab, preprocess, preprocess_to_device  # noqa: E402
 
 
 def load_model(checkpoint_path, device="cuda"):
@@ -55,7 +55,7 @@ def batch_generate_captions(model, image_paths, vocab, device="cuda", method="gr
     """Many images -> captions, batched into one generate call for greedy (ref :158-180)."""
     if method != "greedy":
         return [generate_caption(model, p, vocab, device, method, max_len)[0] for p in image_paths]
-    imgs = torch.stack([preprocess(p, "crop") for p in image_paths]).to(device)
+    imgs = preprocess_to_device(image_paths, "crop", device)
     caps, _ = _captions(model, imgs, vocab, method, max_len)
     for p, c in zip(image_paths, caps):
         print(f"  {os.path.basename(p)}: {c}")
