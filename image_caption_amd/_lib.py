@@ -90,7 +90,7 @@ SIGNATURES = {
     "icap_decode_beam": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                  c_void_p, c_void_p]),
     "icap_decoder_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
-                                     c_void_p]),
+                                     c_void_p, c_void_p]),
     "icap_set_graphs": (c_int, [c_void_p, c_int]),
     "icap_profile_enable": (c_int, [c_void_p, c_int]),
     "icap_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(c_long),

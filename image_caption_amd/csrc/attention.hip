@@ -206,10 +206,14 @@ __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __
 // qkv rows: (b * n_new + i) with [q | k | v] of width 3D.  Cache kc/vc: [B][H][Lmax][64] fp32.
 // anc (optional, beam search): anc[b * Lmax + j] = the cache row holding this row's key/value of
 // position j < t0 (its ancestor at step j); without it the row's own cache is read.
+// klen (optional, tgt_key_padding_mask): keys j >= klen[b] are masked for every query of row b
+// (a query with no key left gets a zero context, as torch's scaled_dot_product_attention path of
+// nn.MultiheadAttention(need_weights=False) returns for a fully masked row).
 __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restrict__ qkv, int n_new, int t0,
                                                            int H, float* kc, float* vc, int Lmax, int causal,
                                                            float scale, bf16_t* out, long lo, int nsplit,
-                                                           const int32_t* __restrict__ anc) {
+                                                           const int32_t* __restrict__ anc,
+                                                           const int32_t* __restrict__ klen) {
   __shared__ float sq[64];
   __shared__ float sp[512];
   const int h = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
@@ -224,7 +228,8 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restri
   }
   for (int i = 0; i < n_new; ++i) {
     const int pos = t0 + i;
-    const int nkeys = causal ? pos + 1 : t0 + n_new;
+    int nkeys = causal ? pos + 1 : t0 + n_new;
+    if (klen) nkeys = min(nkeys, max(klen[b], 0));
     __syncthreads();
     sq[lane] = rows[i * ld + h * 64 + lane];
     __syncthreads();
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restri
       else vv = vcb + (long)key * 64;
       acc = fmaf(sp[key], vv[lane], acc);
     }
-    st_planes(out, ((long)b * n_new + i) * D + h * 64 + lane, lo, nsplit, acc / l);
+    st_planes(out, ((long)b * n_new + i) * D + h * 64 + lane, lo, nsplit, nkeys > 0 ? acc / l : 0.f);
   }
 }
 
@@ -306,10 +311,10 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
 
 hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int H, float* kc, float* vc, int Lmax,
                                 int causal, float scale, bf16_t* out, long lo, int nsplit, hipStream_t s,
-                                const int32_t* anc) {
+                                const int32_t* anc, const int32_t* klen) {
   if (t0 + n_new > Lmax || t0 + n_new > 512 || (anc && n_new != 1)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(dec_self_attn_kernel, dim3(H, B), dim3(64), 0, s, qkv, n_new, t0, H, kc, vc, Lmax, causal,
-                     scale, out, lo, nsplit, anc);
+                     scale, out, lo, nsplit, anc, klen);
   return hipGetLastError();
 }
 

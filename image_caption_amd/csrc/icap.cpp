@@ -609,7 +609,8 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
 // B here counts KV rows (sequences); mem_rpi = decoder rows per memory image (default n_new; the
 // beam slots of an image for beam search); anc = beam ancestry table for the self-attention.
 void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int Lmax, int causal,
-                    int S, hipStream_t s, const int32_t* anc = nullptr, int mem_rpi = 0) {
+                    int S, hipStream_t s, const int32_t* anc = nullptr, int mem_rpi = 0,
+                    const int32_t* klen = nullptr) {
   const icap_model_desc& d = h->d;
   const int D = d.d_model, H = d.nhead, F = d.dim_ff, rows = B * n_new, ns = h->ns;
   if (mem_rpi <= 0) mem_rpi = n_new;
@@ -622,7 +623,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
     h->wgemm(b.a, D, b.aL, L.sa_qkv.w, D, L.sa_qkv.b, rows, 3 * D, D, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, WAVE_2x2,
              1, 0, s);
     HIPCHK(launch_dec_self_attn(b.qkv, B, n_new, t0, H, b.kc + l * kv_layer, b.vc + l * kv_layer, Lmax, causal,
-                                0.125f, b.o, b.aL, ns, s, anc));
+                                0.125f, b.o, b.aL, ns, s, anc, klen));
     h->wgemm(b.o, D, b.aL, L.sa_out.w, D, nullptr, rows, D, D, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_D,
              PS, s);
     HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_D, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
@@ -911,7 +912,7 @@ int icap_decode_beam(icap_handle* h, const float* memory, int B, int S, int max_
 }
 
 int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const float* memory, int S, int causal,
-                         float* logits, void* stream) {
+                         const int32_t* key_lengths, float* logits, void* stream) {
   return guarded([&] {
     REQUIRE(h && tgt && memory && logits && B > 0 && T > 0, "bad arguments");
     REQUIRE(T <= h->d.pe_len, "sequence longer than the positional-encoding table");
@@ -922,7 +923,7 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
     HIPCHK(launch_split_f32(memory, b.memL, b.memp, b.memL, h->ns, s));
     const float scale = (float)std::sqrt((double)D);
     HIPCHK(launch_embed(tgt, T, 0, rows, T, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
-    decoder_layers(h, b, B, T, 0, T, causal, S, s);
+    decoder_layers(h, b, B, T, 0, T, causal, S, s, nullptr, 0, key_lengths);
     HeadArgs ha{};
     ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = h->d.vocab;
     ha.logits = logits; ha.ld_logits = h->d.vocab;

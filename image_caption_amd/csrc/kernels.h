@@ -121,7 +121,7 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
 // Decoder self-attention with fp32 KV cache; n_new query rows per image starting at t0.
 hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int H, float* kc, float* vc,
                                 int Lmax, int causal, float scale, bf16_t* out, long lo, int nsplit,
-                                hipStream_t s, const int32_t* anc = nullptr);
+                                hipStream_t s, const int32_t* anc = nullptr, const int32_t* klen = nullptr);
 // Cross-attention in the key-absorbed form on MFMA: rows hold q~_h = q_h·Wk_h (8 heads x 512) as bf16
 // planes (plane stride qt_lo); memory (images, S, 512) as bf16 planes (mem_lo); context planes out.
 hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* mem, long mem_lo, int rows,

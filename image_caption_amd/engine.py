@@ -257,13 +257,22 @@ class Engine:
                                         lens.data_ptr(), stream_ptr(self.device)), "icap_decode_beam")
         return ids, lens
 
-    def decoder_forward(self, tgt: torch.Tensor, memory: torch.Tensor, causal: bool) -> torch.Tensor:
+    def decoder_forward(self, tgt: torch.Tensor, memory: torch.Tensor, causal: bool,
+                        key_lengths: torch.Tensor | None = None) -> torch.Tensor:
+        """Full-prefix decoder: tgt (B,T) -> logits (B,T,V).  key_lengths (B,): tgt_key_padding_mask as
+        lengths (keys j >= key_lengths[b] masked), None = no padding mask."""
         t = tgt.to(device=self.device, dtype=torch.int32).contiguous()
         mem = memory.to(device=self.device, dtype=torch.float32).contiguous()
         B, T = t.shape
+        kl = None
+        if key_lengths is not None:
+            kl = key_lengths.to(device=self.device, dtype=torch.int32).contiguous()
+            if kl.shape != (B,):
+                raise ValueError(f"key_lengths must have shape ({B},), got {tuple(kl.shape)}")
         logits = torch.empty(B, T, self.vocab, device=self.device, dtype=torch.float32)
         check(self.lib.icap_decoder_forward(self.handle, t.data_ptr(), B, T, mem.data_ptr(), mem.shape[1],
-                                            int(bool(causal)), logits.data_ptr(), stream_ptr(self.device)),
+                                            int(bool(causal)), None if kl is None else kl.data_ptr(),
+                                            logits.data_ptr(), stream_ptr(self.device)),
               "icap_decoder_forward")
         return logits
 

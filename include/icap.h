@@ -107,6 +107,16 @@ int icap_encode_grid_tail(icap_handle* h, const float* feats, int B, float* memo
  * Replaces: GridFeatureEncoder.forward, models/grid_transformer_model.py:86-108 (self.cnn included). */
 int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, void* stream);
 
+/* Eval preprocessing on the GPU, bit-identical to the reference's torchvision-on-PIL transforms:
+ * decoded RGB uint8 images (HWC, any size; image b at pixels + offsets[b]) -> out (B,3,S,S) fp32
+ * normalised with the ImageNet mean/std.  geom (B x 8 int32: in_h, in_w, resized h, resized w,
+ * crop top, crop left, first source row, source row count) selects Resize(256)+CenterCrop(S) or
+ * Resize((S,S)); tmp holds B x max_rows x S x 4 bytes.  Model-independent (no handle).
+ * Replaces: the transforms.Compose of scripts/inference_vit_transformer.py:75-80 /
+ * scripts/inference_grid_transformer.py:43-47 (utils/deepfashion_dataset.py:223-228 for eval). */
+int icap_preprocess(const uint8_t* pixels, const int64_t* offsets, const int32_t* geom, int B, int S, int max_rows,
+                    uint8_t* tmp, float* out, void* stream);
+
 /* Greedy decode of max_len-1 steps with a KV cache: ids (B,max_len) int32, column 0 = start.
  * step_logits (max_len-1,B,vocab) fp32 is optional (NULL to skip).  The reference's batch-global
  * stop rule (break when every latest token == end) is applied by the caller on the returned ids.
@@ -132,10 +142,13 @@ int icap_decode_sample(icap_handle* h, const float* memory, int B, int S, int ma
                        int end_token, const float* uniforms, int32_t* ids, float* logp, void* stream);
 
 /* Full-prefix decoder forward: tgt (B,T) int32 -> logits (B,T,vocab) fp32, causal or unmasked.
- * Replaces: TransformerDecoder.forward, models/vit_transformer_model.py:155-182 (no padding masks;
- * causal=0 is the scripts/inference.py:79 call without tgt_mask). */
+ * key_lengths (B int32, device, optional): tgt_key_padding_mask as lengths - keys j >= key_lengths[b]
+ * are masked in the self-attention (NULL = no padding mask).
+ * Replaces: TransformerDecoder.forward, models/vit_transformer_model.py:155-182 (causal=0 is the
+ * scripts/inference.py:79 call without tgt_mask); with key_lengths, the teacher-forced forward
+ * ViTTransformerCaptioning.forward vit:216-255 (lengths) / grid:185-207 (lengths - 1). */
 int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const float* memory, int S,
-                         int causal, float* logits, void* stream);
+                         int causal, const int32_t* key_lengths, float* logits, void* stream);
 
 /* Enable (1, default) / disable (0) hipGraph capture of the decode loop: the first decode call
  * with a new (B, S, max_len, mode) runs eagerly, the next captures ~80 kernels x (max_len-1)

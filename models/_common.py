@@ -27,8 +27,9 @@ class PositionalEncoding(nn.Module):
 
 class TransformerDecoder(nn.Module):
     """Token embedding * sqrt(d) + PE -> 6 post-LN nn.TransformerDecoderLayer -> fc_out
-    (vit:103-182, grid:113-158).  In eval/no-grad on a GPU the forward runs on the HIP engine
-    (icap_decoder_forward): causal mask or no mask, no padding masks."""
+    (vit:103-182, grid:113-158).  In eval on a GPU the forward runs on the HIP engine
+    (icap_decoder_forward): causal mask or no mask, with or without a tgt_key_padding_mask of the
+    form the captioners build (True on a suffix of each row = key lengths)."""
 
     def __init__(self, vocab_size, d_model=512, nhead=8, num_layers=6, dim_feedforward=2048, dropout=0.1,
                  max_len=100):
@@ -56,10 +57,13 @@ class TransformerDecoder(nn.Module):
     def forward(self, tgt, memory, tgt_mask=None, tgt_key_padding_mask=None, memory_key_padding_mask=None):
         owner = owner_of(self)
         T = tgt.shape[1]
-        if (owner is not None and tgt_key_padding_mask is None and memory_key_padding_mask is None
+        if (owner is not None and memory_key_padding_mask is None
                 and (tgt_mask is None or is_causal_mask(tgt_mask, T)) and not self.training
                 and owner.use_hip(memory)):
-            return owner.hip_engine(memory.device).decoder_forward(tgt, memory, causal=tgt_mask is not None)
+            klen = suffix_mask_lengths(tgt_key_padding_mask, T) if tgt_key_padding_mask is not None else None
+            if tgt_key_padding_mask is None or klen is not None:
+                return owner.hip_engine(memory.device).decoder_forward(tgt, memory, causal=tgt_mask is not None,
+                                                                       key_lengths=klen)
         x = self.pos_encoder(self.embedding(tgt) * math.sqrt(self.d_model))
         x = self.transformer_decoder(x, memory, tgt_mask=tgt_mask, tgt_key_padding_mask=tgt_key_padding_mask,
                                      memory_key_padding_mask=memory_key_padding_mask)
@@ -67,10 +71,26 @@ class TransformerDecoder(nn.Module):
 
 
 def padding_mask(tgt: torch.Tensor, lengths) -> torch.Tensor:
-    """True at positions >= length (vit:257-274)."""
+    """vit:257-274 / grid:209-216: mask[i, length:] = True when length < seq_len - Python slicing,
+    so a negative length (grid's lengths - 1 of an empty caption) masks only the last -length keys."""
     B, T = tgt.shape
-    lens = torch.as_tensor([int(l) for l in lengths], device=tgt.device)
+    starts = []
+    for l in lengths:
+        l = int(l)
+        starts.append(T if l >= T else (l if l >= 0 else max(T + l, 0)))
+    lens = torch.as_tensor(starts, device=tgt.device)
     return torch.arange(T, device=tgt.device)[None, :] >= lens[:, None]
+
+
+def suffix_mask_lengths(mask: torch.Tensor, T: int):
+    """(B,) key lengths of a bool key-padding mask that is True exactly on a suffix of every row
+    (what padding_mask builds), else None (the mask then stays on the PyTorch path)."""
+    if mask.dtype != torch.bool or mask.dim() != 2 or mask.shape[1] != T:
+        return None
+    klen = (~mask).sum(1)
+    if not torch.equal(mask, torch.arange(T, device=mask.device)[None, :] >= klen[:, None]):
+        return None
+    return klen
 
 
 def greedy_torch(model, images, start_token, end_token, max_len):

@@ -58,8 +58,10 @@ def gelu_erf(x: Tensor) -> Tensor:
 
 
 def mha(q_in: Tensor, kv_in: Tensor, in_w: Tensor, in_b: Tensor, out_w: Tensor,
-        out_b: Tensor, nhead: int, causal: bool) -> Tensor:
-    """torch `F.multi_head_attention_forward` semantics (batch_first), no dropout."""
+        out_b: Tensor, nhead: int, causal: bool, key_pad: Optional[Tensor] = None) -> Tensor:
+    """torch `F.multi_head_attention_forward` semantics (batch_first), no dropout.  key_pad (B,S)
+    bool masks keys; a query left with no key gets a zero context, which is what the
+    scaled_dot_product_attention path (need_weights=False, the TransformerDecoderLayer call) returns."""
     B, T, D = q_in.shape
     S = kv_in.shape[1]
     hd = D // nhead
@@ -73,7 +75,10 @@ def mha(q_in: Tensor, kv_in: Tensor, in_w: Tensor, in_b: Tensor, out_w: Tensor,
     if causal:
         m = torch.ones(T, S, dtype=torch.bool).triu(1 + S - T)
         s = s.masked_fill(m, float("-inf"))
+    if key_pad is not None:
+        s = s.masked_fill(key_pad[:, None, None, :], float("-inf"))
     p = torch.softmax(s, dim=-1)
+    p = torch.nan_to_num(p, nan=0.0)  # fully masked rows
     o = (p @ v).transpose(1, 2).reshape(B, T, D)
     return linear(o, out_w, out_b)
 
@@ -162,8 +167,27 @@ def grid_encode(sd: Dict[str, Tensor], images: Tensor) -> Tensor:
 
 
 # --------------------------------------------------------------------------- decoder
+def padding_mask(tgt: Tensor, lengths) -> Tensor:
+    """`_generate_padding_mask` (vit:257-274): mask[i, length:] = True when length < seq_len, with
+    Python slicing (a negative length masks the last -length positions)."""
+    B, T = tgt.shape
+    mask = torch.zeros(B, T, dtype=torch.bool)
+    for i, length in enumerate(lengths):
+        if int(length) < T:
+            mask[i, int(length):] = True
+    return mask
+
+
+def training_forward(sd: Dict[str, Tensor], memory: Tensor, captions: Tensor, lengths, grid: bool = False) -> Tensor:
+    """Teacher-forced forward after the encoder: vit:216-255 (padding from lengths) or grid:185-207
+    (padding from lengths - 1)."""
+    tgt = captions[:, :-1]
+    lens = [int(l) - 1 for l in lengths] if grid else lengths
+    return decoder_forward(sd, tgt, memory, True, key_pad=padding_mask(tgt, lens))
+
+
 def decoder_forward(sd: Dict[str, Tensor], tgt: Tensor, memory: Tensor, causal: bool = True,
-                    nhead: int = 8) -> Tensor:
+                    nhead: int = 8, key_pad: Optional[Tensor] = None) -> Tensor:
     """`TransformerDecoder.forward` (vit:155-182): tgt (B,T) int -> logits (B,T,V)."""
     emb = sd["decoder.embedding.weight"]
     d = emb.shape[1]
@@ -173,7 +197,7 @@ def decoder_forward(sd: Dict[str, Tensor], tgt: Tensor, memory: Tensor, causal: 
     while f"decoder.transformer_decoder.layers.{i}.norm1.weight" in sd:
         p = f"decoder.transformer_decoder.layers.{i}."
         h = mha(x, x, sd[p + "self_attn.in_proj_weight"], sd[p + "self_attn.in_proj_bias"],
-                sd[p + "self_attn.out_proj.weight"], sd[p + "self_attn.out_proj.bias"], nhead, causal)
+                sd[p + "self_attn.out_proj.weight"], sd[p + "self_attn.out_proj.bias"], nhead, causal, key_pad)
         x = layer_norm(x + h, sd[p + "norm1.weight"], sd[p + "norm1.bias"], 1e-5)
         h = mha(x, memory, sd[p + "multihead_attn.in_proj_weight"], sd[p + "multihead_attn.in_proj_bias"],
                 sd[p + "multihead_attn.out_proj.weight"], sd[p + "multihead_attn.out_proj.bias"], nhead, False)

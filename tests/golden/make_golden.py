@@ -19,8 +19,8 @@ What is restated because its module cannot import here:
     around the reference decoder module, with torch.multinomial replaced by inverse-CDF sampling
     on fixed uniforms.
 
-Usage: python tests/golden/make_golden.py [beam_vit]   (writes tests/golden/*.npz, ~2 min on 8 cores;
-       with beam_vit only the beam-search fixture)
+Usage: python tests/golden/make_golden.py [beam_vit|forward]   (writes tests/golden/*.npz, ~2 min on
+       8 cores; with beam_vit / forward only that fixture)
 """
 from __future__ import annotations
 
@@ -123,11 +123,49 @@ def make_beam(ref, sd, imgs, out):
     out["beam_vit"] = (len(cases),)
 
 
+def make_forward(ref, out):
+    # (vii) teacher-forced training forward with padding masks: the reference's OWN
+    # ViTTransformerCaptioning.forward (vit:216-255, padding from caption_lengths) and the Grid form
+    # (grid:185-207: padding from caption_lengths - 1, restated around the reference decoder and its
+    # own _generate_padding_mask, since grid_transformer_model.py imports torchvision).  Lengths cover
+    # a full row, a partial one, 1, 0 (every key masked) and, for Grid, -1 (mask[i, -1:] slicing).
+    from models.grid_transformer_model import GridFeatureEncoder
+
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0))
+    rng = np.random.Generator(np.random.PCG64(11))
+    caps = rng.integers(0, W.VOCAB_SIZE, size=(4, 17)).astype(np.int64)
+    caps[:, 0] = W.START_TOKEN
+    captions = torch.from_numpy(caps)
+    vit_len = [17, 9, 1, 0]
+    model = ref_vit_model(ref, W.to_torch(W.vit_state_dict(0)))
+    with torch.no_grad():
+        vit_logits = model(imgs, captions, vit_len)
+    gsd = W.to_torch(W.grid_state_dict(0))
+    genc = GridFeatureEncoder(pretrained_cnn=False)
+    genc.load_state_dict({k[len("encoder."):]: v for k, v in gsd.items() if k.startswith("encoder.")}, strict=True)
+    gdec = ref_decoder(ref, gsd)
+    grid_len = [17, 9, 2, 0]
+    with torch.no_grad():
+        gmem = genc.eval()(imgs)
+        tgt = captions[:, :-1]
+        pad = ref.ViTTransformerCaptioning._generate_padding_mask(None, tgt, [l - 1 for l in grid_len])
+        grid_logits = gdec(tgt, gmem, tgt_mask=gdec.generate_square_subsequent_mask(tgt.size(1), "cpu"),
+                           tgt_key_padding_mask=pad)
+    np.savez_compressed(os.path.join(HERE, "forward_b4.npz"), captions=caps, vit_lengths=np.array(vit_len),
+                        grid_lengths=np.array(grid_len), vit_logits=vit_logits.numpy(),
+                        grid_logits=grid_logits.numpy())
+    out["forward_b4"] = vit_logits.shape
+
+
 def main():
     torch.manual_seed(0)
     torch.set_num_threads(os.cpu_count() or 8)
     ref = load_ref_vit_module()
     out = {}
+    if sys.argv[1:] == ["forward"]:  # regenerate only the training-forward fixture
+        make_forward(ref, out)
+        print(out)
+        return
     if sys.argv[1:] == ["beam_vit"]:  # regenerate only the beam fixture
         make_beam(ref, W.to_torch(W.vit_state_dict(0)), torch.from_numpy(W.synthetic_images(4, seed=0)), out)
         print(out)
@@ -214,6 +252,7 @@ def main():
                         memory_head=gmem[:, :4, :16].numpy(), logits_tf=gtf.numpy(), margins=top2(gtf))
     out["grid_b4"] = gids.shape
     make_beam(ref, sd, imgs, out)
+    make_forward(ref, out)
     for k, v in out.items():
         print(k, tuple(v) if hasattr(v, "__len__") else v)
 

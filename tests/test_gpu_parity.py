@@ -272,3 +272,32 @@ def test_dropin_beam_search_runs_hip(cuda, vit_sd):
     sel = [j for j in range(len(g["image"])) if g["image"][j] == 0 and g["beam"][j] == 5][0]
     n = int(g["lengths"][sel])
     assert out.shape == (1, n) and np.array_equal(out[0].cpu().numpy(), g["ids"][sel][:n])
+
+
+@pytest.mark.parametrize("kind", ["vit", "grid"])
+def test_dropin_training_forward_with_padding_masks(cuda, kind):
+    """model(images, captions, caption_lengths) in eval (validation-loss form) runs encoder and
+    masked decoder on HIP and matches the reference's forward (forward_b4.npz), including a row
+    whose keys are all masked (ViT length 0) and Grid's lengths - 1 slicing (length 0 -> -1)."""
+    g = gold("forward_b4.npz")
+    if kind == "vit":
+        from models.vit_transformer_model import build_model
+
+        m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False})
+        m.load_state_dict(W.to_torch(W.vit_state_dict(0)))
+    else:
+        from models.grid_transformer_model import build_model
+
+        m = build_model(W.VOCAB_SIZE, {"pretrained_cnn": False})
+        m.load_state_dict(W.to_torch(W.grid_state_dict(0)))
+    m = m.to(cuda).eval()
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    caps = torch.from_numpy(g["captions"]).to(cuda)
+    eng = m.hip_engine(cuda)
+    calls = []
+    orig = eng.decoder_forward
+    eng.decoder_forward = lambda *a, **k: calls.append(k.get("key_lengths")) or orig(*a, **k)
+    with torch.no_grad():
+        out = m(imgs, caps, g[f"{kind}_lengths"].tolist())
+    assert len(calls) == 1 and calls[0] is not None  # the masked forward ran on HIP
+    assert np.abs(out.cpu().numpy() - g[f"{kind}_logits"]).max() < 1e-3

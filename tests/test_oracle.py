@@ -176,3 +176,17 @@ def test_beam_search_matches_reference(vit_sd):
         sd["decoder.fc_out.bias"] = b
         got = O.beam_from_memory(sd, mem[i:i + 1], W.START_TOKEN, W.END_TOKEN, 30, int(k))
         assert got.shape[1] == n and np.array_equal(got[0].numpy(), row[:n])
+
+
+def test_training_forward_matches_reference(vit_sd):
+    """Oracle teacher-forced forward with padding masks vs the reference's own forward
+    (forward_b4.npz: vit:216-255 lengths, grid:185-207 lengths - 1, incl. fully masked rows)."""
+    g = gold("forward_b4.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0))
+    caps = torch.from_numpy(g["captions"])
+    with torch.no_grad():
+        vit = O.training_forward(vit_sd, O.vit_encode(vit_sd, imgs), caps, g["vit_lengths"].tolist())
+        gsd = W.to_torch(W.grid_state_dict(0))
+        grid = O.training_forward(gsd, O.grid_encode(gsd, imgs), caps, g["grid_lengths"].tolist(), grid=True)
+    assert np.abs(vit.numpy() - g["vit_logits"]).max() < 1e-4
+    assert np.abs(grid.numpy() - g["grid_logits"]).max() < 1e-4
