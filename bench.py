@@ -154,6 +154,8 @@ def main():
         refs = [[torch.randint(1, 100, (int(torch.randint(5, 13, (1,), generator=gen)),), generator=gen).tolist()]
                 for _ in range(total)]
         uni = torch.rand(L - 1, B, generator=gen).to(dev)
+        ref_rows, ref_off = cider.pack_references(refs, W.PAD_TOKEN, W.END_TOKEN, W.VOCAB_SIZE)
+        ref_rows, ref_off = ref_rows.to(dev), ref_off.to(dev)
 
         def step():  # noqa: F811
             mem = encode()
@@ -163,11 +165,13 @@ def main():
                 sid, gid = parallel.gather_rows(sid, total), parallel.gather_rows(gid, total)
             sid, gid = sid.long(), apply_stop_rule(gid.long(), W.END_TOKEN)
             sid = sid[:, : sample_stop_length(sid, W.END_TOKEN)]
-            if rank == 0:
-                cap = lambda r: cider.caption_ids(r, W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN)
-                s_r = cider.cider_d([cap(r) for r in sid.tolist()], refs)[1]
-                g_r = cider.cider_d([cap(r) for r in gid.tolist()], refs)[1]
-                return torch.tensor(s_r) - torch.tensor(g_r)
+            if rank == 0:  # CIDEr-D of both sets over the GLOBAL batch, one GPU pass (icap_cider_d)
+                hyp = torch.full((2 * total, max(sid.shape[1], gid.shape[1])), W.PAD_TOKEN, dtype=torch.int32,
+                                 device=dev)
+                hyp[:total, : sid.shape[1]] = sid
+                hyp[total:, : gid.shape[1]] = gid
+                r = cider.cider_d_device(hyp, ref_rows, ref_off, W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN).float()
+                return r[:total] - r[total:]
             return gid
 
     for _ in range(args.warmup):

@@ -95,3 +95,63 @@ def caption_ids(row: Sequence[int], start: int, end: int, pad: int) -> List[int]
         if t != start and t != pad:
             out.append(int(t))
     return out
+
+
+def cider_d_device(hyp, refs, ref_off, start: int, end: int, pad: int):
+    """CIDEr-D on the GPU (libicap icap_cider_d): hyp (n_hyp, Lh) raw id rows, hypothesis k scored
+    against image k % B; refs (n_ref, Lr) raw id rows with image i's references at rows
+    ref_off[i] .. ref_off[i+1] (ref_off: B + 1).  <start>/<pad> are dropped and rows end at <end>
+    (caption_ids semantics).  Returns float64 scores (n_hyp,) on the hyp's device, equal to
+    cider_d([caption_ids(h)], [[caption_ids(r) ...]]) per image up to double rounding."""
+    import torch
+
+    from . import _lib
+
+    lib = _lib.load()
+    dev = hyp.device
+    if dev.type != "cuda":
+        raise _lib.IcapError("icap_cider_d needs GPU tensors")
+    h = hyp.to(dtype=torch.int32).contiguous()
+    r = refs.to(device=dev, dtype=torch.int32).contiguous()
+    off = torch.as_tensor(ref_off, dtype=torch.int32).to(dev).contiguous()
+    B = off.numel() - 1
+    if r.numel() == 0:  # no reference rows at all: keep a valid pointer
+        r = torch.full((1, 1), end, dtype=torch.int32, device=dev)
+    n_ref, Lr = r.shape
+    ws_bytes = lib.icap_cider_workspace_bytes(n_ref, Lr)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    scores = torch.empty(h.shape[0], dtype=torch.float64, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(lib.icap_cider_d(h.data_ptr(), h.shape[0], h.shape[1], B, r.data_ptr(), n_ref, Lr, off.data_ptr(),
+                                    start, end, pad, scores.data_ptr(), ws.data_ptr(), ws_bytes, status.data_ptr(),
+                                    _lib.stream_ptr(dev)), "icap_cider_d")
+    if int(status.item()):
+        raise _lib.IcapError("icap_cider_d: an image's reference set exceeds 4096 distinct n-grams")
+    return scores
+
+
+def pack_references(refs: Sequence[Sequence[Sequence]], pad: int, end: int, vocab_size: int):
+    """Per-image reference token lists (ids, or words already mapped) -> (rows (n_ref, Lr) int32 padded
+    with <pad> and terminated by <end>, ref_off (B + 1)).  Words that are not ids get fresh ids above
+    the vocabulary, consistently within the call, so their n-grams stay distinct."""
+    import torch
+
+    extra: Dict = {}
+    rows, off = [], [0]
+    for rs in refs:
+        for ref in rs:
+            ids = []
+            for t in ref:
+                if not isinstance(t, int):
+                    t = extra.setdefault(t, vocab_size + len(extra))
+                ids.append(int(t))
+            rows.append(ids)
+        off.append(len(rows))
+    Lr = max([len(x) for x in rows] + [0]) + 1
+    mat = torch.full((max(len(rows), 1), Lr), pad, dtype=torch.int32)
+    for i, ids in enumerate(rows):
+        if ids:
+            mat[i, : len(ids)] = torch.tensor(ids, dtype=torch.int32)
+        mat[i, len(ids)] = end
+    return mat, torch.tensor(off, dtype=torch.int32)

@@ -876,6 +876,19 @@ int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, 
   });
 }
 
+size_t icap_cider_workspace_bytes(long n_ref, int Lr) { return cider_workspace_bytes(n_ref, Lr); }
+
+int icap_cider_d(const int32_t* hyp, int n_hyp, int Lh, int B, const int32_t* refs, int n_ref, int Lr,
+                 const int32_t* ref_off, int start_token, int end_token, int pad_token, double* scores,
+                 void* workspace, size_t workspace_bytes, int32_t* status, void* stream) {
+  return guarded([&] {
+    REQUIRE(hyp && refs && ref_off && scores && workspace && status, "bad arguments");
+    REQUIRE(Lh <= CIDER_MAX_TOKENS && Lr <= CIDER_MAX_TOKENS, "caption rows longer than 192 tokens");
+    HIPCHK(launch_cider(hyp, n_hyp, Lh, B, refs, n_ref, Lr, ref_off, start_token, end_token, pad_token, scores,
+                        workspace, workspace_bytes, status, (hipStream_t)stream));
+  });
+}
+
 int icap_preprocess(const uint8_t* pixels, const int64_t* offsets, const int32_t* geom, int B, int S, int max_rows,
                     uint8_t* tmp, float* out, void* stream) {
   return guarded([&] {

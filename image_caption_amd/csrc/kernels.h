@@ -98,6 +98,13 @@ hipError_t launch_subsample2(const bf16_t* x, long xlo, int B, int H, int W, int
 hipError_t launch_maxpool3s2(const bf16_t* x, long xlo, int B, int H, int W, int C, int OH, int OW, bf16_t* out,
                              long lo, int nsplit, hipStream_t s);
 // [Cout][Kp] bf16 with k = (kh*kwp + kw)*cp + c (cp >= cin, kwp >= k; padding taps/channels are 0)
+// CIDEr-D on token-id rows (cider.hip): hypothesis k belongs to image k % B; image i's references
+// are rows ref_off[i] .. ref_off[i+1]; rows are raw ids (<start>/<pad> dropped, cut at <end>)
+constexpr int CIDER_MAX_TOKENS = 192;
+size_t cider_workspace_bytes(long ref_rows, int Lr);
+hipError_t launch_cider(const int32_t* hyp, int n_hyp, int Lh, int B, const int32_t* refs, int n_ref, int Lr,
+                        const int32_t* ref_off, int start, int end, int pad, double* scores, void* ws,
+                        size_t ws_bytes, int* overflow, hipStream_t s);
 // On-GPU eval preprocessing (preprocess.hip): uint8 RGB images -> normalised (B,3,S,S) fp32
 hipError_t launch_preprocess(const uint8_t* px, const int64_t* offs, const int32_t* geom, int B, int S, int max_rows,
                              uint8_t* tmp, float* out, hipStream_t s);

@@ -107,6 +107,21 @@ int icap_encode_grid_tail(icap_handle* h, const float* feats, int B, float* memo
  * Replaces: GridFeatureEncoder.forward, models/grid_transformer_model.py:86-108 (self.cnn included). */
 int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, void* stream);
 
+/* CIDEr-D rewards on the GPU over token-id rows (pycocoevalcap CiderScorer: n = 1..4, tf-idf with
+ * the document frequency over THIS call's reference sets, clipped cosine, Gaussian length penalty,
+ * sigma 6, x10).  hyp (n_hyp, Lh) int32: hypothesis k scores against image k % B (n_hyp = H * B lets
+ * several hypothesis sets - SCST sample and greedy - share one df pass); refs (n_ref, Lr) int32, image
+ * i's references are rows ref_off[i] .. ref_off[i+1] (ref_off: B+1 int32).  Rows are raw ids:
+ * <start>/<pad> are dropped and a row ends at its first <end>.  Lh, Lr <= 192.  scores (n_hyp) fp64.
+ * workspace >= icap_cider_workspace_bytes(n_ref, Lr) device bytes; status (1 int32, device) is set
+ * non-zero when an image's reference set exceeds 4096 distinct n-grams (scores then invalid).
+ * Replaces: CiderRewardCalculator.compute_reward -> Cider().compute_score, utils/scst_loss.py:20-54,
+ * called twice per SCST step (:179-180). */
+size_t icap_cider_workspace_bytes(long n_ref, int Lr);
+int icap_cider_d(const int32_t* hyp, int n_hyp, int Lh, int B, const int32_t* refs, int n_ref, int Lr,
+                 const int32_t* ref_off, int start_token, int end_token, int pad_token, double* scores,
+                 void* workspace, size_t workspace_bytes, int32_t* status, void* stream);
+
 /* Eval preprocessing on the GPU, bit-identical to the reference's torchvision-on-PIL transforms:
  * decoded RGB uint8 images (HWC, any size; image b at pixels + offsets[b]) -> out (B,3,S,S) fp32
  * normalised with the ImageNet mean/std.  geom (B x 8 int32: in_h, in_w, resized h, resized w,

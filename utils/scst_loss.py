@@ -10,7 +10,8 @@ Changes on the hot path:
     without dropout (the reference samples in train mode with dropout 0.1 active, :161);
   * when autograd is on, the sampled sequence's log-probs are recomputed teacher-forced through
     the PyTorch decoder (train mode) so the REINFORCE loss has a gradient;
-  * CIDEr-D is image_caption_amd.cider on token ids (pycocoevalcap is absent; parity unpinned).
+  * CIDEr-D is image_caption_amd.cider on token ids (pycocoevalcap is absent; parity unpinned); on
+    the HIP path both reward sets are scored in one GPU pass (icap_cider_d, cider.hip).
 BLEU / combined rewards and MixedLoss are training-only and not provided.
 """
 from __future__ import annotations
@@ -83,12 +84,23 @@ class SCSTLoss(nn.Module):
         with torch.no_grad():
             greedy_ids = model.generate(images, start, end, max_len, method="greedy")
         refs = [[_split(r, vocab) for r in (rs if isinstance(rs, list) else [rs])] for rs in references]
-        s_r = self.reward_calculator.compute_reward_ids(
-            [_cider.caption_ids(r, start, end, pad) for r in sample_ids.tolist()], refs)
-        g_r = self.reward_calculator.compute_reward_ids(
-            [_cider.caption_ids(r, start, end, pad) for r in greedy_ids.tolist()], refs)
-        s_r = torch.tensor(s_r, device=device, dtype=torch.float)
-        g_r = torch.tensor(g_r, device=device, dtype=torch.float)
+        if sample_ids.is_cuda and getattr(model, "hip_backend", "torch") != "torch":
+            # both reward sets in one GPU CIDEr-D pass over token ids (icap_cider_d)
+            B = sample_ids.shape[0]
+            rows, off = _cider.pack_references(refs, pad, end, max(vocab.values()) + 1)
+            hyp = torch.full((2 * B, max(sample_ids.shape[1], greedy_ids.shape[1])), pad, dtype=torch.int32,
+                             device=sample_ids.device)
+            hyp[:B, : sample_ids.shape[1]] = sample_ids
+            hyp[B:, : greedy_ids.shape[1]] = greedy_ids
+            r = _cider.cider_d_device(hyp, rows, off, start, end, pad).to(device=device, dtype=torch.float)
+            s_r, g_r = r[:B], r[B:]
+        else:
+            s_r = self.reward_calculator.compute_reward_ids(
+                [_cider.caption_ids(r, start, end, pad) for r in sample_ids.tolist()], refs)
+            g_r = self.reward_calculator.compute_reward_ids(
+                [_cider.caption_ids(r, start, end, pad) for r in greedy_ids.tolist()], refs)
+            s_r = torch.tensor(s_r, device=device, dtype=torch.float)
+            g_r = torch.tensor(g_r, device=device, dtype=torch.float)
         adv = s_r - g_r
         loss = -(adv * sample_log_probs.sum(dim=1)).mean()
         return loss, {"sample_reward": s_r.mean().item(), "greedy_reward": g_r.mean().item(),
