@@ -120,6 +120,9 @@ struct icap_handle {
   icap_model_desc d{};
   bool use_graphs = true;
   hipStream_t cap_stream = nullptr;
+  int dec_branches = 2;                 // ICAP_DEC_BRANCHES: independent decode chains per batch
+  hipStream_t aux_stream = nullptr;     // second chain's stream
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   DecodeGraph dg[2];  // one captured loop per mode (0 greedy, 1 sample): SCST alternates them
   int ns = 2;  // activation planes (1 = bf16, 2 = hi/lo)
   std::vector<void*> owned;
@@ -182,6 +185,9 @@ struct icap_handle {
       for (DevBuf* b : {&g.ids, &g.lg, &g.uni, &g.lp}) b->release();
     }
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
+    if (aux_stream) (void)hipStreamDestroy(aux_stream);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col}) b->release();
@@ -571,7 +577,21 @@ struct DecodeBufs {
   float *x, *qkv, *kc, *vc, *part;
   bf16_t *a, *q, *qt, *c, *o, *hb, *memp;
   long aL, qL, cL, hL, memL;
+  size_t kvl;  // KV-cache stride between layers (of the whole buffer)
+  long PS;     // split-K slab stride (of the whole buffer)
 };
+
+// Rows [r0, r0 + n) of a decode buffer set (every plane / slab / layer stride stays the whole
+// buffer's), for decoding a batch as independent sub-batches; mem_rows = memory images per row.
+DecodeBufs sub_bufs(const DecodeBufs& b, const icap_model_desc& d, int r0, int Lmax, int S) {
+  const int D = d.d_model, H = d.nhead;
+  DecodeBufs v = b;
+  v.x += (size_t)r0 * D; v.a += (size_t)r0 * D; v.qkv += (size_t)r0 * 3 * D; v.q += (size_t)r0 * D;
+  v.qt += (size_t)r0 * H * D; v.c += (size_t)r0 * H * D; v.o += (size_t)r0 * D; v.hb += (size_t)r0 * d.dim_ff;
+  v.kc += (size_t)r0 * H * Lmax * 64; v.vc += (size_t)r0 * H * Lmax * 64;
+  v.part += (size_t)r0 * D; v.memp += (size_t)r0 * S * D;
+  return v;
+}
 
 // rows: decoder rows per pass; B: memory images; kv_rows: KV-cache rows (default B; B*K for beams)
 DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_rows = 0) {
@@ -598,6 +618,8 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   b.vc = b.kc + (size_t)d.n_dec_layers * kv_rows * H * Lmax * 64;
   b.memp = h->d_memp.as<bf16_t>(); b.memL = (long)B * S * D;
   b.aL = (long)rows * D; b.qL = (long)rows * D; b.cL = (long)rows * H * D; b.hL = (long)rows * d.dim_ff;
+  b.kvl = (size_t)kv_rows * H * Lmax * 64;
+  b.PS = (long)rows * D;
   return b;
 }
 
@@ -614,8 +636,8 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
   const icap_model_desc& d = h->d;
   const int D = d.d_model, H = d.nhead, F = d.dim_ff, rows = B * n_new, ns = h->ns;
   if (mem_rpi <= 0) mem_rpi = n_new;
-  const size_t kv_layer = (size_t)B * H * Lmax * 64;
-  const long PS = (long)rows * D;  // partial slab stride
+  const size_t kv_layer = b.kvl;
+  const long PS = b.PS;  // partial slab stride
   const int KS_D = 4, KS_F = 8;    // split-K of the K=512 and K=dim_ff residual GEMMs
   for (int l = 0; l < d.n_dec_layers; ++l) {
     const DecLayer& L = h->dec[l];
@@ -682,21 +704,41 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
     fin = h->d_fin.as<uint8_t>();
     HIPCHK(hipMemsetAsync(fin, 0, B, s));
   }
-  for (int t = 0; t + 1 < max_len; ++t) {
-    decoder_layers(h, b, B, 1, t, max_len, 1, S, s);
-    HeadArgs ha{};
-    ha.x = b.x; ha.rows = B; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = d.vocab;
-    ha.logits = step_logits ? step_logits + (size_t)t * B * d.vocab : nullptr;
-    ha.ld_logits = d.vocab;
-    ha.ids = ids; ha.ld_ids = max_len; ha.id_col = t + 1;
-    ha.uniforms = uniforms ? uniforms + (size_t)t * B : nullptr;
-    ha.logp = logp ? logp + t : nullptr; ha.ld_logp = max_len - 1;
-    ha.finished = fin; ha.end_token = end;
-    if (t + 2 < max_len) {
-      ha.emb = h->emb; ha.pe = h->pe; ha.pe_pos = t + 1; ha.emb_scale = scale;
-      ha.x_next = b.x; ha.a_next = b.a; ha.lo = b.aL; ha.nsplit = h->ns;
+  // The images are independent: with dec_branches = 2 the two halves of the batch decode as two
+  // independent chains on two streams (two parallel branches of the captured graph), so their
+  // latency-bound launches can overlap.
+  const int nb = (h->dec_branches > 1 && B >= 64) ? 2 : 1;
+  if (nb == 2) {
+    if (!h->aux_stream) HIPCHK(hipStreamCreateWithFlags(&h->aux_stream, hipStreamNonBlocking));
+    if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    if (!h->ev_join) HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(h->ev_fork, s));
+    HIPCHK(hipStreamWaitEvent(h->aux_stream, h->ev_fork, 0));
+  }
+  for (int part = 0; part < nb; ++part) {
+    const int r0 = part * (B / 2), n = nb == 1 ? B : (part ? B - B / 2 : B / 2);
+    hipStream_t st = part ? h->aux_stream : s;
+    DecodeBufs v = sub_bufs(b, d, r0, max_len, S);
+    for (int t = 0; t + 1 < max_len; ++t) {
+      decoder_layers(h, v, n, 1, t, max_len, 1, S, st);
+      HeadArgs ha{};
+      ha.x = v.x; ha.rows = n; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = d.vocab;
+      ha.logits = step_logits ? step_logits + ((size_t)t * B + r0) * d.vocab : nullptr;
+      ha.ld_logits = d.vocab;
+      ha.ids = ids + (size_t)r0 * max_len; ha.ld_ids = max_len; ha.id_col = t + 1;
+      ha.uniforms = uniforms ? uniforms + (size_t)t * B + r0 : nullptr;
+      ha.logp = logp ? logp + (size_t)r0 * (max_len - 1) + t : nullptr; ha.ld_logp = max_len - 1;
+      ha.finished = fin ? fin + r0 : nullptr; ha.end_token = end;
+      if (t + 2 < max_len) {
+        ha.emb = h->emb; ha.pe = h->pe; ha.pe_pos = t + 1; ha.emb_scale = scale;
+        ha.x_next = v.x; ha.a_next = v.a; ha.lo = v.aL; ha.nsplit = h->ns;
+      }
+      HIPCHK(launch_head(ha, st));
     }
-    HIPCHK(launch_head(ha, s));
+  }
+  if (nb == 2) {
+    HIPCHK(hipEventRecord(h->ev_join, h->aux_stream));
+    HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
   }
 }
 
@@ -829,6 +871,7 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
     try {
       h->d = *desc;
       h->ns = desc->precision == ICAP_PREC_BF16X2 ? 2 : 1;
+      if (const char* v = getenv("ICAP_DEC_BRANCHES")) h->dec_branches = std::max(1, std::min(2, atoi(v)));
       pack(h, (hipStream_t)stream);
       HIPCHK(hipStreamSynchronize((hipStream_t)stream));
     } catch (...) {
@@ -839,6 +882,7 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
     h->d.dec_layers = nullptr;
     h->d.vit_layers_w = nullptr;
     h->d.enc_layers = nullptr;
+    h->d.trunk = nullptr;
     *out = h;
   });
 }
