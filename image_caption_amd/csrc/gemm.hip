@@ -762,16 +762,22 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
 // share their A rows in that XCD's L2.
 namespace {
 
-template <int NS, int NW, int NOMFMA = 0, int CONV = 0>  // measurement variants: 1 = no MFMA, 2 = staging only
-__global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
+// BMT = 128 with NW = 8 and NST = 2: the same 64 x 64 wave tiles in a 128 x 256 block tile with a
+// 2-stage ring (64 KiB of LDS), so two blocks share a CU and one's epilogue overlaps the other's
+// k-loop (the output-heavy, short-K trunk GEMMs).
+template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0>
+__global__ __launch_bounds__(NW * 64, BMT == 128 ? 4 : 1) void gemm_256_kernel(GemmArgs p) {
   constexpr int WGM = NW / 4;                       // wave grid WGM x 4
-  constexpr int BM = 256, BN = 256, WM = BM / WGM, WN = 64, TM = WM / 16, TN = WN / 16;
+  constexpr int BM = BMT, BN = 256, WM = BM / WGM, WN = 64, TM = WM / 16, TN = WN / 16;
   constexpr int KS = 32;                            // k per stage (one MFMA k-step)
-  constexpr int OPB = BM * KS * 2;                  // 16 KiB per operand tile per stage
-  constexpr int STAGE = (NS + 1) * OPB;             // A planes + W share one stage
-  constexpr int NSTAGE = NS == 2 ? 3 : 4;           // 144 / 128 KiB of LDS
-  constexpr int IPW = OPB / 1024 / NW;              // 1 KiB DMA instructions per wave per operand
-  constexpr int PER_STAGE = IPW * (NS + 1);         // DMA instructions per wave per stage
+  constexpr int OPB = BM * KS * 2;                  // A bytes per plane per stage (16 KiB at BM 256)
+  constexpr int OPBW = BN * KS * 2;                 // W bytes per stage (16 KiB)
+  constexpr int STAGE = NS * OPB + OPBW;            // A planes + W share one stage
+  constexpr int NSTAGE = NST ? NST : (NS == 2 ? 3 : 4);  // 144 / 128 KiB of LDS at BM 256
+  constexpr int IPW = OPB / 1024 / NW;              // 1 KiB DMA instructions per wave per A plane
+  constexpr int IPWW = OPBW / 1024 / NW;            // ... for W
+  static_assert(IPW >= 1 && IPWW >= 1 && WM % 16 == 0, "tile / wave shape");
+  constexpr int PER_STAGE = IPW * NS + IPWW;        // DMA instructions per wave per stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -788,10 +794,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
   // Stage image: per operand tile, rows of 64 B (32 bf16 of k); one DMA instruction = 16 rows.
   // 16-byte chunk c of row r lives at chunk c ^ sw(r), sw(r) = ((r >> 3) & 1) << 1, which makes
   // the ds_read_b128 fragment reads (16 rows x one chunk per lane group) bank-conflict free.
-  const int srow = wave * IPW * 16 + (lane >> 2);
-  const int schunk = (lane & 3) ^ (((srow >> 3) & 1) << 1);
+  const int srow = wave * IPW * 16 + (lane >> 2), srow_w = wave * IPWW * 16 + (lane >> 2);
+  const int schunk = (lane & 3) ^ (((srow >> 3) & 1) << 1);  // (row >> 3) & 1 is the same for both
   const bf16_t* a_base = p.A + (long)min(m0 + srow, M - 1) * p.lda + schunk * 8;
-  const bf16_t* b_base = p.W + (long)min(n0 + srow, p.N - 1) * p.ldw + schunk * 8;
+  const bf16_t* b_base = p.W + (long)min(n0 + srow_w, p.N - 1) * p.ldw + schunk * 8;
   const long a_step = 16 * p.lda, b_step = 16 * p.ldw;
   const bool a_tail = m0 + BM > M;
   ConvRow cr[CONV ? IPW : 1];
@@ -828,9 +834,9 @@ __global__ __launch_bounds__(NW * 64) void gemm_256_kernel(GemmArgs p) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < IPW; ++i)
+    for (int i = 0; i < IPWW; ++i)
       __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(b_base + kin + i * b_step),
-                                       (LDS_AS void*)(s0 + NS * OPB + (wave * IPW + i) * 1024), 16, 0, 0);
+                                       (LDS_AS void*)(s0 + NS * OPB + (wave * IPWW + i) * 1024), 16, 0, 0);
   };
 
   f32x4 acc[TM][TN];
@@ -1049,6 +1055,27 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
                           (const void*)gemm_256_kernel<1, 16, 0, 1>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
     if (e != hipSuccess) return e;
+  }
+  // 128 x 256 tiles, 2-stage ring, 2 blocks per CU for K >= ICAP_GEMM_TALL_MIN_K (default 128; 0 = off):
+  // ViT 42.9 -> 41.8 ms/step (MLP-out's 591 tiles become 1182: 4.6 instead of 2.3 rounds), trunk
+  // conv3 203 -> 177 us; at K = 64 the 3-stage 256 x 256 ring stays ahead (tools/halfk_sweep.sh)
+  static int tall_min_k = -1;
+  if (tall_min_k < 0) {
+    const char* v = getenv("ICAP_GEMM_TALL_MIN_K");
+    tall_min_k = v ? atoi(v) : 128;
+  }
+  if (tall_min_k && g.K >= tall_min_k && (nw == 8 || nw == 16)) {
+    const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
+    constexpr int ldsh = 2 * (2 * 128 * 32 * 2 + 256 * 32 * 2), ldsh1 = 2 * (128 * 32 * 2 + 256 * 32 * 2);
+    if (g.cv && g.cv != 1) return hipErrorInvalidValue;
+    if (g.nsplit == 2) {
+      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 1, 128, 2>), dim3(nwgh), dim3(512), ldsh, s, g);
+      else hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 0, 128, 2>), dim3(nwgh), dim3(512), ldsh, s, g);
+    } else {
+      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 1, 128, 2>), dim3(nwgh), dim3(512), ldsh1, s, g);
+      else hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2>), dim3(nwgh), dim3(512), ldsh1, s, g);
+    }
+    return hipGetLastError();
   }
   const int nwg = (g.N / 256) * ((g.M + 255) / 256);
   const GemmArgs& g2 = g;
