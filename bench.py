@@ -53,10 +53,9 @@ def pmc_traffic(kernel: str, headline: bool = True):
             table = json.load(f)
     except (OSError, ValueError):
         return None
-    for name, row in table.items():
-        if name.split("<")[0] == kernel:
-            return int(row["traffic_bytes"])
-    return None
+    rows = [row for name, row in table.items() if name.split("<")[0] == kernel]  # every template variant
+    n = sum(r["launches"] for r in rows)
+    return int(sum(r["traffic_bytes"] * r["launches"] for r in rows) / n) if n else None
 
 
 def log(*a):
