@@ -274,6 +274,168 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restri
   }
 }
 
+// Pipelined form for longer sequences (ViT, N = 197): K and V stream through a 4-deep LDS ring of
+// 32-key chunks (Kh, Vh, Kl, Vl: 16 KiB per chunk, one LDS-DMA instruction per wave) while the waves
+// compute - each wave keeps its query tile's online-softmax state (running max, sum, 16 x 64 context)
+// across chunks, so loads of chunks c+1..c+3 are in flight during chunk c instead of one 112 KiB
+// stage-then-compute.  Counted vmcnt + raw s_barrier as in the GEMMs.
+// HM: qkv in the head-major layout of GemmArgs::hm_n ([image][q|k|v x head][token][64]), so one
+// (image, head)'s K and V rows are contiguous 128-byte rows; else row-major [token][3 D].
+template <bool SPLIT, bool HM>
+__global__ __launch_bounds__(1024) void enc_attention_pipe_kernel(const bf16_t* __restrict__ qkv, long ld, long lo,
+                                                                  int N, int H, float scale, bf16_t* out,
+                                                                  long out_ld, long out_lo) {
+  constexpr int NW = 16, CK = 32, NBUF = 4;
+  constexpr int MAT = CK * 128;                // one [32][64] bf16 matrix
+  constexpr int NMAT = SPLIT ? 4 : 2;          // Kh, Vh (, Kl, Vl)
+  constexpr int CHUNK = NMAT * MAT;
+  constexpr int INS = NMAT * CK / 8;           // 1 KiB DMA instructions per chunk (16 / 8)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int D = H * 64;
+  const long rs = HM ? 64 : ld;  // row stride of Q / K / V
+  const bf16_t* qb = HM ? qkv + ((long)b * 3 * H + h) * N * 64 : qkv + (long)b * N * ld + h * 64;
+  const bf16_t* kb = HM ? qb + (long)H * N * 64 : qb + D;
+  const bf16_t* vb = HM ? qb + 2L * H * N * 64 : qb + 2 * D;
+  const int fr = lane & 15, g = lane >> 4;
+  const int nqt = (N + 15) / 16, nch = (N + CK - 1) / CK;
+  const int lrow = lane >> 3, lch = lane & 7;
+
+  auto stage = [&](int c, int buf) {
+    if (wave < INS) {  // SPLIT: every wave issues one instruction
+      const int mat = wave / (CK / 8), part = wave % (CK / 8);
+      const int row = part * 8 + lrow, key = c * CK + row;
+      const bool isK = !(mat & 1);
+      const int ch = isK ? lch ^ (row & 7) : lch;
+      const bf16_t* src = (isK ? kb : vb) + (mat >= 2 ? lo : 0) + (long)min(key, N - 1) * rs + ch * 8;
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
+                                       (LDS_AS void*)(smem + buf * CHUNK + mat * MAT + part * 1024), 16, 0, 0);
+    }
+  };
+
+  bf16x8 qh[2], ql[2];
+  const bool active = wave < nqt;
+  if (active) {
+    const int q = min(wave * 16 + fr, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16_t* src = qb + (long)q * rs + ks * 32 + g * 8;
+      qh[ks] = *(const bf16x8*)src;
+      if (SPLIT) ql[ks] = *(const bf16x8*)(src + lo);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NBUF - 1; ++c)
+    if (c < nch) stage(c, c);
+
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int q4 = fr >> 2, p4 = fr & 3;
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    const int younger = min(NBUF - 2, nch - 1 - c);
+    if (!SPLIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // 8 of 16 waves issue: not uniform
+    else if (younger >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (c + NBUF - 1 < nch) stage(c + NBUF - 1, (c + NBUF - 1) % NBUF);
+    if (!active) continue;
+    const char* Kh = smem + (c % NBUF) * CHUNK;
+    const char* Vh = Kh + MAT;
+    const char* Kl = Kh + 2 * MAT;
+    const char* Vl = Kh + 3 * MAT;
+    f32x4 s[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int row = u * 16 + fr;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int off = row * 128 + (((ks * 4 + g) ^ (row & 7)) << 4);
+        const bf16x8 kh = *(const bf16x8*)(Kh + off);
+        acc = mfma16(kh, qh[ks], acc);
+        if (SPLIT) {
+          const bf16x8 kl = *(const bf16x8*)(Kl + off);
+          acc = mfma16(kl, qh[ks], acc);
+          acc = mfma16(kh, ql[ks], acc);
+        }
+      }
+      s[u] = acc;
+    }
+    float cm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = c * CK + u * 16 + g * 4 + r;
+        const float v = key < N ? s[u][r] * scale : -INFINITY;
+        s[u][r] = v;
+        cm = fmaxf(cm, v);
+      }
+    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    const float m_new = fmaxf(m, cm);  // finite: every chunk holds at least one real key
+    const float alpha = __expf(m - m_new);
+    m = m_new;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(s[u][r] - m_new);
+        s[u][r] = e;
+        l += e;
+      }
+    bf16x8 ph, pl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ph[j] = (__bf16)s[0][j];
+      ph[4 + j] = (__bf16)s[1][j];
+      if (SPLIT) {
+        pl[j] = (__bf16)(s[0][j] - (float)ph[j]);
+        pl[4 + j] = (__bf16)(s[1][j] - (float)ph[4 + j]);
+      }
+    }
+    const int key0 = 4 * g + q4;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int off0 = key0 * 128 + (dt * 16 + 4 * p4) * 2, off1 = off0 + 16 * 128;
+      const bf16x8 vh = tr_pair(Vh + off0, Vh + off1);
+      o[dt] = mfma16(vh, ph, o[dt]);
+      if (SPLIT) {
+        const bf16x8 vl = tr_pair(Vl + off0, Vl + off1);
+        o[dt] = mfma16(vl, ph, o[dt]);
+        o[dt] = mfma16(vh, pl, o[dt]);
+      }
+    }
+  }
+  if (!active) return;
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  const int qq = wave * 16 + fr;
+  if (qq < N) {
+    bf16_t* dst = out + ((long)b * N + qq) * out_ld + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16_t hv[4], lv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) split_bf(o[dt][r] * inv, hv[r], lv[r]);
+      const int d = dt * 16 + 4 * g;
+      *(u32x2*)(dst + d) = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+      if (SPLIT)
+        *(u32x2*)(dst + out_lo + d) =
+            (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+    }
+  }
+}
+
 template <int NKT, bool SPLIT>
 hipError_t run_enc(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale, bf16_t* out,
                    long out_ld, long out_lo, hipStream_t s) {
@@ -296,11 +458,37 @@ hipError_t run_enc(const bf16_t* qkv, long ld, long lo, int B, int N, int H, flo
 }  // namespace
 
 hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale,
-                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s) {
+                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s, int head_major) {
   if (N <= 0 || B <= 0) return hipErrorInvalidValue;
+  if (head_major && (N <= 64 || N > 256)) return hipErrorInvalidValue;  // only the pipelined form reads it
   if (N <= 64) {
     return nsplit == 2 ? run_enc<4, true>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s)
                        : run_enc<4, false>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s);
+  }
+  static int pipe = -1;  // ICAP_ENC_ATTN_PIPE=0 selects the stage-everything form for N > 64
+  if (pipe < 0) {
+    const char* v = getenv("ICAP_ENC_ATTN_PIPE");
+    pipe = v ? atoi(v) : 1;
+  }
+  if ((pipe || head_major) && N <= 256) {  // 16 query tiles = 16 waves
+    const int lds = 4 * (nsplit == 2 ? 4 : 2) * 32 * 128;
+    const dim3 gr(H, B), bl(1024);
+    if (nsplit == 2) {
+      if (head_major)
+        hipLaunchKernelGGL((enc_attention_pipe_kernel<true, true>), gr, bl, lds, s, qkv, ld, lo, N, H, scale, out,
+                           out_ld, out_lo);
+      else
+        hipLaunchKernelGGL((enc_attention_pipe_kernel<true, false>), gr, bl, lds, s, qkv, ld, lo, N, H, scale, out,
+                           out_ld, out_lo);
+    } else {
+      if (head_major)
+        hipLaunchKernelGGL((enc_attention_pipe_kernel<false, true>), gr, bl, lds, s, qkv, ld, lo, N, H, scale, out,
+                           out_ld, out_lo);
+      else
+        hipLaunchKernelGGL((enc_attention_pipe_kernel<false, false>), gr, bl, lds, s, qkv, ld, lo, N, H, scale, out,
+                           out_ld, out_lo);
+    }
+    return hipGetLastError();
   }
   if (N <= 224) {
     return nsplit == 2 ? run_enc<14, true>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s)

@@ -159,7 +159,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
         else if (p.epi == EPI_RELU) v = fmaxf(v, 0.f);
         const long orow = p.rm_group ? (long)(row / p.rm_group) * p.rm_stride + p.rm_off + row % p.rm_group
                                      : (long)row;
-        const long o = (long)bz * p.c_batch + orow * p.ldc + col;
+        const long o = p.hm_n ? (((long)(row / p.hm_n) * (p.N / 64) + col / 64) * p.hm_n + row % p.hm_n) * 64 + col % 64
+                              : (long)bz * p.c_batch + orow * p.ldc + col;
         if (p.out == OUT_F32) {
           ((float*)p.C)[o] = v;
         } else if (p.out == OUT_F32_RESID) {
@@ -212,6 +213,7 @@ int gemm_tile_class(const GemmArgs& g) {
 
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
+  if (g.hm_n && (g.out != OUT_SPLIT || g.N % 64 || g.batch != 1 || g.rm_group || g.M % g.hm_n)) return hipErrorInvalidValue;
   if (g.K % BK != 0 || g.N % 64 != 0 || (g.nsplit != 1 && g.nsplit != 2)) return hipErrorInvalidValue;
   if (g.cv && (g.batch != 1 || !g.cv_zero || (g.cv == 1 && g.cv_cshift < 6) || g.cv_OHW <= 0 || g.cv_OW <= 0))
     return hipErrorInvalidValue;
@@ -699,8 +701,11 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
   for (int i = 0; i < TM; ++i) {
     const int m = mb + i * 16 + fr;
     const int mc = min(m, M - 1);
-    orow[i] = (int)((p.rm_group ? (long)(mc / p.rm_group) * p.rm_stride + p.rm_off + mc % p.rm_group : (long)mc) *
-                    p.ldc);
+    if (p.hm_n)  // head-major: this wave's 64 columns [nb, nb + 64) are one head block
+      orow[i] = (int)((((long)(mc / p.hm_n) * (p.N / 64) + nb / 64) * p.hm_n + mc % p.hm_n) * 64 - nb);
+    else
+      orow[i] = (int)((p.rm_group ? (long)(mc / p.rm_group) * p.rm_stride + p.rm_off + mc % p.rm_group : (long)mc) *
+                      p.ldc);
     if (m >= M) orow[i] = -1 - orow[i];
   }
 
@@ -766,7 +771,7 @@ namespace {
 // 2-stage ring (64 KiB of LDS), so two blocks share a CU and one's epilogue overlaps the other's
 // k-loop (the output-heavy, short-K trunk GEMMs).
 template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0>
-__global__ __launch_bounds__(NW * 64, BMT == 128 ? 4 : 1) void gemm_256_kernel(GemmArgs p) {
+__global__ __launch_bounds__(NW * 64, BMT == 128 ? 4 : (BMT == 64 ? 3 : 1)) void gemm_256_kernel(GemmArgs p) {
   constexpr int WGM = NW / 4;                       // wave grid WGM x 4
   constexpr int BM = BMT, BN = 256, WM = BM / WGM, WN = 64, TM = WM / 16, TN = WN / 16;
   constexpr int KS = 32;                            // k per stage (one MFMA k-step)
@@ -1063,6 +1068,18 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
   if (tall_min_k < 0) {
     const char* v = getenv("ICAP_GEMM_TALL_MIN_K");
     tall_min_k = v ? atoi(v) : 128;
+  }
+  static int tall_bm = 0;  // ICAP_GEMM_TALL_BM: 128 (default) or 64 (64 x 256 tiles, 4 waves, 3 blocks per CU)
+  if (!tall_bm) {
+    const char* v = getenv("ICAP_GEMM_TALL_BM");
+    tall_bm = v && atoi(v) == 64 ? 64 : 128;
+  }
+  if (tall_min_k && g.K >= tall_min_k && (nw == 8 || nw == 16) && tall_bm == 64 && !g.cv) {
+    const int nwgq = (g.N / 256) * ((g.M + 63) / 64);
+    constexpr int ldsq = 2 * (2 * 64 * 32 * 2 + 256 * 32 * 2), ldsq1 = 2 * (64 * 32 * 2 + 256 * 32 * 2);
+    if (g.nsplit == 2) hipLaunchKernelGGL((gemm_256_kernel<2, 4, 0, 0, 64, 2>), dim3(nwgq), dim3(256), ldsq, s, g);
+    else hipLaunchKernelGGL((gemm_256_kernel<1, 4, 0, 0, 64, 2>), dim3(nwgq), dim3(256), ldsq1, s, g);
+    return hipGetLastError();
   }
   if (tall_min_k && g.K >= tall_min_k && (nw == 8 || nw == 16)) {
     const int nwgh = (g.N / 256) * ((g.M + 127) / 128);

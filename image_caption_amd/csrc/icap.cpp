@@ -245,8 +245,9 @@ struct icap_handle {
 
   // ---------------------------------------------------------------- GEMM helper
   void gemm(const bf16_t* A, long lda, long a_lo, const Lin& W, int M, void* C, long ldc, long c_lo, int epi,
-            int out, hipStream_t s) {
+            int out, hipStream_t s, int hm_n = 0) {
     GemmArgs g = gemm_args();
+    g.hm_n = hm_n;
     g.A = A; g.lda = lda; g.a_lo = a_lo;
     g.W = W.w; g.ldw = W.K;
     g.bias = W.b;
@@ -276,11 +277,11 @@ struct icap_handle {
     timed(PROF_GEMM_WAVE, flops, bytes, s, [&] { HIPCHK(launch_chain_dec(a, s)); });
   }
   void attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, bf16_t* out, long out_ld, long out_lo,
-                 hipStream_t s) {
+                 hipStream_t s, int head_major = 0) {
     const double flops = 4.0 * B * H * (double)N * N * 64;
     const double bytes = 2.0 * ns * B * (double)N * H * 64 * 4;
     timed(PROF_ENC_ATTN, flops, bytes, s,
-          [&] { HIPCHK(launch_enc_attention(qkv, ld, lo, B, N, H, 0.125f, out, out_ld, out_lo, ns, s)); });
+          [&] { HIPCHK(launch_enc_attention(qkv, ld, lo, B, N, H, 0.125f, out, out_ld, out_lo, ns, s, head_major)); });
   }
 };
 
@@ -380,6 +381,11 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   const icap_model_desc& d = h->d;
   const int V = d.vit_dim, g = d.image / d.patch, np = g * g, T = np + 1, M = B * T, Dm = d.d_model;
   const int Kp = 3 * d.patch * d.patch, ns = h->ns;
+  static const int hm_env = [] {
+    const char* v = getenv("ICAP_QKV_HEAD_MAJOR");  // measurement knob: 0 = row-major QKV
+    return v ? atoi(v) : 1;
+  }();
+  const int hm = hm_env && T > 64 && T <= 256 ? T : 0;
   h->e_patch.ensure((size_t)B * np * Kp * 2 * ns);
   h->e_x.ensure((size_t)M * V * 4);
   h->e_a.ensure((size_t)M * V * 2 * ns);
@@ -407,8 +413,9 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
   for (const VitLayer& L : h->vit) {
     HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
-    h->gemm(a, V, aL, L.qkv, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s);
-    h->attention(qkv, 3 * V, qL, B, T, d.vit_heads, a, V, aL, s);
+    // QKV written head-major ([image][q|k|v x head][token][64]) for the attention's contiguous rows
+    h->gemm(a, V, aL, L.qkv, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s, hm);
+    h->attention(qkv, 3 * V, qL, B, T, d.vit_heads, a, V, aL, s, hm ? 1 : 0);
     h->gemm(a, V, aL, L.out, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s);
     HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
     h->gemm(a, V, aL, L.mlp0, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);

@@ -29,6 +29,10 @@ struct GemmArgs {
   //   cv = 2: 7x7 / stride 2 stem over a zero-bordered NHWC4 image A [B][cv_H][cv_W][4] (border 3),
   //           k = (kh*8 + kw)*4 + c, i.e. one 32-deep k-step = one kernel row = 64 contiguous bytes
   int cv, cv_H, cv_W, cv_cshift, cv_OW, cv_OHW, cv_stride; const bf16_t* cv_zero;
+  // head-major split output (hm_n = tokens per image, 0 = off): element (row, col) of the bf16 planes
+  // goes to ((row / hm_n * (N / 64) + col / 64) * hm_n + row % hm_n) * 64 + col % 64, i.e. the QKV
+  // projection as [image][q|k|v x head][token][64] - one head's rows contiguous for the attention
+  int hm_n;
 };
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
@@ -123,8 +127,9 @@ hipError_t launch_f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t
 hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s);
 
 // Encoder self-attention (non-causal) over N tokens, heads of 64, MFMA bf16 (nsplit 1 or 2).
+// head_major: qkv written with GemmArgs::hm_n = N (N in (64, 256])
 hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale,
-                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s);
+                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s, int head_major = 0);
 // Decoder self-attention with fp32 KV cache; n_new query rows per image starting at t0.
 hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int H, float* kc, float* vc,
                                 int Lmax, int causal, float scale, bf16_t* out, long lo, int nsplit,

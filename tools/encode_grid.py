@@ -1,5 +1,5 @@
-"""Run the Grid encoder (HIP ResNet trunk + tail) ITERS times at batch B, for trunk profiles.
-usage: python tools/encode_grid.py [ITERS] [B]"""
+"""Run an encoder ITERS times at batch B, for kernel profiles (default the Grid encoder: HIP ResNet
+trunk + tail).  usage: python tools/encode_grid.py [ITERS] [B] [vit|grid]"""
 import os
 import sys
 
@@ -11,8 +11,10 @@ from image_caption_amd.engine import Engine  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+kind = sys.argv[3] if len(sys.argv) > 3 else "grid"
 dev = torch.device("cuda", 0)
-eng = Engine(W.to_torch(W.grid_state_dict(0)), "grid", {}, device=dev)
+sd = W.vit_state_dict(0) if kind == "vit" else W.grid_state_dict(0)
+eng = Engine(W.to_torch(sd), kind, {}, device=dev)
 imgs = torch.from_numpy(W.synthetic_images(B, seed=1)).to(dev)
 for _ in range(iters):
     mem = eng.encode(imgs)
