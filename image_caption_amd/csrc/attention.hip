@@ -281,15 +281,17 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restri
 // stage-then-compute.  Counted vmcnt + raw s_barrier as in the GEMMs.
 // HM: qkv in the head-major layout of GemmArgs::hm_n ([image][q|k|v x head][token][64]), so one
 // (image, head)'s K and V rows are contiguous 128-byte rows; else row-major [token][3 D].
-template <bool SPLIT, bool HM>
-__global__ __launch_bounds__(1024) void enc_attention_pipe_kernel(const bf16_t* __restrict__ qkv, long ld, long lo,
-                                                                  int N, int H, float scale, bf16_t* out,
-                                                                  long out_ld, long out_lo) {
-  constexpr int NW = 16, CK = 32, NBUF = 4;
+// QPW query tiles per wave: 16 / QPW waves per block (QPW = 2: 8 waves, two blocks per CU).
+template <bool SPLIT, bool HM, int QPW>
+__global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pipe_kernel(
+    const bf16_t* __restrict__ qkv, long ld, long lo, int N, int H, float scale, bf16_t* out, long out_ld,
+    long out_lo) {
+  constexpr int NW = 16 / QPW, CK = 32, NBUF = 4;
   constexpr int MAT = CK * 128;                // one [32][64] bf16 matrix
   constexpr int NMAT = SPLIT ? 4 : 2;          // Kh, Vh (, Kl, Vl)
   constexpr int CHUNK = NMAT * MAT;
   constexpr int INS = NMAT * CK / 8;           // 1 KiB DMA instructions per chunk (16 / 8)
+  constexpr int IPW = INS / NW > 0 ? INS / NW : 1;  // per wave (waves >= INS / IPW issue)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int h = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -301,137 +303,155 @@ __global__ __launch_bounds__(1024) void enc_attention_pipe_kernel(const bf16_t* 
   const int fr = lane & 15, g = lane >> 4;
   const int nqt = (N + 15) / 16, nch = (N + CK - 1) / CK;
   const int lrow = lane >> 3, lch = lane & 7;
+  const bool uniform_issue = INS % NW == 0;  // every wave issues IPW instructions per chunk
 
   auto stage = [&](int c, int buf) {
-    if (wave < INS) {  // SPLIT: every wave issues one instruction
-      const int mat = wave / (CK / 8), part = wave % (CK / 8);
-      const int row = part * 8 + lrow, key = c * CK + row;
-      const bool isK = !(mat & 1);
-      const int ch = isK ? lch ^ (row & 7) : lch;
-      const bf16_t* src = (isK ? kb : vb) + (mat >= 2 ? lo : 0) + (long)min(key, N - 1) * rs + ch * 8;
-      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
-                                       (LDS_AS void*)(smem + buf * CHUNK + mat * MAT + part * 1024), 16, 0, 0);
+#pragma unroll
+    for (int k = 0; k < IPW; ++k) {
+      const int ins = wave * IPW + k;
+      if (ins < INS) {
+        const int mat = ins / (CK / 8), part = ins % (CK / 8);
+        const int row = part * 8 + lrow, key = c * CK + row;
+        const bool isK = !(mat & 1);
+        const int ch = isK ? lch ^ (row & 7) : lch;
+        const bf16_t* src = (isK ? kb : vb) + (mat >= 2 ? lo : 0) + (long)min(key, N - 1) * rs + ch * 8;
+        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
+                                         (LDS_AS void*)(smem + buf * CHUNK + mat * MAT + part * 1024), 16, 0, 0);
+      }
     }
   };
 
-  bf16x8 qh[2], ql[2];
-  const bool active = wave < nqt;
-  if (active) {
-    const int q = min(wave * 16 + fr, N - 1);
+  bf16x8 qh[QPW][2], ql[QPW][2];
+#pragma unroll
+  for (int t = 0; t < QPW; ++t) {
+    const int q = min((wave + t * NW) * 16 + fr, N - 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16_t* src = qb + (long)q * rs + ks * 32 + g * 8;
-      qh[ks] = *(const bf16x8*)src;
-      if (SPLIT) ql[ks] = *(const bf16x8*)(src + lo);
+      qh[t][ks] = *(const bf16x8*)src;
+      if (SPLIT) ql[t][ks] = *(const bf16x8*)(src + lo);
     }
   }
 #pragma unroll
   for (int c = 0; c < NBUF - 1; ++c)
     if (c < nch) stage(c, c);
 
-  float m = -INFINITY, l = 0.f;
-  f32x4 o[4];
+  float m[QPW], l[QPW];
+  f32x4 o[QPW][4];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < QPW; ++t) {
+    m[t] = -INFINITY;
+    l[t] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[t][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
   const int q4 = fr >> 2, p4 = fr & 3;
 #pragma unroll 1
   for (int c = 0; c < nch; ++c) {
     const int younger = min(NBUF - 2, nch - 1 - c);
-    if (!SPLIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // 8 of 16 waves issue: not uniform
-    else if (younger >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    if (!uniform_issue) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * IPW) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (c + NBUF - 1 < nch) stage(c + NBUF - 1, (c + NBUF - 1) % NBUF);
-    if (!active) continue;
     const char* Kh = smem + (c % NBUF) * CHUNK;
     const char* Vh = Kh + MAT;
     const char* Kl = Kh + 2 * MAT;
     const char* Vl = Kh + 3 * MAT;
-    f32x4 s[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const int row = u * 16 + fr;
+    for (int t = 0; t < QPW; ++t) {
+      if ((wave + t * NW) >= nqt) break;  // wave-uniform
+      f32x4 s[2];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int off = row * 128 + (((ks * 4 + g) ^ (row & 7)) << 4);
-        const bf16x8 kh = *(const bf16x8*)(Kh + off);
-        acc = mfma16(kh, qh[ks], acc);
+      for (int u = 0; u < 2; ++u) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const int row = u * 16 + fr;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int off = row * 128 + (((ks * 4 + g) ^ (row & 7)) << 4);
+          const bf16x8 kh = *(const bf16x8*)(Kh + off);
+          acc = mfma16(kh, qh[t][ks], acc);
+          if (SPLIT) {
+            const bf16x8 kl = *(const bf16x8*)(Kl + off);
+            acc = mfma16(kl, qh[t][ks], acc);
+            acc = mfma16(kh, ql[t][ks], acc);
+          }
+        }
+        s[u] = acc;
+      }
+      float cm = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = c * CK + u * 16 + g * 4 + r;
+          const float v = key < N ? s[u][r] * scale : -INFINITY;
+          s[u][r] = v;
+          cm = fmaxf(cm, v);
+        }
+      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      const float m_new = fmaxf(m[t], cm);  // finite: every chunk holds at least one real key
+      const float alpha = __expf(m[t] - m_new);
+      m[t] = m_new;
+      l[t] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[t][dt] *= alpha;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __expf(s[u][r] - m_new);
+          s[u][r] = e;
+          l[t] += e;
+        }
+      bf16x8 ph, pl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ph[j] = (__bf16)s[0][j];
+        ph[4 + j] = (__bf16)s[1][j];
         if (SPLIT) {
-          const bf16x8 kl = *(const bf16x8*)(Kl + off);
-          acc = mfma16(kl, qh[ks], acc);
-          acc = mfma16(kh, ql[ks], acc);
+          pl[j] = (__bf16)(s[0][j] - (float)ph[j]);
+          pl[4 + j] = (__bf16)(s[1][j] - (float)ph[4 + j]);
         }
       }
-      s[u] = acc;
-    }
-    float cm = -INFINITY;
+      const int key0 = 4 * g + q4;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = c * CK + u * 16 + g * 4 + r;
-        const float v = key < N ? s[u][r] * scale : -INFINITY;
-        s[u][r] = v;
-        cm = fmaxf(cm, v);
-      }
-    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-    const float m_new = fmaxf(m, cm);  // finite: every chunk holds at least one real key
-    const float alpha = __expf(m - m_new);
-    m = m_new;
-    l *= alpha;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = __expf(s[u][r] - m_new);
-        s[u][r] = e;
-        l += e;
-      }
-    bf16x8 ph, pl;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ph[j] = (__bf16)s[0][j];
-      ph[4 + j] = (__bf16)s[1][j];
-      if (SPLIT) {
-        pl[j] = (__bf16)(s[0][j] - (float)ph[j]);
-        pl[4 + j] = (__bf16)(s[1][j] - (float)ph[4 + j]);
-      }
-    }
-    const int key0 = 4 * g + q4;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int off0 = key0 * 128 + (dt * 16 + 4 * p4) * 2, off1 = off0 + 16 * 128;
-      const bf16x8 vh = tr_pair(Vh + off0, Vh + off1);
-      o[dt] = mfma16(vh, ph, o[dt]);
-      if (SPLIT) {
-        const bf16x8 vl = tr_pair(Vl + off0, Vl + off1);
-        o[dt] = mfma16(vl, ph, o[dt]);
-        o[dt] = mfma16(vh, pl, o[dt]);
+      for (int dt = 0; dt < 4; ++dt) {
+        const int off0 = key0 * 128 + (dt * 16 + 4 * p4) * 2, off1 = off0 + 16 * 128;
+        const bf16x8 vh = tr_pair(Vh + off0, Vh + off1);
+        o[t][dt] = mfma16(vh, ph, o[t][dt]);
+        if (SPLIT) {
+          const bf16x8 vl = tr_pair(Vl + off0, Vl + off1);
+          o[t][dt] = mfma16(vl, ph, o[t][dt]);
+          o[t][dt] = mfma16(vh, pl, o[t][dt]);
+        }
       }
     }
   }
-  if (!active) return;
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  const float inv = 1.f / l;
-  const int qq = wave * 16 + fr;
-  if (qq < N) {
-    bf16_t* dst = out + ((long)b * N + qq) * out_ld + h * 64;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      bf16_t hv[4], lv[4];
+  for (int t = 0; t < QPW; ++t) {
+    const int qt = wave + t * NW;
+    if (qt >= nqt) break;
+    float lt = l[t];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = 1.f / lt;
+    const int qq = qt * 16 + fr;
+    if (qq < N) {
+      bf16_t* dst = out + ((long)b * N + qq) * out_ld + h * 64;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) split_bf(o[dt][r] * inv, hv[r], lv[r]);
-      const int d = dt * 16 + 4 * g;
-      *(u32x2*)(dst + d) = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
-      if (SPLIT)
-        *(u32x2*)(dst + out_lo + d) =
-            (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16_t hv[4], lv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) split_bf(o[t][dt][r] * inv, hv[r], lv[r]);
+        const int d = dt * 16 + 4 * g;
+        *(u32x2*)(dst + d) = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+        if (SPLIT)
+          *(u32x2*)(dst + out_lo + d) =
+              (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+      }
     }
   }
 }
@@ -470,24 +490,24 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
     const char* v = getenv("ICAP_ENC_ATTN_PIPE");
     pipe = v ? atoi(v) : 1;
   }
-  if ((pipe || head_major) && N <= 256) {  // 16 query tiles = 16 waves
+  static int qpw = 0;  // ICAP_ENC_ATTN_QPW: query tiles per wave (1: 16 waves, 2: 8 waves, 2 blocks/CU)
+  if (!qpw) {
+    const char* v = getenv("ICAP_ENC_ATTN_QPW");
+    qpw = v && atoi(v) == 2 ? 2 : 1;
+  }
+  if ((pipe || head_major) && N <= 256) {  // 16 query tiles
     const int lds = 4 * (nsplit == 2 ? 4 : 2) * 32 * 128;
-    const dim3 gr(H, B), bl(1024);
-    if (nsplit == 2) {
-      if (head_major)
-        hipLaunchKernelGGL((enc_attention_pipe_kernel<true, true>), gr, bl, lds, s, qkv, ld, lo, N, H, scale, out,
-                           out_ld, out_lo);
-      else
-        hipLaunchKernelGGL((enc_attention_pipe_kernel<true, false>), gr, bl, lds, s, qkv, ld, lo, N, H, scale, out,
-                           out_ld, out_lo);
+    const dim3 gr(H, B), bl(1024 / qpw);
+#define ICAP_ENC_PIPE(SP, HMJ, Q) \
+  hipLaunchKernelGGL((enc_attention_pipe_kernel<SP, HMJ, Q>), gr, bl, lds, s, qkv, ld, lo, N, H, scale, out, out_ld, out_lo)
+    if (qpw == 2) {
+      if (nsplit == 2) { if (head_major) ICAP_ENC_PIPE(true, true, 2); else ICAP_ENC_PIPE(true, false, 2); }
+      else { if (head_major) ICAP_ENC_PIPE(false, true, 2); else ICAP_ENC_PIPE(false, false, 2); }
     } else {
-      if (head_major)
-        hipLaunchKernelGGL((enc_attention_pipe_kernel<false, true>), gr, bl, lds, s, qkv, ld, lo, N, H, scale, out,
-                           out_ld, out_lo);
-      else
-        hipLaunchKernelGGL((enc_attention_pipe_kernel<false, false>), gr, bl, lds, s, qkv, ld, lo, N, H, scale, out,
-                           out_ld, out_lo);
+      if (nsplit == 2) { if (head_major) ICAP_ENC_PIPE(true, true, 1); else ICAP_ENC_PIPE(true, false, 1); }
+      else { if (head_major) ICAP_ENC_PIPE(false, true, 1); else ICAP_ENC_PIPE(false, false, 1); }
     }
+#undef ICAP_ENC_PIPE
     return hipGetLastError();
   }
   if (N <= 224) {
