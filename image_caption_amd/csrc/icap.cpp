@@ -709,7 +709,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   if (uniforms) {
     h->d_fin.ensure((size_t)B);
     fin = h->d_fin.as<uint8_t>();
-    HIPCHK(hipMemsetAsync(fin, 0, B, s));
+    HIPCHK(launch_fill_u8(fin, B, 0, s));  // a kernel node: reset on every graph replay
   }
   // The images are independent: with dec_branches = 2 the two halves of the batch decode as two
   // independent chains on two streams (two parallel branches of the captured graph), so their

@@ -121,6 +121,9 @@ hipError_t launch_bn_fold(const float* g, const float* b, const float* mean, con
                           float* scale, float* shift, hipStream_t s);
 hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0, const float* emb,
                         const float* pe, int D, float scale, float* x, bf16_t* a, long lo, int nsplit, hipStream_t s);
+// byte fill as a kernel (captured into decode graphs: a captured small hipMemsetAsync was not
+// re-applied on the second replay of the sampled-decode graph, ROCm 7.2)
+hipError_t launch_fill_u8(uint8_t* p, long n, uint8_t value, hipStream_t s);
 hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hipStream_t s);
 hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int nsplit, hipStream_t s);
 hipError_t launch_f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);

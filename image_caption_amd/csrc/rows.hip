@@ -186,6 +186,10 @@ __global__ void embed_kernel(const int32_t* tok, long tok_ld, int fixed_tok, int
   }
 }
 
+__global__ void fill_u8_kernel(uint8_t* p, long n, uint8_t value) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = value;
+}
+
 __global__ void fill_col_kernel(int32_t* ids, int B, long ld, int col, int value) {
   for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x) ids[(long)b * ld + col] = value;
 }
@@ -278,6 +282,11 @@ hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows
                         const float* pe, int D, float scale, float* x, bf16_t* a, long lo, int nsplit, hipStream_t s) {
   hipLaunchKernelGGL(embed_kernel, dim3(grid_for((long)rows * D)), dim3(256), 0, s, tok, tok_ld, fixed_tok, rows, T,
                      t0, emb, pe, D, scale, x, a, lo, nsplit);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_u8(uint8_t* p, long n, uint8_t value, hipStream_t s) {
+  hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, value);
   return hipGetLastError();
 }
 

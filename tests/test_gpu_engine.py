@@ -38,3 +38,29 @@ def test_vit_encode_and_greedy(cuda, vit_sd, precision):
         assert (logits.cpu()[: ref_tr.shape[0]] - ref_tr).abs().max().item() < 1e-3
     else:
         assert lerr < 1e-1, lerr
+
+
+def test_two_chain_decode_matches_one_chain(cuda, vit_sd, monkeypatch):
+    """The batch decoded as two independent graph branches (ICAP_DEC_BRANCHES=2, the default) gives
+    the same greedy ids, step logits and sampled ids / log-probs as one chain, for an odd batch (uneven
+    halves 48 + 49), eagerly and on graph replay."""
+    from image_caption_amd.engine import Engine
+
+    B, L = 97, 12
+    mem = torch.from_numpy(np.random.Generator(np.random.PCG64(21)).standard_normal((B, 49, 512)).astype(np.float32))
+    mem = mem.to(cuda)
+    uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(3)).to(cuda)
+    out = {}
+    for nb in ("1", "2"):
+        monkeypatch.setenv("ICAP_DEC_BRANCHES", nb)
+        eng = Engine(vit_sd, "vit", {}, device=cuda)
+        runs = []
+        for _ in range(3):  # eager, capture, replay
+            ids, lg = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L, want_logits=True)
+            sid, lp = eng.sample(mem, uni, W.START_TOKEN, W.END_TOKEN, L)
+            runs.append((ids.cpu(), lg.cpu(), sid.cpu(), lp.cpu()))
+        for r in runs[1:]:
+            assert all(torch.equal(a, b) for a, b in zip(r, runs[0]))
+        out[nb] = runs[0]
+    for a, b in zip(out["1"], out["2"]):
+        assert torch.equal(a, b)
