@@ -714,7 +714,8 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   // The images are independent: with dec_branches = 2 the two halves of the batch decode as two
   // independent chains on two streams (two parallel branches of the captured graph), so their
   // latency-bound launches can overlap.
-  const int nb = (h->dec_branches > 1 && B >= 64) ? 2 : 1;
+  // (two chains pay from 128 rows each: B = 256 +3.4 %, B = 128 -6 %, tools/ab_env.sh)
+  const int nb = (h->dec_branches > 1 && B >= 256) ? 2 : 1;
   if (nb == 2) {
     if (!h->aux_stream) HIPCHK(hipStreamCreateWithFlags(&h->aux_stream, hipStreamNonBlocking));
     if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));

@@ -41,12 +41,12 @@ def test_vit_encode_and_greedy(cuda, vit_sd, precision):
 
 
 def test_two_chain_decode_matches_one_chain(cuda, vit_sd, monkeypatch):
-    """The batch decoded as two independent graph branches (ICAP_DEC_BRANCHES=2, the default) gives
-    the same greedy ids, step logits and sampled ids / log-probs as one chain, for an odd batch (uneven
-    halves 48 + 49), eagerly and on graph replay."""
+    """The batch decoded as two independent graph branches (ICAP_DEC_BRANCHES=2, the default, from
+    B = 256) gives the same greedy ids, step logits and sampled ids / log-probs as one chain, for an
+    odd batch (uneven halves 128 + 129), eagerly and on graph replay."""
     from image_caption_amd.engine import Engine
 
-    B, L = 97, 12
+    B, L = 257, 12
     mem = torch.from_numpy(np.random.Generator(np.random.PCG64(21)).standard_normal((B, 49, 512)).astype(np.float32))
     mem = mem.to(cuda)
     uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(3)).to(cuda)
