@@ -553,18 +553,28 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = (float*)(smem + 2 * BUF);         // [8 d-groups][2 tiles][4 regs][64 lanes]
   float* tot = red + 8 * 512;                    // [2 tiles][4 regs][64 lanes]
-  const int r = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int skt = wave & 1, sdg = wave >> 1;     // score role: key tile, d-group
-  const bf16_t* mb = mem + (long)(r / rows_per_image) * S * DM;
+  // Two query rows of the same image per block: MFMA column fr = (row fr >> 3, head fr & 7), so the
+  // second row rides in the columns a single row leaves empty and the image's memory is streamed
+  // once for both (beam slots, teacher-forced positions); with one row per image the odd columns
+  // stay empty as before.
+  const int bpi = (rows_per_image + 1) / 2;      // blocks per image
+  const int img = blockIdx.x / bpi, pair = blockIdx.x - img * bpi;
+  const int slot = 2 * pair + (fr >> 3);         // this column's row within the image
+  const bool valid = slot < rows_per_image;
+  const long r = (long)img * rows_per_image + slot;
+  const int hd = fr & 7;
+  const bf16_t* mb = mem + (long)img * S * DM;
   const int nchunks = (S + CK - 1) / CK;
 
-  // q~ fragments (B operand of the scores): head fr (zero for fr >= 8), d = 64 sdg + 32 ks + 8 fq + j
+  // q~ fragments (B operand of the scores): column (row, head), d = 64 sdg + 32 ks + 8 fq + j
   bf16x8 qh[2], ql[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    const long off = (long)r * H * DM + fr * DM + sdg * 64 + ks * 32 + fq * 8;
-    if (fr < H) {
+    const long off = r * H * DM + hd * DM + sdg * 64 + ks * 32 + fq * 8;
+    if (valid) {
       qh[ks] = *(const bf16x8*)(qt + off);
       if (NS == 2) ql[ks] = *(const bf16x8*)(qt + qt_lo + off);
     } else {
@@ -690,10 +700,10 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
       stage(c + 2, c & 1);
     }
   }
-  // C^T layout: lane holds head fr, d = 16dt + 4fq + r (4 consecutive d) -> 8-byte plane stores
-  if (fr < H) {
+  // C^T layout: lane holds column (row, head), d = 16dt + 4fq + r (4 consecutive d) -> 8-byte stores
+  if (valid) {
     const float inv = 1.f / l_run;
-    bf16_t* dst = out + (long)r * H * DM + fr * DM + wave * 32;
+    bf16_t* dst = out + r * H * DM + hd * DM + wave * 32;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
       bf16_t hv[4], lv[4];
@@ -727,11 +737,13 @@ hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* me
     if (e != hipSuccess) return e;
     attr = true;
   }
+  if (rows_per_image <= 0 || rows % rows_per_image) return hipErrorInvalidValue;
+  const int blocks = rows / rows_per_image * ((rows_per_image + 1) / 2);  // two rows of an image per block
   if (nsplit == 2)
-    hipLaunchKernelGGL(cross_attn_mfma_kernel<2>, dim3(rows), dim3(1024), lds, s, qt, qt_lo, mem, mem_lo,
+    hipLaunchKernelGGL(cross_attn_mfma_kernel<2>, dim3(blocks), dim3(1024), lds, s, qt, qt_lo, mem, mem_lo,
                        rows_per_image, S, scale, out, out_lo);
   else
-    hipLaunchKernelGGL(cross_attn_mfma_kernel<1>, dim3(rows), dim3(1024), lds, s, qt, qt_lo, mem, mem_lo,
+    hipLaunchKernelGGL(cross_attn_mfma_kernel<1>, dim3(blocks), dim3(1024), lds, s, qt, qt_lo, mem, mem_lo,
                        rows_per_image, S, scale, out, out_lo);
   return hipGetLastError();
 }
