@@ -146,6 +146,7 @@ def main():
 
     if args.mode == "scst":
         from image_caption_amd import cider
+        from image_caption_amd.scst import sample_and_greedy
         from utils.scst_loss import sample_stop_length
 
         gen = torch.Generator(device="cpu").manual_seed(5)
@@ -158,8 +159,8 @@ def main():
 
         def step():  # noqa: F811
             mem = encode()
-            sid, _ = eng.sample(mem, uni, W.START_TOKEN, W.END_TOKEN, L)
-            gid, _ = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L)
+            # sampled + greedy decodes of the same memory, concurrently on two streams
+            sid, _, gid = sample_and_greedy(eng, mem, uni, W.START_TOKEN, W.END_TOKEN, L)
             if ws > 1:
                 sid, gid = parallel.gather_rows(sid, total), parallel.gather_rows(gid, total)
             sid, gid = sid.long(), apply_stop_rule(gid.long(), W.END_TOKEN)

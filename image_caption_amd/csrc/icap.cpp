@@ -177,7 +177,12 @@ struct icap_handle {
   // workspaces
   DevBuf e_x, e_a, e_qkv, e_h, e_patch;  // encoder
   DevBuf t_x, t_y, t_1, t_2, t_r, t_col;  // ResNet trunk (NHWC planes)
-  DevBuf d_x, d_a, d_qkv, d_q, d_qt, d_c, d_o, d_h, d_kv, d_fin, d_part, d_memp, d_beam;  // decoder
+  // decoder workspaces, one set per decode mode (0: greedy / beam / teacher-forced, 1: sampled), so
+  // the greedy and sampled graphs of an SCST step can replay concurrently on two streams
+  struct DecWS {
+    DevBuf x, a, qkv, q, qt, c, o, h, kv, fin, part, memp;
+  } dws[2];
+  DevBuf d_beam;
 
   ~icap_handle() {
     for (DecodeGraph& g : dg) {
@@ -191,9 +196,9 @@ struct icap_handle {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col}) b->release();
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_x, &d_a, &d_qkv, &d_q, &d_qt, &d_c, &d_o, &d_h, &d_memp, &d_beam,
-                      &d_kv, &d_fin, &d_part})
-      b->release();
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_beam}) b->release();
+    for (DecWS& w : dws)
+      for (DevBuf* b : {&w.x, &w.a, &w.qkv, &w.q, &w.qt, &w.c, &w.o, &w.h, &w.kv, &w.fin, &w.part, &w.memp}) b->release();
   }
 
   void* alloc(size_t bytes) {
@@ -601,29 +606,30 @@ DecodeBufs sub_bufs(const DecodeBufs& b, const icap_model_desc& d, int r0, int L
 }
 
 // rows: decoder rows per pass; B: memory images; kv_rows: KV-cache rows (default B; B*K for beams)
-DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_rows = 0) {
+DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_rows = 0, int wsi = 0) {
   if (kv_rows <= 0) kv_rows = B;
   const icap_model_desc& d = h->d;
   const int D = d.d_model, ns = h->ns, H = d.nhead;
-  h->d_x.ensure((size_t)rows * D * 4);
-  h->d_a.ensure((size_t)rows * D * 2 * ns);
-  h->d_qkv.ensure((size_t)rows * 3 * D * 4);
-  h->d_q.ensure((size_t)rows * D * 2 * ns);
-  h->d_qt.ensure((size_t)rows * H * D * 2 * ns);
-  h->d_memp.ensure((size_t)B * S * D * 2 * ns);
-  h->d_c.ensure((size_t)rows * H * D * 2 * ns);
-  h->d_o.ensure((size_t)rows * D * 2 * ns);
-  h->d_h.ensure((size_t)rows * d.dim_ff * 2 * ns);
-  h->d_kv.ensure((size_t)2 * d.n_dec_layers * kv_rows * H * Lmax * 64 * 4);
-  h->d_part.ensure((size_t)MAX_KSPLIT * rows * D * 4);
+  icap_handle::DecWS& w = h->dws[wsi];
+  w.x.ensure((size_t)rows * D * 4);
+  w.a.ensure((size_t)rows * D * 2 * ns);
+  w.qkv.ensure((size_t)rows * 3 * D * 4);
+  w.q.ensure((size_t)rows * D * 2 * ns);
+  w.qt.ensure((size_t)rows * H * D * 2 * ns);
+  w.memp.ensure((size_t)B * S * D * 2 * ns);
+  w.c.ensure((size_t)rows * H * D * 2 * ns);
+  w.o.ensure((size_t)rows * D * 2 * ns);
+  w.h.ensure((size_t)rows * d.dim_ff * 2 * ns);
+  w.kv.ensure((size_t)2 * d.n_dec_layers * kv_rows * H * Lmax * 64 * 4);
+  w.part.ensure((size_t)MAX_KSPLIT * rows * D * 4);
   DecodeBufs b;
-  b.x = h->d_x.as<float>(); b.a = h->d_a.as<bf16_t>(); b.qkv = h->d_qkv.as<float>();
-  b.q = h->d_q.as<bf16_t>(); b.qt = h->d_qt.as<bf16_t>(); b.c = h->d_c.as<bf16_t>();
-  b.o = h->d_o.as<bf16_t>(); b.hb = h->d_h.as<bf16_t>();
-  b.kc = h->d_kv.as<float>();
-  b.part = h->d_part.as<float>();
+  b.x = w.x.as<float>(); b.a = w.a.as<bf16_t>(); b.qkv = w.qkv.as<float>();
+  b.q = w.q.as<bf16_t>(); b.qt = w.qt.as<bf16_t>(); b.c = w.c.as<bf16_t>();
+  b.o = w.o.as<bf16_t>(); b.hb = w.h.as<bf16_t>();
+  b.kc = w.kv.as<float>();
+  b.part = w.part.as<float>();
   b.vc = b.kc + (size_t)d.n_dec_layers * kv_rows * H * Lmax * 64;
-  b.memp = h->d_memp.as<bf16_t>(); b.memL = (long)B * S * D;
+  b.memp = w.memp.as<bf16_t>(); b.memL = (long)B * S * D;
   b.aL = (long)rows * D; b.qL = (long)rows * D; b.cL = (long)rows * H * D; b.hL = (long)rows * d.dim_ff;
   b.kvl = (size_t)kv_rows * H * Lmax * 64;
   b.PS = (long)rows * D;
@@ -699,16 +705,16 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   REQUIRE(B > 0 && max_len >= 1, "bad batch / max_len");
   REQUIRE(max_len <= d.pe_len, "max_len exceeds the positional-encoding table (PositionalEncoding max_len)");
   REQUIRE(S > 0 && S <= 256, "memory length must be in [1, 256]");
-  const int D = d.d_model;
-  DecodeBufs b = dec_bufs(h, B, B, max_len, S);
+  const int D = d.d_model, wsi = uniforms ? 1 : 0;
+  DecodeBufs b = dec_bufs(h, B, B, max_len, S, 0, wsi);
   const float scale = (float)std::sqrt((double)D);
   if (mem) HIPCHK(launch_split_f32(mem, b.memL, b.memp, b.memL, h->ns, s));
   HIPCHK(launch_fill_col(ids, B, max_len, 0, start, s));
   HIPCHK(launch_embed(nullptr, 0, start, B, 1, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
   uint8_t* fin = nullptr;
   if (uniforms) {
-    h->d_fin.ensure((size_t)B);
-    fin = h->d_fin.as<uint8_t>();
+    h->dws[wsi].fin.ensure((size_t)B);
+    fin = h->dws[wsi].fin.as<uint8_t>();
     HIPCHK(launch_fill_u8(fin, B, 0, s));  // a kernel node: reset on every graph replay
   }
   // The images are independent: with dec_branches = 2 the two halves of the batch decode as two
@@ -779,8 +785,8 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
       g.uni.ensure((size_t)(max_len - 1) * B * 4);
       g.lp.ensure((size_t)B * (max_len - 1) * 4);
     }
-    dec_bufs(h, B, B, max_len, S);  // make sure nothing allocates during capture
-    if (mode) h->d_fin.ensure((size_t)B);
+    dec_bufs(h, B, B, max_len, S, 0, mode);  // make sure nothing allocates during capture
+    if (mode) h->dws[mode].fin.ensure((size_t)B);
     if (!h->cap_stream) HIPCHK(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(hipStreamSynchronize(s));
     const bool prof = h->prof_on;
@@ -802,7 +808,7 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     h->prof_on = prof;
     g.gen = g_ws_generation;
   }
-  DecodeBufs b = dec_bufs(h, B, B, max_len, S);  // no allocation: sized at capture
+  DecodeBufs b = dec_bufs(h, B, B, max_len, S, 0, mode);  // no allocation: sized at capture
   HIPCHK(launch_split_f32(mem, b.memL, b.memp, b.memL, h->ns, s));
   if (mode) HIPCHK(hipMemcpyAsync(g.uni.p, uniforms, (size_t)(max_len - 1) * B * 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipGraphLaunch(g.exec, s));
@@ -852,8 +858,8 @@ void decode_beam(icap_handle* h, const float* mem, int B, int S, int max_len, in
     HeadArgs ha{};
     ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = V;
     ha.logits = logits; ha.ld_logits = V;
-    h->d_fin.ensure((size_t)rows * 4);  // scratch argmax ids
-    ha.ids = h->d_fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
+    h->dws[0].fin.ensure((size_t)rows * 4);  // scratch argmax ids
+    ha.ids = h->dws[0].fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
     HIPCHK(launch_head(ha, s));
     HIPCHK(launch_beam_select(logits, V, B, K, t, max_len, grid_variant, end, seq[cur], seq[cur ^ 1], anc[cur],
                               anc[cur ^ 1], sc[cur], sc[cur ^ 1], kcur, done, ncomp, best_score, best_seq, best_len,
@@ -992,8 +998,8 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
     HeadArgs ha{};
     ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = h->d.vocab;
     ha.logits = logits; ha.ld_logits = h->d.vocab;
-    h->d_fin.ensure((size_t)rows * 4);  // scratch ids
-    ha.ids = h->d_fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
+    h->dws[0].fin.ensure((size_t)rows * 4);  // scratch ids
+    ha.ids = h->dws[0].fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
     HIPCHK(launch_head(ha, s));
   });
 }

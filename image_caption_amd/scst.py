@@ -45,6 +45,34 @@ class TeacherForcedLogProbs(nn.Module):
         return masked_token_logp(logits, ids, self.end_token)
 
 
+_STREAMS = {}
+
+
+def sample_and_greedy(eng, memory: torch.Tensor, uniforms: torch.Tensor, start: int, end: int, max_len: int):
+    """The SCST step's two decodes of one memory, the sampled one (icap_decode_sample) and the
+    greedy baseline (icap_decode_greedy), replayed CONCURRENTLY on two streams: each decode mode owns
+    its workspace and captured graph, and both are latency-bound chains of small kernels that leave
+    most CUs idle.  Returns (sample_ids, sample_logp, greedy_ids) ready on the current stream."""
+    dev = memory.device
+    cur = torch.cuda.current_stream(dev)
+    if dev not in _STREAMS:
+        _STREAMS[dev] = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+    s1, s2 = _STREAMS[dev]
+    s1.wait_stream(cur)
+    s2.wait_stream(cur)
+    with torch.cuda.stream(s1):
+        sid, lp = eng.sample(memory, uniforms, start, end, max_len)
+    with torch.cuda.stream(s2):
+        gid, _ = eng.greedy_raw(memory, start, end, max_len)
+    for t, st in ((memory, s1), (memory, s2), (uniforms, s1)):
+        t.record_stream(st)
+    cur.wait_stream(s1)
+    cur.wait_stream(s2)
+    for t in (sid, lp, gid):
+        t.record_stream(cur)
+    return sid, lp, gid
+
+
 def _pad_cols(x: torch.Tensor, L: int, value: int) -> torch.Tensor:
     if x.shape[1] >= L:
         return x

@@ -118,3 +118,22 @@ def test_scst_rewards_gpu_equal_cpu(cuda):
     s_gpu, g_gpu = rewards(sid.to(cuda), gid.to(cuda), refs.to(cuda), W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN)
     assert torch.allclose(s_gpu.cpu(), s_cpu, atol=1e-6) and torch.allclose(g_gpu.cpu(), g_cpu, atol=1e-6)
     assert s_cpu.abs().sum() > 0
+
+
+@pytest.mark.gpu
+def test_concurrent_sample_and_greedy_equal_sequential(cuda):
+    """scst.sample_and_greedy (both decode graphs replayed concurrently on two streams, one workspace
+    per decode mode) returns exactly what the two sequential calls return, on every replay."""
+    from image_caption_amd.engine import Engine
+    from image_caption_amd.scst import sample_and_greedy
+
+    eng = Engine(W.to_torch(W.vit_state_dict(0)), "vit", {}, device=cuda)
+    g = torch.Generator().manual_seed(2)
+    mem = torch.randn(96, 49, 512, generator=g).to(cuda)
+    uni = torch.rand(11, 96, generator=g).to(cuda)
+    ref_s, ref_lp = eng.sample(mem, uni, W.START_TOKEN, W.END_TOKEN, 12)
+    ref_g, _ = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, 12)
+    for _ in range(4):  # eager, capture, replays
+        sid, lp, gid = sample_and_greedy(eng, mem, uni, W.START_TOKEN, W.END_TOKEN, 12)
+        torch.cuda.synchronize()
+        assert torch.equal(sid, ref_s) and torch.equal(lp, ref_lp) and torch.equal(gid, ref_g)
