@@ -349,10 +349,12 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
 #pragma unroll 1
   for (int c = 0; c < nch; ++c) {
     const int younger = min(NBUF - 2, nch - 1 - c);
-    if (!uniform_issue) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * IPW) : "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // lgkmcnt(0): this wave's LDS reads of the slot read last iteration must be done before the
+    // barrier after which another wave refills that slot
+    if (!uniform_issue) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * IPW) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(IPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (c + NBUF - 1 < nch) stage(c + NBUF - 1, (c + NBUF - 1) % NBUF);
     const char* Kh = smem + (c % NBUF) * CHUNK;

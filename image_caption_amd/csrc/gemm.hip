@@ -858,9 +858,11 @@ __global__ __launch_bounds__(NW * 64, BMT == 128 ? 4 : (BMT == 64 ? 3 : 1)) void
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt must have landed for every wave: leave the younger prefetched stages in flight
     const int younger = min(NSTAGE - 2, nk - 1 - kt);
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_STAGE) : "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STAGE) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // lgkmcnt(0): this wave's LDS reads of the previous step must be done before the barrier that
+    // lets other waves' DMA overwrite that buffer (a 2-stage ring refills it one step later)
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * PER_STAGE) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // refill the buffer read in iteration kt-1 (every wave has passed this barrier)
     if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);

@@ -58,6 +58,8 @@ struct DevBuf {
     n = 0;
     HIPCHK(hipMalloc(&p, bytes));
     n = bytes;
+    static const bool poison = getenv("ICAP_POISON") && atoi(getenv("ICAP_POISON"));
+    if (poison) HIPCHK(hipMemset(p, 0xFF, bytes));  // debug: NaN in fp32 and bf16 - exposes reads of unwritten workspace
   }
   void release() {
     if (p) (void)hipFree(p);

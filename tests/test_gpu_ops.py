@@ -114,3 +114,41 @@ def test_enc_attention(cuda, B, N, H, nsplit):
     got = value(out if nsplit == 2 else out[0], nsplit)
     tol = 3e-2 if nsplit == 1 else 2e-4
     assert (got - ref).abs().max().item() < tol
+
+
+def test_full_chip_kernels_repeat_bitwise(cuda):
+    """Races between a wave's LDS reads and another wave's LDS-DMA refill of the same ring slot show
+    up as run-to-run differences: the 128x256 two-blocks-per-CU GEMM (full chip, M = 50432, K = 768
+    and 3072) and the pipelined encoder attention (B = 256, N = 197) are run repeatedly in one
+    process and must reproduce bit for bit, and match the fp64 reference."""
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    for M, N, K in ((50432, 768, 768), (50432, 768, 3072)):
+        a = torch.randn(M, K, generator=g).to(cuda)
+        w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(cuda)
+        bias = torch.randn(N, generator=g).to(cuda)
+        A = planes(a, 2)
+        outs = []
+        for _ in range(8):
+            C = torch.empty(M, N, device=cuda)
+            L.check(lib.icap_op_gemm(A.data_ptr(), K, M * K, 2, w.data_ptr(), bias.data_ptr(), C.data_ptr(), N, 0,
+                                     M, N, K, 0, 0, L.stream_ptr()), "gemm")
+            outs.append(C)
+        torch.cuda.synchronize()
+        assert all(torch.equal(o, outs[0]) for o in outs[1:])
+        rows = torch.arange(0, M, 997, device=cuda)
+        ref = (A[0].double() + A[1].double())[rows] @ w.double().t()
+        ref = ref + bias.double()
+        assert (outs[0][rows].double() - ref).abs().max().item() < 2e-4 * max(1.0, ref.abs().max().item())
+    B, Nt, H = 256, 197, 12
+    D = H * 64
+    qkv = (torch.randn(B * Nt, 3 * D, generator=g) * 1.5).to(cuda)
+    P = planes(qkv, 2)
+    outs = []
+    for _ in range(6):
+        out = torch.zeros(2, B * Nt, D, device=cuda, dtype=torch.bfloat16)
+        L.check(lib.icap_op_enc_attention(P.data_ptr(), B * Nt * 3 * D, B, Nt, H, out.data_ptr(), B * Nt * D, 2,
+                                          L.stream_ptr()), "attn")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, outs[0]) for o in outs[1:])
