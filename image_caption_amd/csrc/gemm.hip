@@ -770,11 +770,15 @@ namespace {
 // BMT = 128 with NW = 8 and NST = 2: the same 64 x 64 wave tiles in a 128 x 256 block tile with a
 // 2-stage ring (64 KiB of LDS), so two blocks share a CU and one's epilogue overlaps the other's
 // k-loop (the output-heavy, short-K trunk GEMMs).
-template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0>
-__global__ __launch_bounds__(NW * 64, BMT == 128 ? 4 : (BMT == 64 ? 3 : 1)) void gemm_256_kernel(GemmArgs p) {
+// KSD = 64: 64-deep stages (two MFMA k-steps): every operand row segment is a full 128-B line
+// (8 rows x 128 B per DMA instruction, chunk c of row r at c ^ (r & 7)) and half the barriers.
+template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0, int KSD = 32>
+__global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64 ? 3 : 1)) void gemm_256_kernel(
+    GemmArgs p) {
   constexpr int WGM = NW / 4;                       // wave grid WGM x 4
   constexpr int BM = BMT, BN = 256, WM = BM / WGM, WN = 64, TM = WM / 16, TN = WN / 16;
-  constexpr int KS = 32;                            // k per stage (one MFMA k-step)
+  constexpr int KS = KSD;                           // k per stage (one or two MFMA k-steps)
+  constexpr int RPI = KS == 64 ? 8 : 16;            // rows per 1 KiB DMA instruction
   constexpr int OPB = BM * KS * 2;                  // A bytes per plane per stage (16 KiB at BM 256)
   constexpr int OPBW = BN * KS * 2;                 // W bytes per stage (16 KiB)
   constexpr int STAGE = NS * OPB + OPBW;            // A planes + W share one stage
@@ -799,16 +803,19 @@ __global__ __launch_bounds__(NW * 64, BMT == 128 ? 4 : (BMT == 64 ? 3 : 1)) void
   // Stage image: per operand tile, rows of 64 B (32 bf16 of k); one DMA instruction = 16 rows.
   // 16-byte chunk c of row r lives at chunk c ^ sw(r), sw(r) = ((r >> 3) & 1) << 1, which makes
   // the ds_read_b128 fragment reads (16 rows x one chunk per lane group) bank-conflict free.
-  const int srow = wave * IPW * 16 + (lane >> 2), srow_w = wave * IPWW * 16 + (lane >> 2);
-  const int schunk = (lane & 3) ^ (((srow >> 3) & 1) << 1);  // (row >> 3) & 1 is the same for both
+  const int srow = KS == 64 ? wave * IPW * 8 + (lane >> 3) : wave * IPW * 16 + (lane >> 2);
+  const int srow_w = KS == 64 ? wave * IPWW * 8 + (lane >> 3) : wave * IPWW * 16 + (lane >> 2);
+  // (the swizzle depends on row bits that are equal for srow and srow_w: instruction bases are
+  // multiples of RPI)
+  const int schunk = KS == 64 ? (lane & 7) ^ (srow & 7) : (lane & 3) ^ (((srow >> 3) & 1) << 1);
   const bf16_t* a_base = p.A + (long)min(m0 + srow, M - 1) * p.lda + schunk * 8;
   const bf16_t* b_base = p.W + (long)min(n0 + srow_w, p.N - 1) * p.ldw + schunk * 8;
-  const long a_step = 16 * p.lda, b_step = 16 * p.ldw;
+  const long a_step = RPI * p.lda, b_step = RPI * p.ldw;
   const bool a_tail = m0 + BM > M;
   ConvRow cr[CONV ? IPW : 1];
   if (CONV)
 #pragma unroll
-    for (int i = 0; i < IPW; ++i) cr[i] = conv_row(p, min(m0 + srow + i * 16, M - 1));
+    for (int i = 0; i < IPW; ++i) cr[i] = conv_row(p, min(m0 + srow + i * RPI, M - 1));
   auto stage = [&](int kt, int buf) {
     const int kin = kt * KS;
     char* s0 = smem + buf * STAGE;
@@ -833,7 +840,7 @@ __global__ __launch_bounds__(NW * 64, BMT == 128 ? 4 : (BMT == 64 ? 3 : 1)) void
       for (int i = 0; i < IPW; ++i) {
         const bf16_t* src = Ab + i * a_step;
         if (CONV) src = conv_src<CONV>(p, p.A + pl * p.a_lo, cr[CONV ? i : 0], kin + schunk * 8);
-        else if (a_tail && m0 + srow + i * 16 >= M) src = Ab + (long)(M - 1 - m0 - srow) * p.lda;
+        else if (a_tail && m0 + srow + i * RPI >= M) src = Ab + (long)(M - 1 - m0 - srow) * p.lda;
         __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
                                          (LDS_AS void*)(s0 + pl * OPB + (wave * IPW + i) * 1024), 16, 0, 0);
       }
@@ -868,23 +875,41 @@ __global__ __launch_bounds__(NW * 64, BMT == 128 ? 4 : (BMT == 64 ? 3 : 1)) void
     if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
     const char* s0 = smem + (kt % NSTAGE) * STAGE;
     if (NOMFMA >= 2) continue;
-    bf16x8 bfr[TN];
+    if constexpr (KS == 64) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + NS * OPB + (wn * WN + j * 16) * 64 + foff);
+      for (int ks = 0; ks < 2; ++ks) {
+        const int fo = fr * 128 + (((ks * 4 + fq) ^ (fr & 7)) << 4);
+        bf16x8 bfr[TN];
 #pragma unroll
-    for (int pl = 0; pl < NS; ++pl)
+        for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + NS * OPB + (wn * WN + j * 16) * 128 + fo);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const bf16x8 af = *(const bf16x8*)(s0 + pl * OPB + (wm * WM + i * 16) * 64 + foff);
+        for (int pl = 0; pl < NS; ++pl)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if (NOMFMA) {  // measurement variant: staging pipeline only (keeps the fragment reads live)
-            asm volatile("" ::"v"(af), "v"(bfr[j]));
-          } else {
-            acc[i][j] = mfma16(bfr[j], af, acc[i][j]);  // D = W·A^T
+          for (int i = 0; i < TM; ++i) {
+            const bf16x8 af = *(const bf16x8*)(s0 + pl * OPB + (wm * WM + i * 16) * 128 + fo);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af, acc[i][j]);
+          }
+      }
+    } else {
+      bf16x8 bfr[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + NS * OPB + (wn * WN + j * 16) * 64 + foff);
+#pragma unroll
+      for (int pl = 0; pl < NS; ++pl)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8 af = *(const bf16x8*)(s0 + pl * OPB + (wm * WM + i * 16) * 64 + foff);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if (NOMFMA) {  // measurement variant: staging pipeline only (keeps the fragment reads live)
+              asm volatile("" ::"v"(af), "v"(bfr[j]));
+            } else {
+              acc[i][j] = mfma16(bfr[j], af, acc[i][j]);  // D = W·A^T
+            }
           }
         }
-      }
+    }
   }
 
   epilogue_256<TM, TN>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
@@ -1081,6 +1106,36 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
     constexpr int ldsq = 2 * (2 * 64 * 32 * 2 + 256 * 32 * 2), ldsq1 = 2 * (64 * 32 * 2 + 256 * 32 * 2);
     if (g.nsplit == 2) hipLaunchKernelGGL((gemm_256_kernel<2, 4, 0, 0, 64, 2>), dim3(nwgq), dim3(256), ldsq, s, g);
     else hipLaunchKernelGGL((gemm_256_kernel<1, 4, 0, 0, 64, 2>), dim3(nwgq), dim3(256), ldsq1, s, g);
+    return hipGetLastError();
+  }
+  static int tall_ks = 0;  // ICAP_GEMM_TALL_KS: 32 (default) or 64 (64-deep stages, 128 KiB, 1 block per CU)
+  if (!tall_ks) {
+    const char* v = getenv("ICAP_GEMM_TALL_KS");
+    tall_ks = v && atoi(v) == 64 ? 64 : 32;
+  }
+  if (tall_min_k && g.K >= tall_min_k && (nw == 8 || nw == 16) && tall_ks == 64 && g.K % 64 == 0) {
+    const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
+    constexpr int lds64 = 2 * (2 * 128 * 64 * 2 + 256 * 64 * 2), lds64_1 = 2 * (128 * 64 * 2 + 256 * 64 * 2);
+    static bool attr64 = false;
+    if (!attr64) {
+      hipError_t e = hipSuccess;
+      for (const void* f : {(const void*)gemm_256_kernel<2, 8, 0, 0, 128, 2, 64>,
+                            (const void*)gemm_256_kernel<2, 8, 0, 1, 128, 2, 64>})
+        if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds64);
+      for (const void* f : {(const void*)gemm_256_kernel<1, 8, 0, 0, 128, 2, 64>,
+                            (const void*)gemm_256_kernel<1, 8, 0, 1, 128, 2, 64>})
+        if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds64_1);
+      if (e != hipSuccess) return e;
+      attr64 = true;
+    }
+    if (g.cv && g.cv != 1) return hipErrorInvalidValue;
+    if (g.nsplit == 2) {
+      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 1, 128, 2, 64>), dim3(nwgh), dim3(512), lds64, s, g);
+      else hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 0, 128, 2, 64>), dim3(nwgh), dim3(512), lds64, s, g);
+    } else {
+      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 1, 128, 2, 64>), dim3(nwgh), dim3(512), lds64_1, s, g);
+      else hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 64>), dim3(nwgh), dim3(512), lds64_1, s, g);
+    }
     return hipGetLastError();
   }
   if (tall_min_k && g.K >= tall_min_k && (nw == 8 || nw == 16)) {
