@@ -1179,3 +1179,153 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
   }
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// int8 two-slice encoder GEMM for the LayerNorm-fed projections (ViT QKV, MLP-1, final projection
+// in ICAP_PREC_I8X2).  Both operands are 16-bit fixed point under a per-row scale, held as two int8
+// slices: v = s (256 v1 + v2), v1 in [-127, 127], v2 in [-128, 127] (the activation slices come from
+// layernorm_i8_kernel, the weight slices from pack_i8_rows_kernel).  The product is
+//   A.W^T = s_a s_w (65536 A1.W1 + 256 (A1.W2 + A2.W1) + A2.W2)
+// with the last term (<= 2^-16 of the first, below the representation's own rounding) dropped, so
+// three v_mfma_i32_16x16x64_i8 per 64-deep k-step and 16x16 tile; int32 accumulation is exact
+// (|A1.W1| <= K 127^2 < 2^31 for K < 133k).  Against the bf16x2 form (A as hi/lo bf16 planes, W
+// bf16: 6 staged bytes per k per row pair, two bf16 MFMAs per 32-deep k-step) this stages 4 bytes per k
+// and does 3/4 of the MFMA cycles (the i8 16x16x64 MFMA takes the cycles of bf16 16x16x32).
+// Block tile 128 x 256 (8 waves as 2 x 4, each 64 x 64 = 4 x 4 MFMA tiles with a high and a mid int32
+// accumulator set: 128 accumulator registers, so one block per CU), 64-deep stages of four operand
+// tiles (A1, A2: 128 rows; W1, W2: 256 rows; rows of 64 B with the gemm_256 chunk swizzle) in a
+// 3-stage LDS ring (144 KiB) filled by global_load_lds, counted vmcnt + raw barrier, XCD remap.
+// Fragment reads are the bf16 kernel's (16 B of one row per lane): the same byte positions feed
+// the A and B operands, so the k labelling inside the MFMA does not matter.
+namespace {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+template <int NSTAGE>
+__global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
+  constexpr int NW = 8, BM = 128, BN = 256, WM = 64, WN = 64, TM = WM / 16, TN = WN / 16;
+  constexpr int OPB = BM * 64, OPBW = BN * 64;     // bytes per A / W slice per stage
+  constexpr int STAGE = 2 * OPB + 2 * OPBW;         // 48 KiB
+  constexpr int IPW = OPB / 1024 / NW, IPWW = OPBW / 1024 / NW;
+  constexpr int PER_STAGE = 2 * IPW + 2 * IPWW;     // DMA instructions per wave per stage
+  static_assert(IPW >= 1 && IPWW >= 1, "tile / wave shape");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
+  const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int bm = wg / nbn, bn = wg - bm * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int M = p.M, nk = p.K / 64;
+
+  const int srow = wave * IPW * 16 + (lane >> 2), srow_w = wave * IPWW * 16 + (lane >> 2);
+  const int schunk = (lane & 3) ^ (((srow >> 3) & 1) << 1);
+  const char* A = (const char*)p.A;
+  const char* Wt = (const char*)p.W;
+  const long b_step = 16 * p.ldw;
+  const char* a_base[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) a_base[i] = A + (long)min(m0 + srow + i * 16, M - 1) * p.lda + schunk * 16;
+  const char* b_base = Wt + (long)min(n0 + srow_w, p.N - 1) * p.ldw + schunk * 16;
+  auto stage = [&](int kt, int buf) {
+    const int kin = kt * 64;
+    char* s0 = smem + buf * STAGE;
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+      for (int i = 0; i < IPW; ++i)
+        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(a_base[i] + pl * p.a_lo + kin),
+                                         (LDS_AS void*)(s0 + pl * OPB + (wave * IPW + i) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+      for (int i = 0; i < IPWW; ++i)
+        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(b_base + pl * p.w_lo + kin + i * b_step),
+                                         (LDS_AS void*)(s0 + 2 * OPB + pl * OPBW + (wave * IPWW + i) * 1024), 16, 0,
+                                         0);
+  };
+
+  i32x4 ah[TM][TN], am[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) ah[i][j] = am[i][j] = (i32x4){0, 0, 0, 0};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int foff = fr * 64 + ((fq ^ (((fr >> 3) & 1) << 1)) << 4);
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) stage(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int younger = min(NSTAGE - 2, nk - 1 - kt);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * PER_STAGE) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    const char* s0 = smem + (kt % NSTAGE) * STAGE;
+    i32x4 w1[TN], w2[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      w1[j] = *(const i32x4*)(s0 + 2 * OPB + (wn * WN + j * 16) * 64 + foff);
+      w2[j] = *(const i32x4*)(s0 + 2 * OPB + OPBW + (wn * WN + j * 16) * 64 + foff);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const i32x4 a1 = *(const i32x4*)(s0 + (wm * WM + i * 16) * 64 + foff);
+      const i32x4 a2 = *(const i32x4*)(s0 + OPB + (wm * WM + i * 16) * 64 + foff);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        ah[i][j] = mfma_i8(w1[j], a1, ah[i][j]);  // D = W.A^T, as the bf16 kernel
+        am[i][j] = mfma_i8(w2[j], a1, am[i][j]);
+        am[i][j] = mfma_i8(w1[j], a2, am[i][j]);
+      }
+    }
+  }
+
+  const int mb = m0 + wm * WM, nb = n0 + wn * WN;
+  f32x4 acc[TM][TN];
+  f32x4 ws[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) ws[j] = *(const f32x4*)(p.w_scale + nb + j * 16 + 4 * fq);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const float sa = p.a_scale[min(mb + i * 16 + fr, M - 1)];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[i][j][e] = fmaf((float)ah[i][j][e], 65536.f, (float)am[i][j][e] * 256.f) * (sa * ws[j][e]);
+  }
+  GemmArgs pe = p;
+  pe.scale = nullptr;
+  pe.res = nullptr;
+  epilogue_256<TM, TN>(pe, acc, mb, nb, fr, fq);
+}
+
+}  // namespace
+
+hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
+  if (g.M <= 0 || g.N % 256 || g.K % 64 || g.batch != 1 || !g.a_scale || !g.w_scale || g.cv || g.scale || g.res ||
+      g.lda < g.K || g.ldw < g.K || (g.lda & 15) || (g.ldw & 15) || (g.a_lo & 15) || (g.w_lo & 15))
+    return hipErrorInvalidValue;
+  if (g.hm_n && (g.out != OUT_SPLIT || g.N % 64 || g.rm_group || g.M % g.hm_n)) return hipErrorInvalidValue;
+  const long last_row = g.rm_group ? (long)((g.M - 1) / g.rm_group) * g.rm_stride + g.rm_off + g.rm_group : g.M;
+  if (last_row * g.ldc >= (1L << 31)) return hipErrorInvalidValue;  // epilogue uses 32-bit row offsets
+  constexpr int NST = 3, lds = NST * (2 * 128 * 64 + 2 * 256 * 64);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_i8_kernel<NST>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nwg = (g.N / 256) * ((g.M + 127) / 128);
+  hipLaunchKernelGGL((gemm_i8_kernel<NST>), dim3(nwg), dim3(512), lds, s, g);
+  return hipGetLastError();
+}

@@ -75,12 +75,18 @@ struct Lin {  // packed nn.Linear: bf16 W [N][K] + fp32 bias
   float* b = nullptr;
   int N = 0, K = 0;
 };
+struct Lin8 {  // nn.Linear as int8 two-slice planes [2][N][K] + per-row scale (ICAP_PREC_I8X2)
+  int8_t* w = nullptr;
+  float *sw = nullptr, *b = nullptr;
+  int N = 0, K = 0;
+};
 struct LN {
   float *w = nullptr, *b = nullptr;
 };
 struct VitLayer {
   LN ln1, ln2;
   Lin qkv, out, mlp0, mlp3;
+  Lin8 qkv8, mlp08;
 };
 struct EncLayer {
   Lin qkv, out, lin1, lin2;
@@ -127,6 +133,7 @@ struct icap_handle {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   DecodeGraph dg[2];  // one captured loop per mode (0 greedy, 1 sample): SCST alternates them
   int ns = 2;  // activation planes (1 = bf16, 2 = hi/lo)
+  bool i8 = false;  // ICAP_PREC_I8X2: LayerNorm-fed ViT GEMMs on int8 two-slice operands
   std::vector<void*> owned;
   // decoder
   float *emb = nullptr, *pe = nullptr, *fc_w = nullptr, *fc_b = nullptr;
@@ -134,6 +141,7 @@ struct icap_handle {
   // vit
   float *cls = nullptr, *pos = nullptr, *vit_ln_w = nullptr, *vit_ln_b = nullptr;
   Lin conv, proj;
+  Lin8 proj8;
   std::vector<VitLayer> vit;
   // grid
   float* enc_pe = nullptr;
@@ -177,7 +185,7 @@ struct icap_handle {
   }
 
   // workspaces
-  DevBuf e_x, e_a, e_qkv, e_h, e_patch;  // encoder
+  DevBuf e_x, e_a, e_qkv, e_h, e_patch, e_sa;  // encoder (e_sa: int8 row scales)
   DevBuf t_x, t_y, t_1, t_2, t_r, t_col;  // ResNet trunk (NHWC planes)
   // decoder workspaces, one set per decode mode (0: greedy / beam / teacher-forced, 1: sampled), so
   // the greedy and sampled graphs of an SCST step can replay concurrently on two streams
@@ -198,7 +206,7 @@ struct icap_handle {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col}) b->release();
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &d_beam}) b->release();
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &d_beam}) b->release();
     for (DecWS& w : dws)
       for (DevBuf* b : {&w.x, &w.a, &w.qkv, &w.q, &w.qt, &w.c, &w.o, &w.h, &w.kv, &w.fin, &w.part, &w.memp}) b->release();
   }
@@ -224,6 +232,17 @@ struct icap_handle {
   Lin lin(const float* w, const float* b, int N, int K, hipStream_t s) {
     Lin l;
     l.w = own_bf16(w, (size_t)N * K, s);
+    l.b = b ? own_f32(b, N, s) : nullptr;
+    l.N = N;
+    l.K = K;
+    return l;
+  }
+  Lin8 lin8(const float* w, const float* b, int N, int K, hipStream_t s) {
+    REQUIRE(w != nullptr, "missing parameter pointer");
+    Lin8 l;
+    l.w = (int8_t*)alloc((size_t)2 * N * K);
+    l.sw = (float*)alloc((size_t)N * 4);
+    HIPCHK(launch_pack_i8_rows(w, N, K, l.w, (long)N * K, l.sw, s));
     l.b = b ? own_f32(b, N, s) : nullptr;
     l.N = N;
     l.K = K;
@@ -262,6 +281,21 @@ struct icap_handle {
     g.M = M; g.N = W.N; g.K = W.K; g.nsplit = ns; g.c_planes = ns;
     g.epi = epi; g.out = out;
     run_gemm(g, s);
+  }
+  // int8 two-slice GEMM: A = int8 planes [2][M][K] (plane stride a_lo bytes) with row scales sa
+  void gemm8(const int8_t* A, long a_lo, const float* sa, const Lin8& W, int M, void* C, long ldc, long c_lo, int epi,
+             int out, hipStream_t s, int hm_n = 0) {
+    GemmArgs g = gemm_args();
+    g.hm_n = hm_n;
+    g.A = (const bf16_t*)A; g.lda = W.K; g.a_lo = a_lo; g.a_scale = sa;
+    g.W = (const bf16_t*)W.w; g.ldw = W.K; g.w_lo = (long)W.N * W.K; g.w_scale = W.sw;
+    g.bias = W.b;
+    g.C = C; g.ldc = ldc; g.c_lo = c_lo;
+    g.M = M; g.N = W.N; g.K = W.K; g.nsplit = 2; g.c_planes = ns;
+    g.epi = epi; g.out = out;
+    const double flops = 2.0 * M * W.N * W.K;
+    const double bytes = 2.0 * ((double)M * W.K + (double)W.N * W.K);
+    timed(PROF_GEMM_I8, flops, bytes, s, [&] { HIPCHK(launch_gemm_i8(g, s)); });
   }
   // decode-step GEMM (wave tiles, optional split-K into fp32 partial slabs)
   void wgemm(const bf16_t* A, long lda, long a_lo, const bf16_t* W, long ldw, const float* bias, int M, int N, int K,
@@ -336,11 +370,16 @@ void pack(icap_handle* h, hipStream_t s) {
       o.ln2 = h->ln(L.ln_2, V, s);
       o.mlp0 = h->lin(L.mlp0_w, L.mlp0_b, d.vit_mlp, V, s);
       o.mlp3 = h->lin(L.mlp3_w, L.mlp3_b, V, d.vit_mlp, s);
+      if (h->i8) {
+        o.qkv8 = h->lin8(L.attn.in_w, L.attn.in_b, 3 * V, V, s);
+        o.mlp08 = h->lin8(L.mlp0_w, L.mlp0_b, d.vit_mlp, V, s);
+      }
       h->vit.push_back(o);
     }
     h->vit_ln_w = h->own_f32(d.vit_ln_w, V, s);
     h->vit_ln_b = h->own_f32(d.vit_ln_b, V, s);
     h->proj = h->lin(d.proj_w, d.proj_b, D, V, s);
+    if (h->i8) h->proj8 = h->lin8(d.proj_w, d.proj_b, D, V, s);
   } else if (d.kind == ICAP_KIND_GRID) {
     h->proj = h->lin(d.proj_w, d.proj_b, D, d.cnn_dim, s);
     if (d.n_trunk) {
@@ -404,6 +443,15 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   bf16_t* qkv = h->e_qkv.as<bf16_t>();
   bf16_t* hb = h->e_h.as<bf16_t>();
   const long pL = (long)B * np * Kp, aL = (long)M * V, qL = (long)M * 3 * V, hL = (long)M * d.vit_mlp;
+  // ICAP_PREC_I8X2: the LayerNorm outputs as int8 two-slice planes [2][M][V] (in e_a, which the
+  // bf16x2 planes of the attention output reuse afterwards) + row scales
+  int8_t* a8 = (int8_t*)a;
+  const long a8L = (long)M * V;
+  float* sa = nullptr;
+  if (h->i8) {
+    h->e_sa.ensure((size_t)M * 4);
+    sa = h->e_sa.as<float>();
+  }
 
   HIPCHK(launch_im2col_patches(img, B, 3, d.image, d.patch, patch, pL, ns, s));
   {  // patch-embed GEMM: rows (b, p) -> x[b*T + 1 + p] with conv bias + pos[1 + p]
@@ -419,17 +467,32 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   }
   HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
   for (const VitLayer& L : h->vit) {
-    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
     // QKV written head-major ([image][q|k|v x head][token][64]) for the attention's contiguous rows
-    h->gemm(a, V, aL, L.qkv, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s, hm);
+    if (h->i8) {
+      HIPCHK(launch_layernorm_i8(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, a8, V, a8L, sa, s));
+      h->gemm8(a8, a8L, sa, L.qkv8, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s, hm);
+    } else {
+      HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
+      h->gemm(a, V, aL, L.qkv, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s, hm);
+    }
     h->attention(qkv, 3 * V, qL, B, T, d.vit_heads, a, V, aL, s, hm ? 1 : 0);
     h->gemm(a, V, aL, L.out, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s);
-    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
-    h->gemm(a, V, aL, L.mlp0, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);
+    if (h->i8) {
+      HIPCHK(launch_layernorm_i8(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, a8, V, a8L, sa, s));
+      h->gemm8(a8, a8L, sa, L.mlp08, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);
+    } else {
+      HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
+      h->gemm(a, V, aL, L.mlp0, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);
+    }
     h->gemm(hb, d.vit_mlp, hL, L.mlp3, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s);
   }
   // final LN on patch rows only (drop CLS), then projection 768 -> d_model
   const long a2L = (long)B * np * V;
+  if (h->i8) {
+    HIPCHK(launch_layernorm_i8(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, a8, V, a2L, sa, s));
+    h->gemm8(a8, a2L, sa, h->proj8, B * np, memory, Dm, 0, EPI_NONE, OUT_F32, s);
+    return;
+  }
   HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, nullptr, 0, a, V, a2L, ns, s));
   h->gemm(a, V, a2L, h->proj, B * np, memory, Dm, 0, EPI_NONE, OUT_F32, s);
 }
@@ -882,11 +945,14 @@ const char* icap_last_error(void) { return g_err.c_str(); }
 int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
   return guarded([&] {
     REQUIRE(desc && out, "null argument");
-    REQUIRE(desc->precision == ICAP_PREC_BF16 || desc->precision == ICAP_PREC_BF16X2, "bad precision");
+    REQUIRE(desc->precision == ICAP_PREC_BF16 || desc->precision == ICAP_PREC_BF16X2 ||
+                desc->precision == ICAP_PREC_I8X2,
+            "bad precision");
     icap_handle* h = new icap_handle();
     try {
       h->d = *desc;
-      h->ns = desc->precision == ICAP_PREC_BF16X2 ? 2 : 1;
+      h->ns = desc->precision == ICAP_PREC_BF16 ? 1 : 2;
+      h->i8 = desc->precision == ICAP_PREC_I8X2 && desc->kind == ICAP_KIND_VIT;
       if (const char* v = getenv("ICAP_DEC_BRANCHES")) h->dec_branches = std::max(1, std::min(2, atoi(v)));
       pack(h, (hipStream_t)stream);
       HIPCHK(hipStreamSynchronize((hipStream_t)stream));
@@ -1063,6 +1129,29 @@ int icap_op_layernorm(const float* x, int rows, int D, const float* w, const flo
   return guarded([&] {
     HIPCHK(launch_layernorm(x, D, rows, D, 0, 0, 0, w, b, eps, out_f32, D, out_bf, D, bf_lo, nsplit,
                             (hipStream_t)stream));
+  });
+}
+
+int icap_op_pack_i8(const float* x, int rows, int K, int8_t* out, long lo, float* scale, void* stream) {
+  return guarded([&] { HIPCHK(launch_pack_i8_rows(x, rows, K, out, lo, scale, (hipStream_t)stream)); });
+}
+
+int icap_op_layernorm_i8(const float* x, int rows, int D, const float* w, const float* b, float eps, int8_t* out,
+                         long lo, float* scale, void* stream) {
+  return guarded([&] {
+    HIPCHK(launch_layernorm_i8(x, D, rows, D, 0, 0, 0, w, b, eps, out, D, lo, scale, (hipStream_t)stream));
+  });
+}
+
+int icap_op_gemm_i8(const int8_t* A, long a_lo, const float* a_scale, const int8_t* W, long w_lo, const float* w_scale,
+                    const float* bias, float* C, int M, int N, int K, int epi, void* stream) {
+  return guarded([&] {
+    GemmArgs g = gemm_args();
+    g.A = (const bf16_t*)A; g.lda = K; g.a_lo = a_lo; g.a_scale = a_scale; g.nsplit = 2;
+    g.W = (const bf16_t*)W; g.ldw = K; g.w_lo = w_lo; g.w_scale = w_scale; g.bias = bias;
+    g.C = C; g.ldc = N;
+    g.M = M; g.N = N; g.K = K; g.epi = epi; g.out = OUT_F32;
+    HIPCHK(launch_gemm_i8(g, (hipStream_t)stream));
   });
 }
 

@@ -65,6 +65,97 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
 }
 
+// int8 two-slice quantisation (the operand form of gemm_i8_kernel): 16-bit fixed point relative to
+// the row maximum, q = rint(v / s) in [-32639, 32639], v1 = (q + 128) >> 8 in [-127, 127],
+// v2 = q - 256 v1 in [-128, 127]; four consecutive values -> one 32-bit word per slice.
+__device__ __forceinline__ void q2_pack4(const float* y, float inv, uint32_t& hi, uint32_t& lo) {
+  hi = lo = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int qv = __float2int_rn(fminf(fmaxf(y[k] * inv, -32639.f), 32639.f));
+    const int v1 = (qv + 128) >> 8, v2 = qv - (v1 << 8);
+    hi |= (uint32_t)(v1 & 0xff) << (8 * k);
+    lo |= (uint32_t)(v2 & 0xff) << (8 * k);
+  }
+}
+
+// layernorm_kernel's row statistics, output as int8 two-slice planes + the row scale (one wave per row)
+template <int PER>
+__global__ __launch_bounds__(256) void layernorm_i8_kernel(const float* __restrict__ x, long ldx, int rows,
+                                                           int in_group, long in_stride, long in_off,
+                                                           const float* __restrict__ w, const float* __restrict__ b,
+                                                           float eps, int8_t* out, long ld, long lo,
+                                                           float* __restrict__ scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = PER * 64;
+  const long irow = in_group ? (long)(row / in_group) * in_stride + in_off + row % in_group : (long)row;
+  const float* xr = x + irow * ldx;
+  float v[PER];
+#pragma unroll
+  for (int c = 0; c < PER / 4; ++c) {
+    f32x4 t = *(const f32x4*)(xr + c * 256 + lane * 4);
+    v[c * 4 + 0] = t[0]; v[c * 4 + 1] = t[1]; v[c * 4 + 2] = t[2]; v[c * 4 + 3] = t[3];
+  }
+  float sm = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) sm += v[i];
+  const float mean = wave_sum(sm) / (float)D;
+  float qs = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { const float d = v[i] - mean; qs += d * d; }
+  const float var = wave_sum(qs) / (float)D;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < PER / 4; ++c) {
+    const int col = c * 256 + lane * 4;
+    f32x4 wv = *(const f32x4*)(w + col), bv = *(const f32x4*)(b + col);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[c * 4 + k] = (v[c * 4 + k] - mean) * rstd * wv[k] + bv[k];
+      amax = fmaxf(amax, fabsf(v[c * 4 + k]));
+    }
+  }
+  amax = wave_max(amax);
+  const float inv = amax > 0.f ? 32639.f / amax : 0.f;
+  if (lane == 0) scale[row] = amax / 32639.f;
+  int8_t* o = out + (long)row * ld;
+#pragma unroll
+  for (int c = 0; c < PER / 4; ++c) {
+    uint32_t hi, lw;
+    q2_pack4(v + c * 4, inv, hi, lw);
+    *(uint32_t*)(o + c * 256 + lane * 4) = hi;
+    *(uint32_t*)(o + lo + c * 256 + lane * 4) = lw;
+  }
+}
+
+// weight rows fp32 [N][K] -> int8 two-slice planes [N][K] + per-row scale (one wave per row, once at pack time)
+__global__ __launch_bounds__(256) void pack_i8_rows_kernel(const float* __restrict__ w, int N, int K, int8_t* out,
+                                                           long lo, float* __restrict__ scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const float* wr = w + (long)row * K;
+  float amax = 0.f;
+  for (int k = lane * 4; k < K; k += 256) {
+    const f32x4 t = *(const f32x4*)(wr + k);
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(t[0]), fabsf(t[1])), fmaxf(fabsf(t[2]), fabsf(t[3]))));
+  }
+  amax = wave_max(amax);
+  const float inv = amax > 0.f ? 32639.f / amax : 0.f;
+  if (lane == 0) scale[row] = amax / 32639.f;
+  for (int k = lane * 4; k < K; k += 256) {
+    const f32x4 t = *(const f32x4*)(wr + k);
+    const float y[4] = {t[0], t[1], t[2], t[3]};
+    uint32_t hi, lw;
+    q2_pack4(y, inv, hi, lw);
+    *(uint32_t*)(out + (long)row * K + k) = hi;
+    *(uint32_t*)(out + lo + (long)row * K + k) = lw;
+  }
+}
+
 // Post-LN residual block tail: x = LN(x + sum_s parts[s] + bias) in place, plus bf16 planes of
 // the result.  Reduces the split-K partial slabs of the preceding decode GEMM (no atomics).
 // x = LN(x + sum_s parts[s] + bias) in place, plus the bf16 planes of the result.  One block of
@@ -238,6 +329,28 @@ hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_gr
                        w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit);
   else
     return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_layernorm_i8(const float* x, long ldx, int rows, int D, int in_group, long in_stride, long in_off,
+                               const float* w, const float* b, float eps, int8_t* out, long ld, long lo, float* scale,
+                               hipStream_t s) {
+  if ((ld & 3) || (lo & 3)) return hipErrorInvalidValue;
+  dim3 grid((rows + 3) / 4);
+  if (D == 512)
+    hipLaunchKernelGGL(layernorm_i8_kernel<8>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off, w,
+                       b, eps, out, ld, lo, scale);
+  else if (D == 768)
+    hipLaunchKernelGGL(layernorm_i8_kernel<12>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off, w,
+                       b, eps, out, ld, lo, scale);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_i8_rows(const float* w, int N, int K, int8_t* out, long lo, float* scale, hipStream_t s) {
+  if (N <= 0 || K <= 0 || K % 4 || (lo & 3)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_i8_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, w, N, K, out, lo, scale);
   return hipGetLastError();
 }
 

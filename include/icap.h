@@ -29,6 +29,8 @@ extern "C" {
 
 #define ICAP_PREC_BF16 1   /* bf16 operands, fp32 accumulate                                  */
 #define ICAP_PREC_BF16X2 2 /* activations as hi+lo bf16 pairs (~16 mantissa bits), fp32 acc  */
+#define ICAP_PREC_I8X2 3   /* bf16x2, except the LayerNorm-fed ViT GEMMs (QKV, MLP-1, projection):
+                              both operands as two int8 slices (16-bit fixed point per row), int32 acc */
 
 typedef struct icap_handle icap_handle;
 
@@ -192,6 +194,15 @@ int icap_op_gemm(const uint16_t* A, long lda, long a_lo, int nsplit, const uint1
                  void* C, long ldc, long c_lo, int M, int N, int K, int epi, int out, void* stream);
 int icap_op_layernorm(const float* x, int rows, int D, const float* w, const float* b, float eps,
                       float* out_f32, uint16_t* out_bf, long bf_lo, int nsplit, void* stream);
+/* int8 two-slice operands (ICAP_PREC_I8X2): rows -> planes out[r*K + k], out[lo + r*K + k] with
+   v = scale[r] (256 x1 + x2), 16-bit fixed point relative to the row maximum (pack: any fp32 rows;
+   layernorm_i8: the LayerNorm of the rows, then the same quantisation). */
+int icap_op_pack_i8(const float* x, int rows, int K, int8_t* out, long lo, float* scale, void* stream);
+int icap_op_layernorm_i8(const float* x, int rows, int D, const float* w, const float* b, float eps, int8_t* out,
+                         long lo, float* scale, void* stream);
+/* C (M,N) fp32 = epi(dequant(A) dequant(W)^T + bias) on the int8 two-slice GEMM (N % 256 == 0, K % 64 == 0). */
+int icap_op_gemm_i8(const int8_t* A, long a_lo, const float* a_scale, const int8_t* W, long w_lo, const float* w_scale,
+                    const float* bias, float* C, int M, int N, int K, int epi, void* stream);
 /* qkv planes (B*N, 3*H*64) -> out planes (B*N, H*64), non-causal softmax(QK^T/8)V. */
 int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uint16_t* out, long out_lo,
                           int nsplit, void* stream);

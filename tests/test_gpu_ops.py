@@ -152,3 +152,83 @@ def test_full_chip_kernels_repeat_bitwise(cuda):
         outs.append(out)
     torch.cuda.synchronize()
     assert all(torch.equal(o, outs[0]) for o in outs[1:])
+
+
+# ------------------------------------------------------------------ int8 two-slice operands (i8x2)
+def _dequant(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    return (256.0 * q[0].double() + q[1].double()) * s.double()[:, None]
+
+
+def _pack_i8(L, lib, x: torch.Tensor):
+    rows, K = x.shape
+    q = torch.empty(2, rows, K, device=x.device, dtype=torch.int8)
+    s = torch.empty(rows, device=x.device)
+    L.check(lib.icap_op_pack_i8(x.data_ptr(), rows, K, q.data_ptr(), rows * K, s.data_ptr(), L.stream_ptr()), "pack")
+    return q, s
+
+
+@pytest.mark.parametrize("rows,K", [(1000, 768), (7, 3072), (64, 512)])
+def test_pack_i8_roundtrip(cuda, rows, K):
+    """16-bit fixed point per row: |x - s (256 x1 + x2)| <= s / 2 (+ the fp32 rounding of x / s near
+    2^15, < 2^-7 s), x1 in [-127, 127]; zero rows stay zero."""
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(rows + K)
+    x = (torch.randn(rows, K, generator=g) * torch.logspace(-3, 2, rows)[:, None]).to(cuda)
+    x[3] = 0.0
+    q, s = _pack_i8(L, lib, x)
+    torch.cuda.synchronize()
+    assert q[0].abs().max().item() <= 127
+    err = (_dequant(q, s) - x.double()).abs()
+    assert (err <= s.double()[:, None] * (0.5 + 2 ** -7) + 1e-30).all(), err.max().item()
+    assert s[3].item() == 0.0 and (q[:, 3] == 0).all()
+    amax = x.abs().amax(1).double()
+    assert torch.allclose(s.double() * 32639, amax, rtol=1e-6)
+
+
+def test_layernorm_i8(cuda):
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(5)
+    rows, D = 777, 768
+    x = (torch.randn(rows, D, generator=g) * 3 + 1).to(cuda)
+    w = torch.randn(D, generator=g).to(cuda)
+    b = torch.randn(D, generator=g).to(cuda)
+    q = torch.empty(2, rows, D, device=cuda, dtype=torch.int8)
+    s = torch.empty(rows, device=cuda)
+    L.check(lib.icap_op_layernorm_i8(x.data_ptr(), rows, D, w.data_ptr(), b.data_ptr(), 1e-6, q.data_ptr(), rows * D,
+                                     s.data_ptr(), L.stream_ptr()), "ln i8")
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.layer_norm(x.double(), (D,), w.double(), b.double(), 1e-6)
+    err = (_dequant(q, s) - ref).abs()
+    assert (err <= s.double()[:, None] * (0.5 + 2 ** -7) + 1e-5 * ref.abs().amax(1, keepdim=True)).all(), err.max().item()
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 768, 768), (50432, 2304, 768), (129, 512, 1024)])
+@pytest.mark.parametrize("epi", [0, 1])
+def test_gemm_i8(cuda, M, N, K, epi):
+    """The int8 two-slice GEMM equals its defining formula exactly up to fp32 rounding
+    (65536 A1.W1 + 256 (A1.W2 + A2.W1), scales, bias), and the fp64 product of the original fp32
+    operands within the representation's 16-bit bound."""
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    a = torch.randn(M, K, generator=g).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    qa, sa = _pack_i8(L, lib, a)
+    qw, sw = _pack_i8(L, lib, w)
+    C = torch.empty(M, N, device=cuda)
+    L.check(lib.icap_op_gemm_i8(qa.data_ptr(), M * K, sa.data_ptr(), qw.data_ptr(), N * K, sw.data_ptr(),
+                                bias.data_ptr(), C.data_ptr(), M, N, K, epi, L.stream_ptr()), "gemm i8")
+    torch.cuda.synchronize()
+    rows = slice(0, M) if M <= 4096 else torch.randperm(M, generator=g)[:2048].to(cuda)
+    a1, a2 = qa[0][rows].double(), qa[1][rows].double()
+    w1, w2 = qw[0].double(), qw[1].double()
+    acc = 65536.0 * (a1 @ w1.t()) + 256.0 * (a1 @ w2.t() + a2 @ w1.t())
+    form = acc * sa.double()[rows][:, None] * sw.double()[None, :] + bias.double()
+    exact = a[rows].double() @ w.double().t() + bias.double()
+    if epi == 1:
+        form = torch.nn.functional.gelu(form)
+        exact = torch.nn.functional.gelu(exact)
+    Cr = C[rows].double()
+    scale = max(1.0, exact.abs().max().item())
+    assert (Cr - form).abs().max().item() < 2e-6 * scale
+    assert (Cr - exact).abs().max().item() < 2e-4 * scale

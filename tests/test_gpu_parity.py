@@ -47,6 +47,31 @@ def test_vit_golden_ids_and_logits(vit_engine, cuda):
     assert np.abs(tf.cpu().numpy() - g["logits_tf"]).max() < 1e-3
 
 
+def test_vit_golden_i8x2(vit_sd, cuda):
+    """i8x2 mode (LayerNorm-fed ViT GEMMs on int8 two-slice operands, the rest bf16x2): the same
+    bar as bf16x2 - golden ids identical, logits within 1e-3 (CPU emulation, tools/numerics_i8.py:
+    logit error <= 3e-5 over 29 steps, 0 of 2880 tokens differ at B = 96)."""
+    from image_caption_amd.engine import Engine
+
+    eng = Engine(vit_sd, "vit", {}, precision="i8x2", device=cuda)
+    g = gold("vit_b4.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    mem = eng.encode(imgs)
+    assert np.abs(mem[:, :4, :16].cpu().numpy() - g["memory_head"]).max() < 1e-3
+    ids = eng.greedy(mem, W.START_TOKEN, W.END_TOKEN, 30).cpu().numpy()
+    assert np.array_equal(ids, g["ids"])
+    tf = eng.decoder_forward(torch.from_numpy(g["ids"][:, :-1]).to(cuda), mem, causal=True)
+    assert np.abs(tf.cpu().numpy() - g["logits_tf"]).max() < 1e-3
+    # against the fp32 oracle on more images
+    imgs = torch.from_numpy(W.synthetic_images(24, seed=7))
+    ref_mem = O.vit_encode(vit_sd, imgs)
+    mem = eng.encode(imgs.to(cuda))
+    assert (mem.cpu() - ref_mem).abs().max().item() < 2e-3
+    ref = O.greedy_from_memory(vit_sd, ref_mem, W.START_TOKEN, W.END_TOKEN, 30)
+    ids = eng.greedy(mem, W.START_TOKEN, W.END_TOKEN, 30).cpu()
+    assert torch.equal(ids, ref)
+
+
 def test_decoder_forward_golden(vit_engine, cuda):
     from tests.golden.make_golden import decoder_ops_memory
 

@@ -36,7 +36,7 @@ def linear(x, w, b):
     y = mm(x, w.t())
     return y + b if b is not None else y
 
-def mha(q_in, kv_in, in_w, in_b, out_w, out_b, nhead, causal):
+def mha(q_in, kv_in, in_w, in_b, out_w, out_b, nhead, causal, key_pad=None):
     B, T, D = q_in.shape; S = kv_in.shape[1]; hd = D // nhead
     q = linear(q_in, in_w[:D], in_b[:D]); k = linear(kv_in, in_w[D:2*D], in_b[D:2*D]); v = linear(kv_in, in_w[2*D:], in_b[2*D:])
     q = q.view(B, T, nhead, hd).transpose(1, 2); k = k.view(B, S, nhead, hd).transpose(1, 2); v = v.view(B, S, nhead, hd).transpose(1, 2)
@@ -63,7 +63,9 @@ if __name__ == "__main__":
     t = time.time(); mem0, ids0, tr0 = run(sd, img, "fp32", "fp32"); print("fp32", time.time() - t)
     marg = O.top2_margin(tr0)
     print("min margin", marg.min().item(), "frac<1e-3", (marg < 1e-3).float().mean().item())
-    for enc, dec in ([("bf16x2", "bf16x2")] if B > 16 else [("bf16", "bf16"), ("bf16", "bf16x2"), ("bf16x2", "bf16x2")]):
+    modes = [tuple(m.split("/")) for m in sys.argv[2].split(",")] if len(sys.argv) > 2 else \
+        ([("bf16x2", "bf16x2")] if B > 16 else [("bf16", "bf16"), ("bf16", "bf16x2"), ("bf16x2", "bf16x2")])
+    for enc, dec in modes:
         mem, ids, tr = run(sd, img, enc, dec)
         # teacher-forced first-step error
         dl = (tr[0] - tr0[0]).abs().max().item()
