@@ -90,7 +90,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--max-len", type=int, default=30)
-    ap.add_argument("--precision", default="bf16x2", choices=sorted(_lib.PRECISIONS))
+    ap.add_argument("--precision", default="i8x2", choices=sorted(_lib.PRECISIONS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")

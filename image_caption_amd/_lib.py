@@ -104,11 +104,11 @@ SIGNATURES = {
     "icap_op_layernorm": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_long,
                                   c_int, c_void_p]),
     "icap_op_enc_attention": (c_int, [c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
-    "icap_op_pack_i8": (c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p, c_void_p]),
-    "icap_op_layernorm_i8": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_long, c_void_p,
+    "icap_op_pack_i8": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "icap_op_layernorm_i8": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
                                      c_void_p]),
-    "icap_op_gemm_i8": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_int,
-                                c_int, c_int, c_int, c_void_p]),
+    "icap_op_gemm_i8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                c_int, c_int, c_void_p]),
 }
 
 _LIB = None

@@ -795,7 +795,15 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
   const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
   const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int bm = wg / nbn, bn = wg - bm * nbn;
+  int bm, bn;
+  if (p.raster_group > 0) {  // groups of raster_group row bands, column tiles outermost inside a group
+    const int G = p.raster_group, grp = wg / (G * nbn), gm = min(G, nbm - grp * G), idx = wg - grp * G * nbn;
+    bn = idx / gm;
+    bm = grp * G + (idx - bn * gm);
+  } else {
+    bm = wg / nbn;
+    bn = wg - bm * nbn;
+  }
   const int m0 = bm * BM, n0 = bn * BN;
   const int M = p.M, K = p.K;
   const int nk = K / KS;
@@ -1064,7 +1072,18 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs p) {
 
 }  // namespace
 
-hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
+hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s);
+hipError_t launch_gemm_256(const GemmArgs& g0, hipStream_t s) {
+  static int group = -1;  // ICAP_GEMM_GROUP: tile raster of the bf16 encoder GEMM (0 = row-band major)
+  if (group < 0) {
+    const char* v = getenv("ICAP_GEMM_GROUP");
+    group = v ? std::max(0, atoi(v)) : 0;
+  }
+  GemmArgs g = g0;
+  if (!g.raster_group) g.raster_group = group;
+  return launch_gemm_256_(g, s);
+}
+hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N % 256 || g.K % 32 || g.batch != 1 || (g.nsplit != 1 && g.nsplit != 2))
     return hipErrorInvalidValue;
   const long last_row = g.rm_group ? (long)((g.M - 1) / g.rm_group) * g.rm_stride + g.rm_off + g.rm_group : g.M;
@@ -1191,12 +1210,13 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s) {
 // (|A1.W1| <= K 127^2 < 2^31 for K < 133k).  Against the bf16x2 form (A as hi/lo bf16 planes, W
 // bf16: 6 staged bytes per k per row pair, two bf16 MFMAs per 32-deep k-step) this stages 4 bytes per k
 // and does 3/4 of the MFMA cycles (the i8 16x16x64 MFMA takes the cycles of bf16 16x16x32).
+// Operand row images are [K/64][2][64]: a 64-deep stage of one row is ONE full 128-B line holding
+// both slices (half the L2 requests of 64-B row segments).
 // Block tile 128 x 256 (8 waves as 2 x 4, each 64 x 64 = 4 x 4 MFMA tiles with a high and a mid int32
-// accumulator set: 128 accumulator registers, so one block per CU), 64-deep stages of four operand
-// tiles (A1, A2: 128 rows; W1, W2: 256 rows; rows of 64 B with the gemm_256 chunk swizzle) in a
-// 3-stage LDS ring (144 KiB) filled by global_load_lds, counted vmcnt + raw barrier, XCD remap.
-// Fragment reads are the bf16 kernel's (16 B of one row per lane): the same byte positions feed
-// the A and B operands, so the k labelling inside the MFMA does not matter.
+// accumulator set: 128 accumulator registers, so one block per CU), stages of two operand tiles
+// (A: 128 rows, W: 256 rows, 128 B each; 16-B chunk c of row r at c ^ (r & 7)) in a 3-stage LDS ring
+// (144 KiB) filled by global_load_lds, counted vmcnt + raw barrier, XCD remap.  The same LDS byte
+// positions feed the A and B operands, so the k labelling inside the MFMA does not matter.
 namespace {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -1208,10 +1228,10 @@ __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
 template <int NSTAGE>
 __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
   constexpr int NW = 8, BM = 128, BN = 256, WM = 64, WN = 64, TM = WM / 16, TN = WN / 16;
-  constexpr int OPB = BM * 64, OPBW = BN * 64;     // bytes per A / W slice per stage
-  constexpr int STAGE = 2 * OPB + 2 * OPBW;         // 48 KiB
+  constexpr int OPB = BM * 128, OPBW = BN * 128;  // bytes per A / W tile per stage (both slices)
+  constexpr int STAGE = OPB + OPBW;               // 48 KiB
   constexpr int IPW = OPB / 1024 / NW, IPWW = OPBW / 1024 / NW;
-  constexpr int PER_STAGE = 2 * IPW + 2 * IPWW;     // DMA instructions per wave per stage
+  constexpr int PER_STAGE = IPW + IPWW;           // DMA instructions per wave per stage
   static_assert(IPW >= 1 && IPWW >= 1, "tile / wave shape");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -1220,35 +1240,39 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
   const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
   const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int bm = wg / nbn, bn = wg - bm * nbn;
+  int bm, bn;
+  if (p.raster_group > 0) {  // groups of raster_group row bands, column tiles outermost inside a group
+    const int G = p.raster_group, grp = wg / (G * nbn), gm = min(G, nbm - grp * G), idx = wg - grp * G * nbn;
+    bn = idx / gm;
+    bm = grp * G + (idx - bn * gm);
+  } else {
+    bm = wg / nbn;
+    bn = wg - bm * nbn;
+  }
   const int m0 = bm * BM, n0 = bn * BN;
   const int M = p.M, nk = p.K / 64;
+  const long ld = 2L * p.K;  // row image bytes
 
-  const int srow = wave * IPW * 16 + (lane >> 2), srow_w = wave * IPWW * 16 + (lane >> 2);
-  const int schunk = (lane & 3) ^ (((srow >> 3) & 1) << 1);
-  const char* A = (const char*)p.A;
-  const char* Wt = (const char*)p.W;
-  const long b_step = 16 * p.ldw;
-  const char* a_base[IPW];
+  // one DMA instruction = 8 rows x 128 B; lane -> row lane >> 3, LDS chunk lane & 7 holding source
+  // chunk (lane & 7) ^ (row & 7) (instruction bases are multiples of 8 rows)
+  const int schunk = ((lane & 7) ^ (lane >> 3)) * 16;
+  const char* a_src[IPW];
 #pragma unroll
-  for (int i = 0; i < IPW; ++i) a_base[i] = A + (long)min(m0 + srow + i * 16, M - 1) * p.lda + schunk * 16;
-  const char* b_base = Wt + (long)min(n0 + srow_w, p.N - 1) * p.ldw + schunk * 16;
+  for (int i = 0; i < IPW; ++i)
+    a_src[i] = (const char*)p.A + (long)min(m0 + (wave * IPW + i) * 8 + (lane >> 3), M - 1) * ld + schunk;
+  const char* b_src = (const char*)p.W + (long)(n0 + wave * IPWW * 8 + (lane >> 3)) * ld + schunk;
+  const long b_step = 8 * ld;
   auto stage = [&](int kt, int buf) {
-    const int kin = kt * 64;
+    const int kin = kt * 128;
     char* s0 = smem + buf * STAGE;
 #pragma unroll
-    for (int pl = 0; pl < 2; ++pl)
+    for (int i = 0; i < IPW; ++i)
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(a_src[i] + kin),
+                                       (LDS_AS void*)(s0 + (wave * IPW + i) * 1024), 16, 0, 0);
 #pragma unroll
-      for (int i = 0; i < IPW; ++i)
-        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(a_base[i] + pl * p.a_lo + kin),
-                                         (LDS_AS void*)(s0 + pl * OPB + (wave * IPW + i) * 1024), 16, 0, 0);
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl)
-#pragma unroll
-      for (int i = 0; i < IPWW; ++i)
-        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(b_base + pl * p.w_lo + kin + i * b_step),
-                                         (LDS_AS void*)(s0 + 2 * OPB + pl * OPBW + (wave * IPWW + i) * 1024), 16, 0,
-                                         0);
+    for (int i = 0; i < IPWW; ++i)
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(b_src + i * b_step + kin),
+                                       (LDS_AS void*)(s0 + OPB + (wave * IPWW + i) * 1024), 16, 0, 0);
   };
 
   i32x4 ah[TM][TN], am[TM][TN];
@@ -1258,12 +1282,13 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
     for (int j = 0; j < TN; ++j) ah[i][j] = am[i][j] = (i32x4){0, 0, 0, 0};
 
   const int fr = lane & 15, fq = lane >> 4;
-  const int foff = fr * 64 + ((fq ^ (((fr >> 3) & 1) << 1)) << 4);
+  const int f1 = fr * 128 + ((fq ^ (fr & 7)) << 4), f2 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
     if (s < nk) stage(s, s);
   for (int kt = 0; kt < nk; ++kt) {
     const int younger = min(NSTAGE - 2, nk - 1 - kt);
+    // lgkmcnt(0): this wave's LDS reads of the slot refilled below are complete before the barrier
     if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * PER_STAGE) : "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1273,13 +1298,13 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
     i32x4 w1[TN], w2[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      w1[j] = *(const i32x4*)(s0 + 2 * OPB + (wn * WN + j * 16) * 64 + foff);
-      w2[j] = *(const i32x4*)(s0 + 2 * OPB + OPBW + (wn * WN + j * 16) * 64 + foff);
+      w1[j] = *(const i32x4*)(s0 + OPB + (wn * WN + j * 16) * 128 + f1);
+      w2[j] = *(const i32x4*)(s0 + OPB + (wn * WN + j * 16) * 128 + f2);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const i32x4 a1 = *(const i32x4*)(s0 + (wm * WM + i * 16) * 64 + foff);
-      const i32x4 a2 = *(const i32x4*)(s0 + OPB + (wm * WM + i * 16) * 64 + foff);
+      const i32x4 a1 = *(const i32x4*)(s0 + (wm * WM + i * 16) * 128 + f1);
+      const i32x4 a2 = *(const i32x4*)(s0 + (wm * WM + i * 16) * 128 + f2);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         ah[i][j] = mfma_i8(w1[j], a1, ah[i][j]);  // D = W.A^T, as the bf16 kernel
@@ -1303,6 +1328,54 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
       for (int e = 0; e < 4; ++e)
         acc[i][j][e] = fmaf((float)ah[i][j][e], 65536.f, (float)am[i][j][e] * 256.f) * (sa * ws[j][e]);
   }
+  if (p.out == OUT_SPLIT && p.c_planes == 2 && !p.rm_group && !p.addend) {
+    // Split-plane output staged through LDS: the MFMA layout gives each lane 4 columns of one row
+    // (32-B row segments per wave store); transposed through LDS every lane stores 16 B and a wave
+    // covers whole 512-B rows (full 128-B lines; one head block = one line in the head-major form).
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (p.bias) {
+          const f32x4 bv = *(const f32x4*)(p.bias + nb + j * 16 + 4 * fq);
+          acc[i][j] += bv;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (p.epi == EPI_GELU) acc[i][j][e] = gelu_erf_fast(acc[i][j][e]);
+          else if (p.epi == EPI_RELU) acc[i][j][e] = fmaxf(acc[i][j][e], 0.f);
+        }
+      }
+    constexpr int PITCH = BN * 2 + 16, PLANE = BM * PITCH;  // 528-B rows: 16 rows of one column hit distinct banks
+    static_assert(2 * PLANE <= NSTAGE * STAGE, "epilogue tile exceeds the ring");
+    __syncthreads();  // every wave is past its last ring read
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        bf16_t h[4], l[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split_bf(acc[i][j][e], h[e], l[e]);
+        char* d = smem + (wm * WM + i * 16 + fr) * PITCH + (wn * WN + j * 16 + 4 * fq) * 2;
+        *(u32x2*)d = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+        *(u32x2*)(d + PLANE) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
+      }
+    __syncthreads();
+    bf16_t* C = (bf16_t*)p.C;
+#pragma unroll 4
+    for (int c = tid; c < BM * (BN / 8); c += NW * 64) {
+      const int row = c / (BN / 8), ch = c % (BN / 8), m = m0 + row;
+      if (m >= M) continue;
+      const int col = n0 + ch * 8;
+      const long o = p.hm_n ? (((long)(m / p.hm_n) * (p.N / 64) + col / 64) * p.hm_n + m % p.hm_n) * 64 + col % 64
+                            : (long)m * p.ldc + col;
+      const u32x4 vh = *(const u32x4*)(smem + row * PITCH + ch * 16);
+      const u32x4 vl = *(const u32x4*)(smem + PLANE + row * PITCH + ch * 16);
+      *(u32x4*)(C + o) = vh;
+      *(u32x4*)(C + o + p.c_lo) = vl;
+    }
+    return;
+  }
   GemmArgs pe = p;
   pe.scale = nullptr;
   pe.res = nullptr;
@@ -1312,13 +1385,12 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
 }  // namespace
 
 hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
-  if (g.M <= 0 || g.N % 256 || g.K % 64 || g.batch != 1 || !g.a_scale || !g.w_scale || g.cv || g.scale || g.res ||
-      g.lda < g.K || g.ldw < g.K || (g.lda & 15) || (g.ldw & 15) || (g.a_lo & 15) || (g.w_lo & 15))
+  if (g.M <= 0 || g.N % 256 || g.K % 64 || g.batch != 1 || !g.a_scale || !g.w_scale || g.cv || g.scale || g.res)
     return hipErrorInvalidValue;
   if (g.hm_n && (g.out != OUT_SPLIT || g.N % 64 || g.rm_group || g.M % g.hm_n)) return hipErrorInvalidValue;
   const long last_row = g.rm_group ? (long)((g.M - 1) / g.rm_group) * g.rm_stride + g.rm_off + g.rm_group : g.M;
   if (last_row * g.ldc >= (1L << 31)) return hipErrorInvalidValue;  // epilogue uses 32-bit row offsets
-  constexpr int NST = 3, lds = NST * (2 * 128 * 64 + 2 * 256 * 64);
+  constexpr int NST = 3, lds = NST * (128 * 128 + 256 * 128);
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)gemm_i8_kernel<NST>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -1326,6 +1398,13 @@ hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
     attr = true;
   }
   const int nwg = (g.N / 256) * ((g.M + 127) / 128);
-  hipLaunchKernelGGL((gemm_i8_kernel<NST>), dim3(nwg), dim3(512), lds, s, g);
+  static int group = -1;  // ICAP_I8_GROUP: tile raster (0 = row-band major; 16: qkv 373 -> 338 us, mlp0 525 -> 459)
+  if (group < 0) {
+    const char* v = getenv("ICAP_I8_GROUP");
+    group = v ? std::max(0, atoi(v)) : 16;
+  }
+  GemmArgs gg = g;
+  gg.raster_group = group;
+  hipLaunchKernelGGL((gemm_i8_kernel<NST>), dim3(nwg), dim3(512), lds, s, gg);
   return hipGetLastError();
 }

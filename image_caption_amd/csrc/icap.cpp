@@ -75,7 +75,7 @@ struct Lin {  // packed nn.Linear: bf16 W [N][K] + fp32 bias
   float* b = nullptr;
   int N = 0, K = 0;
 };
-struct Lin8 {  // nn.Linear as int8 two-slice planes [2][N][K] + per-row scale (ICAP_PREC_I8X2)
+struct Lin8 {  // nn.Linear as int8 two-slice row images [N][K/64][2][64] + per-row scale (ICAP_PREC_I8X2)
   int8_t* w = nullptr;
   float *sw = nullptr, *b = nullptr;
   int N = 0, K = 0;
@@ -242,7 +242,7 @@ struct icap_handle {
     Lin8 l;
     l.w = (int8_t*)alloc((size_t)2 * N * K);
     l.sw = (float*)alloc((size_t)N * 4);
-    HIPCHK(launch_pack_i8_rows(w, N, K, l.w, (long)N * K, l.sw, s));
+    HIPCHK(launch_pack_i8_rows(w, N, K, l.w, l.sw, s));
     l.b = b ? own_f32(b, N, s) : nullptr;
     l.N = N;
     l.K = K;
@@ -282,13 +282,13 @@ struct icap_handle {
     g.epi = epi; g.out = out;
     run_gemm(g, s);
   }
-  // int8 two-slice GEMM: A = int8 planes [2][M][K] (plane stride a_lo bytes) with row scales sa
-  void gemm8(const int8_t* A, long a_lo, const float* sa, const Lin8& W, int M, void* C, long ldc, long c_lo, int epi,
-             int out, hipStream_t s, int hm_n = 0) {
+  // int8 two-slice GEMM: A = int8 row images [M][K/64][2][64] with row scales sa
+  void gemm8(const int8_t* A, const float* sa, const Lin8& W, int M, void* C, long ldc, long c_lo, int epi, int out,
+             hipStream_t s, int hm_n = 0) {
     GemmArgs g = gemm_args();
     g.hm_n = hm_n;
-    g.A = (const bf16_t*)A; g.lda = W.K; g.a_lo = a_lo; g.a_scale = sa;
-    g.W = (const bf16_t*)W.w; g.ldw = W.K; g.w_lo = (long)W.N * W.K; g.w_scale = W.sw;
+    g.A = (const bf16_t*)A; g.a_scale = sa;
+    g.W = (const bf16_t*)W.w; g.w_scale = W.sw;
     g.bias = W.b;
     g.C = C; g.ldc = ldc; g.c_lo = c_lo;
     g.M = M; g.N = W.N; g.K = W.K; g.nsplit = 2; g.c_planes = ns;
@@ -443,10 +443,9 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   bf16_t* qkv = h->e_qkv.as<bf16_t>();
   bf16_t* hb = h->e_h.as<bf16_t>();
   const long pL = (long)B * np * Kp, aL = (long)M * V, qL = (long)M * 3 * V, hL = (long)M * d.vit_mlp;
-  // ICAP_PREC_I8X2: the LayerNorm outputs as int8 two-slice planes [2][M][V] (in e_a, which the
-  // bf16x2 planes of the attention output reuse afterwards) + row scales
+  // ICAP_PREC_I8X2: the LayerNorm outputs as int8 two-slice row images [M][V/64][2][64] (in e_a,
+  // which the bf16x2 planes of the attention output reuse afterwards) + row scales
   int8_t* a8 = (int8_t*)a;
-  const long a8L = (long)M * V;
   float* sa = nullptr;
   if (h->i8) {
     h->e_sa.ensure((size_t)M * 4);
@@ -469,8 +468,8 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   for (const VitLayer& L : h->vit) {
     // QKV written head-major ([image][q|k|v x head][token][64]) for the attention's contiguous rows
     if (h->i8) {
-      HIPCHK(launch_layernorm_i8(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, a8, V, a8L, sa, s));
-      h->gemm8(a8, a8L, sa, L.qkv8, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s, hm);
+      HIPCHK(launch_layernorm_i8(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, a8, sa, s));
+      h->gemm8(a8, sa, L.qkv8, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s, hm);
     } else {
       HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
       h->gemm(a, V, aL, L.qkv, M, qkv, 3 * V, qL, EPI_NONE, OUT_SPLIT, s, hm);
@@ -478,8 +477,8 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
     h->attention(qkv, 3 * V, qL, B, T, d.vit_heads, a, V, aL, s, hm ? 1 : 0);
     h->gemm(a, V, aL, L.out, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s);
     if (h->i8) {
-      HIPCHK(launch_layernorm_i8(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, a8, V, a8L, sa, s));
-      h->gemm8(a8, a8L, sa, L.mlp08, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);
+      HIPCHK(launch_layernorm_i8(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, a8, sa, s));
+      h->gemm8(a8, sa, L.mlp08, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);
     } else {
       HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
       h->gemm(a, V, aL, L.mlp0, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);
@@ -489,8 +488,8 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   // final LN on patch rows only (drop CLS), then projection 768 -> d_model
   const long a2L = (long)B * np * V;
   if (h->i8) {
-    HIPCHK(launch_layernorm_i8(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, a8, V, a2L, sa, s));
-    h->gemm8(a8, a2L, sa, h->proj8, B * np, memory, Dm, 0, EPI_NONE, OUT_F32, s);
+    HIPCHK(launch_layernorm_i8(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, a8, sa, s));
+    h->gemm8(a8, sa, h->proj8, B * np, memory, Dm, 0, EPI_NONE, OUT_F32, s);
     return;
   }
   HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, nullptr, 0, a, V, a2L, ns, s));
@@ -1132,25 +1131,24 @@ int icap_op_layernorm(const float* x, int rows, int D, const float* w, const flo
   });
 }
 
-int icap_op_pack_i8(const float* x, int rows, int K, int8_t* out, long lo, float* scale, void* stream) {
-  return guarded([&] { HIPCHK(launch_pack_i8_rows(x, rows, K, out, lo, scale, (hipStream_t)stream)); });
+int icap_op_pack_i8(const float* x, int rows, int K, int8_t* out, float* scale, void* stream) {
+  return guarded([&] { HIPCHK(launch_pack_i8_rows(x, rows, K, out, scale, (hipStream_t)stream)); });
 }
 
 int icap_op_layernorm_i8(const float* x, int rows, int D, const float* w, const float* b, float eps, int8_t* out,
-                         long lo, float* scale, void* stream) {
-  return guarded([&] {
-    HIPCHK(launch_layernorm_i8(x, D, rows, D, 0, 0, 0, w, b, eps, out, D, lo, scale, (hipStream_t)stream));
-  });
+                         float* scale, void* stream) {
+  return guarded([&] { HIPCHK(launch_layernorm_i8(x, D, rows, D, 0, 0, 0, w, b, eps, out, scale, (hipStream_t)stream)); });
 }
 
-int icap_op_gemm_i8(const int8_t* A, long a_lo, const float* a_scale, const int8_t* W, long w_lo, const float* w_scale,
-                    const float* bias, float* C, int M, int N, int K, int epi, void* stream) {
+int icap_op_gemm_i8(const int8_t* A, const float* a_scale, const int8_t* W, const float* w_scale, const float* bias,
+                    void* C, int M, int N, int K, int epi, int out, int hm_n, void* stream) {
   return guarded([&] {
+    REQUIRE(out == OUT_F32 || out == OUT_SPLIT, "out must be OUT_F32 or OUT_SPLIT");
     GemmArgs g = gemm_args();
-    g.A = (const bf16_t*)A; g.lda = K; g.a_lo = a_lo; g.a_scale = a_scale; g.nsplit = 2;
-    g.W = (const bf16_t*)W; g.ldw = K; g.w_lo = w_lo; g.w_scale = w_scale; g.bias = bias;
-    g.C = C; g.ldc = N;
-    g.M = M; g.N = N; g.K = K; g.epi = epi; g.out = OUT_F32;
+    g.A = (const bf16_t*)A; g.a_scale = a_scale; g.nsplit = 2;
+    g.W = (const bf16_t*)W; g.w_scale = w_scale; g.bias = bias;
+    g.C = C; g.ldc = N; g.c_lo = (long)M * N; g.hm_n = hm_n;
+    g.M = M; g.N = N; g.K = K; g.epi = epi; g.out = out;
     HIPCHK(launch_gemm_i8(g, (hipStream_t)stream));
   });
 }

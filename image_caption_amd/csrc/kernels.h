@@ -33,10 +33,11 @@ struct GemmArgs {
   // goes to ((row / hm_n * (N / 64) + col / 64) * hm_n + row % hm_n) * 64 + col % 64, i.e. the QKV
   // projection as [image][q|k|v x head][token][64] - one head's rows contiguous for the attention
   int hm_n;
-  // int8 two-slice operands (launch_gemm_i8 only): A and W are int8 planes (A, A + a_lo; W, W + w_lo;
-  // lda / ldw / a_lo / w_lo in BYTES), v = s (256 x1 + x2) with a per-row scale: a_scale[M] for A,
-  // w_scale[N] for W
-  const float* a_scale; const float* w_scale; long w_lo;
+  int raster_group;  // tile raster inside an XCD: groups of raster_group row bands, column tiles outer (0: row-band major)
+  // int8 two-slice operands (launch_gemm_i8 only): A and W are int8 row images [rows][K/64][2][64]
+  // (row stride 2K bytes; lda / ldw / a_lo unused), v = s (256 x1 + x2) with a per-row scale:
+  // a_scale[M] for A, w_scale[N] for W
+  const float* a_scale; const float* w_scale;
 };
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
@@ -47,13 +48,13 @@ hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s);
 // int8 two-slice GEMM (batch 1, N % 256 == 0, K % 64 == 0): acc = 65536 A1.W1 + 256 (A1.W2 + A2.W1)
 // in int32, then * a_scale[m] * w_scale[n] and the gemm_256 epilogue (bias, GELU, head-major, ...)
 hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s);
-// LayerNorm rows -> int8 two-slice planes: y = LN(x); s = max|y| / 32639; q = rint(y / s);
-// x1 = (q + 128) >> 8, x2 = q - 256 x1 (out[row * ld], out[lo + row * ld]); scale[row] = s
+// LayerNorm rows -> int8 two-slice row images: y = LN(x); s = max|y| / 32639; q = rint(y / s);
+// x1 = (q + 128) >> 8, x2 = q - 256 x1, element k of row r at out[r*2D + (k/64)*128 + slice*64 + k%64];
+// scale[row] = s
 hipError_t launch_layernorm_i8(const float* x, long ldx, int rows, int D, int in_group, long in_stride, long in_off,
-                               const float* w, const float* b, float eps, int8_t* out, long ld, long lo, float* scale,
-                               hipStream_t s);
-// fp32 [N][K] rows -> int8 two-slice planes (out, out + lo, row stride K) + per-row scale
-hipError_t launch_pack_i8_rows(const float* w, int N, int K, int8_t* out, long lo, float* scale, hipStream_t s);
+                               const float* w, const float* b, float eps, int8_t* out, float* scale, hipStream_t s);
+// fp32 [N][K] rows -> int8 two-slice row images (same layout, K % 64 == 0) + per-row scale
+hipError_t launch_pack_i8_rows(const float* w, int N, int K, int8_t* out, float* scale, hipStream_t s);
 enum { PROF_GEMM_128 = 0, PROF_GEMM_64 = 1, PROF_ENC_ATTN = 2, PROF_CROSS_ATTN = 3, PROF_GEMM_WAVE = 4, PROF_GEMM_256 = 5,
        PROF_GEMM_I8 = 6 };
 

@@ -67,7 +67,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 
 // int8 two-slice quantisation (the operand form of gemm_i8_kernel): 16-bit fixed point relative to
 // the row maximum, q = rint(v / s) in [-32639, 32639], v1 = (q + 128) >> 8 in [-127, 127],
-// v2 = q - 256 v1 in [-128, 127]; four consecutive values -> one 32-bit word per slice.
+// v2 = q - 256 v1 in [-128, 127]; four consecutive values -> one 32-bit word per slice.  Row image
+// [K/64][2][64]: the two slices of a 64-deep k block share one 128-B line, so each GEMM stage row
+// is one full-line request.
 __device__ __forceinline__ void q2_pack4(const float* y, float inv, uint32_t& hi, uint32_t& lo) {
   hi = lo = 0;
 #pragma unroll
@@ -84,7 +86,7 @@ template <int PER>
 __global__ __launch_bounds__(256) void layernorm_i8_kernel(const float* __restrict__ x, long ldx, int rows,
                                                            int in_group, long in_stride, long in_off,
                                                            const float* __restrict__ w, const float* __restrict__ b,
-                                                           float eps, int8_t* out, long ld, long lo,
+                                                           float eps, int8_t* out,
                                                            float* __restrict__ scale) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -121,19 +123,20 @@ __global__ __launch_bounds__(256) void layernorm_i8_kernel(const float* __restri
   amax = wave_max(amax);
   const float inv = amax > 0.f ? 32639.f / amax : 0.f;
   if (lane == 0) scale[row] = amax / 32639.f;
-  int8_t* o = out + (long)row * ld;
+  int8_t* o = out + (long)row * 2 * D;
 #pragma unroll
   for (int c = 0; c < PER / 4; ++c) {
     uint32_t hi, lw;
     q2_pack4(v + c * 4, inv, hi, lw);
-    *(uint32_t*)(o + c * 256 + lane * 4) = hi;
-    *(uint32_t*)(o + lo + c * 256 + lane * 4) = lw;
+    const int k = c * 256 + lane * 4, off = (k >> 6) * 128 + (k & 63);  // [K/64][2][64] row image
+    *(uint32_t*)(o + off) = hi;
+    *(uint32_t*)(o + off + 64) = lw;
   }
 }
 
 // weight rows fp32 [N][K] -> int8 two-slice planes [N][K] + per-row scale (one wave per row, once at pack time)
 __global__ __launch_bounds__(256) void pack_i8_rows_kernel(const float* __restrict__ w, int N, int K, int8_t* out,
-                                                           long lo, float* __restrict__ scale) {
+                                                           float* __restrict__ scale) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
@@ -151,8 +154,9 @@ __global__ __launch_bounds__(256) void pack_i8_rows_kernel(const float* __restri
     const float y[4] = {t[0], t[1], t[2], t[3]};
     uint32_t hi, lw;
     q2_pack4(y, inv, hi, lw);
-    *(uint32_t*)(out + (long)row * K + k) = hi;
-    *(uint32_t*)(out + lo + (long)row * K + k) = lw;
+    int8_t* o = out + (long)row * 2 * K + (k >> 6) * 128 + (k & 63);  // [K/64][2][64] row image
+    *(uint32_t*)o = hi;
+    *(uint32_t*)(o + 64) = lw;
   }
 }
 
@@ -333,24 +337,22 @@ hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_gr
 }
 
 hipError_t launch_layernorm_i8(const float* x, long ldx, int rows, int D, int in_group, long in_stride, long in_off,
-                               const float* w, const float* b, float eps, int8_t* out, long ld, long lo, float* scale,
-                               hipStream_t s) {
-  if ((ld & 3) || (lo & 3)) return hipErrorInvalidValue;
+                               const float* w, const float* b, float eps, int8_t* out, float* scale, hipStream_t s) {
   dim3 grid((rows + 3) / 4);
   if (D == 512)
     hipLaunchKernelGGL(layernorm_i8_kernel<8>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off, w,
-                       b, eps, out, ld, lo, scale);
+                       b, eps, out, scale);
   else if (D == 768)
     hipLaunchKernelGGL(layernorm_i8_kernel<12>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off, w,
-                       b, eps, out, ld, lo, scale);
+                       b, eps, out, scale);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
-hipError_t launch_pack_i8_rows(const float* w, int N, int K, int8_t* out, long lo, float* scale, hipStream_t s) {
-  if (N <= 0 || K <= 0 || K % 4 || (lo & 3)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pack_i8_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, w, N, K, out, lo, scale);
+hipError_t launch_pack_i8_rows(const float* w, int N, int K, int8_t* out, float* scale, hipStream_t s) {
+  if (N <= 0 || K <= 0 || K % 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_i8_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, w, N, K, out, scale);
   return hipGetLastError();
 }
 

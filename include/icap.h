@@ -194,15 +194,17 @@ int icap_op_gemm(const uint16_t* A, long lda, long a_lo, int nsplit, const uint1
                  void* C, long ldc, long c_lo, int M, int N, int K, int epi, int out, void* stream);
 int icap_op_layernorm(const float* x, int rows, int D, const float* w, const float* b, float eps,
                       float* out_f32, uint16_t* out_bf, long bf_lo, int nsplit, void* stream);
-/* int8 two-slice operands (ICAP_PREC_I8X2): rows -> planes out[r*K + k], out[lo + r*K + k] with
-   v = scale[r] (256 x1 + x2), 16-bit fixed point relative to the row maximum (pack: any fp32 rows;
-   layernorm_i8: the LayerNorm of the rows, then the same quantisation). */
-int icap_op_pack_i8(const float* x, int rows, int K, int8_t* out, long lo, float* scale, void* stream);
+/* int8 two-slice operands (ICAP_PREC_I8X2): fp32 rows -> row images out[r*2K + (k/64)*128 + j*64 + k%64]
+   (slice j = 0, 1) with v = scale[r] (256 x1 + x2), 16-bit fixed point relative to the row maximum
+   (pack: the rows as given; layernorm_i8: their LayerNorm, then the same quantisation). K % 64 == 0. */
+int icap_op_pack_i8(const float* x, int rows, int K, int8_t* out, float* scale, void* stream);
 int icap_op_layernorm_i8(const float* x, int rows, int D, const float* w, const float* b, float eps, int8_t* out,
-                         long lo, float* scale, void* stream);
-/* C (M,N) fp32 = epi(dequant(A) dequant(W)^T + bias) on the int8 two-slice GEMM (N % 256 == 0, K % 64 == 0). */
-int icap_op_gemm_i8(const int8_t* A, long a_lo, const float* a_scale, const int8_t* W, long w_lo, const float* w_scale,
-                    const float* bias, float* C, int M, int N, int K, int epi, void* stream);
+                         float* scale, void* stream);
+/* C = epi(dequant(A) dequant(W)^T + bias) on the int8 two-slice GEMM (N % 256 == 0, K % 64 == 0):
+   out 0 = fp32 (M,N); out 2 = bf16 hi/lo planes [2][M][N], head-major when hm_n > 0 (the encoder's
+   QKV form, element (m, n) at ((m / hm_n * N/64 + n / 64) * hm_n + m % hm_n) * 64 + n % 64). */
+int icap_op_gemm_i8(const int8_t* A, const float* a_scale, const int8_t* W, const float* w_scale, const float* bias,
+                    void* C, int M, int N, int K, int epi, int out, int hm_n, void* stream);
 /* qkv planes (B*N, 3*H*64) -> out planes (B*N, H*64), non-causal softmax(QK^T/8)V. */
 int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uint16_t* out, long out_lo,
                           int nsplit, void* stream);

@@ -155,15 +155,23 @@ def test_full_chip_kernels_repeat_bitwise(cuda):
 
 
 # ------------------------------------------------------------------ int8 two-slice operands (i8x2)
+def _slices(q: torch.Tensor):
+    """row images [rows][K/64][2][64] -> (x1, x2) as [rows][K]"""
+    rows = q.shape[0]
+    v = q.view(rows, -1, 2, 64)
+    return v[:, :, 0].reshape(rows, -1), v[:, :, 1].reshape(rows, -1)
+
+
 def _dequant(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
-    return (256.0 * q[0].double() + q[1].double()) * s.double()[:, None]
+    x1, x2 = _slices(q)
+    return (256.0 * x1.double() + x2.double()) * s.double()[:, None]
 
 
 def _pack_i8(L, lib, x: torch.Tensor):
     rows, K = x.shape
-    q = torch.empty(2, rows, K, device=x.device, dtype=torch.int8)
+    q = torch.empty(rows, 2 * K, device=x.device, dtype=torch.int8)
     s = torch.empty(rows, device=x.device)
-    L.check(lib.icap_op_pack_i8(x.data_ptr(), rows, K, q.data_ptr(), rows * K, s.data_ptr(), L.stream_ptr()), "pack")
+    L.check(lib.icap_op_pack_i8(x.data_ptr(), rows, K, q.data_ptr(), s.data_ptr(), L.stream_ptr()), "pack")
     return q, s
 
 
@@ -177,10 +185,10 @@ def test_pack_i8_roundtrip(cuda, rows, K):
     x[3] = 0.0
     q, s = _pack_i8(L, lib, x)
     torch.cuda.synchronize()
-    assert q[0].abs().max().item() <= 127
+    assert _slices(q)[0].abs().max().item() <= 127
     err = (_dequant(q, s) - x.double()).abs()
     assert (err <= s.double()[:, None] * (0.5 + 2 ** -7) + 1e-30).all(), err.max().item()
-    assert s[3].item() == 0.0 and (q[:, 3] == 0).all()
+    assert s[3].item() == 0.0 and (q[3] == 0).all()
     amax = x.abs().amax(1).double()
     assert torch.allclose(s.double() * 32639, amax, rtol=1e-6)
 
@@ -192,9 +200,9 @@ def test_layernorm_i8(cuda):
     x = (torch.randn(rows, D, generator=g) * 3 + 1).to(cuda)
     w = torch.randn(D, generator=g).to(cuda)
     b = torch.randn(D, generator=g).to(cuda)
-    q = torch.empty(2, rows, D, device=cuda, dtype=torch.int8)
+    q = torch.empty(rows, 2 * D, device=cuda, dtype=torch.int8)
     s = torch.empty(rows, device=cuda)
-    L.check(lib.icap_op_layernorm_i8(x.data_ptr(), rows, D, w.data_ptr(), b.data_ptr(), 1e-6, q.data_ptr(), rows * D,
+    L.check(lib.icap_op_layernorm_i8(x.data_ptr(), rows, D, w.data_ptr(), b.data_ptr(), 1e-6, q.data_ptr(),
                                      s.data_ptr(), L.stream_ptr()), "ln i8")
     torch.cuda.synchronize()
     ref = torch.nn.functional.layer_norm(x.double(), (D,), w.double(), b.double(), 1e-6)
@@ -202,7 +210,7 @@ def test_layernorm_i8(cuda):
     assert (err <= s.double()[:, None] * (0.5 + 2 ** -7) + 1e-5 * ref.abs().amax(1, keepdim=True)).all(), err.max().item()
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 768, 768), (50432, 2304, 768), (129, 512, 1024)])
+@pytest.mark.parametrize("M,N,K", [(1000, 768, 768), (50432, 2304, 768), (129, 512, 1024), (1970, 2304, 768)])
 @pytest.mark.parametrize("epi", [0, 1])
 def test_gemm_i8(cuda, M, N, K, epi):
     """The int8 two-slice GEMM equals its defining formula exactly up to fp32 rounding
@@ -216,12 +224,26 @@ def test_gemm_i8(cuda, M, N, K, epi):
     qa, sa = _pack_i8(L, lib, a)
     qw, sw = _pack_i8(L, lib, w)
     C = torch.empty(M, N, device=cuda)
-    L.check(lib.icap_op_gemm_i8(qa.data_ptr(), M * K, sa.data_ptr(), qw.data_ptr(), N * K, sw.data_ptr(),
-                                bias.data_ptr(), C.data_ptr(), M, N, K, epi, L.stream_ptr()), "gemm i8")
+    L.check(lib.icap_op_gemm_i8(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                                C.data_ptr(), M, N, K, epi, 0, 0, L.stream_ptr()), "gemm i8")
+    # split-plane output (LDS-staged epilogue), row-major and head-major
+    Cs = torch.empty(2, M, N, device=cuda, dtype=torch.bfloat16)
+    L.check(lib.icap_op_gemm_i8(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                                Cs.data_ptr(), M, N, K, epi, 2, 0, L.stream_ptr()), "gemm i8 split")
+    hm = 197 if M % 197 == 0 else (M if M <= 256 else 0)
+    Ch = torch.empty(2, M, N, device=cuda, dtype=torch.bfloat16)
+    if hm:
+        L.check(lib.icap_op_gemm_i8(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), bias.data_ptr(),
+                                    Ch.data_ptr(), M, N, K, epi, 2, hm, L.stream_ptr()), "gemm i8 head-major")
     torch.cuda.synchronize()
+    tol = 1e-5 * max(1.0, C.abs().max().item())
+    assert (value(Cs, 2) - C.double()).abs().max().item() < tol
+    if hm:  # [image][N/64][token][64] -> [image*token][N]
+        Chm = Ch.view(2, M // hm, N // 64, hm, 64).permute(0, 1, 3, 2, 4).reshape(2, M, N)
+        assert torch.equal(Chm, Cs)
     rows = slice(0, M) if M <= 4096 else torch.randperm(M, generator=g)[:2048].to(cuda)
-    a1, a2 = qa[0][rows].double(), qa[1][rows].double()
-    w1, w2 = qw[0].double(), qw[1].double()
+    a1, a2 = (t[rows].double() for t in _slices(qa))
+    w1, w2 = (t.double() for t in _slices(qw))
     acc = 65536.0 * (a1 @ w1.t()) + 256.0 * (a1 @ w2.t() + a2 @ w1.t())
     form = acc * sa.double()[rows][:, None] * sw.double()[None, :] + bias.double()
     exact = a[rows].double() @ w.double().t() + bias.double()

@@ -1,5 +1,5 @@
 """HIP path vs the reference-generated goldens and the CPU oracle, through the C-ABI and through
-the drop-in nn.Module surface.  Tolerances: bf16x2 (default) mode - token ids identical, logits
+the drop-in nn.Module surface.  Tolerances: i8x2 (default) and bf16x2 modes - token ids identical, logits
 within 1e-3 (SURVEY/BASELINE north star); bf16 mode - ids identical wherever the reference
 top-2 margin exceeds 0.2, logits within 0.1."""
 import os
@@ -47,13 +47,15 @@ def test_vit_golden_ids_and_logits(vit_engine, cuda):
     assert np.abs(tf.cpu().numpy() - g["logits_tf"]).max() < 1e-3
 
 
-def test_vit_golden_i8x2(vit_sd, cuda):
-    """i8x2 mode (LayerNorm-fed ViT GEMMs on int8 two-slice operands, the rest bf16x2): the same
-    bar as bf16x2 - golden ids identical, logits within 1e-3 (CPU emulation, tools/numerics_i8.py:
-    logit error <= 3e-5 over 29 steps, 0 of 2880 tokens differ at B = 96)."""
+@pytest.mark.parametrize("precision", ["bf16x2", "i8x2"])
+def test_vit_golden_per_precision(vit_sd, cuda, precision):
+    """Both parity modes meet the same bar: golden ids identical, logits within 1e-3, ids equal to
+    the fp32 oracle's on 24 more images.  i8x2 = the LayerNorm-fed ViT GEMMs on int8 two-slice
+    operands (16-bit fixed point), the rest bf16x2 (CPU emulation, tools/numerics_i8.py: logit
+    error <= 3e-5 over 29 steps, 0 of 2880 tokens differ at B = 96; bf16x2 <= 5e-6)."""
     from image_caption_amd.engine import Engine
 
-    eng = Engine(vit_sd, "vit", {}, precision="i8x2", device=cuda)
+    eng = Engine(vit_sd, "vit", {}, precision=precision, device=cuda)
     g = gold("vit_b4.npz")
     imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
     mem = eng.encode(imgs)

@@ -53,16 +53,14 @@ for name, (n, k, epi, out) in SHAPES.items():
     if name in ("qkv", "mlp0"):
         af = torch.randn(m, k, device=dev)
         wf = torch.randn(n, k, device=dev) / k ** 0.5
-        qa = torch.empty(2, m, k, device=dev, dtype=torch.int8)
-        qw = torch.empty(2, n, k, device=dev, dtype=torch.int8)
+        qa = torch.empty(m, 2 * k, device=dev, dtype=torch.int8)
+        qw = torch.empty(n, 2 * k, device=dev, dtype=torch.int8)
         sa, sw = torch.empty(m, device=dev), torch.empty(n, device=dev)
-        lib.icap_op_pack_i8(af.data_ptr(), m, k, qa.data_ptr(), m * k, sa.data_ptr(), _lib.stream_ptr())
-        lib.icap_op_pack_i8(wf.data_ptr(), n, k, qw.data_ptr(), n * k, sw.data_ptr(), _lib.stream_ptr())
-        Cf = torch.empty(m, n, device=dev)
-
-        def i8():
-            lib.icap_op_gemm_i8(qa.data_ptr(), m * k, sa.data_ptr(), qw.data_ptr(), n * k, sw.data_ptr(), b.data_ptr(),
-                                Cf.data_ptr(), m, n, k, epi, _lib.stream_ptr())
+        lib.icap_op_pack_i8(af.data_ptr(), m, k, qa.data_ptr(), sa.data_ptr(), _lib.stream_ptr())
+        lib.icap_op_pack_i8(wf.data_ptr(), n, k, qw.data_ptr(), sw.data_ptr(), _lib.stream_ptr())
+        def i8():  # production form: split planes (QKV head-major)
+            lib.icap_op_gemm_i8(qa.data_ptr(), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), b.data_ptr(),
+                                C.data_ptr(), m, n, k, epi, 2, 197 if name == "qkv" else 0, _lib.stream_ptr())
 
         t2 = timed(i8)
     fl = 2.0 * m * n * k
@@ -70,5 +68,5 @@ for name, (n, k, epi, out) in SHAPES.items():
     tot_lib += t1
     print(f"{name:5s} M={m} N={n} K={k}: icap {t0:8.1f} us  {fl / t0 / 1e6:7.1f} alg-TF/s  {2 * fl / t0 / 1e6:7.1f} "
           f"MFMA-TF/s | hipBLASLt K=2x{k} {t1:8.1f} us {2 * fl / t1 / 1e6:7.1f} TF/s"
-          + (f" | i8x2 (fp32 out) {t2:8.1f} us {fl / t2 / 1e6:7.1f} alg-TF/s" if t2 else ""), flush=True)
+          + (f" | i8x2 {t2:8.1f} us {fl / t2 / 1e6:7.1f} alg-TF/s" if t2 else ""), flush=True)
 print(f"per layer: icap {tot_ours:.1f} us, hipBLASLt {tot_lib:.1f} us")
