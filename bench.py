@@ -39,6 +39,7 @@ from image_caption_amd.engine import Engine, apply_stop_rule  # noqa: E402
 
 METRIC = "captions/sec (224×224, max_len=30, greedy) at 1/2/4/8 MI355X vs CPU ref"
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA, MI355X_MICROARCH.md chip table
+PEAK_I8_TOPS = 5000.0      # dense i8 MFMA (2x bf16 per clock: 16x16x64 i8 = cycles of 16x16x32 bf16), same table
 PEAK_HBM_GBS = 8000.0
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
 
@@ -211,9 +212,17 @@ def main():
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(dom["kernel"], headline)}
         else:
+            # achieved = algorithmic 2MNK per launch / launch time.  The MFMA work behind it: bf16x2 GEMMs
+            # issue 2 bf16 products per algorithmic MAC (hi and lo activation planes), the i8x2 GEMM 3 i8
+            # products (A1.W1, A1.W2, A2.W1) against the i8 peak - reported as mfma_issue_frac.
+            i8 = "i8" in dom["kernel"]
+            peak = PEAK_I8_TOPS if i8 else PEAK_BF16_TFLOPS
+            work = 3 if i8 else (1 if args.precision == "bf16" else 2)
             achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
-            roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(dom["kernel"], headline)}
+            roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak,
+                    "unit": "TFLOP/s", "peak_dtype": "i8" if i8 else "bf16", "frac": round(achieved / peak, 4),
+                    "traffic": pmc_traffic(dom["kernel"], headline),
+                    "mfma_products_per_alg_mac": work, "mfma_issue_frac": round(achieved * work / peak, 4)}
         roof.update({"kernel": dom["kernel"], "launches_per_step": dom["launches"] // args.steps,
                      "avg_launch_us": round(avg_ms * 1e3, 2),
                      "share_of_step": round(dom["ms"] / args.steps / step_ms, 3)})
@@ -227,7 +236,8 @@ def main():
                        "beam": f"captions/sec, beam search (beam {args.beam}, max_len={L})"}[args.mode],
             "value": round(value, 2), "unit": "images/s" if args.mode == "scst" else "captions/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic images N(0,1) + seeded random-init weights",
+            "vs_baseline": None,
+            "dtype": {"bf16": "bf16", "bf16x2": "bf16x2", "i8x2": "i8x2+bf16x2"}[args.precision], "data": "synthetic images N(0,1) + seeded random-init weights",
             "config": {"workload": ("vit_b16 encoder + 6-layer decoder, greedy, 224x224, max_len=30" if args.model == "vit"
                                     else f"grid resnet101 ({'torch/MIOpen fp32' if args.torch_trunk else 'HIP'}) "
                                          "+ 6-layer encoder + 6-layer decoder, greedy, 224x224, max_len=30")
