@@ -100,6 +100,10 @@ def main():
     ap.add_argument("--torch-trunk", action="store_true", help="grid: ResNet trunk via PyTorch/MIOpen fp32")
     ap.add_argument("--mode", default="greedy", choices=["greedy", "scst", "beam"])
     ap.add_argument("--beam", type=int, default=5, help="beam width of --mode beam")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="greedy: overlap the encode of step i+1 with the decode of step i on two streams "
+                         "(image_caption_amd/pipeline.py; measured +2-4 %% with ICAP_DEC_BRANCHES=1, within noise "
+                         "of the default, profiles/r01/v16_pipeline_sweep.txt)")
     args = ap.parse_args()
 
     rank, ws, local = parallel.init()
@@ -175,8 +179,28 @@ def main():
                 return r[:total] - r[total:]
             return gid
 
-    for _ in range(args.warmup):
-        out = step()
+    pipe = None
+    if args.mode == "greedy" and trunk is None and args.pipeline:
+        from image_caption_amd.pipeline import CaptionPipeline
+
+        dcus = int(os.environ.get("ICAP_PIPE_DECODE_CUS", "0")) or None
+        dprio = int(os.environ.get("ICAP_PIPE_DECODE_PRIORITY", "-1"))
+        pipe = CaptionPipeline(eng, W.START_TOKEN, W.END_TOKEN, L, decode_priority=dprio, decode_cus=dcus)
+
+        def post(ids):
+            if ws > 1:
+                ids = parallel.gather_rows(ids, total)
+            return apply_stop_rule(ids.long(), W.END_TOKEN)
+
+    def run_steps(n):
+        if pipe is not None:  # n steps = n batches, encode(i+1) overlapping decode(i)
+            return pipe.run([imgs] * n, post)[-1] if n else None
+        o = None
+        for _ in range(n):
+            o = step()
+        return o
+
+    out = run_steps(args.warmup)
     torch.cuda.synchronize()
 
     eng.profile(True)
@@ -184,8 +208,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
+    out = run_steps(args.steps)
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
@@ -245,7 +268,8 @@ def main():
                           "beam": f"; beam search, beam {args.beam}"}[args.mode],
                        "per_gpu_batch": B, "global_batch": total, "max_len": L, "precision": args.precision,
                        "decode_steps": L - 1, "output_len": int(out.shape[1]) if args.mode == "greedy" else None,
-                       "parallelism": f"dp{ws}"},
+                       "parallelism": f"dp{ws}",
+                       "pipelined": pipe is not None},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -968,6 +968,37 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
   });
 }
 
+// Streams restricted to a subset of the CUs (hipExtStreamCreateWithCUMask), for running the
+// encoder of one batch beside the decode of the previous one without the two fighting over CUs.
+// The n selected CUs are taken 8 per 32-CU block (bits i with i % 32 < n / 8), which spreads them
+// evenly over the 8 XCDs whether mask bits enumerate CUs XCD-major or XCD-interleaved.
+int icap_stream_create_cu_mask(int n_cus, int complement, int priority, void** out) {
+  return guarded([&] {
+    REQUIRE(out, "null argument");
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, dev));
+    const int total = prop.multiProcessorCount;
+    REQUIRE(total % 32 == 0 && n_cus > 0 && n_cus < total && n_cus % (total / 32) == 0,
+            "n_cus must be a positive multiple of (CUs / 32) below the CU count");
+    const int per_block = n_cus / (total / 32);
+    std::vector<uint32_t> mask((total + 31) / 32, 0u);
+    for (int i = 0; i < total; ++i) {
+      const bool sel = (i % 32) < per_block;
+      if (sel != (complement != 0)) mask[i / 32] |= 1u << (i % 32);
+    }
+    hipStream_t st = nullptr;
+    HIPCHK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    (void)priority;
+    *out = st;
+  });
+}
+
+int icap_stream_destroy(void* stream) {
+  return guarded([&] { HIPCHK(hipStreamDestroy((hipStream_t)stream)); });
+}
+
 int icap_destroy(icap_handle* h) {
   return guarded([&] {
     if (h) {

@@ -1,0 +1,96 @@
+"""Batch-pipelined captioning: the encoder of batch i+1 runs while batch i decodes.
+
+The greedy decode of a batch (`_greedy_search`'s loop, vit:296-325) is a chain of small, latency-bound
+launches (29 steps x 6 layers x ~11 kernels, replayed from a hipGraph) that leaves most of the chip
+idle, while the next batch's encoder is a handful of large MFMA GEMMs that fill it.  Running them on
+two streams - the decode on a high-priority stream, so its workgroups take CUs as soon as encoder
+blocks retire - overlaps the two phases of consecutive batches.  Every batch still goes through the
+exact same kernels, so the captions are bit-identical to `Engine.greedy(Engine.encode(x))` per batch.
+
+Buffer hand-off: each batch's memory tensor is allocated on the encoder stream and marked with
+`record_stream(decode stream)`, so the caching allocator does not hand it to a later encode before
+the decode that reads it has finished; the decode graph copies it into its own buffer on entry.
+"""
+from __future__ import annotations
+
+from typing import Callable, Iterable, List, Optional
+
+import torch
+
+from . import _lib
+from .engine import Engine
+
+
+class CaptionPipeline:
+    """decode_cus = None: two ordinary streams, the decode one at high priority.  decode_cus = n: the
+    decode stream runs on n CUs and the encoder stream on the others (icap_stream_create_cu_mask),
+    so neither phase waits for the other's workgroups to retire before it gets a CU."""
+
+    def __init__(self, engine: Engine, start: int, end: int, max_len: int, decode_priority: int = -1,
+                 decode_cus: Optional[int] = None):
+        import ctypes
+
+        self.eng = engine
+        self.start, self.end, self.max_len = int(start), int(end), int(max_len)
+        dev = engine.device
+        self._owned = []
+        if decode_cus:
+            lib = engine.lib
+            ptrs = []
+            for comp in (0, 1):
+                p = ctypes.c_void_p()
+                _lib.check(lib.icap_stream_create_cu_mask(int(decode_cus), comp, 0, ctypes.byref(p)),
+                           "icap_stream_create_cu_mask")
+                ptrs.append(p.value)
+            self._owned = ptrs
+            self.dec_stream = torch.cuda.ExternalStream(ptrs[0], device=dev)
+            self.enc_stream = torch.cuda.ExternalStream(ptrs[1], device=dev)
+        else:
+            lo, hi = torch.cuda.Stream.priority_range()
+            prio = max(min(decode_priority, lo), hi)
+            self.enc_stream = torch.cuda.Stream(device=dev, priority=0)
+            self.dec_stream = torch.cuda.Stream(device=dev, priority=prio)
+
+    def __del__(self):
+        for p in getattr(self, "_owned", []):
+            try:
+                torch.cuda.synchronize(self.eng.device)
+                self.eng.lib.icap_stream_destroy(p)
+            except Exception:
+                pass
+        self._owned = []
+
+    def run(self, batches: Iterable[torch.Tensor],
+            post: Optional[Callable[[torch.Tensor], object]] = None) -> List[object]:
+        """Greedy-caption every batch; returns post(ids) per batch (default: the raw int32 ids
+        (B, max_len) before the stop rule).  `post` runs on the decode stream right after its batch's
+        decode was enqueued and the NEXT batch's encode was enqueued, so a host sync inside it (the stop
+        rule's length) waits for this decode while the encoder keeps the GPU busy."""
+        eng, E, D = self.eng, self.enc_stream, self.dec_stream
+        cur = torch.cuda.current_stream(eng.device)
+        it = iter(batches)
+        outs: List[object] = []
+        first = next(it, None)
+        if first is None:
+            return outs
+        E.wait_stream(cur)  # inputs produced on the caller's stream
+        D.wait_stream(cur)
+        with torch.cuda.stream(E):
+            mem = eng.encode(first)
+        nxt = next(it, None)
+        while mem is not None:
+            ev = E.record_event()
+            D.wait_event(ev)
+            mem.record_stream(D)
+            with torch.cuda.stream(D):
+                ids, _ = eng.greedy_raw(mem, self.start, self.end, self.max_len)
+            mem = None
+            if nxt is not None:
+                with torch.cuda.stream(E):
+                    mem = eng.encode(nxt)
+                nxt = next(it, None)
+            with torch.cuda.stream(D):
+                outs.append(post(ids) if post is not None else ids)
+        cur.wait_stream(D)
+        cur.wait_stream(E)
+        return outs

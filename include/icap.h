@@ -194,6 +194,11 @@ int icap_op_gemm(const uint16_t* A, long lda, long a_lo, int nsplit, const uint1
                  void* C, long ldc, long c_lo, int M, int N, int K, int epi, int out, void* stream);
 int icap_op_layernorm(const float* x, int rows, int D, const float* w, const float* b, float eps,
                       float* out_f32, uint16_t* out_bf, long bf_lo, int nsplit, void* stream);
+/* A stream whose kernels run only on n_cus of the device's CUs (8 per 32-CU block, i.e. spread over
+   the XCDs), or on the other CUs when complement != 0 (image_caption_amd/pipeline.py: encoder and
+   decoder of consecutive batches side by side).  Destroy with icap_stream_destroy. */
+int icap_stream_create_cu_mask(int n_cus, int complement, int priority, void** out);
+int icap_stream_destroy(void* stream);
 /* int8 two-slice operands (ICAP_PREC_I8X2): fp32 rows -> row images out[r*2K + (k/64)*128 + j*64 + k%64]
    (slice j = 0, 1) with v = scale[r] (256 x1 + x2), 16-bit fixed point relative to the row maximum
    (pack: the rows as given; layernorm_i8: their LayerNorm, then the same quantisation). K % 64 == 0. */

@@ -64,3 +64,27 @@ def test_two_chain_decode_matches_one_chain(cuda, vit_sd, monkeypatch):
         out[nb] = runs[0]
     for a, b in zip(out["1"], out["2"]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [8, 256])
+def test_pipeline_matches_sequential(cuda, vit_sd, B):
+    """CaptionPipeline (encode of batch i+1 on one stream while batch i decodes on a high-priority
+    stream) returns exactly the ids of encode + greedy run batch by batch, through the eager, capture
+    and replay calls of the decode graph."""
+    from image_caption_amd.engine import Engine
+    from image_caption_amd.pipeline import CaptionPipeline
+
+    eng = Engine(vit_sd, "vit", {}, device=cuda)
+    batches = [torch.from_numpy(W.synthetic_images(B, seed=s)).to(cuda) for s in (11, 12, 13, 14)]
+    seq = [eng.greedy_raw(eng.encode(b), 107, 108, 30)[0].cpu() for b in batches]
+    got = CaptionPipeline(eng, 107, 108, 30).run(batches)
+    torch.cuda.synchronize()
+    assert len(got) == len(seq)
+    for a, b in zip(got, seq):
+        assert torch.equal(a.cpu(), b)
+    # with a host-syncing post step (the stop rule), as the bench runs it
+    from image_caption_amd.engine import apply_stop_rule
+
+    got2 = CaptionPipeline(eng, 107, 108, 30).run(batches, lambda ids: apply_stop_rule(ids.long(), 108))
+    for a, b in zip(got2, seq):
+        assert torch.equal(a.cpu(), apply_stop_rule(b.long(), 108))
