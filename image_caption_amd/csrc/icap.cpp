@@ -129,8 +129,9 @@ struct icap_handle {
   bool use_graphs = true;
   hipStream_t cap_stream = nullptr;
   int dec_branches = 2;                 // ICAP_DEC_BRANCHES: independent decode chains per batch
-  hipStream_t aux_stream = nullptr;     // second chain's stream
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  static constexpr int MAX_BRANCHES = 4;
+  hipStream_t aux_stream[MAX_BRANCHES] = {};  // streams of chains 1.. (chain 0 runs on the caller's)
+  hipEvent_t ev_fork = nullptr, ev_join[MAX_BRANCHES] = {};
   DecodeGraph dg[2];  // one captured loop per mode (0 greedy, 1 sample): SCST alternates them
   int ns = 2;  // activation planes (1 = bf16, 2 = hi/lo)
   bool i8 = false;  // ICAP_PREC_I8X2: LayerNorm-fed ViT GEMMs on int8 two-slice operands
@@ -200,9 +201,11 @@ struct icap_handle {
       for (DevBuf* b : {&g.ids, &g.lg, &g.uni, &g.lp}) b->release();
     }
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
-    if (aux_stream) (void)hipStreamDestroy(aux_stream);
+    for (hipStream_t a : aux_stream)
+      if (a) (void)hipStreamDestroy(a);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
+    for (hipEvent_t e : ev_join)
+      if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col}) b->release();
@@ -785,17 +788,24 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   // independent chains on two streams (two parallel branches of the captured graph), so their
   // latency-bound launches can overlap.
   // (two chains pay from 128 rows each: B = 256 +3.4 %, B = 128 -6 %, tools/ab_env.sh)
-  const int nb = (h->dec_branches > 1 && B >= 256) ? 2 : 1;
-  if (nb == 2) {
-    if (!h->aux_stream) HIPCHK(hipStreamCreateWithFlags(&h->aux_stream, hipStreamNonBlocking));
+  static const int min_rows = [] {  // ICAP_DEC_MIN_ROWS: smallest chain (64-row chains measured slower)
+    const char* v = getenv("ICAP_DEC_MIN_ROWS");
+    return v ? std::max(16, atoi(v)) : 128;
+  }();
+  int nb = 1;
+  while (nb * 2 <= h->dec_branches && B / (nb * 2) >= min_rows) nb *= 2;
+  if (nb > 1) {
     if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-    if (!h->ev_join) HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     HIPCHK(hipEventRecord(h->ev_fork, s));
-    HIPCHK(hipStreamWaitEvent(h->aux_stream, h->ev_fork, 0));
+    for (int i = 1; i < nb; ++i) {
+      if (!h->aux_stream[i]) HIPCHK(hipStreamCreateWithFlags(&h->aux_stream[i], hipStreamNonBlocking));
+      if (!h->ev_join[i]) HIPCHK(hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming));
+      HIPCHK(hipStreamWaitEvent(h->aux_stream[i], h->ev_fork, 0));
+    }
   }
   for (int part = 0; part < nb; ++part) {
-    const int r0 = part * (B / 2), n = nb == 1 ? B : (part ? B - B / 2 : B / 2);
-    hipStream_t st = part ? h->aux_stream : s;
+    const int r0 = (int)((long)B * part / nb), n = (int)((long)B * (part + 1) / nb) - r0;
+    hipStream_t st = part ? h->aux_stream[part] : s;
     DecodeBufs v = sub_bufs(b, d, r0, max_len, S);
     for (int t = 0; t + 1 < max_len; ++t) {
       decoder_layers(h, v, n, 1, t, max_len, 1, S, st);
@@ -814,9 +824,9 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
       HIPCHK(launch_head(ha, st));
     }
   }
-  if (nb == 2) {
-    HIPCHK(hipEventRecord(h->ev_join, h->aux_stream));
-    HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
+  for (int i = 1; i < nb; ++i) {
+    HIPCHK(hipEventRecord(h->ev_join[i], h->aux_stream[i]));
+    HIPCHK(hipStreamWaitEvent(s, h->ev_join[i], 0));
   }
 }
 
@@ -952,7 +962,7 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
       h->d = *desc;
       h->ns = desc->precision == ICAP_PREC_BF16 ? 1 : 2;
       h->i8 = desc->precision == ICAP_PREC_I8X2 && desc->kind == ICAP_KIND_VIT;
-      if (const char* v = getenv("ICAP_DEC_BRANCHES")) h->dec_branches = std::max(1, std::min(2, atoi(v)));
+      if (const char* v = getenv("ICAP_DEC_BRANCHES")) h->dec_branches = std::max(1, std::min(icap_handle::MAX_BRANCHES, atoi(v)));
       pack(h, (hipStream_t)stream);
       HIPCHK(hipStreamSynchronize((hipStream_t)stream));
     } catch (...) {
