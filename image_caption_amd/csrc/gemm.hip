@@ -1225,7 +1225,7 @@ __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
   return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
 }
 
-template <int NSTAGE>
+template <int NSTAGE, int NOMFMA = 0>
 __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
   constexpr int NW = 8, BM = 128, BN = 256, WM = 64, WN = 64, TM = WM / 16, TN = WN / 16;
   constexpr int OPB = BM * 128, OPBW = BN * 128;  // bytes per A / W tile per stage (both slices)
@@ -1307,6 +1307,10 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
       const i32x4 a2 = *(const i32x4*)(s0 + (wm * WM + i * 16) * 128 + f2);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
+        if (NOMFMA) {  // measurement variant (ICAP_I8_NOMFMA): staging + fragment reads only
+          asm volatile("" ::"v"(a1), "v"(a2), "v"(w1[j]), "v"(w2[j]));
+          continue;
+        }
         ah[i][j] = mfma_i8(w1[j], a1, ah[i][j]);  // D = W.A^T, as the bf16 kernel
         am[i][j] = mfma_i8(w2[j], a1, am[i][j]);
         am[i][j] = mfma_i8(w1[j], a2, am[i][j]);
@@ -1371,8 +1375,13 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
                             : (long)m * p.ldc + col;
       const u32x4 vh = *(const u32x4*)(smem + row * PITCH + ch * 16);
       const u32x4 vl = *(const u32x4*)(smem + PLANE + row * PITCH + ch * 16);
-      *(u32x4*)(C + o) = vh;
-      *(u32x4*)(C + o + p.c_lo) = vl;
+      if (p.nt_store) {  // streamed past the caches: keeps the operands resident in L2 / MALL
+        __builtin_nontemporal_store(vh, (u32x4*)(C + o));
+        __builtin_nontemporal_store(vl, (u32x4*)(C + o + p.c_lo));
+      } else {
+        *(u32x4*)(C + o) = vh;
+        *(u32x4*)(C + o + p.c_lo) = vl;
+      }
     }
     return;
   }
@@ -1393,18 +1402,24 @@ hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
   constexpr int NST = 3, lds = NST * (128 * 128 + 256 * 128);
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_i8_kernel<NST>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
+    for (const void* f : {(const void*)gemm_i8_kernel<NST>, (const void*)gemm_i8_kernel<NST, 1>}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e != hipSuccess) return e;
+    }
     attr = true;
   }
+  static const int nomfma = getenv("ICAP_I8_NOMFMA") ? atoi(getenv("ICAP_I8_NOMFMA")) : 0;
   const int nwg = (g.N / 256) * ((g.M + 127) / 128);
   static int group = -1;  // ICAP_I8_GROUP: tile raster (0 = row-band major; 16: qkv 373 -> 338 us, mlp0 525 -> 459)
   if (group < 0) {
     const char* v = getenv("ICAP_I8_GROUP");
     group = v ? std::max(0, atoi(v)) : 16;
   }
+  static const int nt = getenv("ICAP_I8_NT_STORE") ? atoi(getenv("ICAP_I8_NT_STORE")) : 0;
   GemmArgs gg = g;
   gg.raster_group = group;
-  hipLaunchKernelGGL((gemm_i8_kernel<NST>), dim3(nwg), dim3(512), lds, s, gg);
+  gg.nt_store = nt;
+  if (nomfma) hipLaunchKernelGGL((gemm_i8_kernel<NST, 1>), dim3(nwg), dim3(512), lds, s, gg);
+  else hipLaunchKernelGGL((gemm_i8_kernel<NST>), dim3(nwg), dim3(512), lds, s, gg);
   return hipGetLastError();
 }

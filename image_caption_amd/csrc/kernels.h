@@ -33,6 +33,7 @@ struct GemmArgs {
   // goes to ((row / hm_n * (N / 64) + col / 64) * hm_n + row % hm_n) * 64 + col % 64, i.e. the QKV
   // projection as [image][q|k|v x head][token][64] - one head's rows contiguous for the attention
   int hm_n;
+  int nt_store;      // split-plane outputs with nontemporal stores (gemm_i8 LDS epilogue)
   int raster_group;  // tile raster inside an XCD: groups of raster_group row bands, column tiles outer (0: row-band major)
   // int8 two-slice operands (launch_gemm_i8 only): A and W are int8 row images [rows][K/64][2][64]
   // (row stride 2K bytes; lda / ldw / a_lo unused), v = s (256 x1 + x2) with a per-row scale:

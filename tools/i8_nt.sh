@@ -1,0 +1,9 @@
+#!/bin/bash
+# nontemporal split-plane stores in the i8 GEMM (ICAP_I8_NT_STORE): shape timing + headline bench.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+for P in 1 0; do
+  echo "== ICAP_I8_NT_STORE=$P"
+  ICAP_I8_NT_STORE=$P timeout -k 10 120 python tools/gemm_shapes.py 20 2>/dev/null | grep -E "qkv|mlp0" | sed 's/.*| i8x2/i8x2/' || exit 1
+  ICAP_I8_NT_STORE=$P timeout -k 10 150 python bench.py --no-cpu-baseline 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d["value"], d["ms_per_step"], d["roofline"]["avg_launch_us"])' || exit 1
+done
