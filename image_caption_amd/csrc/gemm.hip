@@ -1319,6 +1319,7 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
   }
 
   const int mb = m0 + wm * WM, nb = n0 + wn * WN;
+  if (NOMFMA == 2) return;  // measurement: staging only, no epilogue
   f32x4 acc[TM][TN];
   f32x4 ws[TN];
 #pragma unroll
@@ -1402,7 +1403,8 @@ hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
   constexpr int NST = 3, lds = NST * (128 * 128 + 256 * 128);
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)gemm_i8_kernel<NST>, (const void*)gemm_i8_kernel<NST, 1>}) {
+    for (const void* f : {(const void*)gemm_i8_kernel<NST>, (const void*)gemm_i8_kernel<NST, 1>,
+                          (const void*)gemm_i8_kernel<NST, 2>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       if (e != hipSuccess) return e;
     }
@@ -1419,7 +1421,8 @@ hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
   GemmArgs gg = g;
   gg.raster_group = group;
   gg.nt_store = nt;
-  if (nomfma) hipLaunchKernelGGL((gemm_i8_kernel<NST, 1>), dim3(nwg), dim3(512), lds, s, gg);
+  if (nomfma == 2) hipLaunchKernelGGL((gemm_i8_kernel<NST, 2>), dim3(nwg), dim3(512), lds, s, gg);
+  else if (nomfma) hipLaunchKernelGGL((gemm_i8_kernel<NST, 1>), dim3(nwg), dim3(512), lds, s, gg);
   else hipLaunchKernelGGL((gemm_i8_kernel<NST>), dim3(nwg), dim3(512), lds, s, gg);
   return hipGetLastError();
 }
