@@ -1225,9 +1225,11 @@ __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
   return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
 }
 
-template <int NSTAGE, int NOMFMA = 0>
-__global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
-  constexpr int NW = 8, BM = 128, BN = 256, WM = 64, WN = 64, TM = WM / 16, TN = WN / 16;
+// BNT = 128: 128 x 128 tiles of 4 waves (2 x 2), a 2-stage 64 KiB ring and two blocks per CU, so one
+// block's epilogue overlaps the other's k-loop (ICAP_I8_TILE=128).
+template <int NSTAGE, int NOMFMA = 0, int BNT = 256>
+__global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(GemmArgs p) {
+  constexpr int NW = BNT / 32, BM = 128, BN = BNT, WM = 64, WN = 64, TM = WM / 16, TN = WN / 16;
   constexpr int OPB = BM * 128, OPBW = BN * 128;  // bytes per A / W tile per stage (both slices)
   constexpr int STAGE = OPB + OPBW;               // 48 KiB
   constexpr int IPW = OPB / 1024 / NW, IPWW = OPBW / 1024 / NW;
@@ -1236,7 +1238,7 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / (NW / 2), wn = wave % (NW / 2);
   const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
   const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
@@ -1351,9 +1353,16 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
           else if (p.epi == EPI_RELU) acc[i][j][e] = fmaxf(acc[i][j][e], 0.f);
         }
       }
-    constexpr int PITCH = BN * 2 + 16, PLANE = BM * PITCH;  // 528-B rows: 16 rows of one column hit distinct banks
+    // 528-B rows (BN = 256): 16 rows of one column hit distinct banks.  The whole tile when it fits
+    // the ring (BN = 256), else in row halves of one wave row each (BN = 128: 2 x 64 KiB > 64 KiB).
+    constexpr int PITCH = BN * 2 + 16, NH = 2 * BM * PITCH <= NSTAGE * STAGE ? 1 : 2, HR = BM / NH;
+    constexpr int PLANE = HR * PITCH;
     static_assert(2 * PLANE <= NSTAGE * STAGE, "epilogue tile exceeds the ring");
-    __syncthreads();  // every wave is past its last ring read
+    bf16_t* C = (bf16_t*)p.C;
+#pragma unroll
+    for (int hf = 0; hf < NH; ++hf) {
+    __syncthreads();  // every wave is past its last ring read / the previous half's reads
+    if (NH == 1 || wm == hf) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1361,15 +1370,15 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
         bf16_t h[4], l[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) split_bf(acc[i][j][e], h[e], l[e]);
-        char* d = smem + (wm * WM + i * 16 + fr) * PITCH + (wn * WN + j * 16 + 4 * fq) * 2;
+        char* d = smem + ((NH == 1 ? wm * WM : 0) + i * 16 + fr) * PITCH + (wn * WN + j * 16 + 4 * fq) * 2;
         *(u32x2*)d = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
         *(u32x2*)(d + PLANE) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
       }
+    }
     __syncthreads();
-    bf16_t* C = (bf16_t*)p.C;
 #pragma unroll 4
-    for (int c = tid; c < BM * (BN / 8); c += NW * 64) {
-      const int row = c / (BN / 8), ch = c % (BN / 8), m = m0 + row;
+    for (int c = tid; c < HR * (BN / 8); c += NW * 64) {
+      const int row = c / (BN / 8), ch = c % (BN / 8), m = m0 + hf * HR + row;
       if (m >= M) continue;
       const int col = n0 + ch * 8;
       const long o = p.hm_n ? (((long)(m / p.hm_n) * (p.N / 64) + col / 64) * p.hm_n + m % p.hm_n) * 64 + col % 64
@@ -1383,6 +1392,7 @@ __global__ __launch_bounds__(512, 1) void gemm_i8_kernel(GemmArgs p) {
         *(u32x4*)(C + o) = vh;
         *(u32x4*)(C + o + p.c_lo) = vl;
       }
+    }
     }
     return;
   }
@@ -1421,6 +1431,27 @@ hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
   GemmArgs gg = g;
   gg.raster_group = group;
   gg.nt_store = nt;
+  // ICAP_I8_TILE: 128 (default) = 128 x 128 tiles, two blocks per CU; 256 = 128 x 256 tiles, one
+  // block per CU.  Headline bench 6531 -> 6563 captions/s (QKV 370 -> 367 us, MLP-1 540 -> 500 us);
+  // a persistent 128 x 256 form (ring prefetch across tile seams, stores drained under the next
+  // tile's k-steps) measured 6548 and a 4-wave one-wave-per-SIMD form with fragment prefetch was
+  // slower still (QKV 491 us): every form lands near 365 us for QKV (profiles/r01/v17_i8_forms.txt).
+  static const int tile = getenv("ICAP_I8_TILE") ? atoi(getenv("ICAP_I8_TILE")) : 128;
+  if (tile == 128 && g.N % 128 == 0) {
+    constexpr int lds128 = 2 * (128 * 128 + 128 * 128);
+    static bool attr128 = false;
+    if (!attr128) {
+      for (const void* f : {(const void*)gemm_i8_kernel<2, 0, 128>, (const void*)gemm_i8_kernel<2, 1, 128>}) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds128);
+        if (e != hipSuccess) return e;
+      }
+      attr128 = true;
+    }
+    const int nwg128 = (g.N / 128) * ((g.M + 127) / 128);
+    if (nomfma) hipLaunchKernelGGL((gemm_i8_kernel<2, 1, 128>), dim3(nwg128), dim3(256), lds128, s, gg);
+    else hipLaunchKernelGGL((gemm_i8_kernel<2, 0, 128>), dim3(nwg128), dim3(256), lds128, s, gg);
+    return hipGetLastError();
+  }
   if (nomfma == 2) hipLaunchKernelGGL((gemm_i8_kernel<NST, 2>), dim3(nwg), dim3(512), lds, s, gg);
   else if (nomfma) hipLaunchKernelGGL((gemm_i8_kernel<NST, 1>), dim3(nwg), dim3(512), lds, s, gg);
   else hipLaunchKernelGGL((gemm_i8_kernel<NST>), dim3(nwg), dim3(512), lds, s, gg);
