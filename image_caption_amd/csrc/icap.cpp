@@ -803,11 +803,13 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
       HIPCHK(hipStreamWaitEvent(h->aux_stream[i], h->ev_fork, 0));
     }
   }
-  for (int part = 0; part < nb; ++part) {
-    const int r0 = (int)((long)B * part / nb), n = (int)((long)B * (part + 1) / nb) - r0;
-    hipStream_t st = part ? h->aux_stream[part] : s;
-    DecodeBufs v = sub_bufs(b, d, r0, max_len, S);
-    for (int t = 0; t + 1 < max_len; ++t) {
+  // step-major issue order: launched eagerly, the chains' kernels reach their streams interleaved
+  // (a captured graph has the same dependencies either way)
+  for (int t = 0; t + 1 < max_len; ++t) {
+    for (int part = 0; part < nb; ++part) {
+      const int r0 = (int)((long)B * part / nb), n = (int)((long)B * (part + 1) / nb) - r0;
+      hipStream_t st = part ? h->aux_stream[part] : s;
+      DecodeBufs v = sub_bufs(b, d, r0, max_len, S);
       decoder_layers(h, v, n, 1, t, max_len, 1, S, st);
       HeadArgs ha{};
       ha.x = v.x; ha.rows = n; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = d.vocab;

@@ -33,6 +33,30 @@ __global__ __launch_bounds__(128) void k_ln(float* __restrict__ x, const float* 
   *(f32x4*)(x + row * 512 + col) = (v - mean) * 0.999f;
 }
 
+// one function for both bodies: is the alternation cost tied to switching kernel objects?
+__global__ __launch_bounds__(256) void k_multi(int mode, float* __restrict__ x, const float* __restrict__ parts,
+                                               const f32x4* __restrict__ a, f32x4* __restrict__ b, long n) {
+  if (mode == 0) {
+    const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (i < n) b[i] = a[i] * 1.5f;
+    return;
+  }
+  __shared__ float red[2];
+  const int row = blockIdx.x, col = threadIdx.x * 4;
+  f32x4 v = *(const f32x4*)(x + row * 512 + col);
+  f32x4 pp[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) pp[s] = *(const f32x4*)(parts + s * 131072 + row * 512 + col);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) v += pp[s];
+  float sm = v[0] + v[1] + v[2] + v[3];
+  for (int o = 32; o; o >>= 1) sm += __shfl_xor(sm, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sm;
+  __syncthreads();
+  const float mean = (red[0] + red[1]) / 512.f;
+  *(f32x4*)(x + row * 512 + col) = (v - mean) * 0.999f;
+}
+
 template <class F>
 float graph_time(F launch, hipStream_t s, int n = 100) {
   hipGraph_t g;
@@ -132,6 +156,49 @@ int main() {
       hipLaunchKernelGGL(k_copy, dim3(n / 256), dim3(256), 0, s, (const f32x4*)A, B, n);
     }, s, 50);
     printf("alt ln/copy(indep) : %6.2f us/kernel\n", t);
+    t = graph_time([&] {
+      hipLaunchKernelGGL(k_multi, dim3(256), dim3(128), 0, s, 1, x, parts, (const f32x4*)A, B, n);
+      hipLaunchKernelGGL(k_multi, dim3(n / 256), dim3(256), 0, s, 0, x, parts, (const f32x4*)A, B, n);
+    }, s, 50);
+    printf("alt ln/copy merged kernel : %6.2f us/kernel\n", t);
+    t = graph_time([&] {
+      hipLaunchKernelGGL(k_multi, dim3(256), dim3(128), 0, s, 1, x, parts, (const f32x4*)A, B, n);
+    }, s, 100);
+    printf("merged kernel ln only : %6.2f us/kernel\n", t);
+    t = graph_time([&] {
+      hipLaunchKernelGGL(k_multi, dim3(n / 256), dim3(256), 0, s, 0, x, parts, (const f32x4*)A, B, n);
+    }, s, 100);
+    printf("merged kernel copy only : %6.2f us/kernel\n", t);
+    t = graph_time([&] {
+      hipLaunchKernelGGL(k_copy, dim3(n / 256), dim3(256), 0, s, (const f32x4*)A, B, n);
+    }, s, 100);
+    printf("copy 1MiB only : %6.2f us/kernel\n", t);
+    // what changes between consecutive dispatches makes them slow: grid size, LDS size, mode arg
+    t = graph_time([&] {
+      hipLaunchKernelGGL(k_copy, dim3(n / 256), dim3(256), 0, s, (const f32x4*)A, B, n);
+      hipLaunchKernelGGL(k_copy, dim3(n / 512), dim3(256), 0, s, (const f32x4*)A, B, n / 2);
+    }, s, 50);
+    printf("alt copy grid 256 / 128 blocks (same block size) : %6.2f us/kernel\n", t);
+    t = graph_time([&] {
+      hipLaunchKernelGGL(k_copy, dim3(n / 256), dim3(256), 0, s, (const f32x4*)A, B, n);
+      hipLaunchKernelGGL(k_copy, dim3(n / 256), dim3(256), 8192, s, (const f32x4*)A, B, n);
+    }, s, 50);
+    printf("alt copy dyn LDS 0 / 8 KiB : %6.2f us/kernel\n", t);
+    t = graph_time([&] {
+      hipLaunchKernelGGL(k_multi, dim3(256), dim3(256), 0, s, 1, x, parts, (const f32x4*)A, B, n);
+      hipLaunchKernelGGL(k_multi, dim3(n / 256), dim3(256), 0, s, 0, x, parts, (const f32x4*)A, B, n);
+    }, s, 50);
+    printf("alt merged ln/copy, both 256 threads : %6.2f us/kernel\n", t);
+    t = graph_time([&] {
+      hipLaunchKernelGGL(k_multi, dim3(256), dim3(256), 0, s, 1, x, parts, (const f32x4*)A, B, n);
+      hipLaunchKernelGGL(k_multi, dim3(256), dim3(256), 0, s, 0, x, parts, (const f32x4*)A, B, 256 * 256);
+    }, s, 50);
+    printf("alt merged ln/copy, same grid and block : %6.2f us/kernel\n", t);
+    t = graph_time([&] {
+      hipLaunchKernelGGL(k_copy, dim3(256), dim3(256), 0, s, (const f32x4*)A, B, 256 * 256);
+      hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, s, (float*)nullptr + 1);
+    }, s, 50);
+    printf("alt copy/empty, same grid and block : %6.2f us/kernel\n", t);
     // stream launches (no graph) for the ln/copy alternation
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
