@@ -11,6 +11,8 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 
 #define GLOBAL_AS __attribute__((address_space(1)))
 #define LDS_AS __attribute__((address_space(3)))
@@ -26,6 +28,18 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 __device__ __forceinline__ void split_bf(float v, bf16_t& hi, bf16_t& lo) {
   hi = f2bf(v);
   lo = f2bf(v - bf2f(hi));
+}
+
+// Two values at once: v_cvt_pk_bf16_f32 rounds both (RNE) into one dword (element 0 in the low half);
+// hi/lo as split_bf, both planes packed.  Half the conversions and none of the shift/or packing of
+// two split_bf calls.
+__device__ __forceinline__ uint32_t pack_bf2(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
+}
+__device__ __forceinline__ void split_bf2(f32x2 v, uint32_t& hi, uint32_t& lo) {
+  hi = pack_bf2(v);
+  const f32x2 hf = {__uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+  lo = pack_bf2(v - hf);
 }
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -62,5 +76,26 @@ __device__ __forceinline__ float gelu_erf_fast(float v) {
   y = fmaf(y, t, -1.26551223f);
   const float erfc_z = t * __expf(fmaf(-z, z, y));
   return 0.5f * v * (v >= 0.f ? 2.f - erfc_z : erfc_z);
+}
+// gelu_erf_fast on two values with packed FMAs (v_pk_fma_f32 / v_pk_mul_f32: the ten-term chain
+// issues five instructions per value pair instead of ten); the same operations, so the same results.
+__device__ __forceinline__ f32x2 gelu_erf_fast2(f32x2 v) {
+  const f32x2 z = __builtin_elementwise_abs(v) * 0.70710678118654752f;
+  const f32x2 den = __builtin_elementwise_fma(z, (f32x2)0.5f, (f32x2)1.f);
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 y = 0.17087277f;
+  y = __builtin_elementwise_fma(y, t, (f32x2)-0.82215223f);
+  y = __builtin_elementwise_fma(y, t, (f32x2)1.48851587f);
+  y = __builtin_elementwise_fma(y, t, (f32x2)-1.13520398f);
+  y = __builtin_elementwise_fma(y, t, (f32x2)0.27886807f);
+  y = __builtin_elementwise_fma(y, t, (f32x2)-0.18628806f);
+  y = __builtin_elementwise_fma(y, t, (f32x2)0.09678418f);
+  y = __builtin_elementwise_fma(y, t, (f32x2)0.37409196f);
+  y = __builtin_elementwise_fma(y, t, (f32x2)1.00002368f);
+  y = __builtin_elementwise_fma(y, t, (f32x2)-1.26551223f);
+  const f32x2 ex = __builtin_elementwise_fma(-z, z, y);
+  const f32x2 erfc_z = t * (f32x2){__expf(ex.x), __expf(ex.y)};
+  const f32x2 r = {v.x >= 0.f ? 2.f - erfc_z.x : erfc_z.x, v.y >= 0.f ? 2.f - erfc_z.y : erfc_z.y};
+  return 0.5f * v * r;
 }
 

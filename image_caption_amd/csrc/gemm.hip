@@ -1347,10 +1347,12 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
           const f32x4 bv = *(const f32x4*)(p.bias + nb + j * 16 + 4 * fq);
           acc[i][j] += bv;
         }
+        if (p.epi == EPI_GELU) {  // packed: the epilogue VALU is what the MLP-1 launch spends most on
+          const f32x2 g0 = gelu_erf_fast2(acc[i][j].xy), g1 = gelu_erf_fast2(acc[i][j].zw);
+          acc[i][j] = (f32x4){g0.x, g0.y, g1.x, g1.y};
+        } else if (p.epi == EPI_RELU) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (p.epi == EPI_GELU) acc[i][j][e] = gelu_erf_fast(acc[i][j][e]);
-          else if (p.epi == EPI_RELU) acc[i][j][e] = fmaxf(acc[i][j][e], 0.f);
+          for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaxf(acc[i][j][e], 0.f);
         }
       }
     // 528-B rows (BN = 256): 16 rows of one column hit distinct banks.  The whole tile when it fits
@@ -1367,12 +1369,12 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        bf16_t h[4], l[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) split_bf(acc[i][j][e], h[e], l[e]);
+        uint32_t h0, l0, h1, l1;
+        split_bf2(acc[i][j].xy, h0, l0);
+        split_bf2(acc[i][j].zw, h1, l1);
         char* d = smem + ((NH == 1 ? wm * WM : 0) + i * 16 + fr) * PITCH + (wn * WN + j * 16 + 4 * fq) * 2;
-        *(u32x2*)d = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
-        *(u32x2*)(d + PLANE) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
+        *(u32x2*)d = (u32x2){h0, h1};
+        *(u32x2*)(d + PLANE) = (u32x2){l0, l1};
       }
     }
     __syncthreads();
