@@ -1214,7 +1214,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
 // both slices (half the L2 requests of 64-B row segments).
 // Block tile 128 x 256 (8 waves as 2 x 4, each 64 x 64 = 4 x 4 MFMA tiles with a high and a mid int32
 // accumulator set: 128 accumulator registers, so one block per CU), stages of two operand tiles
-// (A: 128 rows, W: 256 rows, 128 B each; 16-B chunk c of row r at c ^ (r & 7)) in a 3-stage LDS ring
+// (A: 128 rows, W: 256 rows, 128 B each; 16-B chunk c of row r at c ^ ((r >> 1) & 7)) in a 3-stage LDS ring
 // (144 KiB) filled by global_load_lds, counted vmcnt + raw barrier, XCD remap.  The same LDS byte
 // positions feed the A and B operands, so the k labelling inside the MFMA does not matter.
 namespace {
@@ -1257,12 +1257,17 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
 
   // one DMA instruction = 8 rows x 128 B; lane -> row lane >> 3, LDS chunk lane & 7 holding source
   // chunk (lane & 7) ^ (row & 7) (instruction bases are multiples of 8 rows)
-  const int schunk = ((lane & 7) ^ (lane >> 3)) * 16;
+  // LDS chunk c of row r holds source chunk c ^ ((r >> 1) & 7): a ds_read_b128 pass (16 rows at 128-B
+  // stride, one logical chunk) then covers all 64 banks - with c ^ (r & 7) rows r and r + 8 shared
+  // banks (PMC: 6.1 M conflict cycles against 9.9 M LDS-active per launch).  Instruction q covers rows
+  // 8q..8q+7, so (r >> 1) & 7 = 4 (q & 1) + (lane >> 4); IPW and IPWW are even, so q & 1 = i & 1.
+  static_assert(IPW % 2 == 0 && IPWW % 2 == 0, "swizzle parity");
+  const int sch[2] = {((lane & 7) ^ (lane >> 4)) * 16, ((lane & 7) ^ (4 + (lane >> 4))) * 16};
   const char* a_src[IPW];
 #pragma unroll
   for (int i = 0; i < IPW; ++i)
-    a_src[i] = (const char*)p.A + (long)min(m0 + (wave * IPW + i) * 8 + (lane >> 3), M - 1) * ld + schunk;
-  const char* b_src = (const char*)p.W + (long)(n0 + wave * IPWW * 8 + (lane >> 3)) * ld + schunk;
+    a_src[i] = (const char*)p.A + (long)min(m0 + (wave * IPW + i) * 8 + (lane >> 3), M - 1) * ld + sch[i & 1];
+  const char* b_src = (const char*)p.W + (long)(n0 + wave * IPWW * 8 + (lane >> 3)) * ld;
   const long b_step = 8 * ld;
   auto stage = [&](int kt, int buf) {
     const int kin = kt * 128;
@@ -1273,7 +1278,7 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
                                        (LDS_AS void*)(s0 + (wave * IPW + i) * 1024), 16, 0, 0);
 #pragma unroll
     for (int i = 0; i < IPWW; ++i)
-      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(b_src + i * b_step + kin),
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(b_src + i * b_step + sch[i & 1] + kin),
                                        (LDS_AS void*)(s0 + OPB + (wave * IPWW + i) * 1024), 16, 0, 0);
   };
 
@@ -1284,7 +1289,7 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
     for (int j = 0; j < TN; ++j) ah[i][j] = am[i][j] = (i32x4){0, 0, 0, 0};
 
   const int fr = lane & 15, fq = lane >> 4;
-  const int f1 = fr * 128 + ((fq ^ (fr & 7)) << 4), f2 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
+  const int f1 = fr * 128 + ((fq ^ ((fr >> 1) & 7)) << 4), f2 = fr * 128 + (((4 + fq) ^ ((fr >> 1) & 7)) << 4);
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
     if (s < nk) stage(s, s);
