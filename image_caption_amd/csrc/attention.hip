@@ -39,6 +39,16 @@ __device__ __forceinline__ bf16x8 tr_pair(const char* p0, const char* p1) {
   return __builtin_bit_cast(bf16x8, c);
 }
 
+// LDS chunk swizzles of the [keys][64] K / V matrices (16-B chunk c of row r stored at c ^ swz(r)),
+// chosen for the 64-bank LDS: a ds_read_b128 pass covers 16 consecutive K rows at one logical chunk
+// (bank = 32 (r & 1) + 4 chunk: (r >> 1) & 7 spreads the 8 rows of each parity over 8 chunks; the
+// former r & 7 put rows r and r + 8 on the same banks, 2-way), and a ds_read_b64_tr_b16 pass covers
+// 8 consecutive V rows x 2 chunks x 2 halves (the 4 rows of one parity need disjoint chunk pairs:
+// 2 ((r >> 1) & 3); unswizzled V rows were 4-way conflicts).  PMC before: 26.8 M bank-conflict
+// cycles against 8.1 M LDS-active cycles per launch.
+__device__ __forceinline__ int kswz(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int vswz(int r) { return ((r >> 1) & 3) << 1; }
+
 template <int NKT, bool SPLIT, int NW>
 __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __restrict__ qkv, long ld, long lo,
                                                             int N, int H, float scale, bf16_t* out,
@@ -56,8 +66,9 @@ __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __
   const bf16_t* base = qkv + (long)b * N * ld;
 
   // stage K and V by LDS-DMA, one instruction = 8 rows x 128 B (full lines), lane-linear image:
-  // K chunk c of row r stored at c ^ (r & 7) (pre-swizzled on the source; conflict-free row-fragment
-  // reads), V plain for the transposed reads.  Rows >= N repeat row N - 1: their scores are masked to
+  // chunk c of row r stored at c ^ kswz(r) (K) / c ^ vswz(r) (V), pre-swizzled on the source
+  // (conflict-free fragment and transposed reads; PMC before: 1.57 M conflict cycles against 0.46 M
+  // LDS-active per Grid launch).  Rows >= N repeat row N - 1: their scores are masked to
   // -inf and their V rows meet p = 0.  All waves issue (LDS-DMA ingest scales with issuing waves).
   const int fr = lane & 15, g = lane >> 4;
   const int nqt = (N + 15) / 16;
@@ -78,7 +89,7 @@ __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __
     for (int ins = wave; ins < NMAT * PER_MAT; ins += NW) {
       const int mat = ins / PER_MAT, row = (ins - mat * PER_MAT) * 8 + lrow;  // mat: Kh, Vh, Kl, Vl
       const bool isK = !(mat & 1);
-      const int ch = isK ? lch ^ (row & 7) : lch;
+      const int ch = lch ^ (isK ? kswz(row) : vswz(row));
       const bf16_t* src = base + (mat >= 2 ? lo : 0) + (long)min(row, N - 1) * ld + (isK ? D : 2 * D) + h * 64 + ch * 8;
       __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
                                        (LDS_AS void*)(smem + mat * MAT + (ins - mat * PER_MAT) * 1024), 16, 0, 0);
@@ -110,7 +121,7 @@ __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __
         const int row = kt * 16 + fr;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          const int off = row * 128 + (((ks * 4 + g) ^ (row & 7)) << 4);
+          const int off = row * 128 + (((ks * 4 + g) ^ kswz(row)) << 4);
           const bf16x8 kh = *(const bf16x8*)(Kh + off);
           acc = mfma16(kh, qh[ks], acc);
           if (SPLIT) {
@@ -170,7 +181,8 @@ __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __
         const int key0 = 16 * (c0 + u) + 4 * g + q4;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
-          const int off0 = key0 * 128 + (dt * 16 + 4 * p4) * 2, off1 = off0 + 16 * 128;
+          const int off0 = key0 * 128 + (((dt * 2 + (p4 >> 1)) ^ vswz(key0)) << 4) + (p4 & 1) * 8;
+          const int off1 = off0 + 16 * 128;
           const bf16x8 vh = tr_pair(Vh + off0, Vh + off1);
           o[dt] = mfma16(vh, ph, o[dt]);
           if (SPLIT) {
@@ -282,15 +294,6 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restri
 // HM: qkv in the head-major layout of GemmArgs::hm_n ([image][q|k|v x head][token][64]), so one
 // (image, head)'s K and V rows are contiguous 128-byte rows; else row-major [token][3 D].
 // QPW query tiles per wave: 16 / QPW waves per block (QPW = 2: 8 waves, two blocks per CU).
-// LDS chunk swizzles of the [32 keys][64] chunk matrices (16-B chunk c of row r stored at c ^ swz(r)),
-// chosen for the 64-bank LDS: a ds_read_b128 pass covers 16 consecutive K rows at one logical chunk
-// (bank = 32 (r & 1) + 4 chunk: (r >> 1) & 7 spreads the 8 rows of each parity over 8 chunks; the
-// former r & 7 put rows r and r + 8 on the same banks, 2-way), and a ds_read_b64_tr_b16 pass covers
-// 8 consecutive V rows x 2 chunks x 2 halves (the 4 rows of one parity need disjoint chunk pairs:
-// 2 ((r >> 1) & 3); unswizzled V rows were 4-way conflicts).  PMC before: 26.8 M bank-conflict
-// cycles against 8.1 M LDS-active cycles per launch.
-__device__ __forceinline__ int kswz(int r) { return (r >> 1) & 7; }
-__device__ __forceinline__ int vswz(int r) { return ((r >> 1) & 3) << 1; }
 
 template <bool SPLIT, bool HM, int QPW>
 __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pipe_kernel(
