@@ -792,8 +792,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
     const char* v = getenv("ICAP_DEC_MIN_ROWS");
     return v ? std::max(16, atoi(v)) : 128;
   }();
-  int nb = 1;
-  while (nb * 2 <= h->dec_branches && B / (nb * 2) >= min_rows) nb *= 2;
+  const int nb = std::max(1, std::min(h->dec_branches, B / min_rows));
   if (nb > 1) {
     if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventRecord(h->ev_fork, s));
