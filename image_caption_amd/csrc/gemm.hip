@@ -1227,8 +1227,14 @@ __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
 
 // BNT = 128: 128 x 128 tiles of 4 waves (2 x 2), a 2-stage 64 KiB ring and two blocks per CU, so one
 // block's epilogue overlaps the other's k-loop (ICAP_I8_TILE=128).
-template <int NSTAGE, int NOMFMA = 0, int BNT = 256>
+// KSC = 1: A carries one scale per (row, 128-deep k block) (a_kscale[M][K/128]: the block-scaled GELU
+// output of MLP-1, whose producer tiles do not own whole rows).  The int32 accumulators then run over
+// the two k-steps of a block only and are folded into fp32 accumulators at its end,
+// acc += 256 s_a[row][kb] (256 hi + mid) - 256 hi + mid is exact in int32 for a 128-deep block
+// (|.| <= 128 (256 127^2 + 2 127 128) < 2^30) - before the column scale s_w in the epilogue.
+template <int NSTAGE, int NOMFMA = 0, int BNT = 256, int KSC = 0>
 __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(GemmArgs p) {
+  static_assert(!KSC || NSTAGE == 2, "block scales are loaded one k-step ahead under the ring's vmcnt(0)");
   constexpr int NW = BNT / 32, BM = 128, BN = BNT, WM = 64, WN = 64, TM = WM / 16, TN = WN / 16;
   constexpr int OPB = BM * 128, OPBW = BN * 128;  // bytes per A / W tile per stage (both slices)
   constexpr int STAGE = OPB + OPBW;               // 48 KiB
@@ -1283,12 +1289,26 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
   };
 
   i32x4 ah[TM][TN], am[TM][TN];
+  f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) ah[i][j] = am[i][j] = (i32x4){0, 0, 0, 0};
+    for (int j = 0; j < TN; ++j) {
+      ah[i][j] = am[i][j] = (i32x4){0, 0, 0, 0};
+      if (KSC) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
 
   const int fr = lane & 15, fq = lane >> 4;
+  // KSC: this lane's A rows (one per MFMA row tile) and their block scales for the current k-step
+  const float* ksrc[TM];
+  float skc[TM];
+  if (KSC) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      ksrc[i] = p.a_kscale + (long)min(m0 + wm * WM + i * 16 + fr, M - 1) * (nk >> 1);
+      skc[i] = ksrc[i][0];
+    }
+  }
   const int f1 = fr * 128 + ((fq ^ ((fr >> 1) & 7)) << 4), f2 = fr * 128 + (((4 + fq) ^ ((fr >> 1) & 7)) << 4);
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
@@ -1301,6 +1321,11 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    float skn[TM];
+    if (KSC) {  // next k-step's block scales (complete at the next iteration's vmcnt(0))
+#pragma unroll
+      for (int i = 0; i < TM; ++i) skn[i] = ksrc[i][min((kt >> 1) + 1, (nk >> 1) - 1)];
+    }
     const char* s0 = smem + (kt % NSTAGE) * STAGE;
     i32x4 w1[TN], w2[TN];
 #pragma unroll
@@ -1318,27 +1343,107 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
           asm volatile("" ::"v"(a1), "v"(a2), "v"(w1[j]), "v"(w2[j]));
           continue;
         }
+        if (KSC) {
+          const i32x4 z = {0, 0, 0, 0};
+          const bool first = !(kt & 1);
+          ah[i][j] = mfma_i8(w1[j], a1, first ? z : ah[i][j]);
+          am[i][j] = mfma_i8(w2[j], a1, first ? z : am[i][j]);
+          am[i][j] = mfma_i8(w1[j], a2, am[i][j]);
+          if (!first) {
+            const float s8 = skc[i] * 256.f;
+            const i32x4 t = (ah[i][j] << 8) + am[i][j];
+            const f32x4 tf = {(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
+            acc[i][j] = __builtin_elementwise_fma(tf, (f32x4)s8, acc[i][j]);
+          }
+          continue;
+        }
         ah[i][j] = mfma_i8(w1[j], a1, ah[i][j]);  // D = W.A^T, as the bf16 kernel
         am[i][j] = mfma_i8(w2[j], a1, am[i][j]);
         am[i][j] = mfma_i8(w1[j], a2, am[i][j]);
       }
     }
+    if (KSC && (kt & 1)) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) skc[i] = skn[i];
+    }
   }
 
   const int mb = m0 + wm * WM, nb = n0 + wn * WN;
   if (NOMFMA == 2) return;  // measurement: staging only, no epilogue
-  f32x4 acc[TM][TN];
   f32x4 ws[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) ws[j] = *(const f32x4*)(p.w_scale + nb + j * 16 + 4 * fq);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const float sa = p.a_scale[min(mb + i * 16 + fr, M - 1)];
+    const float sa = KSC ? 1.f : p.a_scale[min(mb + i * 16 + fr, M - 1)];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        acc[i][j][e] = fmaf((float)ah[i][j][e], 65536.f, (float)am[i][j][e] * 256.f) * (sa * ws[j][e]);
+        acc[i][j][e] = KSC ? acc[i][j][e] * ws[j][e]
+                           : fmaf((float)ah[i][j][e], 65536.f, (float)am[i][j][e] * 256.f) * (sa * ws[j][e]);
+  }
+  if (BNT == 128 && p.out == OUT_I8K) {
+    // Block-scaled int8 two-slice output: a tile's 128 columns of a row are one 128-deep k block of the
+    // consumer; the block maximum is a 16-value lane max, two xor shuffles over the 4 lanes (fq) holding
+    // the row in a wave, and the max of the two wave columns through LDS.  The tile's row image
+    // (2 x 128 B = 256 contiguous bytes of the [M][N/64][2][64] output row) is assembled in LDS, then
+    // stored as full 16-B chunks.
+    constexpr int PITCH8 = BN * 2 + 16;  // 272 B: rows fr of a 4-B column group hit distinct banks
+    static_assert(BM * PITCH8 + 2 * BM * 4 <= NSTAGE * STAGE, "epilogue tile exceeds the ring");
+    float* wmax = (float*)(smem + BM * PITCH8);  // [2 wave columns][BM rows]
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (p.bias) acc[i][j] += *(const f32x4*)(p.bias + nb + j * 16 + 4 * fq);
+        if (p.epi == EPI_GELU) {
+          const f32x2 g0 = gelu_erf_fast2(acc[i][j].xy), g1 = gelu_erf_fast2(acc[i][j].zw);
+          acc[i][j] = (f32x4){g0.x, g0.y, g1.x, g1.y};
+        } else if (p.epi == EPI_RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaxf(acc[i][j][e], 0.f);
+        }
+      }
+    __syncthreads();  // every wave is past its last ring read
+    const int nkb = p.N / 128;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float mx = 0.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fabsf(acc[i][j][e]));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (fq == 0) wmax[wn * BM + wm * WM + i * 16 + fr] = mx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * WM + i * 16 + fr;
+      const float mx = fmaxf(wmax[row], wmax[BM + row]);
+      const float inv = mx > 0.f ? 32639.f / mx : 0.f;
+      if (wn == 0 && fq == 0 && m0 + row < M) p.c_kscale[(long)(m0 + row) * nkb + n0 / 128] = mx / 32639.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float y[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        uint32_t hi, lo;
+        q2_pack4(y, inv, hi, lo);
+        char* d = smem + row * PITCH8 + wn * 128 + j * 16 + 4 * fq;
+        *(uint32_t*)d = hi;
+        *(uint32_t*)(d + 64) = lo;
+      }
+    }
+    __syncthreads();
+    char* C8 = (char*)p.C + (long)n0 * 2;
+#pragma unroll 4
+    for (int c = tid; c < BM * (BN * 2 / 16); c += NW * 64) {
+      const int row = c / (BN * 2 / 16), ch = c % (BN * 2 / 16), m = m0 + row;
+      if (m >= M) continue;
+      *(u32x4*)(C8 + (long)m * 2 * p.N + ch * 16) = *(const u32x4*)(smem + row * PITCH8 + ch * 16);
+    }
+    return;
   }
   if (p.out == OUT_SPLIT && p.c_planes == 2 && !p.rm_group && !p.addend) {
     // Split-plane output staged through LDS: the MFMA layout gives each lane 4 columns of one row
@@ -1412,8 +1517,11 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
 }  // namespace
 
 hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
-  if (g.M <= 0 || g.N % 256 || g.K % 64 || g.batch != 1 || !g.a_scale || !g.w_scale || g.cv || g.scale || g.res)
+  const bool blocks = g.a_kscale || g.out == OUT_I8K;  // block-scaled forms: 128 x 128 tiles only
+  if (g.M <= 0 || (blocks ? g.N % 128 : g.N % 256) || g.K % (g.a_kscale ? 128 : 64) || g.batch != 1 || !(g.a_scale || g.a_kscale) ||
+      !g.w_scale || g.cv || g.scale || g.res)
     return hipErrorInvalidValue;
+  if (g.out == OUT_I8K && (!g.c_kscale || g.hm_n || g.rm_group || g.addend)) return hipErrorInvalidValue;
   if (g.hm_n && (g.out != OUT_SPLIT || g.N % 64 || g.rm_group || g.M % g.hm_n)) return hipErrorInvalidValue;
   const long last_row = g.rm_group ? (long)((g.M - 1) / g.rm_group) * g.rm_stride + g.rm_off + g.rm_group : g.M;
   if (last_row * g.ldc >= (1L << 31)) return hipErrorInvalidValue;  // epilogue uses 32-bit row offsets
@@ -1444,18 +1552,20 @@ hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
   // tile's k-steps) measured 6548 and a 4-wave one-wave-per-SIMD form with fragment prefetch was
   // slower still (QKV 491 us): every form lands near 365 us for QKV (profiles/r01/v17_i8_forms.txt).
   static const int tile = getenv("ICAP_I8_TILE") ? atoi(getenv("ICAP_I8_TILE")) : 128;
-  if (tile == 128 && g.N % 128 == 0) {
+  if ((tile == 128 && g.N % 128 == 0) || blocks) {
     constexpr int lds128 = 2 * (128 * 128 + 128 * 128);
     static bool attr128 = false;
     if (!attr128) {
-      for (const void* f : {(const void*)gemm_i8_kernel<2, 0, 128>, (const void*)gemm_i8_kernel<2, 1, 128>}) {
+      for (const void* f : {(const void*)gemm_i8_kernel<2, 0, 128>, (const void*)gemm_i8_kernel<2, 1, 128>,
+                            (const void*)gemm_i8_kernel<2, 0, 128, 1>}) {
         const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds128);
         if (e != hipSuccess) return e;
       }
       attr128 = true;
     }
     const int nwg128 = (g.N / 128) * ((g.M + 127) / 128);
-    if (nomfma) hipLaunchKernelGGL((gemm_i8_kernel<2, 1, 128>), dim3(nwg128), dim3(256), lds128, s, gg);
+    if (g.a_kscale) hipLaunchKernelGGL((gemm_i8_kernel<2, 0, 128, 1>), dim3(nwg128), dim3(256), lds128, s, gg);
+    else if (nomfma) hipLaunchKernelGGL((gemm_i8_kernel<2, 1, 128>), dim3(nwg128), dim3(256), lds128, s, gg);
     else hipLaunchKernelGGL((gemm_i8_kernel<2, 0, 128>), dim3(nwg128), dim3(256), lds128, s, gg);
     return hipGetLastError();
   }

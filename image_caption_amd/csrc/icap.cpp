@@ -86,7 +86,7 @@ struct LN {
 struct VitLayer {
   LN ln1, ln2;
   Lin qkv, out, mlp0, mlp3;
-  Lin8 qkv8, mlp08;
+  Lin8 qkv8, mlp08, mlp38;
 };
 struct EncLayer {
   Lin qkv, out, lin1, lin2;
@@ -135,6 +135,7 @@ struct icap_handle {
   DecodeGraph dg[2];  // one captured loop per mode (0 greedy, 1 sample): SCST alternates them
   int ns = 2;  // activation planes (1 = bf16, 2 = hi/lo)
   bool i8 = false;  // ICAP_PREC_I8X2: LayerNorm-fed ViT GEMMs on int8 two-slice operands
+  bool i8k = false;  // ... and MLP-2 on the block-scaled int8 GELU output (ICAP_I8_MLP2=1, opt-in)
   std::vector<void*> owned;
   // decoder
   float *emb = nullptr, *pe = nullptr, *fc_w = nullptr, *fc_b = nullptr;
@@ -186,7 +187,7 @@ struct icap_handle {
   }
 
   // workspaces
-  DevBuf e_x, e_a, e_qkv, e_h, e_patch, e_sa;  // encoder (e_sa: int8 row scales)
+  DevBuf e_x, e_a, e_qkv, e_h, e_patch, e_sa, e_hs;  // encoder (e_sa: int8 row scales, e_hs: MLP block scales)
   DevBuf t_x, t_y, t_1, t_2, t_r, t_col;  // ResNet trunk (NHWC planes)
   // decoder workspaces, one set per decode mode (0: greedy / beam / teacher-forced, 1: sampled), so
   // the greedy and sampled graphs of an SCST step can replay concurrently on two streams
@@ -209,7 +210,7 @@ struct icap_handle {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col}) b->release();
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &d_beam}) b->release();
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam}) b->release();
     for (DecWS& w : dws)
       for (DevBuf* b : {&w.x, &w.a, &w.qkv, &w.q, &w.qt, &w.c, &w.o, &w.h, &w.kv, &w.fin, &w.part, &w.memp}) b->release();
   }
@@ -286,11 +287,13 @@ struct icap_handle {
     run_gemm(g, s);
   }
   // int8 two-slice GEMM: A = int8 row images [M][K/64][2][64] with row scales sa
+  // (a_kscale: A block-scaled per (row, 128-deep k block) instead of sa; out = OUT_I8K writes C as block-scaled
+  // int8 row images with their scales in c_kscale)
   void gemm8(const int8_t* A, const float* sa, const Lin8& W, int M, void* C, long ldc, long c_lo, int epi, int out,
-             hipStream_t s, int hm_n = 0) {
+             hipStream_t s, int hm_n = 0, const float* a_kscale = nullptr, float* c_kscale = nullptr) {
     GemmArgs g = gemm_args();
     g.hm_n = hm_n;
-    g.A = (const bf16_t*)A; g.a_scale = sa;
+    g.A = (const bf16_t*)A; g.a_scale = sa; g.a_kscale = a_kscale; g.c_kscale = c_kscale;
     g.W = (const bf16_t*)W.w; g.w_scale = W.sw;
     g.bias = W.b;
     g.C = C; g.ldc = ldc; g.c_lo = c_lo;
@@ -376,6 +379,7 @@ void pack(icap_handle* h, hipStream_t s) {
       if (h->i8) {
         o.qkv8 = h->lin8(L.attn.in_w, L.attn.in_b, 3 * V, V, s);
         o.mlp08 = h->lin8(L.mlp0_w, L.mlp0_b, d.vit_mlp, V, s);
+        if (h->i8k) o.mlp38 = h->lin8(L.mlp3_w, L.mlp3_b, V, d.vit_mlp, s);
       }
       h->vit.push_back(o);
     }
@@ -454,6 +458,13 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
     h->e_sa.ensure((size_t)M * 4);
     sa = h->e_sa.as<float>();
   }
+  // ICAP_I8_MLP2: the GELU output as block-scaled int8 row images [M][3072/64][2][64] (in e_h) + one scale
+  // per (row, 128-column block), the A operand of MLP-2
+  float* hs = nullptr;
+  if (h->i8k) {
+    h->e_hs.ensure((size_t)M * (d.vit_mlp / 128) * 4);
+    hs = h->e_hs.as<float>();
+  }
 
   HIPCHK(launch_im2col_patches(img, B, 3, d.image, d.patch, patch, pL, ns, s));
   {  // patch-embed GEMM: rows (b, p) -> x[b*T + 1 + p] with conv bias + pos[1 + p]
@@ -481,6 +492,11 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
     h->gemm(a, V, aL, L.out, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s);
     if (h->i8) {
       HIPCHK(launch_layernorm_i8(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, a8, sa, s));
+      if (h->i8k) {
+        h->gemm8(a8, sa, L.mlp08, M, hb, 0, 0, EPI_GELU, OUT_I8K, s, 0, nullptr, hs);
+        h->gemm8((const int8_t*)hb, nullptr, L.mlp38, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s, 0, hs);
+        continue;
+      }
       h->gemm8(a8, sa, L.mlp08, M, hb, d.vit_mlp, hL, EPI_GELU, OUT_SPLIT, s);
     } else {
       HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, aL, ns, s));
@@ -963,6 +979,11 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
       h->d = *desc;
       h->ns = desc->precision == ICAP_PREC_BF16 ? 1 : 2;
       h->i8 = desc->precision == ICAP_PREC_I8X2 && desc->kind == ICAP_KIND_VIT;
+      // measured and rejected as the default: MLP-2 fed by the block-scaled GELU output takes
+      // 1211 us (two-step fold: 256 VGPRs, 30 spilled) / 646 us (per-step fold, 64-column blocks) against
+      // 467 us for the bf16x2 form
+      const char* k8 = getenv("ICAP_I8_MLP2");
+      h->i8k = h->i8 && k8 && atoi(k8) == 1;
       if (const char* v = getenv("ICAP_DEC_BRANCHES")) h->dec_branches = std::max(1, std::min(icap_handle::MAX_BRANCHES, atoi(v)));
       pack(h, (hipStream_t)stream);
       HIPCHK(hipStreamSynchronize((hipStream_t)stream));
@@ -1190,6 +1211,22 @@ int icap_op_gemm_i8(const int8_t* A, const float* a_scale, const int8_t* W, cons
     g.A = (const bf16_t*)A; g.a_scale = a_scale; g.nsplit = 2;
     g.W = (const bf16_t*)W; g.w_scale = w_scale; g.bias = bias;
     g.C = C; g.ldc = N; g.c_lo = (long)M * N; g.hm_n = hm_n;
+    g.M = M; g.N = N; g.K = K; g.epi = epi; g.out = out;
+    HIPCHK(launch_gemm_i8(g, (hipStream_t)stream));
+  });
+}
+
+int icap_op_gemm_i8_blocks(const int8_t* A, const float* a_scale, const float* a_kscale, const int8_t* W,
+                           const float* w_scale, const float* bias, void* C, float* c_kscale, int M, int N, int K,
+                           int epi, int out, void* stream) {
+  return guarded([&] {
+    REQUIRE(out == OUT_F32 || out == OUT_F32_RESID || out == OUT_I8K, "out must be OUT_F32, OUT_F32_RESID or OUT_I8K");
+    REQUIRE((a_scale != nullptr) != (a_kscale != nullptr), "exactly one of a_scale / a_kscale");
+    REQUIRE(out != OUT_I8K || c_kscale != nullptr, "OUT_I8K needs c_kscale");
+    GemmArgs g = gemm_args();
+    g.A = (const bf16_t*)A; g.a_scale = a_scale; g.a_kscale = a_kscale; g.nsplit = 2;
+    g.W = (const bf16_t*)W; g.w_scale = w_scale; g.bias = bias;
+    g.C = C; g.ldc = N; g.c_kscale = c_kscale;
     g.M = M; g.N = N; g.K = K; g.epi = epi; g.out = out;
     HIPCHK(launch_gemm_i8(g, (hipStream_t)stream));
   });

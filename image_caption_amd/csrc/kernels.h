@@ -7,7 +7,10 @@ typedef uint16_t bf16_t;
 
 // Epilogue / output selectors shared by kernels and the host dispatcher.
 enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RELU = 2 };
-enum { OUT_F32 = 0, OUT_BF16 = 1, OUT_SPLIT = 2, OUT_F32_RESID = 3, OUT_PARTIAL = 4 };
+// OUT_I8K (launch_gemm_i8, 128 x 128 tiles only): C as int8 two-slice row images [M][N/64][2][64] with one
+// scale per (row, 128-column block) in c_kscale[M][N/128] - the operand form of a following gemm_i8 with
+// a_kscale (the GELU output of the ViT MLP feeding MLP-2)
+enum { OUT_F32 = 0, OUT_BF16 = 1, OUT_SPLIT = 2, OUT_F32_RESID = 3, OUT_PARTIAL = 4, OUT_I8K = 5 };
 
 // C[b] (+)= epi(A[b] · W[b]^T + bias[b] + addend) with A given as `nsplit` bf16 planes
 // (plane p of row r at A + p*a_lo + r*lda); W is [N][K] bf16 (nn.Linear layout).
@@ -39,6 +42,9 @@ struct GemmArgs {
   // (row stride 2K bytes; lda / ldw / a_lo unused), v = s (256 x1 + x2) with a per-row scale:
   // a_scale[M] for A, w_scale[N] for W
   const float* a_scale; const float* w_scale;
+  // block-scaled A (launch_gemm_i8, 128 x 128 tiles only): one scale per (row, 128-deep k block),
+  // a_kscale[M][K/128] instead of a_scale; c_kscale: the block scales written by out = OUT_I8K
+  const float* a_kscale; float* c_kscale;
 };
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);

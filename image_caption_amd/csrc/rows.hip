@@ -65,22 +65,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
 }
 
-// int8 two-slice quantisation (the operand form of gemm_i8_kernel): 16-bit fixed point relative to
-// the row maximum, q = rint(v / s) in [-32639, 32639], v1 = (q + 128) >> 8 in [-127, 127],
-// v2 = q - 256 v1 in [-128, 127]; four consecutive values -> one 32-bit word per slice.  Row image
-// [K/64][2][64]: the two slices of a 64-deep k block share one 128-B line, so each GEMM stage row
-// is one full-line request.
-__device__ __forceinline__ void q2_pack4(const float* y, float inv, uint32_t& hi, uint32_t& lo) {
-  hi = lo = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int qv = __float2int_rn(fminf(fmaxf(y[k] * inv, -32639.f), 32639.f));
-    const int v1 = (qv + 128) >> 8, v2 = qv - (v1 << 8);
-    hi |= (uint32_t)(v1 & 0xff) << (8 * k);
-    lo |= (uint32_t)(v2 & 0xff) << (8 * k);
-  }
-}
-
 // layernorm_kernel's row statistics, output as int8 two-slice planes + the row scale (one wave per row)
 template <int PER>
 __global__ __launch_bounds__(256) void layernorm_i8_kernel(const float* __restrict__ x, long ldx, int rows,

@@ -210,6 +210,14 @@ int icap_op_layernorm_i8(const float* x, int rows, int D, const float* w, const 
    QKV form, element (m, n) at ((m / hm_n * N/64 + n / 64) * hm_n + m % hm_n) * 64 + n % 64). */
 int icap_op_gemm_i8(const int8_t* A, const float* a_scale, const int8_t* W, const float* w_scale, const float* bias,
                     void* C, int M, int N, int K, int epi, int out, int hm_n, void* stream);
+/* Block-scaled int8 two-slice GEMM (the ViT MLP-2 pair in ICAP_PREC_I8X2; replaces the same
+ * nn.Linear products as icap_op_gemm_i8).  A as [M][K/64][2][64] row images with EITHER a_scale[M]
+ * (one scale per row) OR a_kscale[M][K/128] (one per row and 128-deep k block); out = 0 (fp32 C[M][N]),
+ * 3 (fp32 C += result: residual) or 5 (C as block-scaled int8 row images [M][N/64][2][64], scales to
+ * c_kscale[M][N/128]).  N % 128 == 0, K % 64 == 0 (K % 128 == 0 with a_kscale). */
+int icap_op_gemm_i8_blocks(const int8_t* A, const float* a_scale, const float* a_kscale, const int8_t* W,
+                           const float* w_scale, const float* bias, void* C, float* c_kscale, int M, int N, int K,
+                           int epi, int out, void* stream);
 /* qkv planes (B*N, 3*H*64) -> out planes (B*N, H*64), non-causal softmax(QK^T/8)V. */
 int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uint16_t* out, long out_lo,
                           int nsplit, void* stream);

@@ -283,3 +283,71 @@ def test_gemm_i8_split_repeat_bitwise(cuda):
         if hm:
             got = got.view(2, M // hm, N // 64, hm, 64).permute(0, 1, 3, 2, 4).reshape(2, M, N)
         assert (value(got, 2) - C.double()).abs().max().item() < 1e-5 * max(1.0, C.abs().max().item())
+
+
+def _blocks_dequant(q: torch.Tensor, ks: torch.Tensor) -> torch.Tensor:
+    """[M][N/64][2][64] int8 row images with one scale per (row, 128-column block) -> fp64 [M][N]."""
+    M = q.shape[0]
+    v = q.view(M, -1, 2, 64).double()
+    return ((256.0 * v[:, :, 0] + v[:, :, 1]) * ks.double().repeat_interleave(2, 1)[:, :, None]).reshape(M, -1)
+
+
+@pytest.mark.parametrize("M,K1,N1,N2", [(1000, 768, 3072, 768), (129, 256, 512, 128), (50432, 768, 3072, 768)])
+def test_gemm_i8_block_scaled_pair(cuda, M, K1, N1, N2):
+    """The i8x2 ViT MLP pair: MLP-1 (+ GELU) written as block-scaled int8 row images (OUT_I8K, one scale
+    per row and 128 columns), read by MLP-2 as A with a_kscale, residual-added into fp32.  Checks: the
+    block output is the fp32-output GEMM quantised to 16 bits of its block maximum; MLP-2 equals its
+    defining formula (per 64-deep step 65536 A1.W1 + 256 (A1.W2 + A2.W1), block and column scales, bias) to fp32
+    rounding and the fp64 product of the dequantised operands; full-chip launches repeat bit for bit."""
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + K1 + N1)
+    a = torch.randn(M, K1, generator=g).to(cuda)
+    w1 = (torch.randn(N1, K1, generator=g) / K1 ** 0.5).to(cuda)
+    b1 = torch.randn(N1, generator=g).to(cuda)
+    w2 = (torch.randn(N2, N1, generator=g) / N1 ** 0.5).to(cuda)
+    b2 = torch.randn(N2, generator=g).to(cuda)
+    res = torch.randn(M, N2, generator=g).to(cuda)
+    qa, sa = _pack_i8(L, lib, a)
+    qw1, sw1 = _pack_i8(L, lib, w1)
+    qw2, sw2 = _pack_i8(L, lib, w2)
+    nkb = N1 // 128
+    C1 = torch.empty(M, N1, device=cuda)
+    L.check(lib.icap_op_gemm_i8_blocks(qa.data_ptr(), sa.data_ptr(), None, qw1.data_ptr(), sw1.data_ptr(),
+                                       b1.data_ptr(), C1.data_ptr(), None, M, N1, K1, 1, 0, L.stream_ptr()), "mlp1 f32")
+    outs = []
+    for _ in range(3 if M > 10000 else 1):
+        h = torch.empty(M, 2 * N1, device=cuda, dtype=torch.int8)
+        hs = torch.empty(M, nkb, device=cuda)
+        L.check(lib.icap_op_gemm_i8_blocks(qa.data_ptr(), sa.data_ptr(), None, qw1.data_ptr(), sw1.data_ptr(),
+                                           b1.data_ptr(), h.data_ptr(), hs.data_ptr(), M, N1, K1, 1, 5,
+                                           L.stream_ptr()), "mlp1 i8k")
+        C2 = res.clone()
+        L.check(lib.icap_op_gemm_i8_blocks(h.data_ptr(), None, hs.data_ptr(), qw2.data_ptr(), sw2.data_ptr(),
+                                           b2.data_ptr(), C2.data_ptr(), None, M, N2, N1, 0, 3, L.stream_ptr()),
+                "mlp2 blocks")
+        outs.append((h, hs, C2))
+    torch.cuda.synchronize()
+    h, hs, C2 = outs[0]
+    for o in outs[1:]:
+        assert torch.equal(o[0], h) and torch.equal(o[1], hs) and torch.equal(o[2], C2)
+    rows = slice(0, M) if M <= 4096 else torch.randperm(M, generator=g)[:2048].to(cuda)
+    # block output = quantised fp32 output
+    c1 = C1[rows].double()
+    blk = c1.view(c1.shape[0], nkb, 128)
+    assert torch.allclose(hs[rows].double() * 32639, blk.abs().amax(2), rtol=1e-6, atol=0)
+    deq = _blocks_dequant(h[rows], hs[rows])
+    bound = (hs[rows].double() * (0.5 + 2 ** -7)).repeat_interleave(128, 1) + 1e-30
+    assert ((deq - c1).abs() <= bound).all(), (deq - c1).abs().max().item()
+    # MLP-2 against its defining formula and the fp64 product
+    v = h[rows].view(-1, 2 * nkb, 2, 64).double()
+    x1, x2 = v[:, :, 0], v[:, :, 1]
+    y = qw2.view(N2, 2 * nkb, 2, 64).double()
+    y1, y2 = y[:, :, 0], y[:, :, 1]
+    per = 65536.0 * torch.einsum("mbk,nbk->mbn", x1, y1) + 256.0 * (
+        torch.einsum("mbk,nbk->mbn", x1, y2) + torch.einsum("mbk,nbk->mbn", x2, y1))
+    form = (per * hs[rows].double().repeat_interleave(2, 1)[:, :, None]).sum(1) * sw2.double()[None, :] + b2.double() + res[rows].double()
+    got = C2[rows].double()
+    scale = max(1.0, form.abs().max().item())
+    assert (got - form).abs().max().item() < 2e-6 * scale
+    exact = deq @ w2.double().t() + b2.double() + res[rows].double()
+    assert (got - exact).abs().max().item() < 2e-4 * scale
