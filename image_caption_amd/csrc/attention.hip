@@ -555,13 +555,21 @@ hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int 
 // LDS: two 32-key chunk buffers x planes x 32 KiB, both in flight from the start (chunk c + 2 is
 // issued once chunk c has been consumed); 16-byte chunk c of key row k stored at c ^ (k & 15), so the
 // 16 key rows of a ds_read_b128 group hit 16 different banks.
+// KS = 2: the chunks of a row pair split over two blocks (a block walks 4 chunks instead of 7 at S = 196
+// and the launch fills twice the CUs).  Each block leaves its unnormalised context and softmax
+// statistics in xpart with agent-scope stores, waits for them to complete, and takes a ticket on the
+// pair's counter; the second block merges the two states (always in part order, so the result does
+// not depend on which block finished last), writes the output and resets the counter for the next launch.
 namespace {
 
-template <int NS>
+constexpr int XA_PART_FLOATS = 8 * 1024 + 32;  // per block: context [8][1024 threads] + m, l [16 columns]
+
+template <int NS, int KS>
 __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __restrict__ qt, long qt_lo,
                                                                const bf16_t* __restrict__ mem, long mem_lo,
                                                                int rows_per_image, int S, float scale,
-                                                               bf16_t* out, long out_lo) {
+                                                               bf16_t* out, long out_lo, float* xpart,
+                                                               int* xcnt) {
   constexpr int DM = 512, H = 8, CK = 32;        // model width, heads, keys per chunk
   constexpr int PLANE = CK * DM * 2;             // 32 KiB per plane per chunk
   constexpr int BUF = NS * PLANE;
@@ -576,14 +584,16 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
   // second row rides in the columns a single row leaves empty and the image's memory is streamed
   // once for both (beam slots, teacher-forced positions); with one row per image the odd columns
   // stay empty as before.
-  const int bpi = (rows_per_image + 1) / 2;      // blocks per image
-  const int img = blockIdx.x / bpi, pair = blockIdx.x - img * bpi;
+  const int bpi = (rows_per_image + 1) / 2;      // row pairs per image
+  const int pb = blockIdx.x / KS, part = blockIdx.x - pb * KS;
+  const int img = pb / bpi, pair = pb - img * bpi;
   const int slot = 2 * pair + (fr >> 3);         // this column's row within the image
   const bool valid = slot < rows_per_image;
   const long r = (long)img * rows_per_image + slot;
   const int hd = fr & 7;
   const bf16_t* mb = mem + (long)img * S * DM;
   const int nchunks = (S + CK - 1) / CK;
+  const int cper = (nchunks + KS - 1) / KS, c0 = part * cper, c1 = min(nchunks, c0 + cper);
 
   // q~ fragments (B operand of the scores): column (row, head), d = 64 sdg + 32 ks + 8 fq + j
   bf16x8 qh[2], ql[2];
@@ -622,13 +632,13 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
   float m_run = -INFINITY, l_run = 0.f;
   const int q4 = fr >> 2, p4 = fr & 3;
 
-  stage(0, 0);
-  if (nchunks > 1) stage(1, 1);
-  for (int c = 0; c < nchunks; ++c) {
-    if (c + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_CHUNK) : "memory");
+  stage(c0, 0);
+  if (c0 + 1 < c1) stage(c0 + 1, 1);
+  for (int c = c0; c < c1; ++c) {
+    if (c + 1 < c1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_CHUNK) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const char* cb = smem + (c & 1) * BUF;
+    const char* cb = smem + ((c - c0) & 1) * BUF;
     {  // partial scores: key tile skt, d-group sdg
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
       const int key = skt * 16 + fr;
@@ -711,10 +721,50 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
         acc[dt] = mfma16(vh, pl, acc[dt]);
       }
     }
-    if (c + 2 < nchunks) {
-      __syncthreads();  // every wave is done with buffer c & 1
-      stage(c + 2, c & 1);
+    if (c + 2 < c1) {
+      __syncthreads();  // every wave is done with buffer (c - c0) & 1
+      stage(c + 2, (c - c0) & 1);
     }
+  }
+  if (KS == 2) {
+    float* mine = xpart + ((long)pb * 2 + part) * XA_PART_FLOATS;
+    const float* other = xpart + ((long)pb * 2 + (part ^ 1)) * XA_PART_FLOATS;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        __hip_atomic_store(mine + (dt * 4 + rr) * 1024 + threadIdx.x, acc[dt][rr], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 16) {
+      __hip_atomic_store(mine + 8 * 1024 + threadIdx.x, m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(mine + 8 * 1024 + 16 + threadIdx.x, l_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores are complete
+    __syncthreads();                                   // ... and every thread's
+    int* flag = (int*)(smem + 2 * BUF + (8 * 512 + 512) * 4);  // after the score totals
+    if (threadIdx.x == 0)
+      *flag = __hip_atomic_fetch_add(xcnt + pb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag == 0) return;  // the partner block merges
+    if (threadIdx.x == 0) __hip_atomic_store(xcnt + pb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float om = __hip_atomic_load(other + 8 * 1024 + fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float ol = __hip_atomic_load(other + 8 * 1024 + 16 + fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float oa[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      oa[k] = __hip_atomic_load(other + k * 1024 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // part 0's state first whatever the arrival order
+    const float m0 = part ? om : m_run, m1 = part ? m_run : om;
+    const float l0 = part ? ol : l_run, l1 = part ? l_run : ol;
+    const float mn = fmaxf(m0, m1), f0 = __expf(m0 - mn), f1 = __expf(m1 - mn);
+    l_run = __fadd_rn(__fmul_rn(l0, f0), __fmul_rn(l1, f1));
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float x0 = part ? oa[dt * 4 + rr] : acc[dt][rr], x1 = part ? acc[dt][rr] : oa[dt * 4 + rr];
+        acc[dt][rr] = __fadd_rn(__fmul_rn(x0, f0), __fmul_rn(x1, f1));
+      }
   }
   // C^T layout: lane holds column (row, head), d = 16dt + 4fq + r (4 consecutive d) -> 8-byte stores
   if (valid) {
@@ -734,32 +784,52 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
   }
 }
 
-constexpr int XA_RED_BYTES = (8 * 512 + 512) * 4;
+constexpr int XA_RED_BYTES = (8 * 512 + 512) * 4 + 16;  // + the KS = 2 ticket
 
 }  // namespace
 
+int cross_attn_splits(int S) {
+  // opt-in (ICAP_XATTN_KS=2): 20.7 -> 18.5 us per launch, but the launch then holds every CU and the other
+  // decode chain's kernels slow down: bench 6544 -> 6404 captions/s, beam 2973 -> 2791
+  static const int ks = getenv("ICAP_XATTN_KS") ? atoi(getenv("ICAP_XATTN_KS")) : 1;
+  return ks == 2 && (S + 31) / 32 >= 4 ? 2 : 1;
+}
+
+size_t cross_attn_part_floats(int rows) { return (size_t)rows * 2 * XA_PART_FLOATS; }
+
 hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* mem, long mem_lo, int rows,
                                   int rows_per_image, int S, float scale, bf16_t* out, long out_lo, int nsplit,
-                                  hipStream_t s) {
+                                  hipStream_t s, float* xpart, int* xcnt) {
   if (S <= 0 || rows <= 0 || (nsplit != 1 && nsplit != 2)) return hipErrorInvalidValue;
+  const int ks = xpart && xcnt ? cross_attn_splits(S) : 1;
   const int lds = 2 * nsplit * 32 * 512 * 2 + XA_RED_BYTES;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)cross_attn_mfma_kernel<2>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * 32 * 512 * 2 + XA_RED_BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)cross_attn_mfma_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * 32 * 512 * 2 + XA_RED_BYTES);
-    if (e != hipSuccess) return e;
+    for (const void* f : {(const void*)cross_attn_mfma_kernel<2, 1>, (const void*)cross_attn_mfma_kernel<2, 2>}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * 2 * 32 * 512 * 2 + XA_RED_BYTES);
+      if (e != hipSuccess) return e;
+    }
+    for (const void* f : {(const void*)cross_attn_mfma_kernel<1, 1>, (const void*)cross_attn_mfma_kernel<1, 2>}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * 32 * 512 * 2 + XA_RED_BYTES);
+      if (e != hipSuccess) return e;
+    }
     attr = true;
   }
   if (rows_per_image <= 0 || rows % rows_per_image) return hipErrorInvalidValue;
-  const int blocks = rows / rows_per_image * ((rows_per_image + 1) / 2);  // two rows of an image per block
-  if (nsplit == 2)
-    hipLaunchKernelGGL(cross_attn_mfma_kernel<2>, dim3(blocks), dim3(1024), lds, s, qt, qt_lo, mem, mem_lo,
-                       rows_per_image, S, scale, out, out_lo);
-  else
-    hipLaunchKernelGGL(cross_attn_mfma_kernel<1>, dim3(blocks), dim3(1024), lds, s, qt, qt_lo, mem, mem_lo,
-                       rows_per_image, S, scale, out, out_lo);
+  const int pairs = rows / rows_per_image * ((rows_per_image + 1) / 2);  // two rows of an image per block
+  // KS = 2: xpart [pairs][2][XA_PART_FLOATS] partial states, xcnt [pairs] tickets (zero between launches)
+  float* xp = xpart;
+  int* xc = xcnt;
+#define ICAP_XA(NSV, KSV)                                                                                      \
+  hipLaunchKernelGGL((cross_attn_mfma_kernel<NSV, KSV>), dim3(pairs * KSV), dim3(1024), lds, s, qt, qt_lo, mem, \
+                     mem_lo, rows_per_image, S, scale, out, out_lo, xp, xc)
+  if (nsplit == 2) {
+    if (ks == 2) ICAP_XA(2, 2); else ICAP_XA(2, 1);
+  } else {
+    if (ks == 2) ICAP_XA(1, 2); else ICAP_XA(1, 1);
+  }
+#undef ICAP_XA
   return hipGetLastError();
 }

@@ -192,7 +192,7 @@ struct icap_handle {
   // decoder workspaces, one set per decode mode (0: greedy / beam / teacher-forced, 1: sampled), so
   // the greedy and sampled graphs of an SCST step can replay concurrently on two streams
   struct DecWS {
-    DevBuf x, a, qkv, q, qt, c, o, h, kv, fin, part, memp;
+    DevBuf x, a, qkv, q, qt, c, o, h, kv, fin, part, memp, xpart, xcnt;  // xpart / xcnt: split cross-attention
   } dws[2];
   DevBuf d_beam;
 
@@ -674,6 +674,8 @@ struct DecodeBufs {
   long aL, qL, cL, hL, memL;
   size_t kvl;  // KV-cache stride between layers (of the whole buffer)
   long PS;     // split-K slab stride (of the whole buffer)
+  float* xpart;  // split cross-attention partial states / tickets
+  int* xcnt;
 };
 
 // Rows [r0, r0 + n) of a decode buffer set (every plane / slab / layer stride stays the whole
@@ -685,6 +687,10 @@ DecodeBufs sub_bufs(const DecodeBufs& b, const icap_model_desc& d, int r0, int L
   v.qt += (size_t)r0 * H * D; v.c += (size_t)r0 * H * D; v.o += (size_t)r0 * D; v.hb += (size_t)r0 * d.dim_ff;
   v.kc += (size_t)r0 * H * Lmax * 64; v.vc += (size_t)r0 * H * Lmax * 64;
   v.part += (size_t)r0 * D; v.memp += (size_t)r0 * S * D;
+  if (v.xpart) {
+    v.xpart += cross_attn_part_floats(r0);
+    v.xcnt += r0;
+  }
   return v;
 }
 
@@ -705,11 +711,17 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   w.h.ensure((size_t)rows * d.dim_ff * 2 * ns);
   w.kv.ensure((size_t)2 * d.n_dec_layers * kv_rows * H * Lmax * 64 * 4);
   w.part.ensure((size_t)MAX_KSPLIT * rows * D * 4);
+  if (cross_attn_splits(S) > 1) w.xpart.ensure(cross_attn_part_floats(rows) * 4);
+  if (cross_attn_splits(S) > 1 && w.xcnt.n < (size_t)rows * 4) {  // tickets: zero at rest (each launch resets its own)
+    w.xcnt.ensure((size_t)rows * 4);
+    HIPCHK(hipMemset(w.xcnt.p, 0, w.xcnt.n));
+  }
   DecodeBufs b;
   b.x = w.x.as<float>(); b.a = w.a.as<bf16_t>(); b.qkv = w.qkv.as<float>();
   b.q = w.q.as<bf16_t>(); b.qt = w.qt.as<bf16_t>(); b.c = w.c.as<bf16_t>();
   b.o = w.o.as<bf16_t>(); b.hb = w.h.as<bf16_t>();
   b.kc = w.kv.as<float>();
+  b.xpart = w.xpart.as<float>(); b.xcnt = w.xcnt.as<int>();
   b.part = w.part.as<float>();
   b.vc = b.kc + (size_t)d.n_dec_layers * kv_rows * H * Lmax * 64;
   b.memp = w.memp.as<bf16_t>(); b.memL = (long)B * S * D;
@@ -758,7 +770,8 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       h->chain(c, s);
     }
     h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * ns * (double)(rows / n_new) * S * D, s, [&] {
-      HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, mem_rpi, S, 0.125f, b.c, b.cL, ns, s));
+      HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, mem_rpi, S, 0.125f, b.c, b.cL, ns, s,
+                                    b.xpart, b.xcnt));
     });
     // per head, one launch: o_h = c_h Wv_h^T + bv_h, then slab h = o_h Wo[:, h*64:(h+1)*64]^T; the
     // residual LN sums the H slabs (the output projection as a split-K over heads)

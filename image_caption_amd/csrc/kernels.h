@@ -162,9 +162,13 @@ hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int 
                                 hipStream_t s, const int32_t* anc = nullptr, const int32_t* klen = nullptr);
 // Cross-attention in the key-absorbed form on MFMA: rows hold q~_h = q_h·Wk_h (8 heads x 512) as bf16
 // planes (plane stride qt_lo); memory (images, S, 512) as bf16 planes (mem_lo); context planes out.
+// With xpart (cross_attn_part_floats(rows) floats) and xcnt (rows ints, zero at rest) the keys of
+// a row pair split over cross_attn_splits(S) blocks (opt-in: ICAP_XATTN_KS=2).
 hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* mem, long mem_lo, int rows,
                                   int rows_per_image, int S, float scale, bf16_t* out, long out_lo, int nsplit,
-                                  hipStream_t s);
+                                  hipStream_t s, float* xpart = nullptr, int* xcnt = nullptr);
+int cross_attn_splits(int S);
+size_t cross_attn_part_floats(int rows);
 // Batched beam search (beam.hip): state init, per-step selection, final pick.
 hipError_t launch_beam_init(int B, int K, int start, int Lmax, int32_t* seq_a, int32_t* seq_b, int32_t* anc_a,
                             int32_t* anc_b, float* scores, int* kcur, int* done, int* ncomp, float* best_score,
