@@ -111,6 +111,8 @@ SIGNATURES = {
                                      c_void_p]),
     "icap_op_gemm_i8": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                 c_int, c_int, c_void_p]),
+    "icap_op_gemm_tail_split": (c_int, [c_void_p, c_long, c_long, c_int, c_void_p, c_void_p, c_void_p, c_long, c_int,
+                                        c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "icap_op_gemm_i8_blocks": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_int, c_int, c_int, c_int, c_int, c_void_p]),
 }

@@ -772,7 +772,12 @@ namespace {
 // k-loop (the output-heavy, short-K trunk GEMMs).
 // KSD = 64: 64-deep stages (two MFMA k-steps): every operand row segment is a full 128-B line
 // (8 rows x 128 B per DMA instruction, chunk c of row r at c ^ (r & 7)) and half the barriers.
-template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0, int KSD = 32>
+// TS = 1: tail split (GemmArgs::split_ws): each XCD owns a contiguous range of c tiles (the XCD remap);
+// with S = split_slots block slots per XCD the last c % S tiles (a partial final round, c > S) run as
+// two blocks each, one per K half.  Both halves leave their fp32 partial tile with agent-scope stores,
+// wait for them to complete and take a ticket; the second adds the other's partial (a + b: the same
+// bits whichever finished first) and runs the epilogue.
+template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0, int KSD = 32, int TS = 0>
 __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64 ? 3 : 1)) void gemm_256_kernel(
     GemmArgs p) {
   constexpr int WGM = NW / 4;                       // wave grid WGM x 4
@@ -794,7 +799,24 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
   // XCD-aware bijective remap of the linear block id
   const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
   const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int xbase = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  int wg = xbase + (orig >> 3);
+  const int M = p.M, K = p.K;
+  const int nk = K / KS;
+  int kbeg = 0, kend = nk, part = -1, slot = 0;
+  if (TS) {  // (the launch has 8 x max(c + tail) blocks; the XCD's surplus exits)
+    const int S = p.split_slots, li = orig >> 3, cx = q + (xcd < r);
+    const int tq1 = q + 1 > S ? (q + 1) % S : 0, tq = q > S ? q % S : 0, tail = xcd < r ? tq1 : tq;
+    if (li >= cx + tail) return;
+    if (li >= cx - tail) {
+      const int v = li - (cx - tail);
+      wg = xbase + cx - tail + (v >> 1);
+      part = v & 1;
+      slot = (xcd < r ? xcd * tq1 : r * tq1 + (xcd - r) * tq) + (v >> 1);
+      kbeg = part ? nk / 2 : 0;
+      kend = part ? nk : nk / 2;
+    }
+  }
   int bm, bn;
   if (p.raster_group > 0) {  // groups of raster_group row bands, column tiles outermost inside a group
     const int G = p.raster_group, grp = wg / (G * nbn), gm = min(G, nbm - grp * G), idx = wg - grp * G * nbn;
@@ -805,8 +827,6 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
     bn = wg - bm * nbn;
   }
   const int m0 = bm * BM, n0 = bn * BN;
-  const int M = p.M, K = p.K;
-  const int nk = K / KS;
 
   // Stage image: per operand tile, rows of 64 B (32 bf16 of k); one DMA instruction = 16 rows.
   // 16-byte chunk c of row r lives at chunk c ^ sw(r), sw(r) = ((r >> 3) & 1) << 1, which makes
@@ -869,10 +889,10 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
   const int foff = fr * 64 + ((fq ^ (((fr >> 3) & 1) << 1)) << 4);
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
-    if (s < nk) stage(s, s);
-  for (int kt = 0; kt < nk; ++kt) {
+    if (kbeg + s < kend) stage(kbeg + s, s);
+  for (int kt = kbeg; kt < kend; ++kt) {
     // stage kt must have landed for every wave: leave the younger prefetched stages in flight
-    const int younger = min(NSTAGE - 2, nk - 1 - kt);
+    const int younger = min(NSTAGE - 2, kend - 1 - kt);
     // lgkmcnt(0): this wave's LDS reads of the previous step must be done before the barrier that
     // lets other waves' DMA overwrite that buffer (a 2-stage ring refills it one step later)
     if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * PER_STAGE) : "memory");
@@ -880,8 +900,8 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // refill the buffer read in iteration kt-1 (every wave has passed this barrier)
-    if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
-    const char* s0 = smem + (kt % NSTAGE) * STAGE;
+    if (kt + NSTAGE - 1 < kend) stage(kt + NSTAGE - 1, (kt - kbeg + NSTAGE - 1) % NSTAGE);
+    const char* s0 = smem + ((kt - kbeg) % NSTAGE) * STAGE;
     if (NOMFMA >= 2) continue;
     if constexpr (KS == 64) {
 #pragma unroll
@@ -920,6 +940,33 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
     }
   }
 
+  if (TS && part >= 0) {
+    constexpr int NT = NW * 64, NE = TM * TN * 4;
+    float* mine = p.split_ws + ((long)slot * 2 + part) * NE * NT;
+    const float* other = p.split_ws + ((long)slot * 2 + (part ^ 1)) * NE * NT;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          __hip_atomic_store(mine + ((i * TN + j) * 4 + e) * NT + tid, acc[i][j][e], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial is complete
+    __syncthreads();                                   // ... every thread's (and every ring read)
+    if (tid == 0) *(int*)smem = __hip_atomic_fetch_add(p.split_cnt + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*(volatile int*)smem == 0) return;  // the other half finishes the tile
+    if (tid == 0) __hip_atomic_store(p.split_cnt + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc[i][j][e] += __hip_atomic_load(other + ((i * TN + j) * 4 + e) * NT + tid, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+  }
   epilogue_256<TM, TN>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
 }
 
@@ -1161,6 +1208,16 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
     constexpr int ldsh = 2 * (2 * 128 * 32 * 2 + 256 * 32 * 2), ldsh1 = 2 * (128 * 32 * 2 + 256 * 32 * 2);
     if (g.cv && g.cv != 1) return hipErrorInvalidValue;
+    const int S = g.split_slots, q = nwgh >> 3;
+    if (g.split_ws && g.split_cnt && S > 0 && !g.cv && q + 1 > S && (g.K / 32) % 2 == 0) {
+      const int tq1 = (q + 1) % S, tq = q > S ? q % S : 0;
+      const int per_xcd = std::max(q + 1 + tq1, q + tq);
+      if (g.nsplit == 2)
+        hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 0, 128, 2, 32, 1>), dim3(8 * per_xcd), dim3(512), ldsh, s, g);
+      else
+        hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 1>), dim3(8 * per_xcd), dim3(512), ldsh1, s, g);
+      return hipGetLastError();
+    }
     if (g.nsplit == 2) {
       if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 1, 128, 2>), dim3(nwgh), dim3(512), ldsh, s, g);
       else hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 0, 128, 2>), dim3(nwgh), dim3(512), ldsh, s, g);

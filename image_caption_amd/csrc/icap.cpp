@@ -187,6 +187,8 @@ struct icap_handle {
   }
 
   // workspaces
+  DevBuf e_split, e_scnt;  // GEMM tail split: partial tiles + tickets (zero at rest)
+  int split_slots = -1;     // block slots per XCD of the 128 x 256 GEMM (2 per CU); 0 = tail split off
   DevBuf e_x, e_a, e_qkv, e_h, e_patch, e_sa, e_hs;  // encoder (e_sa: int8 row scales, e_hs: MLP block scales)
   DevBuf t_x, t_y, t_1, t_2, t_r, t_col;  // ResNet trunk (NHWC planes)
   // decoder workspaces, one set per decode mode (0: greedy / beam / teacher-forced, 1: sampled), so
@@ -210,7 +212,7 @@ struct icap_handle {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col}) b->release();
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam}) b->release();
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt}) b->release();
     for (DecWS& w : dws)
       for (DevBuf* b : {&w.x, &w.a, &w.qkv, &w.q, &w.qt, &w.c, &w.o, &w.h, &w.kv, &w.fin, &w.part, &w.memp}) b->release();
   }
@@ -284,7 +286,28 @@ struct icap_handle {
     g.C = C; g.ldc = ldc; g.c_lo = c_lo;
     g.M = M; g.N = W.N; g.K = W.K; g.nsplit = ns; g.c_planes = ns;
     g.epi = epi; g.out = out;
+    if (out == OUT_F32_RESID) tail_split(g);
     run_gemm(g, s);
+  }
+  // residual-output GEMMs (N = 768 / 512: a partial last round of tiles) split their tail tiles in K when
+  // ICAP_GEMM_TAIL=1 (opt-in: measured 344 -> 363 us per launch, bench 6564 -> 6495 captions/s, DESIGN.md
+  // §5); the workspace is allocated on first use, outside any capture
+  void tail_split(GemmArgs& g) {
+    if (split_slots < 0) {
+      const char* v = getenv("ICAP_GEMM_TAIL");
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 0;
+      split_slots = !(v && atoi(v) == 1) || cus < 8 ? 0 : 2 * cus / 8;
+      if (split_slots) {
+        e_split.ensure(gemm_split_ws_bytes(split_slots));
+        e_scnt.ensure((size_t)8 * split_slots * 4);
+        HIPCHK(hipMemset(e_scnt.p, 0, e_scnt.n));
+      }
+    }
+    if (!split_slots) return;
+    g.split_ws = e_split.as<float>();
+    g.split_cnt = e_scnt.as<int>();
+    g.split_slots = split_slots;
   }
   // int8 two-slice GEMM: A = int8 row images [M][K/64][2][64] with row scales sa
   // (a_kscale: A block-scaled per (row, 128-deep k block) instead of sa; out = OUT_I8K writes C as block-scaled
@@ -1195,6 +1218,21 @@ int icap_op_gemm(const uint16_t* A, long lda, long a_lo, int nsplit, const uint1
     g.W = W; g.ldw = K; g.bias = bias;
     g.C = C; g.ldc = ldc; g.c_lo = c_lo;
     g.M = M; g.N = N; g.K = K; g.epi = epi; g.out = out;
+    HIPCHK(launch_gemm(g, (hipStream_t)stream));
+  });
+}
+
+int icap_op_gemm_tail_split(const uint16_t* A, long lda, long a_lo, int nsplit, const uint16_t* W, const float* bias,
+                            float* C, long ldc, int M, int N, int K, int split_slots, float* ws, int* cnt,
+                            void* stream) {
+  return guarded([&] {
+    REQUIRE(split_slots > 0 && ws && cnt, "split_slots, ws and cnt are required");
+    GemmArgs g = gemm_args();
+    g.A = A; g.lda = lda; g.a_lo = a_lo; g.nsplit = nsplit;
+    g.W = W; g.ldw = K; g.bias = bias;
+    g.C = C; g.ldc = ldc;
+    g.M = M; g.N = N; g.K = K; g.epi = EPI_NONE; g.out = OUT_F32_RESID;
+    g.split_ws = ws; g.split_cnt = cnt; g.split_slots = split_slots;
     HIPCHK(launch_gemm(g, (hipStream_t)stream));
   });
 }

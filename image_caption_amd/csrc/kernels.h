@@ -45,7 +45,13 @@ struct GemmArgs {
   // block-scaled A (launch_gemm_i8, 128 x 128 tiles only): one scale per (row, 128-deep k block),
   // a_kscale[M][K/128] instead of a_scale; c_kscale: the block scales written by out = OUT_I8K
   const float* a_kscale; float* c_kscale;
+  // tail split (launch_gemm_256, 128 x 256 tiles, no convolution): per XCD, the tiles of the last partial
+  // round of split_slots block slots run as two K halves merged by the second finisher; split_ws holds
+  // 2 x 128 x 256 fp32 partials per split tile (8 x split_slots tiles), split_cnt its tickets (zero at rest)
+  float* split_ws; int* split_cnt; int split_slots;
 };
+// bytes of split_ws for split_slots block slots per XCD
+inline size_t gemm_split_ws_bytes(int split_slots) { return (size_t)8 * split_slots * 2 * 128 * 256 * 4; }
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
 // Which kernel launch_gemm picks (PROF_GEMM_256 / PROF_GEMM_128 / PROF_GEMM_64).

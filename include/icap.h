@@ -210,6 +210,13 @@ int icap_op_layernorm_i8(const float* x, int rows, int D, const float* w, const 
    QKV form, element (m, n) at ((m / hm_n * N/64 + n / 64) * hm_n + m % hm_n) * 64 + n % 64). */
 int icap_op_gemm_i8(const int8_t* A, const float* a_scale, const int8_t* W, const float* w_scale, const float* bias,
                     void* C, int M, int N, int K, int epi, int out, int hm_n, void* stream);
+/* The residual encoder GEMM (C += A.W^T + bias, fp32 C; the out-projection / MLP-2 products of the ViT
+ * and Grid encoder layers) with its tail split: per XCD, the tiles of the last partial round of
+ * split_slots block slots run as two K halves.  ws: 8 * split_slots * 2 * 128 * 256 floats, cnt:
+ * 8 * split_slots ints, zero on entry and on return. */
+int icap_op_gemm_tail_split(const uint16_t* A, long lda, long a_lo, int nsplit, const uint16_t* W, const float* bias,
+                            float* C, long ldc, int M, int N, int K, int split_slots, float* ws, int* cnt,
+                            void* stream);
 /* Block-scaled int8 two-slice GEMM (the ViT MLP-2 pair in ICAP_PREC_I8X2; replaces the same
  * nn.Linear products as icap_op_gemm_i8).  A as [M][K/64][2][64] row images with EITHER a_scale[M]
  * (one scale per row) OR a_kscale[M][K/128] (one per row and 128-deep k block); out = 0 (fp32 C[M][N]),

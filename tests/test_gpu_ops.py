@@ -351,3 +351,36 @@ def test_gemm_i8_block_scaled_pair(cuda, M, K1, N1, N2):
     assert (got - form).abs().max().item() < 2e-6 * scale
     exact = deq @ w2.double().t() + b2.double() + res[rows].double()
     assert (got - exact).abs().max().item() < 2e-4 * scale
+
+
+@pytest.mark.parametrize("M,N,K,slots", [(50432, 768, 3072, 64), (50432, 768, 768, 64), (50432, 768, 768, 16),
+                                         (12544, 512, 2048, 8)])
+def test_gemm_tail_split(cuda, M, N, K, slots):
+    """The residual encoder GEMM with its last partial round split in K over two blocks per tile (merged by
+    the second finisher through agent-scope stores and a ticket): equal to the unsplit launch up to the
+    fp32 rounding of the two half sums, bit-identical over repeated launches, tickets back at zero."""
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + slots)
+    A = torch.randn(2, M, K, generator=g).to(cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(M, N, generator=g).to(cuda)
+    ref = R.clone()
+    L.check(lib.icap_op_gemm(A.data_ptr(), K, M * K, 2, w.data_ptr(), bias.data_ptr(), ref.data_ptr(), N, 0,
+                             M, N, K, 0, 3, L.stream_ptr()), "gemm resid")
+    ws = torch.empty(8 * slots * 2 * 128 * 256, device=cuda)
+    cnt = torch.zeros(8 * slots, device=cuda, dtype=torch.int32)
+    outs = []
+    for _ in range(4):
+        C = R.clone()
+        L.check(lib.icap_op_gemm_tail_split(A.data_ptr(), K, M * K, 2, w.data_ptr(), bias.data_ptr(), C.data_ptr(), N,
+                                            M, N, K, slots, ws.data_ptr(), cnt.data_ptr(), L.stream_ptr()), "split")
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, outs[0]) for o in outs[1:])
+    assert int(cnt.abs().sum().item()) == 0
+    assert (outs[0] - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())
+    # and the split really ran: a few tail tiles differ from the unsplit sums in their last bits
+    tiles = (N // 256) * ((M + 127) // 128)
+    if (tiles // 8 + 1) > slots:
+        assert not torch.equal(outs[0], ref)
