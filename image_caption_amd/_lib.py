@@ -77,6 +77,7 @@ class ModelDesc(ctypes.Structure):
 # name -> (restype, argtypes); exactly the entry points include/icap.h declares
 SIGNATURES = {
     "icap_abi_version": (c_int, []),
+    "icap_tools_build": (c_int, []),
     "icap_last_error": (ctypes.c_char_p, []),
     "icap_create": (c_int, [POINTER(ModelDesc), c_void_p, POINTER(c_void_p)]),
     "icap_destroy": (c_int, [c_void_p]),
@@ -96,6 +97,7 @@ SIGNATURES = {
     "icap_decoder_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                      c_void_p, c_void_p]),
     "icap_set_graphs": (c_int, [c_void_p, c_int]),
+    "icap_set_decode_chains": (c_int, [c_void_p, c_int]),
     "icap_profile_enable": (c_int, [c_void_p, c_int]),
     "icap_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(c_long),
                                   POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),

@@ -15,16 +15,23 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-u
          "-Wno-unused-variable", "-munsafe-fp-atomics"]
 
 
-def _stale() -> bool:
+FLAVOR = HERE / "build" / "flavor"
+
+
+def _stale(tools: bool = False) -> bool:
     if not LIB.exists():
+        return True
+    if not FLAVOR.exists() or FLAVOR.read_text().strip() != ("tools" if tools else "product"):
         return True
     t = LIB.stat().st_mtime
     deps = [CSRC / s for s in SOURCES] + list(CSRC.glob("*.h")) + [HERE.parent / "include" / "icap.h"]
     return any(p.stat().st_mtime > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = True) -> Path:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = True, tools: bool = False) -> Path:
+    """Product build by default.  tools=True adds -DICAP_TOOLS: the ICAP_* measurement knobs are read
+    from the environment and the measured-and-rejected kernel variants are compiled in (tools/*.sh)."""
+    if not force and not _stale(tools):
         return LIB
     objs = []
     obj_dir = HERE / "build"
@@ -33,7 +40,7 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     for src in SOURCES:
         obj = obj_dir / (src + ".o")
         objs.append(obj)
-        cmd = [HIPCC, *FLAGS, "-x", "hip", "-c", str(CSRC / src), "-o", str(obj)]
+        cmd = [HIPCC, *FLAGS, *(["-DICAP_TOOLS"] if tools else []), "-x", "hip", "-c", str(CSRC / src), "-o", str(obj)]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     for cmd, p in procs:
         out, _ = p.communicate()
@@ -46,8 +53,9 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    FLAVOR.write_text("tools" if tools else "product")
     return LIB
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    print(build(force="--force" in sys.argv or "--tools" in sys.argv, tools="--tools" in sys.argv))

@@ -501,16 +501,9 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
     return nsplit == 2 ? run_enc<4, true>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s)
                        : run_enc<4, false>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s);
   }
-  static int pipe = -1;  // ICAP_ENC_ATTN_PIPE=0 selects the stage-everything form for N > 64
-  if (pipe < 0) {
-    const char* v = getenv("ICAP_ENC_ATTN_PIPE");
-    pipe = v ? atoi(v) : 1;
-  }
-  static int qpw = 0;  // ICAP_ENC_ATTN_QPW: query tiles per wave (1: 16 waves, 2: 8 waves, 2 blocks/CU)
-  if (!qpw) {
-    const char* v = getenv("ICAP_ENC_ATTN_QPW");
-    qpw = v && atoi(v) == 2 ? 2 : 1;
-  }
+  static const int pipe = icap_knob("ICAP_ENC_ATTN_PIPE", 1);  // 0: the stage-everything form for N > 64
+  // ICAP_ENC_ATTN_QPW: query tiles per wave (1: 16 waves, 2: 8 waves, 2 blocks/CU)
+  static const int qpw = icap_knob("ICAP_ENC_ATTN_QPW", 1) == 2 ? 2 : 1;
   if ((pipe || head_major) && N <= 256) {  // 16 query tiles
     const int lds = 4 * (nsplit == 2 ? 4 : 2) * 32 * 128;
     const dim3 gr(H, B), bl(1024 / qpw);
@@ -791,8 +784,13 @@ constexpr int XA_RED_BYTES = (8 * 512 + 512) * 4 + 16;  // + the KS = 2 ticket
 int cross_attn_splits(int S) {
   // opt-in (ICAP_XATTN_KS=2): 20.7 -> 18.5 us per launch, but the launch then holds every CU and the other
   // decode chain's kernels slow down: bench 6544 -> 6404 captions/s, beam 2973 -> 2791
-  static const int ks = getenv("ICAP_XATTN_KS") ? atoi(getenv("ICAP_XATTN_KS")) : 1;
+#ifdef ICAP_TOOLS
+  static const int ks = icap_knob("ICAP_XATTN_KS", 1);
   return ks == 2 && (S + 31) / 32 >= 4 ? 2 : 1;
+#else
+  (void)S;
+  return 1;
+#endif
 }
 
 size_t cross_attn_part_floats(int rows) { return (size_t)rows * 2 * XA_PART_FLOATS; }
@@ -805,12 +803,20 @@ hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* me
   const int lds = 2 * nsplit * 32 * 512 * 2 + XA_RED_BYTES;
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)cross_attn_mfma_kernel<2, 1>, (const void*)cross_attn_mfma_kernel<2, 2>}) {
+    for (const void* f : {(const void*)cross_attn_mfma_kernel<2, 1>
+#ifdef ICAP_TOOLS
+                          , (const void*)cross_attn_mfma_kernel<2, 2>
+#endif
+         }) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * 2 * 32 * 512 * 2 + XA_RED_BYTES);
       if (e != hipSuccess) return e;
     }
-    for (const void* f : {(const void*)cross_attn_mfma_kernel<1, 1>, (const void*)cross_attn_mfma_kernel<1, 2>}) {
+    for (const void* f : {(const void*)cross_attn_mfma_kernel<1, 1>
+#ifdef ICAP_TOOLS
+                          , (const void*)cross_attn_mfma_kernel<1, 2>
+#endif
+         }) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * 32 * 512 * 2 + XA_RED_BYTES);
       if (e != hipSuccess) return e;
@@ -825,11 +831,14 @@ hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* me
 #define ICAP_XA(NSV, KSV)                                                                                      \
   hipLaunchKernelGGL((cross_attn_mfma_kernel<NSV, KSV>), dim3(pairs * KSV), dim3(1024), lds, s, qt, qt_lo, mem, \
                      mem_lo, rows_per_image, S, scale, out, out_lo, xp, xc)
-  if (nsplit == 2) {
-    if (ks == 2) ICAP_XA(2, 2); else ICAP_XA(2, 1);
-  } else {
-    if (ks == 2) ICAP_XA(1, 2); else ICAP_XA(1, 1);
+#ifdef ICAP_TOOLS
+  if (ks == 2) {
+    if (nsplit == 2) ICAP_XA(2, 2); else ICAP_XA(1, 2);
+    return hipGetLastError();
   }
+#endif
+  (void)ks;
+  if (nsplit == 2) ICAP_XA(2, 1); else ICAP_XA(1, 1);
 #undef ICAP_XA
   return hipGetLastError();
 }

@@ -192,11 +192,7 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 int gemm_tile_class(const GemmArgs& g) {
-  static int force = -1;  // measurement knob for the trunk convolutions (GEMMs with a BN scale)
-  if (force < 0) {
-    const char* v = getenv("ICAP_CONV_CLASS");
-    force = v ? atoi(v) : 0;
-  }
+  static const int force = icap_knob("ICAP_CONV_CLASS", 0);  // trunk convolutions (GEMMs with a BN scale)
   if (force && g.scale) {
     if (force == 256 && g.N % 256 == 0 && g.batch == 1) return PROF_GEMM_256;
     if (force == 128 && g.N % 128 == 0) return PROF_GEMM_128;
@@ -1121,11 +1117,8 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs p) {
 
 hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s);
 hipError_t launch_gemm_256(const GemmArgs& g0, hipStream_t s) {
-  static int group = -1;  // ICAP_GEMM_GROUP: tile raster of the bf16 encoder GEMM (0 = row-band major)
-  if (group < 0) {
-    const char* v = getenv("ICAP_GEMM_GROUP");
-    group = v ? std::max(0, atoi(v)) : 0;
-  }
+  // ICAP_GEMM_GROUP: tile raster of the bf16 encoder GEMM (0 = row-band major)
+  static const int group = std::max(0, icap_knob("ICAP_GEMM_GROUP", 0));
   GemmArgs g = g0;
   if (!g.raster_group) g.raster_group = group;
   return launch_gemm_256_(g, s);
@@ -1138,16 +1131,19 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
   constexpr int lds2 = 3 * 3 * 256 * 32 * 2, lds1 = 4 * 2 * 256 * 32 * 2;
   static int nw = 0;
   if (!nw) {
-    const char* v = getenv("ICAP_GEMM256_WAVES");  // experiment knob: 8, 16, or 0 = 8-phase kernel
-    nw = v ? atoi(v) : 16;
+    nw = icap_knob("ICAP_GEMM256_WAVES", 16);  // experiment knob: 8, 16, or 1/2 = 8-phase kernel
     if (nw != 8 && nw != 16 && nw != 1 && nw != 2 && nw != 160 && nw != 161 && nw != 162) nw = 16;
+    hipError_t e = hipSuccess;
+#ifdef ICAP_TOOLS
     for (const void* f : {(const void*)gemm_8ph_kernel<false>, (const void*)gemm_8ph_kernel<true>})
       if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 131072) != hipSuccess)
         return hipErrorInvalidValue;
-    hipError_t e = hipSuccess;
+    for (const void* f : {(const void*)gemm_256_kernel<2, 16, 1>, (const void*)gemm_256_kernel<2, 16, 2>,
+                          (const void*)gemm_256_kernel<2, 16, 3>})
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
+#endif
     for (const void* f : {(const void*)gemm_256_kernel<2, 8>, (const void*)gemm_256_kernel<2, 16>,
-                          (const void*)gemm_256_kernel<2, 16, 1>, (const void*)gemm_256_kernel<2, 16, 2>,
-                          (const void*)gemm_256_kernel<2, 16, 3>, (const void*)gemm_256_kernel<2, 16, 0, 1>})
+                          (const void*)gemm_256_kernel<2, 16, 0, 1>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
     for (const void* f : {(const void*)gemm_256_kernel<1, 8>, (const void*)gemm_256_kernel<1, 16>,
                           (const void*)gemm_256_kernel<1, 16, 0, 1>})
@@ -1157,16 +1153,9 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
   // 128 x 256 tiles, 2-stage ring, 2 blocks per CU for K >= ICAP_GEMM_TALL_MIN_K (default 128; 0 = off):
   // ViT 42.9 -> 41.8 ms/step (MLP-out's 591 tiles become 1182: 4.6 instead of 2.3 rounds), trunk
   // conv3 203 -> 177 us; at K = 64 the 3-stage 256 x 256 ring stays ahead (tools/halfk_sweep.sh)
-  static int tall_min_k = -1;
-  if (tall_min_k < 0) {
-    const char* v = getenv("ICAP_GEMM_TALL_MIN_K");
-    tall_min_k = v ? atoi(v) : 128;
-  }
-  static int tall_bm = 0;  // ICAP_GEMM_TALL_BM: 128 (default) or 64 (64 x 256 tiles, 4 waves, 3 blocks per CU)
-  if (!tall_bm) {
-    const char* v = getenv("ICAP_GEMM_TALL_BM");
-    tall_bm = v && atoi(v) == 64 ? 64 : 128;
-  }
+  static const int tall_min_k = icap_knob("ICAP_GEMM_TALL_MIN_K", 128);
+  // ICAP_GEMM_TALL_BM: 128 (default) or 64 (64 x 256 tiles, 4 waves, 3 blocks per CU)
+  static const int tall_bm = icap_knob("ICAP_GEMM_TALL_BM", 128) == 64 ? 64 : 128;
   if (tall_min_k && g.K >= tall_min_k && (nw == 8 || nw == 16) && tall_bm == 64 && !g.cv) {
     const int nwgq = (g.N / 256) * ((g.M + 63) / 64);
     constexpr int ldsq = 2 * (2 * 64 * 32 * 2 + 256 * 32 * 2), ldsq1 = 2 * (64 * 32 * 2 + 256 * 32 * 2);
@@ -1174,11 +1163,8 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     else hipLaunchKernelGGL((gemm_256_kernel<1, 4, 0, 0, 64, 2>), dim3(nwgq), dim3(256), ldsq1, s, g);
     return hipGetLastError();
   }
-  static int tall_ks = 0;  // ICAP_GEMM_TALL_KS: 32 (default) or 64 (64-deep stages, 128 KiB, 1 block per CU)
-  if (!tall_ks) {
-    const char* v = getenv("ICAP_GEMM_TALL_KS");
-    tall_ks = v && atoi(v) == 64 ? 64 : 32;
-  }
+  // ICAP_GEMM_TALL_KS: 32 (default) or 64 (64-deep stages, 128 KiB, 1 block per CU)
+  static const int tall_ks = icap_knob("ICAP_GEMM_TALL_KS", 32) == 64 ? 64 : 32;
   if (tall_min_k && g.K >= tall_min_k && (nw == 8 || nw == 16) && tall_ks == 64 && g.K % 64 == 0) {
     const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
     constexpr int lds64 = 2 * (2 * 128 * 64 * 2 + 256 * 64 * 2), lds64_1 = 2 * (128 * 64 * 2 + 256 * 64 * 2);
@@ -1208,6 +1194,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
     constexpr int ldsh = 2 * (2 * 128 * 32 * 2 + 256 * 32 * 2), ldsh1 = 2 * (128 * 32 * 2 + 256 * 32 * 2);
     if (g.cv && g.cv != 1) return hipErrorInvalidValue;
+#ifdef ICAP_TOOLS  // tail split of the residual GEMMs: measured and rejected
     const int S = g.split_slots, q = nwgh >> 3;
     if (g.split_ws && g.split_cnt && S > 0 && !g.cv && q + 1 > S && (g.K / 32) % 2 == 0) {
       const int tq1 = (q + 1) % S, tq = q > S ? q % S : 0;
@@ -1218,6 +1205,9 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
         hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 1>), dim3(8 * per_xcd), dim3(512), ldsh1, s, g);
       return hipGetLastError();
     }
+#else
+    if (g.split_slots) return hipErrorNotSupported;
+#endif
     if (g.nsplit == 2) {
       if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 1, 128, 2>), dim3(nwgh), dim3(512), ldsh, s, g);
       else hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 0, 128, 2>), dim3(nwgh), dim3(512), ldsh, s, g);
@@ -1235,6 +1225,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     else hipLaunchKernelGGL((gemm_256_kernel<1, 16, 0, 1>), dim3(nwg), dim3(1024), lds1, s, g2);
     return hipGetLastError();
   }
+#ifdef ICAP_TOOLS  // measured-and-rejected forms: the 8-phase kernel, staging-only variants (wrong results)
   if ((nw == 1 || nw == 2) && g.K % 64 == 0) {
     if (nw == 2) hipLaunchKernelGGL(gemm_8ph_kernel<true>, dim3(nwg), dim3(512), 131072, s, g);
     else hipLaunchKernelGGL(gemm_8ph_kernel<false>, dim3(nwg), dim3(512), 131072, s, g);
@@ -1246,6 +1237,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     else hipLaunchKernelGGL((gemm_256_kernel<2, 16, 3>), dim3(nwg), dim3(1024), lds2, s, g2);
     return hipGetLastError();
   }
+#endif
   if (g.nsplit == 2) {
     if (nw == 16) hipLaunchKernelGGL((gemm_256_kernel<2, 16>), dim3(nwg), dim3(1024), lds2, s, g2);
     else hipLaunchKernelGGL((gemm_256_kernel<2, 8>), dim3(nwg), dim3(512), lds2, s, g2);
@@ -1575,6 +1567,9 @@ __global__ __launch_bounds__(BNT * 2, BNT == 256 ? 1 : 2) void gemm_i8_kernel(Ge
 
 hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
   const bool blocks = g.a_kscale || g.out == OUT_I8K;  // block-scaled forms: 128 x 128 tiles only
+#ifndef ICAP_TOOLS
+  if (blocks) return hipErrorNotSupported;  // measured and rejected: tools build only
+#endif
   if (g.M <= 0 || (blocks ? g.N % 128 : g.N % 256) || g.K % (g.a_kscale ? 128 : 64) || g.batch != 1 || !(g.a_scale || g.a_kscale) ||
       !g.w_scale || g.cv || g.scale || g.res)
     return hipErrorInvalidValue;
@@ -1585,21 +1580,21 @@ hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
   constexpr int NST = 3, lds = NST * (128 * 128 + 256 * 128);
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)gemm_i8_kernel<NST>, (const void*)gemm_i8_kernel<NST, 1>,
-                          (const void*)gemm_i8_kernel<NST, 2>}) {
+    for (const void* f : {(const void*)gemm_i8_kernel<NST>
+#ifdef ICAP_TOOLS
+                          , (const void*)gemm_i8_kernel<NST, 1>, (const void*)gemm_i8_kernel<NST, 2>
+#endif
+         }) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       if (e != hipSuccess) return e;
     }
     attr = true;
   }
-  static const int nomfma = getenv("ICAP_I8_NOMFMA") ? atoi(getenv("ICAP_I8_NOMFMA")) : 0;
+  static const int nomfma = icap_knob("ICAP_I8_NOMFMA", 0);  // staging-only measurement variants (wrong results)
   const int nwg = (g.N / 256) * ((g.M + 127) / 128);
-  static int group = -1;  // ICAP_I8_GROUP: tile raster (0 = row-band major; 16: qkv 373 -> 338 us, mlp0 525 -> 459)
-  if (group < 0) {
-    const char* v = getenv("ICAP_I8_GROUP");
-    group = v ? std::max(0, atoi(v)) : 16;
-  }
-  static const int nt = getenv("ICAP_I8_NT_STORE") ? atoi(getenv("ICAP_I8_NT_STORE")) : 0;
+  // ICAP_I8_GROUP: tile raster (0 = row-band major; 16: qkv 373 -> 338 us, mlp0 525 -> 459)
+  static const int group = std::max(0, icap_knob("ICAP_I8_GROUP", 16));
+  static const int nt = icap_knob("ICAP_I8_NT_STORE", 0);
   GemmArgs gg = g;
   gg.raster_group = group;
   gg.nt_store = nt;
@@ -1608,26 +1603,35 @@ hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s) {
   // a persistent 128 x 256 form (ring prefetch across tile seams, stores drained under the next
   // tile's k-steps) measured 6548 and a 4-wave one-wave-per-SIMD form with fragment prefetch was
   // slower still (QKV 491 us): every form lands near 365 us for QKV (profiles/r01/v17_i8_forms.txt).
-  static const int tile = getenv("ICAP_I8_TILE") ? atoi(getenv("ICAP_I8_TILE")) : 128;
+  static const int tile = icap_knob("ICAP_I8_TILE", 128);
   if ((tile == 128 && g.N % 128 == 0) || blocks) {
     constexpr int lds128 = 2 * (128 * 128 + 128 * 128);
     static bool attr128 = false;
     if (!attr128) {
-      for (const void* f : {(const void*)gemm_i8_kernel<2, 0, 128>, (const void*)gemm_i8_kernel<2, 1, 128>,
-                            (const void*)gemm_i8_kernel<2, 0, 128, 1>}) {
+      for (const void* f : {(const void*)gemm_i8_kernel<2, 0, 128>
+#ifdef ICAP_TOOLS
+                            , (const void*)gemm_i8_kernel<2, 1, 128>, (const void*)gemm_i8_kernel<2, 0, 128, 1>
+#endif
+           }) {
         const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds128);
         if (e != hipSuccess) return e;
       }
       attr128 = true;
     }
     const int nwg128 = (g.N / 128) * ((g.M + 127) / 128);
+#ifdef ICAP_TOOLS
     if (g.a_kscale) hipLaunchKernelGGL((gemm_i8_kernel<2, 0, 128, 1>), dim3(nwg128), dim3(256), lds128, s, gg);
     else if (nomfma) hipLaunchKernelGGL((gemm_i8_kernel<2, 1, 128>), dim3(nwg128), dim3(256), lds128, s, gg);
-    else hipLaunchKernelGGL((gemm_i8_kernel<2, 0, 128>), dim3(nwg128), dim3(256), lds128, s, gg);
+    else
+#endif
+      hipLaunchKernelGGL((gemm_i8_kernel<2, 0, 128>), dim3(nwg128), dim3(256), lds128, s, gg);
     return hipGetLastError();
   }
+#ifdef ICAP_TOOLS
   if (nomfma == 2) hipLaunchKernelGGL((gemm_i8_kernel<NST, 2>), dim3(nwg), dim3(512), lds, s, gg);
   else if (nomfma) hipLaunchKernelGGL((gemm_i8_kernel<NST, 1>), dim3(nwg), dim3(512), lds, s, gg);
-  else hipLaunchKernelGGL((gemm_i8_kernel<NST>), dim3(nwg), dim3(512), lds, s, gg);
+  else
+#endif
+    hipLaunchKernelGGL((gemm_i8_kernel<NST>), dim3(nwg), dim3(512), lds, s, gg);
   return hipGetLastError();
 }

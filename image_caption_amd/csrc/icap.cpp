@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <stdexcept>
@@ -58,7 +59,7 @@ struct DevBuf {
     n = 0;
     HIPCHK(hipMalloc(&p, bytes));
     n = bytes;
-    static const bool poison = getenv("ICAP_POISON") && atoi(getenv("ICAP_POISON"));
+    static const bool poison = icap_knob("ICAP_POISON", 0) != 0;
     if (poison) HIPCHK(hipMemset(p, 0xFF, bytes));  // debug: NaN in fp32 and bf16 - exposes reads of unwritten workspace
   }
   void release() {
@@ -286,7 +287,9 @@ struct icap_handle {
     g.C = C; g.ldc = ldc; g.c_lo = c_lo;
     g.M = M; g.N = W.N; g.K = W.K; g.nsplit = ns; g.c_planes = ns;
     g.epi = epi; g.out = out;
+#ifdef ICAP_TOOLS
     if (out == OUT_F32_RESID) tail_split(g);
+#endif
     run_gemm(g, s);
   }
   // residual-output GEMMs (N = 768 / 512: a partial last round of tiles) split their tail tiles in K when
@@ -294,10 +297,9 @@ struct icap_handle {
   // §5); the workspace is allocated on first use, outside any capture
   void tail_split(GemmArgs& g) {
     if (split_slots < 0) {
-      const char* v = getenv("ICAP_GEMM_TAIL");
       int cus = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 0;
-      split_slots = !(v && atoi(v) == 1) || cus < 8 ? 0 : 2 * cus / 8;
+      split_slots = icap_knob("ICAP_GEMM_TAIL", 0) != 1 || cus < 8 ? 0 : 2 * cus / 8;
       if (split_slots) {
         e_split.ensure(gemm_split_ws_bytes(split_slots));
         e_scnt.ensure((size_t)8 * split_slots * 4);
@@ -457,10 +459,7 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   const icap_model_desc& d = h->d;
   const int V = d.vit_dim, g = d.image / d.patch, np = g * g, T = np + 1, M = B * T, Dm = d.d_model;
   const int Kp = 3 * d.patch * d.patch, ns = h->ns;
-  static const int hm_env = [] {
-    const char* v = getenv("ICAP_QKV_HEAD_MAJOR");  // measurement knob: 0 = row-major QKV
-    return v ? atoi(v) : 1;
-  }();
+  static const int hm_env = icap_knob("ICAP_QKV_HEAD_MAJOR", 1);  // 0 = row-major QKV
   const int hm = hm_env && T > 64 && T <= 256 ? T : 0;
   h->e_patch.ensure((size_t)B * np * Kp * 2 * ns);
   h->e_x.ensure((size_t)M * V * 4);
@@ -840,10 +839,8 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   // independent chains on two streams (two parallel branches of the captured graph), so their
   // latency-bound launches can overlap.
   // (two chains pay from 128 rows each: B = 256 +3.4 %, B = 128 -6 %, tools/ab_env.sh)
-  static const int min_rows = [] {  // ICAP_DEC_MIN_ROWS: smallest chain (64-row chains measured slower)
-    const char* v = getenv("ICAP_DEC_MIN_ROWS");
-    return v ? std::max(16, atoi(v)) : 128;
-  }();
+  // ICAP_DEC_MIN_ROWS: smallest chain (64-row chains measured slower)
+  static const int min_rows = std::max(16, icap_knob("ICAP_DEC_MIN_ROWS", 128));
   const int nb = std::max(1, std::min(h->dec_branches, B / min_rows));
   if (nb > 1) {
     if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
@@ -1004,9 +1001,34 @@ extern "C" {
 int icap_abi_version(void) { return ICAP_ABI_VERSION; }
 const char* icap_last_error(void) { return g_err.c_str(); }
 
+const char* icap_knobs_set() {
+  static const char* const names[] = {
+      "ICAP_CONV_CLASS", "ICAP_GEMM_GROUP", "ICAP_GEMM256_WAVES", "ICAP_GEMM_TALL_MIN_K", "ICAP_GEMM_TALL_BM",
+      "ICAP_GEMM_TALL_KS", "ICAP_I8_NOMFMA", "ICAP_I8_GROUP", "ICAP_I8_NT_STORE", "ICAP_I8_TILE",
+      "ICAP_ENC_ATTN_PIPE", "ICAP_ENC_ATTN_QPW", "ICAP_XATTN_KS", "ICAP_POISON", "ICAP_GEMM_TAIL",
+      "ICAP_QKV_HEAD_MAJOR", "ICAP_DEC_MIN_ROWS", "ICAP_I8_MLP2", "ICAP_DEC_BRANCHES"};
+  for (const char* n : names)
+    if (getenv(n)) return n;
+  return "";
+}
+
+int icap_tools_build(void) {
+#ifdef ICAP_TOOLS
+  return 1;
+#else
+  return 0;
+#endif
+}
+
 int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
   return guarded([&] {
     REQUIRE(desc && out, "null argument");
+#ifndef ICAP_TOOLS
+    if (*icap_knobs_set())
+      throw Fail(std::string(icap_knobs_set()) +
+                 " is set: it is a measurement knob that only a tools build (-DICAP_TOOLS) reads; "
+                 "unset it or build with `python -m image_caption_amd.build --tools`");
+#endif
     REQUIRE(desc->precision == ICAP_PREC_BF16 || desc->precision == ICAP_PREC_BF16X2 ||
                 desc->precision == ICAP_PREC_I8X2,
             "bad precision");
@@ -1018,9 +1040,8 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
       // measured and rejected as the default: MLP-2 fed by the block-scaled GELU output takes
       // 1211 us (two-step fold: 256 VGPRs, 30 spilled) / 646 us (per-step fold, 64-column blocks) against
       // 467 us for the bf16x2 form
-      const char* k8 = getenv("ICAP_I8_MLP2");
-      h->i8k = h->i8 && k8 && atoi(k8) == 1;
-      if (const char* v = getenv("ICAP_DEC_BRANCHES")) h->dec_branches = std::max(1, std::min(icap_handle::MAX_BRANCHES, atoi(v)));
+      h->i8k = h->i8 && icap_tools_build() && icap_knob("ICAP_I8_MLP2", 0) == 1;
+      h->dec_branches = std::max(1, std::min(icap_handle::MAX_BRANCHES, icap_knob("ICAP_DEC_BRANCHES", h->dec_branches)));
       pack(h, (hipStream_t)stream);
       HIPCHK(hipStreamSynchronize((hipStream_t)stream));
     } catch (...) {
@@ -1170,6 +1191,15 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
   });
 }
 
+int icap_set_decode_chains(icap_handle* h, int chains) {
+  return guarded([&] {
+    REQUIRE(h, "null handle");
+    REQUIRE(chains >= 1 && chains <= icap_handle::MAX_BRANCHES, "decode chains must be in [1, 4]");
+    h->dec_branches = chains;
+    for (DecodeGraph& g : h->dg) g.reset();
+  });
+}
+
 int icap_set_graphs(icap_handle* h, int enable) {
   return guarded([&] {
     REQUIRE(h, "null handle");
@@ -1226,6 +1256,7 @@ int icap_op_gemm_tail_split(const uint16_t* A, long lda, long a_lo, int nsplit, 
                             float* C, long ldc, int M, int N, int K, int split_slots, float* ws, int* cnt,
                             void* stream) {
   return guarded([&] {
+    REQUIRE(icap_tools_build(), "measured-and-rejected variant: tools build only (-DICAP_TOOLS)");
     REQUIRE(split_slots > 0 && ws && cnt, "split_slots, ws and cnt are required");
     GemmArgs g = gemm_args();
     g.A = A; g.lda = lda; g.a_lo = a_lo; g.nsplit = nsplit;
@@ -1271,6 +1302,7 @@ int icap_op_gemm_i8_blocks(const int8_t* A, const float* a_scale, const float* a
                            const float* w_scale, const float* bias, void* C, float* c_kscale, int M, int N, int K,
                            int epi, int out, void* stream) {
   return guarded([&] {
+    REQUIRE(icap_tools_build(), "measured-and-rejected variant: tools build only (-DICAP_TOOLS)");
     REQUIRE(out == OUT_F32 || out == OUT_F32_RESID || out == OUT_I8K, "out must be OUT_F32, OUT_F32_RESID or OUT_I8K");
     REQUIRE((a_scale != nullptr) != (a_kscale != nullptr), "exactly one of a_scale / a_kscale");
     REQUIRE(out != OUT_I8K || c_kscale != nullptr, "OUT_I8K needs c_kscale");

@@ -5,6 +5,22 @@
 
 typedef uint16_t bf16_t;
 
+// Measurement knobs (ICAP_* environment variables that select measured-and-rejected variants, tile
+// classes, rasters, ...).  Only a tools build (-DICAP_TOOLS, `python -m image_caption_amd.build --tools`)
+// reads them; the product build compiles every knob to its default and icap_create refuses to run
+// while one is set (icap_knobs_set), so no environment can change what the library computes.
+#ifdef ICAP_TOOLS
+#include <stdlib.h>
+inline int icap_knob(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+#else
+inline int icap_knob(const char*, int dflt) { return dflt; }
+#endif
+// Name of the first knob set in the environment ("" when none); checked by icap_create in a product build.
+extern "C" const char* icap_knobs_set();
+
 // Epilogue / output selectors shared by kernels and the host dispatcher.
 enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RELU = 2 };
 // OUT_I8K (launch_gemm_i8, 128 x 128 tiles only): C as int8 two-slice row images [M][N/64][2][64] with one

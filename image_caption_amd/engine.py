@@ -276,6 +276,10 @@ class Engine:
               "icap_decoder_forward")
         return logits
 
+    def set_decode_chains(self, chains: int) -> None:
+        """Independent decode chains per batch (1..4, default 2, used from 128 rows per chain)."""
+        check(self.lib.icap_set_decode_chains(self.handle, int(chains)), "icap_set_decode_chains")
+
     def set_graphs(self, enable: bool) -> None:
         """hipGraph replay of the decode loop (default on)."""
         check(self.lib.icap_set_graphs(self.handle, int(bool(enable))), "icap_set_graphs")

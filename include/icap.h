@@ -88,6 +88,9 @@ typedef struct {
 } icap_model_desc;
 
 int icap_abi_version(void);
+/* 1 when the library was built with -DICAP_TOOLS (measurement knobs read from the environment and
+ * the measured-and-rejected kernel variants compiled in), 0 for the product build. */
+int icap_tools_build(void);
 const char* icap_last_error(void);
 
 /* Packs the model's weights (bf16 GEMM operands + fp32 small params) into handle-owned memory.
@@ -173,13 +176,20 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
  * the eager calls only). */
 int icap_set_graphs(icap_handle* h, int enable);
 
-/* ---- live kernel timing (bench.py roofline) ---- */
-#define ICAP_PROF_GEMM_128 0   /* gemm_bf16_kernel<128,128,64,64> (encoder GEMMs)      */
-#define ICAP_PROF_GEMM_64 1    /* gemm_bf16_kernel<64,64,32,32>  (decode-step GEMMs)    */
-#define ICAP_PROF_ENC_ATTN 2   /* enc_attention_kernel                                  */
-#define ICAP_PROF_CROSS_ATTN 3 /* cross_attn_absorbed_kernel                            */
-#define ICAP_PROF_GEMM_WAVE 4  /* gemm_dec_kernel (decode-step GEMMs, whole K' range DMA'd to LDS) */
-#define ICAP_PROF_GEMM_256 5   /* gemm_256_kernel (encoder GEMMs, 256 x 256 tiles)      */
+/* Number of independent decode chains a batch is split into (1..4, default 2; used from 128 rows
+ * per chain): the chains are parallel branches of the captured decode graph. */
+int icap_set_decode_chains(icap_handle* h, int chains);
+
+/* ---- live kernel timing (bench.py roofline) ----
+ * Launch classes recorded by icap_profile_* (eager launches only: kernels inside a replayed decode
+ * graph are not event-bracketed; bench.py times the decode phase as a whole instead). */
+#define ICAP_PROF_GEMM_128 0   /* gemm_bf16_kernel<128,128,64,64>: trunk convolutions of that tile class  */
+#define ICAP_PROF_GEMM_64 1    /* gemm_bf16_kernel<64,64,32,32>: small GEMMs (trunk layer1, N <= 128)    */
+#define ICAP_PROF_ENC_ATTN 2   /* enc_attention_pipe_kernel / enc_attention_kernel (encoder self-attention) */
+#define ICAP_PROF_CROSS_ATTN 3 /* cross_attn_mfma_kernel (decoder cross-attention)                         */
+#define ICAP_PROF_GEMM_WAVE 4  /* gemm_dec_kernel / chain_dec_kernel (decode-step GEMMs)                   */
+#define ICAP_PROF_GEMM_256 5   /* gemm_256_kernel: bf16 / bf16x2 encoder GEMMs (128x256 or 256x256 tiles)  */
+#define ICAP_PROF_GEMM_I8 6    /* gemm_i8_kernel: int8 two-slice encoder GEMMs (ICAP_PREC_I8X2)            */
 /* Enable (1) / disable (0) HIP-event bracketing of every hot-kernel launch; clears records. */
 int icap_profile_enable(icap_handle* h, int enable);
 /* Sum over recorded launches of one class: device ms, launch count, algorithmic flops and bytes

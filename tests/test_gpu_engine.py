@@ -40,8 +40,8 @@ def test_vit_encode_and_greedy(cuda, vit_sd, precision):
         assert lerr < 1e-1, lerr
 
 
-def test_two_chain_decode_matches_one_chain(cuda, vit_sd, monkeypatch):
-    """The batch decoded as two independent graph branches (ICAP_DEC_BRANCHES=2, the default, from
+def test_two_chain_decode_matches_one_chain(cuda, vit_sd):
+    """The batch decoded as two independent graph branches (icap_set_decode_chains 2, the default, from
     B = 256) gives the same greedy ids, step logits and sampled ids / log-probs as one chain, for an
     odd batch (uneven halves 128 + 129), eagerly and on graph replay."""
     from image_caption_amd.engine import Engine
@@ -52,8 +52,8 @@ def test_two_chain_decode_matches_one_chain(cuda, vit_sd, monkeypatch):
     uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(3)).to(cuda)
     out = {}
     for nb in ("1", "2"):
-        monkeypatch.setenv("ICAP_DEC_BRANCHES", nb)
         eng = Engine(vit_sd, "vit", {}, device=cuda)
+        eng.set_decode_chains(int(nb))
         runs = []
         for _ in range(3):  # eager, capture, replay
             ids, lg = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L, want_logits=True)

@@ -37,6 +37,24 @@ def test_library_refuses_without_gpu_inputs():
     assert b"bad arguments" in lib.icap_last_error()
 
 
+def test_product_build_refuses_measurement_knobs(monkeypatch):
+    """The product library compiles every ICAP_* measurement knob to its default and icap_create refuses
+    to run while one is set, so no environment can change what it computes (the check precedes any GPU
+    call, so it runs on CPU)."""
+    import ctypes
+
+    from image_caption_amd import _lib
+
+    lib = _lib.load()
+    if lib.icap_tools_build():
+        pytest.skip("tools build")
+    monkeypatch.setenv("ICAP_I8_NOMFMA", "1")
+    h = ctypes.c_void_p()
+    desc = _lib.ModelDesc()
+    assert lib.icap_create(ctypes.byref(desc), None, ctypes.byref(h)) != 0
+    assert b"ICAP_I8_NOMFMA" in lib.icap_last_error() and b"tools build" in lib.icap_last_error()
+
+
 def test_dropin_vit_model_state_dict_and_greedy():
     from models.vit_transformer_model import build_model
 
