@@ -138,6 +138,11 @@ struct icap_handle {
   bool i8 = false;  // ICAP_PREC_I8X2: LayerNorm-fed ViT GEMMs on int8 two-slice operands
   bool i8k = false;  // ... and MLP-2 on the block-scaled int8 GELU output (ICAP_I8_MLP2=1, opt-in)
   std::vector<void*> owned;
+  std::vector<size_t> owned_n;  // bytes of each owned buffer
+  // icap_update_weights re-packs into the buffers icap_create allocated, in the same order: alloc()
+  // then hands them out again (cursor) instead of allocating, so captured decode graphs stay valid
+  bool repack = false;
+  size_t cursor = 0, dec_allocs = 0;  // dec_allocs: buffers of the decoder part (allocated first)
   // decoder
   float *emb = nullptr, *pe = nullptr, *fc_w = nullptr, *fc_b = nullptr;
   std::vector<DecLayer> dec;
@@ -219,9 +224,14 @@ struct icap_handle {
   }
 
   void* alloc(size_t bytes) {
+    if (repack) {
+      REQUIRE(cursor < owned.size() && owned_n[cursor] == bytes, "weight update does not match the packed layout");
+      return owned[cursor++];
+    }
     void* p = nullptr;
     HIPCHK(hipMalloc(&p, bytes));
     owned.push_back(p);
+    owned_n.push_back(bytes);
     return p;
   }
   float* own_f32(const float* src, size_t n, hipStream_t s) {
@@ -359,11 +369,16 @@ struct icap_handle {
 
 namespace {
 
-void pack(icap_handle* h, hipStream_t s) {
+// parts: ICAP_PART_DECODER | ICAP_PART_ENCODER.  On create both, allocating; on an update (h->repack)
+// the selected parts are re-packed into the same buffers.
+void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PART_ENCODER) {
   const icap_model_desc& d = h->d;
   const int D = d.d_model, F = d.dim_ff;
   REQUIRE(d.nhead * 64 == D && d.nhead == 8, "decoder must have 8 heads of 64");
   REQUIRE(d.vocab <= 128, "vocab > 128 unsupported by the head kernel");
+  if (parts & ICAP_PART_DECODER) {
+  h->cursor = 0;
+  h->dec.clear();
   h->emb = h->own_f32(d.emb, (size_t)d.vocab * D, s);
   h->pe = h->own_f32(d.pe, (size_t)d.pe_len * D, s);
   h->fc_w = h->own_f32(d.fc_w, (size_t)d.vocab * D, s);
@@ -386,6 +401,13 @@ void pack(icap_handle* h, hipStream_t s) {
     o.n3 = h->ln(L.norm3, D, s);
     h->dec.push_back(o);
   }
+  if (!h->repack) h->dec_allocs = h->owned.size();
+  }
+  if (!(parts & ICAP_PART_ENCODER)) return;
+  h->cursor = h->dec_allocs;
+  h->vit.clear();
+  h->enc.clear();
+  h->trunk.clear();
   if (d.kind == ICAP_KIND_VIT) {
     const int V = d.vit_dim, np = (d.image / d.patch) * (d.image / d.patch);
     REQUIRE(d.vit_heads * 64 == V, "ViT heads must be 64 wide");
@@ -1086,6 +1108,33 @@ int icap_stream_create_cu_mask(int n_cus, int complement, int priority, void** o
 
 int icap_stream_destroy(void* stream) {
   return guarded([&] { HIPCHK(hipStreamDestroy((hipStream_t)stream)); });
+}
+
+int icap_update_weights(icap_handle* h, const icap_model_desc* desc, int parts, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && desc, "null argument");
+    REQUIRE(parts > 0 && (parts & ~(ICAP_PART_DECODER | ICAP_PART_ENCODER)) == 0, "bad parts");
+    const icap_model_desc& o = h->d;
+    REQUIRE(desc->kind == o.kind && desc->precision == o.precision && desc->d_model == o.d_model &&
+                desc->nhead == o.nhead && desc->dim_ff == o.dim_ff && desc->n_dec_layers == o.n_dec_layers &&
+                desc->vocab == o.vocab && desc->pe_len == o.pe_len && desc->vit_dim == o.vit_dim &&
+                desc->vit_layers == o.vit_layers && desc->vit_mlp == o.vit_mlp && desc->patch == o.patch &&
+                desc->cnn_dim == o.cnn_dim && desc->n_enc_layers == o.n_enc_layers && desc->n_trunk == o.n_trunk,
+            "weight update must keep the model's shapes");
+    REQUIRE(!(parts & ICAP_PART_DECODER) || desc->dec_layers, "decoder layer pointers missing");
+    const hipStream_t s = (hipStream_t)stream;
+    h->d = *desc;
+    h->repack = true;
+    try {
+      pack(h, s, parts);
+    } catch (...) {
+      h->repack = false;
+      h->d.dec_layers = nullptr; h->d.vit_layers_w = nullptr; h->d.enc_layers = nullptr; h->d.trunk = nullptr;
+      throw;
+    }
+    h->repack = false;
+    h->d.dec_layers = nullptr; h->d.vit_layers_w = nullptr; h->d.enc_layers = nullptr; h->d.trunk = nullptr;
+  });
 }
 
 int icap_destroy(icap_handle* h) {

@@ -83,10 +83,34 @@ class Engine:
         self.kind = kind
         self.has_trunk = False
         self.precision = precision
-        sd = {k: v.detach().to(device=device, dtype=torch.float32).contiguous()
-              for k, v in state_dict.items() if torch.is_floating_point(v)}
         self.d_model = int(config.get("d_model", 512))
         self.nhead = int(config.get("nhead", 8))
+        desc, keep = self._desc(state_dict)
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            check(self.lib.icap_create(ctypes.byref(desc), stream_ptr(device), ctypes.byref(handle)), "icap_create")
+        self.handle = handle
+        del keep
+
+    def update_weights(self, state_dict: Dict[str, torch.Tensor], decoder: bool = True, encoder: bool = True) -> None:
+        """Re-pack the decoder and/or encoder weights of `state_dict` (same shapes) into this handle's
+        buffers on the current stream (icap_update_weights): no re-allocation, frozen parts untouched,
+        captured decode graphs kept."""
+        parts = (_lib.PART_DECODER if decoder else 0) | (_lib.PART_ENCODER if encoder else 0)
+        if not parts:
+            return
+        desc, keep = self._desc(state_dict)
+        check(self.lib.icap_update_weights(self.handle, ctypes.byref(desc), parts, stream_ptr(self.device)),
+              "icap_update_weights")
+        torch.cuda.current_stream(self.device).synchronize()  # the fp32 copies in `keep` must outlive the packing
+        del keep
+
+    def _desc(self, state_dict: Dict[str, torch.Tensor]):
+        """icap_model_desc over fp32 device copies of `state_dict` (returned with the objects that must
+        stay alive until the library has read them)."""
+        device, kind = self.device, self.kind
+        sd = {k: v.detach().to(device=device, dtype=torch.float32).contiguous()
+              for k, v in state_dict.items() if torch.is_floating_point(v)}
         emb = sd["decoder.embedding.weight"]
         self.vocab = emb.shape[0]
         self.pe_len = sd["decoder.pos_encoder.pe"].shape[1]
@@ -102,7 +126,7 @@ class Engine:
                                _ln(sd, p + ".norm1"), _ln(sd, p + ".norm2"), _ln(sd, p + ".norm3"))
         dim_ff = sd["decoder.transformer_decoder.layers.0.linear1.weight"].shape[0]
         desc = ModelDesc()
-        desc.precision = _lib.PRECISIONS[precision]
+        desc.precision = _lib.PRECISIONS[self.precision]
         desc.d_model, desc.nhead, desc.dim_ff = self.d_model, self.nhead, dim_ff
         desc.n_dec_layers, desc.vocab, desc.pe_len = n_dec, self.vocab, self.pe_len
         desc.emb = emb.data_ptr()
@@ -110,7 +134,7 @@ class Engine:
         desc.fc_w = sd["decoder.fc_out.weight"].data_ptr()
         desc.fc_b = sd["decoder.fc_out.bias"].data_ptr()
         desc.dec_layers = ctypes.cast(dec, ctypes.POINTER(DecLayerW))
-        keep = [dec]
+        keep = [dec, sd]
         if kind == "vit":
             P = "encoder.vit."
             conv = sd[P + "conv_proj.weight"]
@@ -173,11 +197,7 @@ class Engine:
             self.mem_tokens = 49
         else:
             raise ValueError(f"unknown model kind {kind!r}")
-        handle = ctypes.c_void_p()
-        with torch.cuda.device(device):
-            check(self.lib.icap_create(ctypes.byref(desc), stream_ptr(device), ctypes.byref(handle)), "icap_create")
-        self.handle = handle
-        del keep, sd
+        return desc, keep
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -99,6 +99,14 @@ const char* icap_last_error(void);
 int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out);
 int icap_destroy(icap_handle* h);
 
+/* Re-packs the weights of the selected parts from `desc` (same shapes as at icap_create) into the
+ * handle's existing buffers, in stream order: training loops (SCST) refresh the packed model after an
+ * optimizer step without re-packing frozen parts, re-allocating, or losing the captured decode graphs.
+ * parts: ICAP_PART_DECODER (the TransformerDecoder) and/or ICAP_PART_ENCODER (everything else). */
+#define ICAP_PART_DECODER 1
+#define ICAP_PART_ENCODER 2
+int icap_update_weights(icap_handle* h, const icap_model_desc* desc, int parts, void* stream);
+
 /* images (B,3,224,224) fp32 normalised -> memory (B,196,d_model) fp32.
  * Replaces: VisionTransformerEncoder.forward, models/vit_transformer_model.py:71-100. */
 int icap_encode_vit(icap_handle* h, const float* images, int B, float* memory, void* stream);

@@ -64,14 +64,28 @@ class HipRouted:
         return True
 
     def hip_engine(self, device: torch.device):
+        """The packed engine of this module's current weights.  After an optimizer step only the parts
+        whose tensors changed (decoder / encoder, by data_ptr and version) are re-packed in place
+        (icap_update_weights): frozen encoder weights are not re-packed and the captured decode graphs
+        survive, so an SCST training loop keeps replaying them."""
         from image_caption_amd.engine import Engine
 
-        tensors = [t for t in self.state_dict().values() if torch.is_tensor(t)]
-        key = (str(device), self.hip_precision, tuple((t.data_ptr(), t._version) for t in tensors))
+        sd = self.state_dict()
+
+        def key(prefix_dec: bool):
+            return tuple((k, t.data_ptr(), t._version) for k, t in sd.items()
+                         if torch.is_tensor(t) and k.startswith("decoder.") == prefix_dec)
+
+        base = (str(device), self.hip_precision)
+        kd, ke = key(True), key(False)
         cache = self._hip_cache
-        if cache is not None and cache[0] == key:
-            return cache[1]
-        eng = Engine(self.state_dict(), self._hip_kind, {"d_model": self.d_model},
-                     precision=self.hip_precision, device=device)
-        object.__setattr__(self, "_hip_cache", (key, eng))
+        if cache is not None and cache[0] == base:
+            eng = cache[3]
+            dec, enc = cache[1] != kd, cache[2] != ke
+            if dec or enc:
+                eng.update_weights(sd, decoder=dec, encoder=enc)
+                object.__setattr__(self, "_hip_cache", (base, kd, ke, eng))
+            return eng
+        eng = Engine(sd, self._hip_kind, {"d_model": self.d_model}, precision=self.hip_precision, device=device)
+        object.__setattr__(self, "_hip_cache", (base, kd, ke, eng))
         return eng

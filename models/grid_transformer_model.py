@@ -52,9 +52,16 @@ class GridFeatureEncoder(nn.Module):
             eng = owner.hip_engine(images.device)
             if tuple(images.shape[1:]) == (3, 224, 224):
                 return eng.encode(images)  # HIP trunk + tail
-            with torch.no_grad():  # other image sizes: torch trunk, HIP tail
-                return eng.encode(self.cnn(images.float()))
-        x = self.projection(self.cnn(images))
+            with torch.no_grad():  # other image sizes: torch trunk, then the HIP tail when the map is 7x7
+                feats = self.cnn(images.float())
+                if feats.shape[2] * feats.shape[3] == eng.mem_tokens:
+                    return eng.encode(feats)
+                return self.tail(feats)
+        return self.tail(self.cnn(images))
+
+    def tail(self, feats):
+        """Everything after self.cnn (grid:97-108): 1x1 projection, flatten, PE, encoder layers."""
+        x = self.projection(feats)
         x = x.flatten(2).permute(0, 2, 1)
         return self.transformer_encoder(self.pos_encoder(x))
 

@@ -1,0 +1,122 @@
+"""The drop-in SCST training path on the GPU (utils/scst_loss.py, reference utils/scst_loss.py:136-254)
+and the in-place weight refresh it relies on (icap_update_weights).
+
+* grad-enabled SCSTLoss.forward: the HIP sampler (injected uniforms, inverse CDF) against the PyTorch
+  restatement of the reference loop (`SCSTLoss._sample_torch`) fed the same uniforms, dropout 0: same ids
+  and stop length, log-probs within 1e-3, equal rewards, decoder gradients within 1e-3 relative;
+* Grid in train mode: the ResNet trunk's BatchNorm running statistics take exactly ONE update per
+  SCSTLoss.forward, as in the reference (its sampler encodes once in train mode, `generate` in eval);
+* after an optimizer-style in-place change of decoder (or encoder) weights, `model.hip_engine` re-packs
+  the changed part into the same handle and its outputs equal a freshly packed engine's.
+"""
+import copy
+
+import pytest
+import torch
+
+from image_caption_amd import weights as W
+
+pytestmark = pytest.mark.gpu
+
+VOCAB = {f"w{i}": i for i in range(W.VOCAB_SIZE)}
+VOCAB.update({"<pad>": 0, "<unk>": 106, "<start>": 107, "<end>": 108})
+REFS = [["w1 w2 w3"], ["w4 w5"], ["w6"], ["w7 w8 w9 w10"], ["w3 w3 w9"], ["w11 w2"], ["w5 w6 w7"], ["w8"]]
+
+
+def _vit_model(cuda, backend="auto", dropout=0.0):
+    from models.vit_transformer_model import build_model
+
+    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False, "dropout": dropout, "backend": backend})
+    m.load_state_dict(W.to_torch(W.vit_state_dict(0)))
+    return m.to(cuda)
+
+
+def test_scst_grad_step_matches_torch_sampler(cuda):
+    from utils.scst_loss import SCSTLoss
+
+    B, L = 8, 30
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=5)).to(cuda)
+    uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(17)).to(cuda)
+    hip_m = _vit_model(cuda)
+    ref_m = _vit_model(cuda, backend="torch")
+    hip_m.train()
+    ref_m.train()
+    # sampler outputs
+    ids_h, lp_h = SCSTLoss()._sample_with_log_probs(hip_m, imgs, 107, 108, L, cuda, uni)
+    ids_r, lp_r = SCSTLoss()._sample_with_log_probs(ref_m, imgs, 107, 108, L, cuda, uni)
+    assert ids_h.shape == ids_r.shape and torch.equal(ids_h, ids_r)
+    assert lp_h.requires_grad and lp_r.requires_grad
+    assert (lp_h - lp_r).abs().max().item() < 1e-3
+    # the whole step: loss, rewards, decoder gradients
+    hip_m.zero_grad()
+    ref_m.zero_grad()
+    loss_h, info_h = SCSTLoss()(hip_m, imgs, REFS, VOCAB, cuda, max_len=L, uniforms=uni)
+    loss_r, info_r = SCSTLoss()(ref_m, imgs, REFS, VOCAB, cuda, max_len=L, uniforms=uni)
+    for k in ("sample_reward", "greedy_reward", "advantage"):
+        assert abs(info_h[k] - info_r[k]) < 1e-6, (k, info_h[k], info_r[k])
+    assert abs(loss_h.item() - loss_r.item()) <= 1e-3 * max(1.0, abs(loss_r.item()))
+    loss_h.backward()
+    loss_r.backward()
+    gh = dict(hip_m.decoder.named_parameters())
+    n = 0
+    for name, p in ref_m.decoder.named_parameters():
+        if p.grad is None:
+            continue
+        n += 1
+        a, b = gh[name].grad, p.grad
+        assert a is not None, name
+        assert (a - b).abs().max().item() <= 1e-3 * max(b.abs().max().item(), 1e-6), name
+    assert n > 10
+
+
+def test_scst_grid_batchnorm_updated_once(cuda):
+    """Train-mode Grid SCST: one BatchNorm running-statistics update per step, as the reference."""
+    from models.grid_transformer_model import build_model
+    from utils.scst_loss import SCSTLoss
+
+    B, L = 4, 12
+    m = build_model(W.VOCAB_SIZE, {"pretrained_cnn": False, "dropout": 0.0})
+    m.load_state_dict(W.to_torch(W.grid_state_dict(0)))
+    m = m.to(cuda)
+    twin = copy.deepcopy(m)
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=2)).to(cuda)
+    uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(4)).to(cuda)
+    loss, _ = SCSTLoss()(m, imgs, REFS[:B], VOCAB, cuda, max_len=L, uniforms=uni)
+    loss.backward()
+    twin.train()
+    with torch.no_grad():
+        twin.encoder.cnn(imgs)  # exactly one train-mode pass
+    for (name, a), (_, b) in zip(m.encoder.cnn.named_buffers(), twin.encoder.cnn.named_buffers()):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), name
+
+
+@pytest.mark.parametrize("part", ["decoder", "encoder"])
+def test_engine_refresh_in_place(cuda, part):
+    """model.hip_engine after an in-place weight change re-packs that part into the SAME handle
+    (icap_update_weights), and decodes exactly as an engine packed from scratch."""
+    from image_caption_amd.engine import Engine
+
+    m = _vit_model(cuda)
+    m.eval()
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=8)).to(cuda)
+    with torch.no_grad():
+        eng = m.hip_engine(cuda)
+        for _ in range(3):  # eager, capture, replay: the decode graph exists before the update
+            m.generate(imgs, 107, 108, 30)
+        g = torch.Generator().manual_seed(1)
+        with torch.no_grad():
+            for name, p in m.named_parameters():
+                if name.startswith("decoder.") == (part == "decoder") and p.dim() == 2:
+                    p.add_(0.01 * torch.randn(p.shape, generator=g).to(cuda))
+        eng2 = m.hip_engine(cuda)
+        assert eng2 is eng
+        got = m.generate(imgs, 107, 108, 30)
+        mem = eng.encode(imgs)
+        fresh = Engine(m.state_dict(), "vit", {}, device=cuda)
+        mem_f = fresh.encode(imgs)
+        assert torch.equal(mem, mem_f)
+        want = fresh.greedy(mem_f, 107, 108, 30)
+        assert torch.equal(got, want)
+        lg = eng.decoder_forward(want[:, :-1], mem, causal=True)
+        lg_f = fresh.decoder_forward(want[:, :-1], mem_f, causal=True)
+        assert torch.equal(lg, lg_f)

@@ -114,15 +114,27 @@ class SCSTLoss(nn.Module):
             uniforms = torch.rand(max_len - 1, B, device=images.device)
         if images.is_cuda and getattr(model, "hip_backend", "torch") != "torch":
             eng = model.hip_engine(images.device)
+            feats = None
+            if getattr(model, "_hip_kind", "") == "grid" and model.encoder.cnn.training:
+                # the reference encodes once per step, in train mode (scst_loss:161, :213): the trunk's
+                # BatchNorm normalises with batch statistics and updates its running statistics ONCE.
+                # The eval-folded HIP trunk cannot do that, so the trunk runs here, once (grad as
+                # enabled); the HIP tail takes it for the sampler and the recompute below reuses it
+                feats = model.encoder.cnn(images.float())
             with torch.no_grad():
-                enc_in = model.encoder.cnn(images.float()) if getattr(model, "_hip_kind", "") == "grid" else images
-                mem = eng.encode(enc_in)
+                if feats is not None:
+                    f = feats.detach()
+                    mem = eng.encode(f) if f.shape[2] * f.shape[3] == eng.mem_tokens else model.encoder.tail(f)
+                elif getattr(model, "_hip_kind", "") == "grid" and tuple(images.shape[1:]) != (3, 224, 224):
+                    mem = model.encoder(images)  # eval trunk, other sizes: torch trunk (+ HIP tail on 7x7)
+                else:  # ViT, or a Grid model whose trunk is in eval mode: the whole encoder on HIP
+                    mem = eng.encode(images)
                 ids32, logp = eng.sample(mem, uniforms, start_token, end_token, max_len)
             ids = ids32.long()
             L = sample_stop_length(ids, end_token)
             ids, logp = ids[:, :L], logp[:, : L - 1]
             if torch.is_grad_enabled():
-                memory = model.encoder(images)
+                memory = model.encoder.tail(feats) if feats is not None else model.encoder(images)
                 mask = model.decoder.generate_square_subsequent_mask(L - 1, images.device)
                 logits = model.decoder(ids[:, :-1], memory, tgt_mask=mask)
                 logp = masked_token_logp(logits, ids, end_token)
