@@ -623,7 +623,8 @@ void trunk_conv(icap_handle* h, const Conv& c, const bf16_t* A, long a_ld, long 
 // Images go through in chunks of TRUNK_CHUNK so the stem GEMM grid and the workspaces stay bounded.
 constexpr int TRUNK_CHUNK = 256;
 
-void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStream_t s) {
+// feats (optional): the trunk output as fp32 rows (B, 49, cnn_dim) - self.cnn(images).flatten(2).permute(0, 2, 1)
+void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStream_t s, float* feats = nullptr) {
   const icap_model_desc& d = h->d;
   REQUIRE(!h->trunk.empty(), "handle was created without the ResNet trunk (n_trunk = 0)");
   REQUIRE(d.grid_tokens == 49, "the trunk path expects 224x224 images -> 7x7 grids");
@@ -706,6 +707,9 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
         hw = oh;
       }
     REQUIRE(hw * hw == d.grid_tokens, "trunk output grid != grid_tokens");
+    if (feats)  // trunk features (both planes: the values the tail consumes)
+      HIPCHK(launch_planes_to_f32(X, aL, (long)bc * d.grid_tokens * d.cnn_dim, 2,
+                                  feats + (size_t)b0 * d.grid_tokens * d.cnn_dim, s));
     encode_grid_rows(h, X, aL, bc, memory + (size_t)b0 * d.grid_tokens * d.d_model, s);
   }
 }
@@ -1167,6 +1171,14 @@ int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, 
     REQUIRE(h && images && memory && B > 0, "bad arguments");
     REQUIRE(h->d.kind == ICAP_KIND_GRID, "icap_encode_grid on a non-Grid model");
     encode_grid(h, images, B, memory, (hipStream_t)stream);
+  });
+}
+
+int icap_encode_grid_features(icap_handle* h, const float* images, int B, float* memory, float* feats, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && images && memory && feats && B > 0, "bad arguments");
+    REQUIRE(h->d.kind == ICAP_KIND_GRID, "not a Grid model");
+    encode_grid(h, images, B, memory, (hipStream_t)stream, feats);
   });
 }
 

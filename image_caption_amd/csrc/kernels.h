@@ -171,6 +171,8 @@ hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows
 hipError_t launch_fill_u8(uint8_t* p, long n, uint8_t value, hipStream_t s);
 hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hipStream_t s);
 hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int nsplit, hipStream_t s);
+// bf16 planes -> fp32 (hi + lo)
+hipError_t launch_planes_to_f32(const bf16_t* src, long lo, long n, int nsplit, float* dst, hipStream_t s);
 hipError_t launch_f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);
 hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s);
 

@@ -278,6 +278,12 @@ __global__ void split_f32_kernel(const float* src, long n, bf16_t* dst, long lo,
     store_planes(dst, i, lo, nsplit, src[i]);
 }
 
+// planes (hi at src, lo at src + lo when nsplit == 2) -> fp32 hi + lo
+__global__ void planes_to_f32_kernel(const bf16_t* src, long lo, long n, int nsplit, float* dst) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = nsplit == 2 ? bf2f(src[i]) + bf2f(src[i + lo]) : bf2f(src[i]);
+}
+
 __global__ void f32_to_bf16_kernel(const float* src, bf16_t* dst, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     dst[i] = f2bf(src[i]);
@@ -396,6 +402,11 @@ hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hip
 
 hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int nsplit, hipStream_t s) {
   hipLaunchKernelGGL(split_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, n, dst, lo, nsplit);
+  return hipGetLastError();
+}
+
+hipError_t launch_planes_to_f32(const bf16_t* src, long lo, long n, int nsplit, float* dst, hipStream_t s) {
+  hipLaunchKernelGGL(planes_to_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, lo, n, nsplit, dst);
   return hipGetLastError();
 }
 

@@ -181,6 +181,7 @@ class Engine:
             desc.proj_w = pw.data_ptr()
             desc.proj_b = sd["encoder.projection.bias"].data_ptr()
             desc.cnn_dim = pw.shape[1]
+            self.cnn_dim = int(pw.shape[1])
             desc.grid_tokens = 49
             desc.n_enc_layers = n_enc
             desc.enc_pe = sd["encoder.pos_encoder.pe"].data_ptr()
@@ -231,6 +232,18 @@ class Engine:
             check(self.lib.icap_encode_grid_tail(self.handle, x.data_ptr(), B, mem.data_ptr(),
                                                  stream_ptr(self.device)), "icap_encode_grid_tail")
         return mem
+
+    def encode_grid_features(self, images: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Grid: images (B,3,224,224) -> (memory (B,49,d), trunk features (B,cnn_dim,7,7)) in one pass."""
+        x = images.to(device=self.device, dtype=torch.float32).contiguous()
+        if self.kind != "grid" or not self.has_trunk or tuple(x.shape[1:]) != (3, 224, 224):
+            raise ValueError("encode_grid_features needs a Grid engine with its trunk and (B,3,224,224) images")
+        B = x.shape[0]
+        mem = torch.empty(B, self.mem_tokens, self.d_model, device=self.device, dtype=torch.float32)
+        rows = torch.empty(B, self.mem_tokens, self.cnn_dim, device=self.device, dtype=torch.float32)
+        check(self.lib.icap_encode_grid_features(self.handle, x.data_ptr(), B, mem.data_ptr(), rows.data_ptr(),
+                                                 stream_ptr(self.device)), "icap_encode_grid_features")
+        return mem, rows.permute(0, 2, 1).reshape(B, self.cnn_dim, 7, 7)
 
     # ------------------------------------------------------------------ decoders
     def greedy_raw(self, memory: torch.Tensor, start: int, end: int, max_len: int,

@@ -119,6 +119,9 @@ int icap_encode_grid_tail(icap_handle* h, const float* feats, int B, float* memo
  * MFMA GEMMs over NHWC activation planes (BatchNorm folded into the epilogue), then the tail.
  * Replaces: GridFeatureEncoder.forward, models/grid_transformer_model.py:86-108 (self.cnn included). */
 int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, void* stream);
+/* As icap_encode_grid, and also the trunk output itself: feats (B, 49, cnn_dim) fp32 =
+ * self.cnn(images).flatten(2).permute(0, 2, 1) (grid:94, :100-101), the values the tail consumes. */
+int icap_encode_grid_features(icap_handle* h, const float* images, int B, float* memory, float* feats, void* stream);
 
 /* CIDEr-D rewards on the GPU over token-id rows (pycocoevalcap CiderScorer: n = 1..4, tf-idf with
  * the document frequency over THIS call's reference sets, clipped cosine, Gaussian length penalty,

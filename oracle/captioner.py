@@ -28,8 +28,11 @@ reference import), the algorithm of:
       `torch.multinomial` replaced by inverse-CDF on injected uniforms (documented
       deviation).
 
-The oracle is pinned by `tests/golden/*.npz`, produced by running the reference's own
-decoder / greedy loop code from /root/reference (tests/golden/make_golden.py).
+The oracle is pinned by `tests/golden/*.npz`, produced by running the reference's own code from
+/root/reference (tests/golden/make_golden.py): the ViT and Grid models' encoders, greedy and beam
+loops and training forwards, SCSTLoss._sample_with_log_probs and scripts/inference.py's loop.
+The functions are device-agnostic torch fp32 math: the B = 256 GPU parity tests run the same code on
+the GPU in fp32 (gfx950 has no TF32 path) and tie it to the CPU run on a subset of rows.
 """
 from __future__ import annotations
 
@@ -73,7 +76,7 @@ def mha(q_in: Tensor, kv_in: Tensor, in_w: Tensor, in_b: Tensor, out_w: Tensor,
     v = v.view(B, S, nhead, hd).transpose(1, 2)
     s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
     if causal:
-        m = torch.ones(T, S, dtype=torch.bool).triu(1 + S - T)
+        m = torch.ones(T, S, dtype=torch.bool, device=s.device).triu(1 + S - T)
         s = s.masked_fill(m, float("-inf"))
     if key_pad is not None:
         s = s.masked_fill(key_pad[:, None, None, :], float("-inf"))
@@ -214,7 +217,7 @@ def greedy_from_memory(sd, memory: Tensor, start: int, end: int, max_len: int,
     """`_greedy_search` loop (vit:306-325): returns generated (B,L) int64 and, if asked,
     the per-step last-position logits (steps,B,V)."""
     B = memory.shape[0]
-    generated = torch.full((B, 1), start, dtype=torch.long)
+    generated = torch.full((B, 1), start, dtype=torch.long, device=memory.device)
     trace = []
     for _ in range(max_len - 1):
         out = decoder_forward(sd, generated, memory, causal=True)
@@ -318,8 +321,8 @@ def inverse_cdf_sample(logits: Tensor, u: Tensor) -> Tuple[Tensor, Tensor]:
 def sample_with_log_probs(sd, memory: Tensor, uniforms: Tensor, start: int, end: int, max_len: int):
     """`_sample_with_log_probs` (scst_loss:202-254) with injected uniforms (max_len-1, B)."""
     B = memory.shape[0]
-    generated = torch.full((B, 1), start, dtype=torch.long)
-    finished = torch.zeros(B, dtype=torch.bool)
+    generated = torch.full((B, 1), start, dtype=torch.long, device=memory.device)
+    finished = torch.zeros(B, dtype=torch.bool, device=memory.device)
     lps = []
     with torch.no_grad():
         for step in range(max_len - 1):

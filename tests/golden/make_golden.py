@@ -4,29 +4,33 @@ Runs in the build container only (needs /root/reference, read-only); the fixture
 plain data (npz: inputs' seeds + outputs) and are what travels.  Weights and images come from the
 seeded generator image_caption_amd/weights.py, so any machine can regenerate the inputs.
 
-What is the reference's own code here (imported by file path from /root/reference):
+Every loop below is the reference's own code, imported by file path from /root/reference:
   * models/vit_transformer_model.py: TransformerDecoder (vit:103-182), VisionTransformerEncoder
-    .forward (vit:71-100), ViTTransformerCaptioning.generate/_greedy_search (vit:276-325).
-What is restated because its module cannot import here:
-  * torchvision's ViT-B/16 trunk (absent) -> models/_vision.VisionTransformer, pinned against
-    HF transformers.ViTModel by tests/test_oracle.py;
-  * models/grid_transformer_model.py imports torchvision at module top (grid:8): the Grid golden
-    uses the reference decoder + greedy loop (grid:230-251 is the same algorithm as vit:296-325)
-    over GridFeatureEncoder from models/ (torch path), whose ResNet-101 is pinned against HF
-    ResNetModel;
-  * scripts/inference.py (imports torchvision.transforms) and utils/scst_loss.py (imports
-    pycocoevalcap): their decode loops (inference.py:75-99, scst_loss:220-249) are restated here
-    around the reference decoder module, with torch.multinomial replaced by inverse-CDF sampling
-    on fixed uniforms.
+    .forward (vit:71-100), ViTTransformerCaptioning.generate / _greedy_search / _beam_search / forward
+    (vit:216-420);
+  * models/grid_transformer_model.py: GridTransformerCaptioning with its GridFeatureEncoder.forward
+    (grid:86-110), generate / _greedy_search / _beam_search (grid:222-322) and forward (grid:185-210);
+  * utils/scst_loss.py: SCSTLoss._sample_with_log_probs (scst_loss:202-254), with torch.multinomial
+    replaced by an inverse-CDF draw on fixed uniforms for the duration of the call;
+  * scripts/inference.py: generate_caption (inference.py:60-101, the no-mask loop).
+Third-party modules absent from this image are replaced by import-only stand-ins, visible only while
+the reference module executes (sys.modules is restored afterwards):
+  * torchvision.models (grid:8, vit:8): resnet101 / vit_b_16 / *_Weights from models/_vision.py, the
+    build's restatement of the torchvision architectures (pinned against HF transformers' ViTModel /
+    ResNetModel by tests/test_oracle.py);
+  * torchvision.transforms (inference.py:6): names only, never called (generate_caption takes a tensor);
+  * pycocoevalcap.cider / .bleu (scst_loss:16-17): classes whose construction is a no-op and whose
+    compute_score raises - the sampler never scores.
 
-Usage: python tests/golden/make_golden.py [beam_vit|forward]   (writes tests/golden/*.npz, ~2 min on
-       8 cores; with beam_vit / forward only that fixture)
+Usage: python tests/golden/make_golden.py [beam_vit|forward|grid|sample]   (writes tests/golden/*.npz,
+       ~3 min on 8 cores; with an argument only that fixture)
 """
 from __future__ import annotations
 
 import importlib.util
 import os
 import sys
+import types
 
 import numpy as np
 import torch
@@ -42,12 +46,73 @@ REF = "/root/reference"
 END_BIAS = 1.4  # <end> logit offset of the beam-search fixtures (makes beams finish early)
 
 
-def load_ref_vit_module():
-    spec = importlib.util.spec_from_file_location("ref_vit_transformer_model",
-                                                  os.path.join(REF, "models", "vit_transformer_model.py"))
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
+def _module(name, **attrs):
+    m = types.ModuleType(name)
+    m.__dict__.update(attrs)
+    return m
+
+
+def _shims():
+    """Import-only stand-ins for the third-party modules the reference imports at module top."""
+    from models import _vision
+
+    class _Scorer:  # pycocoevalcap Cider / Bleu: constructible, never used by the sampler
+        def __init__(self, *a, **k):
+            pass
+
+        def compute_score(self, *a, **k):
+            raise RuntimeError("pycocoevalcap is absent: the golden script never scores")
+
+    class _T:  # torchvision.transforms names (inference.py:6), never called by generate_caption
+        def __init__(self, *a, **k):
+            raise RuntimeError("torchvision.transforms is absent")
+
+    tv_models = _module("torchvision.models", resnet101=_vision.resnet101, ResNet101_Weights=_vision.ResNet101_Weights,
+                        vit_b_16=_vision.vit_b_16, ViT_B_16_Weights=_vision.ViT_B_16_Weights)
+    tv_transforms = _module("torchvision.transforms", Compose=_T, Resize=_T, ToTensor=_T, Normalize=_T,
+                            CenterCrop=_T)
+    cider = _module("pycocoevalcap.cider.cider", Cider=_Scorer)
+    bleu = _module("pycocoevalcap.bleu.bleu", Bleu=_Scorer)
+    return {
+        "torchvision": _module("torchvision", models=tv_models, transforms=tv_transforms),
+        "torchvision.models": tv_models, "torchvision.transforms": tv_transforms,
+        "pycocoevalcap": _module("pycocoevalcap"), "pycocoevalcap.cider": _module("pycocoevalcap.cider", cider=cider),
+        "pycocoevalcap.cider.cider": cider, "pycocoevalcap.bleu": _module("pycocoevalcap.bleu", bleu=bleu),
+        "pycocoevalcap.bleu.bleu": bleu,
+    }
+
+
+def load_ref(relpath, name, extra_modules=None):
+    """Execute the reference file /root/reference/<relpath> as module `name`, with the shims (and
+    `extra_modules`) in sys.modules only while it executes."""
+    inject = dict(_shims(), **(extra_modules or {}))
+    saved = {k: sys.modules.get(k) for k in inject}
+    saved_path = list(sys.path)
+    sys.modules.update(inject)
+    try:
+        spec = importlib.util.spec_from_file_location(name, os.path.join(REF, relpath))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+        sys.path[:] = saved_path
     return mod
+
+
+def load_ref_vit_module():
+    return load_ref("models/vit_transformer_model.py", "ref_vit_transformer_model")
+
+
+def ref_grid_model(sd):
+    """The reference GridTransformerCaptioning (grid:161-322), random-init trunk, our weights."""
+    mod = load_ref("models/grid_transformer_model.py", "ref_grid_transformer_model")
+    model = mod.GridTransformerCaptioning(W.VOCAB_SIZE, pretrained_cnn=False)
+    model.load_state_dict(sd, strict=True)
+    return model.eval()
 
 
 def ref_decoder(ref, sd, max_len=100):
@@ -125,12 +190,9 @@ def make_beam(ref, sd, imgs, out):
 
 def make_forward(ref, out):
     # (vii) teacher-forced training forward with padding masks: the reference's OWN
-    # ViTTransformerCaptioning.forward (vit:216-255, padding from caption_lengths) and the Grid form
-    # (grid:185-207: padding from caption_lengths - 1, restated around the reference decoder and its
-    # own _generate_padding_mask, since grid_transformer_model.py imports torchvision).  Lengths cover
+    # ViTTransformerCaptioning.forward (vit:216-255, padding from caption_lengths) and
+    # GridTransformerCaptioning.forward (grid:185-210: padding from caption_lengths - 1).  Lengths cover
     # a full row, a partial one, 1, 0 (every key masked) and, for Grid, -1 (mask[i, -1:] slicing).
-    from models.grid_transformer_model import GridFeatureEncoder
-
     imgs = torch.from_numpy(W.synthetic_images(4, seed=0))
     rng = np.random.Generator(np.random.PCG64(11))
     caps = rng.integers(0, W.VOCAB_SIZE, size=(4, 17)).astype(np.int64)
@@ -140,21 +202,106 @@ def make_forward(ref, out):
     model = ref_vit_model(ref, W.to_torch(W.vit_state_dict(0)))
     with torch.no_grad():
         vit_logits = model(imgs, captions, vit_len)
-    gsd = W.to_torch(W.grid_state_dict(0))
-    genc = GridFeatureEncoder(pretrained_cnn=False)
-    genc.load_state_dict({k[len("encoder."):]: v for k, v in gsd.items() if k.startswith("encoder.")}, strict=True)
-    gdec = ref_decoder(ref, gsd)
+    gmodel = ref_grid_model(W.to_torch(W.grid_state_dict(0)))
     grid_len = [17, 9, 2, 0]
     with torch.no_grad():
-        gmem = genc.eval()(imgs)
-        tgt = captions[:, :-1]
-        pad = ref.ViTTransformerCaptioning._generate_padding_mask(None, tgt, [l - 1 for l in grid_len])
-        grid_logits = gdec(tgt, gmem, tgt_mask=gdec.generate_square_subsequent_mask(tgt.size(1), "cpu"),
-                           tgt_key_padding_mask=pad)
+        grid_logits = gmodel(imgs, captions, grid_len)
     np.savez_compressed(os.path.join(HERE, "forward_b4.npz"), captions=caps, vit_lengths=np.array(vit_len),
                         grid_lengths=np.array(grid_len), vit_logits=vit_logits.numpy(),
                         grid_logits=grid_logits.numpy())
     out["forward_b4"] = vit_logits.shape
+
+
+def make_sample(ref, out):
+    # (v) sampled decode: the reference's OWN SCSTLoss._sample_with_log_probs (scst_loss:202-254) on the
+    # reference ViT model in eval mode (dropout off), torch.multinomial replaced during the call by an
+    # inverse-CDF draw on fixed uniforms (one row of uniforms per call = per decode step)
+    scst = load_ref("utils/scst_loss.py", "ref_scst_loss")
+    model = ref_vit_model(ref, W.to_torch(W.vit_state_dict(0)))
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0))
+    u = torch.from_numpy(np.random.Generator(np.random.PCG64(11)).random((29, 4)).astype(np.float32))
+    step = [0]
+    real = torch.multinomial
+
+    def inverse_cdf(probs, num_samples=1, *a, **k):
+        assert num_samples == 1
+        cdf = probs.cumsum(-1)
+        nxt = (cdf <= u[step[0]].unsqueeze(-1) * cdf[:, -1:]).sum(-1).clamp_max(probs.shape[-1] - 1)
+        step[0] += 1
+        return nxt.unsqueeze(1)
+
+    torch.multinomial = inverse_cdf
+    try:
+        with torch.no_grad():
+            generated, lps = scst.SCSTLoss()._sample_with_log_probs(model, imgs, W.START_TOKEN, W.END_TOKEN, 30,
+                                                                   torch.device("cpu"))
+    finally:
+        torch.multinomial = real
+    np.savez_compressed(os.path.join(HERE, "sample_b4.npz"), uniforms=u.numpy(), ids=generated.numpy(),
+                        log_probs=lps.numpy())
+    out["sample_b4"] = generated.shape
+
+
+def make_nomask(ref, out):
+    # scripts/inference.py's OWN generate_caption (inference.py:60-101: no causal mask, B = 1, stops at
+    # <end>, max_len 20 here) on the reference ViT model; words are "w<id>" so the caption maps back to ids
+    import models  # noqa: F401  (the package the reference's `from models.vit_transformer_model` resolves in)
+
+    inf = load_ref("scripts/inference.py", "ref_inference", {"models.vit_transformer_model": ref})
+    model = ref_vit_model(ref, W.to_torch(W.vit_state_dict(0)))
+    vocab = {f"w{i}": i for i in range(W.VOCAB_SIZE)}
+    vocab.update({"<pad>": W.PAD_TOKEN, "<unk>": 106, "<start>": W.START_TOKEN, "<end>": W.END_TOKEN})
+    img = torch.from_numpy(W.synthetic_images(4, seed=0))[0]
+    cap = inf.generate_caption(model, img, vocab, torch.device("cpu"), max_len=20)
+    ids = [vocab[w] for w in cap.split()]
+    np.savez_compressed(os.path.join(HERE, "nomask_b1.npz"), ids=np.array(ids, dtype=np.int64), caption=np.array(cap))
+    out["nomask_b1"] = len(ids)
+
+
+def make_grid(out):
+    # (iv) Grid: the reference's OWN GridTransformerCaptioning (trunk = the torchvision-named restatement)
+    # generate(greedy) at B = 4, its trunk features (B, 2048, 7, 7) and memory, teacher-forced logits of
+    # its ids; then _beam_search (grid:253-322) one image per call as the reference loops, with the
+    # <end> logit raised by END_BIAS so beams finish and the Grid stop tests (completed >= live) fire
+    from oracle import captioner as O
+
+    gsd = W.to_torch(W.grid_state_dict(0))
+    gmodel = ref_grid_model(gsd)
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0))
+    with torch.no_grad():
+        feats = gmodel.encoder.cnn(imgs)
+        gmem = gmodel.encoder(imgs)
+        gids = gmodel.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=30, method="greedy")
+    gtf = teacher_forced(gmodel.decoder, gmem, gids)
+    np.savez_compressed(os.path.join(HERE, "grid_b4.npz"), weights_seed=0, image_seed=0, max_len=30,
+                        ids=gids.numpy(), memory_sum=gmem.double().sum(dim=(1, 2)).numpy(),
+                        memory_head=gmem[:, :4, :16].numpy(), logits_tf=gtf.numpy(), margins=top2(gtf),
+                        trunk_sum=feats.double().sum(dim=(2, 3)).numpy(), trunk_head=feats[:, :8, :, :].numpy())
+    out["grid_b4"] = gids.shape
+    # <end> offsets for the Grid weights: 2.0 / 2.2 end every beam after 9 / 7 tokens (pruning on the way),
+    # 2.8 ends at the first step (the completed-count stop with one token)
+    cases = [(0.0, 3, 0), (0.0, 3, 1), (2.0, 5, 0), (2.0, 5, 1), (2.2, 5, 2), (2.2, 5, 3), (2.8, 5, 0)]
+    rows, lens, margins = [], [], []
+    for delta, k, i in cases:
+        sdb = dict(gsd)
+        fb = sdb["decoder.fc_out.bias"].clone()
+        fb[W.END_TOKEN] += delta
+        sdb["decoder.fc_out.bias"] = fb
+        gmodel.load_state_dict(sdb, strict=True)
+        with torch.no_grad():
+            seq = gmodel.generate(imgs[i:i + 1], W.START_TOKEN, W.END_TOKEN, max_len=30, method="beam_search",
+                                  beam_size=k)
+            _, margin = O.beam_from_memory(sdb, gmodel.encoder(imgs[i:i + 1]), W.START_TOKEN, W.END_TOKEN, 30, k,
+                                           True, return_margins=True)
+        row = np.full(30, -1, dtype=np.int64)
+        row[: seq.shape[1]] = seq[0].numpy()
+        rows.append(row)
+        lens.append(seq.shape[1])
+        margins.append(margin)
+    np.savez_compressed(os.path.join(HERE, "beam_grid.npz"), end_bias=np.array([c[0] for c in cases]),
+                        beam=np.array([c[1] for c in cases]), image=np.array([c[2] for c in cases]),
+                        ids=np.stack(rows), lengths=np.array(lens), margins=np.array(margins))
+    out["beam_grid"] = (len(cases),)
 
 
 def main():
@@ -162,12 +309,20 @@ def main():
     torch.set_num_threads(os.cpu_count() or 8)
     ref = load_ref_vit_module()
     out = {}
-    if sys.argv[1:] == ["forward"]:  # regenerate only the training-forward fixture
+    only = sys.argv[1] if len(sys.argv) > 1 else None
+    if only == "forward":
         make_forward(ref, out)
-        print(out)
-        return
-    if sys.argv[1:] == ["beam_vit"]:  # regenerate only the beam fixture
+    elif only == "beam_vit":
         make_beam(ref, W.to_torch(W.vit_state_dict(0)), torch.from_numpy(W.synthetic_images(4, seed=0)), out)
+    elif only == "grid":
+        make_grid(out)
+    elif only == "sample":
+        make_sample(ref, out)
+    elif only == "nomask":
+        make_nomask(ref, out)
+    elif only is not None:
+        raise SystemExit(f"unknown fixture {only!r}")
+    if only is not None:
         print(out)
         return
 
@@ -197,60 +352,9 @@ def main():
                         logits_causal=causal.numpy(), logits_nomask=nomask.numpy())
     out["decoder_ops"] = causal.shape
 
-    # scripts/inference.py loop (no causal mask, B=1, max_len=20) around the reference decoder
-    nm_ids = []
-    with torch.no_grad():
-        inputs = torch.tensor([[W.START_TOKEN]])
-        for _ in range(20):
-            pid = int(dec(inputs, mem[:1])[:, -1, :].max(1)[1].item())
-            if pid == W.END_TOKEN:
-                break
-            nm_ids.append(pid)
-            inputs = torch.cat([inputs, torch.tensor([[pid]])], dim=1)
-    np.savez_compressed(os.path.join(HERE, "nomask_b1.npz"), ids=np.array(nm_ids, dtype=np.int64))
-    out["nomask_b1"] = len(nm_ids)
-
-    # (v) sampled decode with fixed uniforms (scst_loss:220-249 loop, inverse-CDF draw)
-    u = torch.from_numpy(np.random.Generator(np.random.PCG64(11)).random((29, 4)).astype(np.float32))
-    B = 4
-    generated = torch.full((B, 1), W.START_TOKEN, dtype=torch.long)
-    finished = torch.zeros(B, dtype=torch.bool)
-    lps = []
-    with torch.no_grad():
-        for step in range(29):
-            logits = dec(generated, mem, tgt_mask=dec.generate_square_subsequent_mask(generated.size(1), "cpu"))[:, -1]
-            probs = torch.softmax(logits, -1)
-            cdf = probs.cumsum(-1)
-            nxt = (cdf <= u[step].unsqueeze(-1) * cdf[:, -1:]).sum(-1).clamp_max(W.VOCAB_SIZE - 1)
-            lps.append(torch.log_softmax(logits, -1).gather(1, nxt.unsqueeze(1)).squeeze(1).masked_fill(finished, 0.0))
-            generated = torch.cat([generated, nxt.unsqueeze(1)], dim=1)
-            finished = finished | (nxt == W.END_TOKEN)
-            if bool(finished.all()):
-                break
-    np.savez_compressed(os.path.join(HERE, "sample_b4.npz"), uniforms=u.numpy(), ids=generated.numpy(),
-                        log_probs=torch.stack(lps, 1).numpy())
-    out["sample_b4"] = generated.shape
-
-    # (iv) Grid: reference greedy loop + decoder over the build's GridFeatureEncoder (torch path)
-    from models.grid_transformer_model import GridFeatureEncoder
-
-    gsd = W.to_torch(W.grid_state_dict(0))
-    genc = GridFeatureEncoder(pretrained_cnn=False)
-    genc.load_state_dict({k[len("encoder."):]: v for k, v in gsd.items() if k.startswith("encoder.")}, strict=True)
-    genc.eval()
-    gmodel = ref.ViTTransformerCaptioning.__new__(ref.ViTTransformerCaptioning)
-    nn.Module.__init__(gmodel)
-    gmodel.vocab_size, gmodel.d_model = W.VOCAB_SIZE, 512
-    gmodel.encoder = genc
-    gmodel.decoder = ref_decoder(ref, gsd)
-    with torch.no_grad():
-        gmem = genc(imgs)
-        gids = gmodel.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=30, method="greedy")
-    gtf = teacher_forced(gmodel.decoder, gmem, gids)
-    np.savez_compressed(os.path.join(HERE, "grid_b4.npz"), weights_seed=0, image_seed=0, max_len=30,
-                        ids=gids.numpy(), memory_sum=gmem.double().sum(dim=(1, 2)).numpy(),
-                        memory_head=gmem[:, :4, :16].numpy(), logits_tf=gtf.numpy(), margins=top2(gtf))
-    out["grid_b4"] = gids.shape
+    make_nomask(ref, out)
+    make_sample(ref, out)
+    make_grid(out)
     make_beam(ref, sd, imgs, out)
     make_forward(ref, out)
     for k, v in out.items():

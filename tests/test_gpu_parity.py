@@ -286,6 +286,30 @@ def test_beam_search_grid_variant_vs_oracle(cuda, vit_sd):
             assert int(lens[i]) == n and np.array_equal(ids[i, :n].cpu().numpy(), ref[0].numpy()), i
 
 
+def test_grid_beam_search_golden(cuda):
+    """The drop-in Grid model's beam search (icap_decode_beam, Grid stop tests, HIP trunk) against the
+    reference's own GridTransformerCaptioning._beam_search (beam_grid.npz, grid:253-322): beams that end
+    after 9 / 7 tokens with pruning, and at the first step; exact wherever the selection margin > 1e-4."""
+    from models.grid_transformer_model import build_model
+
+    g = gold("beam_grid.npz")
+    sd = W.to_torch(W.grid_state_dict(0))
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
+    checked = 0
+    for delta, k, i, row, n, mg in zip(g["end_bias"], g["beam"], g["image"], g["ids"], g["lengths"], g["margins"]):
+        m = build_model(W.VOCAB_SIZE, {"pretrained_cnn": False})
+        m.load_state_dict(_biased(sd, float(delta)))
+        m = m.to(cuda)
+        out = m.generate(imgs[int(i):int(i) + 1], W.START_TOKEN, W.END_TOKEN, max_len=30, method="beam_search",
+                         beam_size=int(k))
+        assert m._hip_cache is not None and out.is_cuda
+        if mg <= 1e-4:
+            continue
+        checked += 1
+        assert out.shape[1] == n and np.array_equal(out[0].cpu().numpy(), row[:n]), (delta, k, i)
+    assert checked >= 5
+
+
 def test_dropin_beam_search_runs_hip(cuda, vit_sd):
     from models.vit_transformer_model import build_model
 

@@ -1,0 +1,174 @@
+"""HIP path vs the oracle at the per-GPU workloads of the BASELINE configs, EVERY row checked.
+
+  config 2  ViT-B/16 + decoder, B = 256, greedy max_len 30 (also config 4's per-rank shard: 256 rows of
+            the 2048-image batch; the gather + batch-global stop rule is the gloo test in test_host.py)
+  config 3  Grid (ResNet-101) + decoder, B = 256, greedy; the trunk features compared directly
+  config 5  ViT SCST reward step per rank: 128 rows, sampled decode + greedy baseline (the two decode
+            graphs replayed concurrently, as bench --mode scst) + CIDEr-D on the GPU vs the host
+
+The oracle (oracle/captioner.py, fp32) runs on the GPU here - the same device-agnostic torch code; gfx950
+has no TF32, so torch fp32 is fp32 - and is tied to its CPU run on a few rows of each workload.
+
+Checks and tolerances (north star: logits within 1e-3, token ids identical):
+  * memory (B, S, 512): max |HIP - oracle| < 1e-3 over all rows; Grid trunk features relative 1e-3,
+    and every image's error is < 1/10 of its distance to the nearest other image (an image mix-up
+    cannot pass);
+  * greedy: the oracle's teacher-forced logits on the HIP ids (every row, every step) within 1e-3 of
+    the HIP step logits; each HIP token = the oracle argmax wherever the oracle's top-2 margin exceeds
+    2x the measured logit error (then by induction the HIP ids ARE the oracle's greedy ids up to the
+    first near-tie; the number of such gated steps is asserted tiny);
+  * sampled: each HIP token = the oracle's inverse-CDF draw on the same uniform wherever the draw is
+    further than 2x the measured probability error from a CDF boundary; log-probs within 1e-3 (zero
+    after <end>, the reference's masked_fill);
+  * CIDEr-D: the GPU pass equals the host restatement to 1e-9 on the decoded ids.
+"""
+import numpy as np
+import pytest
+import torch
+
+from image_caption_amd import weights as W
+from oracle import captioner as O
+
+pytestmark = pytest.mark.gpu
+L = 30
+
+
+def _dev_sd(sd, dev):
+    return {k: v.to(dev) for k, v in sd.items()}
+
+
+@pytest.fixture(scope="module")
+def vit_sd():
+    return W.to_torch(W.vit_state_dict(0))
+
+
+@pytest.fixture(scope="module")
+def grid_sd():
+    return W.to_torch(W.grid_state_dict(0))
+
+
+def _oracle_memory(fn, sd_dev, imgs, chunk=64):
+    with torch.no_grad():
+        return torch.cat([fn(sd_dev, imgs[i:i + chunk]) for i in range(0, imgs.shape[0], chunk)])
+
+
+def _check_greedy(ids, step_logits, sd_dev, mem_o, end):
+    """ids (B, L) int32 HIP greedy output; step_logits (L-1, B, V) its per-step logits."""
+    ids = ids.long()
+    tf = O.teacher_forced_logits(sd_dev, mem_o, ids)                      # (B, L-1, V)
+    hip = step_logits.permute(1, 0, 2)
+    err = (hip - tf).abs().max().item()
+    assert err < 1e-3, f"step logits vs oracle {err}"
+    top = tf.topk(2, dim=-1)
+    margin = top.values[..., 0] - top.values[..., 1]
+    sure = margin > 2 * max(err, 1e-6)
+    agree = ids[:, 1:] == top.indices[..., 0]
+    assert bool(agree[sure].all()), f"{int((~agree & sure).sum())} confident steps disagree"
+    gated = int((~sure).sum())
+    assert gated <= max(2, ids.numel() // 500), f"{gated} near-tie steps"
+    return err, gated
+
+
+def test_config2_vit_b256_every_row(cuda, vit_sd):
+    from image_caption_amd.engine import Engine
+
+    B = 256
+    eng = Engine(vit_sd, "vit", {}, device=cuda)
+    sdd = _dev_sd(vit_sd, cuda)
+    for seed in (1, 2):  # bench rank 0 / rank 1 shards (config 2, config 4 per rank)
+        imgs = torch.from_numpy(W.synthetic_images(B, seed=seed)).to(cuda)
+        mem = eng.encode(imgs)
+        ids, lg = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L, want_logits=True)
+        mem_o = _oracle_memory(O.vit_encode, sdd, imgs)
+        assert (mem - mem_o).abs().max().item() < 1e-3
+        if seed == 1:  # the GPU-run oracle is the CPU oracle
+            rows = [0, 255]
+            cpu = O.vit_encode(vit_sd, imgs[rows].cpu())
+            assert (cpu - mem_o[rows].cpu()).abs().max().item() < 1e-4
+        _check_greedy(ids, lg, sdd, mem_o, W.END_TOKEN)
+        # the teacher-forced HIP decoder (icap_decoder_forward) on the same ids
+        tf = eng.decoder_forward(ids[:, :-1], mem, causal=True)
+        assert (tf - O.teacher_forced_logits(sdd, mem_o, ids.long())).abs().max().item() < 1e-3
+
+
+def test_config3_grid_b256_trunk_and_every_row(cuda, grid_sd):
+    from image_caption_amd.engine import Engine
+
+    B = 256
+    eng = Engine(grid_sd, "grid", {}, device=cuda)
+    sdd = _dev_sd(grid_sd, cuda)
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=3)).to(cuda)
+    mem, feats = eng.encode_grid_features(imgs)
+    feats_o = _oracle_memory(O.resnet101_trunk, sdd, imgs, chunk=32)
+    scale = feats_o.abs().max().item()
+    per_img = (feats - feats_o).abs().flatten(1).amax(1)
+    assert per_img.max().item() < 1e-3 * scale, per_img.max().item() / scale
+    # discriminative: every image's error is far below its distance to the closest other image
+    fo = feats_o.flatten(1)
+    d = torch.cdist(fo[None], fo[None], p=float("inf"))[0] + torch.eye(B, device=cuda) * 1e30
+    assert bool((per_img * 10 < d.amin(1)).all())
+    with torch.no_grad():
+        mem_o = O.grid_encode_tail(sdd, feats_o)
+    assert (mem - mem_o).abs().max().item() < 1e-3
+    rows = [0, 255]
+    with torch.no_grad():
+        cpu = O.grid_encode(grid_sd, imgs[rows].cpu())
+    assert (cpu - mem_o[rows].cpu()).abs().max().item() < 1e-4
+    ids, lg = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L, want_logits=True)
+    _check_greedy(ids, lg, sdd, mem_o, W.END_TOKEN)
+    distinct = len({tuple(r) for r in ids.cpu().tolist()})
+    assert distinct >= 4, distinct  # the rows really differ (the decoder, not the memory, limits variety)
+
+
+def test_config5_scst_reward_step_128_rows(cuda, vit_sd):
+    from image_caption_amd import cider
+    from image_caption_amd.engine import Engine, apply_stop_rule
+    from image_caption_amd.scst import sample_and_greedy
+
+    B = 128
+    eng = Engine(vit_sd, "vit", {}, device=cuda)
+    sdd = _dev_sd(vit_sd, cuda)
+    gen = torch.Generator().manual_seed(5)
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=9)).to(cuda)
+    uni = torch.rand(L - 1, B, generator=gen).to(cuda)
+    mem = eng.encode(imgs)
+    for _ in range(3):  # eager, capture, replay of both decode graphs
+        sid, slp, gid = sample_and_greedy(eng, mem, uni, W.START_TOKEN, W.END_TOKEN, L)
+    torch.cuda.synchronize()
+    mem_o = _oracle_memory(O.vit_encode, sdd, imgs)
+    assert (mem - mem_o).abs().max().item() < 1e-3
+    # sampled rows: the oracle's inverse-CDF draw on the same uniform, gated by the boundary distance
+    s = sid.long()
+    tf = O.teacher_forced_logits(sdd, mem_o, s)                            # (B, L-1, V)
+    probs = torch.softmax(tf, -1)
+    cdf = probs.cumsum(-1)
+    thr = uni.t().unsqueeze(-1) * cdf[..., -1:]
+    draw = (cdf <= thr).sum(-1).clamp_max(W.VOCAB_SIZE - 1)
+    dist = (cdf - thr).abs().amin(-1)
+    lp_o = torch.log_softmax(tf, -1).gather(2, s[:, 1:, None]).squeeze(2)
+    ended = (s[:, 1:] == W.END_TOKEN).long().cumsum(1)
+    before = torch.cat([torch.zeros_like(ended[:, :1]), ended[:, :-1]], 1) > 0
+    lp_o = lp_o.masked_fill(before, 0.0)
+    perr = (slp - lp_o).abs().max().item()
+    assert perr < 1e-3, perr
+    sure = dist > 2e-4
+    assert bool((draw == s[:, 1:])[sure].all())
+    assert int((~sure).sum()) <= 2
+    assert bool((slp[before] == 0).all())
+    # greedy rows (no step logits from the concurrent pair: teacher-forced HIP decoder logits instead)
+    g = gid.long()
+    hip_tf = eng.decoder_forward(gid[:, :-1], mem, causal=True)
+    _check_greedy(gid, hip_tf.permute(1, 0, 2), sdd, mem_o, W.END_TOKEN)
+    # CIDEr-D of both sets (one reference caption per image), GPU pass vs the host restatement
+    refs = [[torch.randint(1, 100, (int(torch.randint(5, 13, (1,), generator=gen)),), generator=gen).tolist()]
+            for _ in range(B)]
+    g = apply_stop_rule(g, W.END_TOKEN)
+    hyp = torch.full((2 * B, L), W.PAD_TOKEN, dtype=torch.int32, device=cuda)
+    hyp[:B, : s.shape[1]] = sid
+    hyp[B:, : g.shape[1]] = g.int()
+    rows, off = cider.pack_references(refs, W.PAD_TOKEN, W.END_TOKEN, W.VOCAB_SIZE)
+    r = cider.cider_d_device(hyp, rows.to(cuda), off.to(cuda), W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN)
+    host = [cider.caption_ids(x, W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN) for x in hyp.cpu().tolist()]
+    want = cider.cider_d(host[:B], refs)[1] + cider.cider_d(host[B:], refs)[1]
+    assert np.abs(r.cpu().numpy() - np.array(want)).max() < 1e-9
+    assert float(np.abs(want).sum()) > 0

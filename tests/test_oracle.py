@@ -40,10 +40,17 @@ def test_vit_greedy_matches_reference(vit_sd):
 
 
 def test_grid_greedy_matches_reference(grid_sd):
+    """grid_b4.npz comes from the reference's own GridTransformerCaptioning (grid:86-110, :222-251); its
+    rows decode different ids, and the trunk features are pinned directly, not only through the tail."""
     g = gold("grid_b4.npz")
     imgs = torch.from_numpy(W.synthetic_images(4, seed=int(g["image_seed"])))
+    feats = O.resnet101_trunk(grid_sd, imgs)
+    assert np.allclose(feats[:, :8].numpy(), g["trunk_head"], atol=2e-5)
+    assert np.allclose(feats.double().sum(dim=(2, 3)).numpy(), g["trunk_sum"], rtol=1e-4, atol=1e-3)
     mem = O.grid_encode(grid_sd, imgs)
+    assert np.allclose(mem[:, :4, :16].numpy(), g["memory_head"], atol=2e-5)
     assert np.allclose(mem.double().sum(dim=(1, 2)).numpy(), g["memory_sum"], rtol=1e-5, atol=1e-2)
+    assert len({tuple(r) for r in g["ids"].tolist()}) >= 3  # image-discriminative fixture
     ids = O.greedy_from_memory(grid_sd, mem, W.START_TOKEN, W.END_TOKEN, int(g["max_len"]))
     assert np.array_equal(ids.numpy(), g["ids"])
     assert np.abs(O.teacher_forced_logits(grid_sd, mem, ids).numpy() - g["logits_tf"]).max() < 1e-4
@@ -175,6 +182,23 @@ def test_beam_search_matches_reference(vit_sd):
         b[W.END_TOKEN] += float(delta)
         sd["decoder.fc_out.bias"] = b
         got = O.beam_from_memory(sd, mem[i:i + 1], W.START_TOKEN, W.END_TOKEN, 30, int(k))
+        assert got.shape[1] == n and np.array_equal(got[0].numpy(), row[:n])
+
+
+def test_grid_beam_search_matches_reference(grid_sd):
+    """oracle.beam_from_memory(grid_variant) vs the reference's own GridTransformerCaptioning._beam_search
+    (grid:253-322): beams ending after 9 / 7 tokens with pruning, and at the first step."""
+    g = gold("beam_grid.npz")
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=0))
+    with torch.no_grad():
+        mem = O.grid_encode(grid_sd, imgs)
+    assert sorted(set(g["lengths"].tolist())) == [2, 8, 10, 30]
+    for delta, k, i, row, n in zip(g["end_bias"], g["beam"], g["image"], g["ids"], g["lengths"]):
+        sd = dict(grid_sd)
+        b = sd["decoder.fc_out.bias"].clone()
+        b[W.END_TOKEN] += float(delta)
+        sd["decoder.fc_out.bias"] = b
+        got = O.beam_from_memory(sd, mem[i:i + 1], W.START_TOKEN, W.END_TOKEN, 30, int(k), grid_variant=True)
         assert got.shape[1] == n and np.array_equal(got[0].numpy(), row[:n])
 
 
