@@ -63,11 +63,36 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# Algorithmic work per caption: encoder FLOPs (MFMA phase) and decode bytes at B = 256
+# (HBM phase: cross-attention memory reads, self-KV reads/writes, amortised weights; KV-cached decoder)
+ENC_FLOP = {"vit": 35.28e9, "grid": 17.58e9}
+DEC_BYTES = {"vit": 83.7e6, "grid": 29.5e6}
+CPU_VALIDATION = os.path.join(ROOT, "profiles", "r02", "cpu_ref_timing.json")
+
+
+def host_threads() -> int:
+    """Threads the CPU baseline may use: the cores this process may run on, capped by OMP_NUM_THREADS
+    when the launcher sets it (the GPU box grants 16 cores of a larger machine and sets it to 16)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds: float, batch: int, max_len: int) -> dict:
     """Oracle (port of the reference algorithm, fp32, full-prefix recompute) on host cores."""
     from oracle import captioner as O
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     torch.set_num_threads(threads)
     sd = W.to_torch(W.vit_state_dict(0))
     imgs = torch.from_numpy(W.synthetic_images(batch, seed=99))
@@ -79,9 +104,19 @@ def cpu_baseline(seconds: float, batch: int, max_len: int) -> dict:
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": round(n * batch / el, 3), "unit": "captions/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/captioner.py greedy_search fp32, {n} call(s) x {batch} images, max_len={max_len}, "
-                      f"{el:.1f} s on {threads} host threads"}
+    out = {"value": round(n * batch / el, 3), "unit": "captions/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+           "sample": f"oracle/captioner.py greedy_search fp32, {n} call(s) x {batch} images, max_len={max_len}, "
+                     f"{el:.1f} s on {threads} host threads (affinity {len(os.sched_getaffinity(0))} cores, "
+                     f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')})"}
+    try:  # the container-side check of the port against the reference's own generate (tools/cpu_ref_timing.py)
+        with open(CPU_VALIDATION) as f:
+            v = json.load(f)
+        out["port_vs_reference"] = {"ratio": v["oracle_over_reference"], "threads": v["threads"],
+                                    "cpu_model": v["cpu_model"], "source": "profiles/r02/cpu_ref_timing.json"}
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def main():
@@ -134,11 +169,28 @@ def main():
                 return eng.encode(trunk(imgs))
         return eng.encode(imgs)
 
+    # phase events of the timed greedy steps (torch's current stream = the stream libicap launches on;
+    # the decode graph's second chain forks from and joins back into it)
+    phase_ev, recording = [], [False]
+
+    def mark():
+        if not recording[0]:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
     def step():
+        e0 = mark()
         mem = encode()
+        e1 = mark()
         ids, _ = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L)
+        e2 = mark()
         if ws > 1:
             ids = parallel.gather_rows(ids, total)
+        e3 = mark()
+        if recording[0]:
+            phase_ev.append((e0, e1, e2, e3))
         return apply_stop_rule(ids.long(), W.END_TOKEN)
 
     if args.mode == "beam":
@@ -204,6 +256,7 @@ def main():
     torch.cuda.synchronize()
 
     eng.profile(True)
+    recording[0] = True
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -218,8 +271,49 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
+    recording[0] = False
     prof = [eng.profile_read(c) for c in sorted(_lib.PROF_NAMES)]
     eng.profile(False)
+    phases = None
+    if phase_ev:  # encoder = MFMA-bound phase, decode = HBM-bound phase (SURVEY.md §8(d) phase-wise roofline)
+        n = len(phase_ev)
+        enc_ms = sum(a.elapsed_time(b) for a, b, _, _ in phase_ev) / n
+        dec_ms = sum(b.elapsed_time(c) for _, b, c, _ in phase_ev) / n
+        gat_ms = sum(c.elapsed_time(d) for _, _, c, d in phase_ev) / n
+        if ws > 1:  # the slowest rank's phases
+            t = torch.tensor([enc_ms, dec_ms, gat_ms], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            enc_ms, dec_ms, gat_ms = t.tolist()
+        enc_tf = ENC_FLOP[args.model] * B / (enc_ms * 1e-3) / 1e12
+        dec_gbs = DEC_BYTES[args.model] * B / (dec_ms * 1e-3) / 1e9
+        phases = {
+            "encoder": {"ms_per_step": round(enc_ms, 3), "bound": "mfma", "achieved": round(enc_tf, 1),
+                        "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(enc_tf / PEAK_BF16_TFLOPS, 4),
+                        "work": f"{ENC_FLOP[args.model] / 1e9:.2f} GFLOP/image algorithmic (SURVEY.md 8d) x {B}"},
+            "decode": {"ms_per_step": round(dec_ms, 3), "bound": "hbm", "achieved": round(dec_gbs, 1),
+                       "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(dec_gbs / PEAK_HBM_GBS, 4),
+                       "work": f"{DEC_BYTES[args.model] / 1e6:.1f} MB/caption algorithmic (SURVEY.md 8d) x {B}, "
+                               f"{L - 1} steps"},
+            "allgather_ms_per_step": round(gat_ms, 3),
+        }
+    # multi-GPU self-check: the stop rule on the gathered ids equals the all-reduce form of SURVEY.md §8(e)
+    # (each rank's per-column "every row ended" mask AND-reduced over ranks), so the line can be verified alone
+    stop_check = None
+    if args.mode == "greedy" and pipe is None:
+        mem = encode()
+        ids, _ = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L)
+        col = (ids[:, 1:] == W.END_TOKEN).all(dim=0).to(torch.int32)
+        if ws > 1:
+            dist.all_reduce(col, op=dist.ReduceOp.MIN)
+            gathered = parallel.gather_rows(ids, total)
+        else:
+            gathered = ids
+        hit = torch.nonzero(col)
+        want = int(hit[0, 0]) + 2 if hit.numel() else L
+        stop_check = {"ranks": ws, "per_rank_batch": B, "gathered_rows": int(gathered.shape[0]),
+                      "output_len": int(apply_stop_rule(gathered.long(), W.END_TOKEN).shape[1]),
+                      "allreduce_len": want}
+        stop_check["ok"] = stop_check["output_len"] == want and stop_check["gathered_rows"] == total
     value = total * args.steps / el
     if rank == 0:
         step_ms = el / args.steps * 1e3
@@ -227,6 +321,8 @@ def main():
         headline = args.model == "vit" and args.mode == "greedy"  # the PMC summary's workload
         avg_ms = dom["ms"] / max(dom["launches"], 1)
         for p in prof:
+            if not p["launches"]:
+                continue
             log(f"  {p['kernel']:34s} launches {p['launches']:6d}  {p['ms'] / args.steps:9.3f} ms/step  "
                 f"{p['flops'] / max(p['ms'], 1e-9) / 1e9:9.1f} TFLOP/s alg  "
                 f"{p['bytes'] / max(p['ms'], 1e-9) / 1e6:9.1f} GB/s operand")
@@ -272,6 +368,10 @@ def main():
                        "pipelined": pipe is not None},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if phases is not None:
+            line["roofline"]["phases"] = phases
+        if stop_check is not None:
+            line["config"]["multi_gpu_check"] = stop_check
         print(json.dumps(line), flush=True)
     if ws > 1:
         dist.barrier()

@@ -51,13 +51,13 @@ def linear(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
 
 
 def layer_norm(x: Tensor, w: Tensor, b: Tensor, eps: float) -> Tensor:
-    mu = x.mean(-1, keepdim=True)
-    var = ((x - mu) ** 2).mean(-1, keepdim=True)
-    return (x - mu) / torch.sqrt(var + eps) * w + b
+    """(x - mean) / sqrt(biased var + eps) * w + b over the last dim (torch's LayerNorm definition)."""
+    return torch.nn.functional.layer_norm(x, (x.shape[-1],), w, b, eps)
 
 
 def gelu_erf(x: Tensor) -> Tensor:
-    return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))
+    """0.5 x (1 + erf(x / sqrt 2)) - the exact GELU of torchvision's MLPBlock."""
+    return torch.nn.functional.gelu(x)
 
 
 def mha(q_in: Tensor, kv_in: Tensor, in_w: Tensor, in_b: Tensor, out_w: Tensor,
@@ -68,12 +68,20 @@ def mha(q_in: Tensor, kv_in: Tensor, in_w: Tensor, in_b: Tensor, out_w: Tensor,
     B, T, D = q_in.shape
     S = kv_in.shape[1]
     hd = D // nhead
-    q = linear(q_in, in_w[:D], in_b[:D])
-    k = linear(kv_in, in_w[D:2 * D], in_b[D:2 * D])
-    v = linear(kv_in, in_w[2 * D:], in_b[2 * D:])
-    q = q.view(B, T, nhead, hd).transpose(1, 2)
-    k = k.view(B, S, nhead, hd).transpose(1, 2)
-    v = v.view(B, S, nhead, hd).transpose(1, 2)
+    if q_in is kv_in:  # self-attention: one packed projection (the same products as three)
+        q, k, v = linear(q_in, in_w, in_b).chunk(3, dim=-1)
+    else:
+        q = linear(q_in, in_w[:D], in_b[:D])
+        k, v = linear(kv_in, in_w[D:], in_b[D:]).chunk(2, dim=-1)
+    q = q.reshape(B, T, nhead, hd).transpose(1, 2)
+    k = k.reshape(B, S, nhead, hd).transpose(1, 2)
+    v = v.reshape(B, S, nhead, hd).transpose(1, 2)
+    if key_pad is None:  # softmax(q k^T / sqrt(hd) [+ causal -inf]) v as one fused CPU primitive
+        causal_mask = None
+        if causal:
+            causal_mask = torch.ones(T, S, dtype=torch.bool, device=q.device).tril(S - T)
+        o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=causal_mask)
+        return linear(o.transpose(1, 2).reshape(B, T, D), out_w, out_b)
     s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
     if causal:
         m = torch.ones(T, S, dtype=torch.bool, device=s.device).triu(1 + S - T)
