@@ -151,9 +151,12 @@ def test_config5_scst_reward_step_128_rows(cuda, vit_sd):
     lp_o = lp_o.masked_fill(before, 0.0)
     perr = (slp - lp_o).abs().max().item()
     assert perr < 1e-3, perr
-    sure = dist > 2e-4
+    # the CDF of the HIP softmax is within max|logit error| of the oracle's (|d cdf| <= sum_k p_k |d z_k|)
+    lerr = (eng.decoder_forward(sid[:, :-1], mem, causal=True) - tf).abs().max().item()
+    assert lerr < 1e-3, lerr
+    sure = dist > 2 * max(lerr, 1e-6)
     assert bool((draw == s[:, 1:])[sure].all())
-    assert int((~sure).sum()) <= 2
+    assert int((~sure).sum()) <= max(2, s.numel() // 500), int((~sure).sum())
     assert bool((slp[before] == 0).all())
     # greedy rows (no step logits from the concurrent pair: teacher-forced HIP decoder logits instead)
     g = gid.long()
