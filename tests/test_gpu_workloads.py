@@ -151,10 +151,12 @@ def test_config5_scst_reward_step_128_rows(cuda, vit_sd):
     lp_o = lp_o.masked_fill(before, 0.0)
     perr = (slp - lp_o).abs().max().item()
     assert perr < 1e-3, perr
-    # the CDF of the HIP softmax is within max|logit error| of the oracle's (|d cdf| <= sum_k p_k |d z_k|)
-    lerr = (eng.decoder_forward(sid[:, :-1], mem, causal=True) - tf).abs().max().item()
-    assert lerr < 1e-3, lerr
-    sure = dist > 2 * max(lerr, 1e-6)
+    # per step, the draw is decided wherever the threshold is further from every CDF boundary than twice
+    # that step's HIP-vs-oracle CDF difference (HIP teacher-forced logits on the same prefix)
+    hip_lg = eng.decoder_forward(sid[:, :-1], mem, causal=True)
+    assert (hip_lg - tf).abs().max().item() < 1e-3
+    cdf_err = (torch.softmax(hip_lg, -1).cumsum(-1) - cdf).abs().amax(-1)
+    sure = dist > 2 * cdf_err + 1e-7
     assert bool((draw == s[:, 1:])[sure].all())
     assert int((~sure).sum()) <= max(2, s.numel() // 500), int((~sure).sum())
     assert bool((slp[before] == 0).all())
