@@ -131,6 +131,8 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graphs", action="store_true", help="launch the decode loop eagerly (no hipGraph)")
+    ap.add_argument("--decode-chains", type=int, default=0,
+                    help="independent decode chains per batch (icap_set_decode_chains; 0 = library default)")
     ap.add_argument("--model", default="vit", choices=["vit", "grid"])
     ap.add_argument("--torch-trunk", action="store_true", help="grid: ResNet trunk via PyTorch/MIOpen fp32")
     ap.add_argument("--mode", default="greedy", choices=["greedy", "scst", "beam"])
@@ -158,6 +160,8 @@ def main():
         trunk = genc.cnn.to(dev).eval()
     if args.no_graphs:
         eng.set_graphs(False)
+    if args.decode_chains:
+        eng.set_decode_chains(args.decode_chains)
     B = args.batch
     total = B * ws
     imgs = torch.from_numpy(W.synthetic_images(B, seed=1 + rank)).to(dev)

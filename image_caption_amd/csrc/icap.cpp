@@ -714,7 +714,7 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
   }
 }
 
-constexpr int MAX_KSPLIT = 8;
+constexpr int MAX_KSPLIT = 16;  // partial slabs: split-K GEMMs, 8 heads (dec_sa), 16 hidden slices (dec_ffn)
 
 struct DecodeBufs {
   float *x, *qkv, *kc, *vc, *part;
@@ -795,17 +795,33 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
   const size_t kv_layer = b.kvl;
   const long PS = b.PS;  // partial slab stride
   const int KS_D = 4, KS_F = 8;    // split-K of the K=512 and K=dim_ff residual GEMMs
+  // one new token per sequence (the decode loops): the fused self-attention and feed-forward blocks
+  // (decode.hip); the teacher-forced / padded forms keep the separate GEMM + attention launches
+  const bool fused = n_new == 1 && !klen && causal && D == 512 && H == 8 && F == 2048 && t0 < 64 && t0 < Lmax;
   for (int l = 0; l < d.n_dec_layers; ++l) {
     const DecLayer& L = h->dec[l];
     // self-attention block
-    h->wgemm(b.a, D, b.aL, L.sa_qkv.w, D, L.sa_qkv.b, rows, 3 * D, D, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, WAVE_2x2,
-             1, 0, s);
-    HIPCHK(launch_dec_self_attn(b.qkv, B, n_new, t0, H, b.kc + l * kv_layer, b.vc + l * kv_layer, Lmax, causal,
-                                0.125f, b.o, b.aL, ns, s, anc, klen));
-    h->wgemm(b.o, D, b.aL, L.sa_out.w, D, nullptr, rows, D, D, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_D,
-             PS, s);
-    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_D, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
-                                     ns, s));
+    if (fused) {
+      DecSaArgs sa{};
+      sa.A = b.a; sa.aL = b.aL; sa.nsplit = ns; sa.rows = rows;
+      sa.Wqkv = L.sa_qkv.w; sa.bqkv = L.sa_qkv.b; sa.Wo = L.sa_out.w;
+      sa.kc = b.kc + l * kv_layer; sa.vc = b.vc + l * kv_layer; sa.Lmax = Lmax; sa.t0 = t0; sa.scale = 0.125f;
+      sa.anc = anc;
+      sa.part = b.part; sa.part_stride = PS;
+      h->timed(PROF_DEC_FUSED, 2.0 * rows * (3.0 * D * D + (double)D * D), 2.0 * (4.0 * D * D + (double)rows * D * ns),
+               s, [&] { HIPCHK(launch_dec_sa(sa, s)); });
+      HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
+                                       ns, s));
+    } else {
+      h->wgemm(b.a, D, b.aL, L.sa_qkv.w, D, L.sa_qkv.b, rows, 3 * D, D, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, WAVE_2x2,
+               1, 0, s);
+      HIPCHK(launch_dec_self_attn(b.qkv, B, n_new, t0, H, b.kc + l * kv_layer, b.vc + l * kv_layer, Lmax, causal,
+                                  0.125f, b.o, b.aL, ns, s, anc, klen));
+      h->wgemm(b.o, D, b.aL, L.sa_out.w, D, nullptr, rows, D, D, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_D,
+               PS, s);
+      HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_D, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
+                                       ns, s));
+    }
     // cross-attention block (key-absorbed)
     // per head, one launch: q_h = a Wq_h^T + bq_h, then qt[:, h*D:(h+1)*D] = q_h Wk_h (bf16 planes)
     {
@@ -835,11 +851,22 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
     HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL, ns,
                                      s));
     // feed-forward block
-    h->wgemm(b.a, D, b.aL, L.lin1.w, D, L.lin1.b, rows, F, D, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, WAVE_2x2, 1, 0, s);
-    h->wgemm(b.hb, F, b.hL, L.lin2.w, F, nullptr, rows, D, F, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_F, PS,
-             s);
-    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_F, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a, b.aL,
-                                     ns, s));
+    if (fused) {
+      DecFfnArgs ff{};
+      ff.A = b.a; ff.aL = b.aL; ff.nsplit = ns; ff.rows = rows;
+      ff.W1 = L.lin1.w; ff.b1 = L.lin1.b; ff.W2 = L.lin2.w;
+      ff.part = b.part; ff.part_stride = PS;
+      h->timed(PROF_DEC_FUSED, 4.0 * rows * (double)D * F, 2.0 * (2.0 * D * F + (double)rows * D * ns), s,
+               [&] { HIPCHK(launch_dec_ffn(ff, s)); });
+      HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, F / 128, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a,
+                                       b.aL, ns, s));
+    } else {
+      h->wgemm(b.a, D, b.aL, L.lin1.w, D, L.lin1.b, rows, F, D, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, WAVE_2x2, 1, 0, s);
+      h->wgemm(b.hb, F, b.hL, L.lin2.w, F, nullptr, rows, D, F, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_F,
+               PS, s);
+      HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_F, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a, b.aL,
+                                       ns, s));
+    }
   }
 }
 

@@ -85,7 +85,7 @@ hipError_t launch_layernorm_i8(const float* x, long ldx, int rows, int D, int in
 // fp32 [N][K] rows -> int8 two-slice row images (same layout, K % 64 == 0) + per-row scale
 hipError_t launch_pack_i8_rows(const float* w, int N, int K, int8_t* out, float* scale, hipStream_t s);
 enum { PROF_GEMM_128 = 0, PROF_GEMM_64 = 1, PROF_ENC_ATTN = 2, PROF_CROSS_ATTN = 3, PROF_GEMM_WAVE = 4, PROF_GEMM_256 = 5,
-       PROF_GEMM_I8 = 6 };
+       PROF_GEMM_I8 = 6, PROF_DEC_FUSED = 7 };
 
 // Decode-step GEMM: each wave streams a (16 TM) x (16 TN) tile's operands into registers (no LDS);
 // block = 4 waves along N.  ksplit > 1 with out = OUT_PARTIAL writes fp32 partial slabs
@@ -122,6 +122,25 @@ struct ChainArgs {
   int M, N2, H, nsplit, out;
 };
 hipError_t launch_chain_dec(const ChainArgs& a, hipStream_t s);
+
+// Fused decode-step blocks (decode.hip), d_model 512, 8 heads of 64, dim_ff 2048, one new token per row.
+// dec_sa: q|k|v of head h for 16 rows (Wqkv [1536][512] bf16, bqkv fp32), the new key/value appended to
+// the fp32 cache kc/vc [rows][8][Lmax][64] at t0 (anc: beam ancestry as dec_self_attn), causal attention
+// over positions 0..t0 (t0 < 64), and slab h of the out-projection part[h][rows][512] (Wo [512][512]).
+struct DecSaArgs {
+  const bf16_t* A; long aL; int nsplit, rows;
+  const bf16_t* Wqkv; const float* bqkv; const bf16_t* Wo;
+  float *kc, *vc; int Lmax, t0; float scale; const int32_t* anc;
+  float* part; long part_stride;
+};
+hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s);
+// dec_ffn: slab j of 16 = relu(a W1[128j:128j+128]^T + b1) W2[:, 128j:128j+128]^T -> part[j][rows][512]
+struct DecFfnArgs {
+  const bf16_t* A; long aL; int nsplit, rows;
+  const bf16_t* W1; const float* b1; const bf16_t* W2;
+  float* part; long part_stride;
+};
+hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s);
 
 // LayerNorm over rows of D fp32 values; optional fp32 output (may alias input) and
 // bf16 hi(/lo) planes.  Input row r is read from (r / in_group) * in_stride + in_off + r % in_group.

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void pack_i8_rows_kernel(const float* __restri
 // D / 4 threads per row (each thread owns 4 consecutive columns), so a decode step's few hundred
 // rows spread over every CU and each lane issues all its loads (x, bias, up to 8 partial slabs) at
 // once: the kernel costs one memory latency, not one per slab.
-constexpr int RLN_MAX_PARTS = 8;
+constexpr int RLN_MAX_PARTS = 16;
 
 template <int NT>
 __global__ __launch_bounds__(NT) void residual_layernorm_kernel(float* __restrict__ x, int rows,
