@@ -5,7 +5,7 @@
 // memory round trip (profiles/r02: QKV GEMM 9.7 us, self-attention 5.8, out-projection 4.8, FFN-1 10.4,
 // FFN-2 10.3 at 256 rows).  These kernels fuse what is row-local:
 //
-//   dec_sa_kernel   block = (16 rows, head h):  q|k|v_h = a Wqkv_h^T + b   (12 column tiles, K = 512)
+//   dec_sa_kernel   block = (16 rows, head h):  q|k|v_h = a Wqkv_h^T + b   (K = 512)
 //                   -> append k, v to the fp32 KV cache at position t0 -> causal attention over the
 //                   t0 + 1 cached keys (one wave per row) -> slab h = ctx_h Wo[:, 64h:64h+64]^T
 //                   (the out-projection as a split-K over heads; residual_layernorm sums the 8 slabs
@@ -13,162 +13,224 @@
 //   dec_ffn_kernel  block = (16 rows, hidden slice j of 128): h_j = relu(a W1_j^T + b1_j), then
 //                   slab j = h_j W2[:, 128j:128j+128]^T (split-K over the 16 slices of dim_ff = 2048)
 //
-// Every weight fragment a wave multiplies is loaded straight into its VGPRs at kernel start (one
-// global_load_dwordx4 per fragment, all in flight at once; no LDS ring, no barrier in the k-loop);
-// the activation rows (a bf16 planes, 16 rows x 512) are DMA'd to LDS once and shared.  So a launch
-// is one memory round trip plus the MFMA chain.  Block order puts the 16 row tiles of one head (SA)
-// or of one slice pair (FFN) on one XCD (blocks b, b + 8, ... share an XCD under round-robin dispatch),
-// so each XCD's L2 serves that weight slice to all of them (speed only; correctness does not depend
-// on placement).
+// Staging (tools/probe_ingest.hip, profiles/r02/probe_ingest.txt): with every CU loading at once, load
+// instructions that each cover 16 rows x 64 B (the MFMA fragment shape) move 8 TB/s chip-wide, ones that
+// cover whole 128-B lines 18-19 TB/s.  So every operand is LDS-DMA'd in 64-deep k-steps as 128-B row
+// images (one instruction = 8 rows x 128 B; 16-byte chunk c of row r stored at c ^ ((r >> 1) & 7), the
+// conflict-free swizzle of the int8 encoder GEMM) and fragments are read from LDS.  A block does two DMA
+// rounds (the weights of a head / slice do not fit 160 KiB next to the activation rows at once).
+// Block order puts the 16 row tiles of one head (SA) or slice pair (FFN) on one XCD (blocks b, b + 8,
+// ... share an XCD under round-robin dispatch) so its L2 serves that slice (speed only).
 //
 // MFMA convention (as gemm_dec_kernel): D = W . X^T with W as the A operand, so lane l holds output
 // row m = l & 15 and the four consecutive output columns n = 4 (l >> 4) + r -> 16-byte stores.
-// LDS image of X per 32-deep k-step and plane: 16 rows x 64 B, 16-byte chunk c of row r at
-// c ^ ((r >> 2) & 3) (conflict-free fragment reads).
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 
 constexpr int DEC_D = 512, DEC_H = 8, DEC_HD = 64, DEC_F = 2048;
-constexpr int DEC_ROWS = 16;    // rows per block
-constexpr int DEC_KS = DEC_D / 32;  // k-steps of the D-wide products
+constexpr int DEC_ROWS = 16;           // rows per block
+constexpr int DEC_K64 = DEC_D / 64;    // 64-deep k-steps of the D-wide products
+constexpr int DEC_LDS = 160 * 1024;    // both kernels: 128 KiB weight region + 32 KiB row region
 
-// X (16 rows x 512, ns planes at plane stride aL) -> LDS [ks][plane][16 rows][64 B], by all 16 waves
-__device__ __forceinline__ void stage_rows(const bf16_t* A, long aL, int ns, int row0, int rows, char* sx) {
+// One DMA instruction: rows 8i .. 8i + 7 x 128 B of src (row stride ld bytes) into the LDS image
+// dst[rows][128 B] (chunk swizzle c ^ ((r >> 1) & 7)).
+__device__ __forceinline__ void dma_8rows(const char* src, long ld, int i, char* dst) {
+  const int lane = threadIdx.x & 63;
+  const int r = i * 8 + (lane >> 3), pos = lane & 7;
+  const char* s = src + (long)r * ld + ((pos ^ ((r >> 1) & 7)) << 4);
+  __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)s, (LDS_AS void*)(dst + i * 1024), 16, 0, 0);
+}
+// nrows x 128 B, instructions spread over the 16 waves starting at wave `first` (balance across calls)
+__device__ __forceinline__ void dma_rows(const char* src, long ld, int nrows, char* dst, int first = 0) {
+  const int wave = threadIdx.x >> 6;
+  for (int i = (wave - first) & 15; i < nrows / 8; i += 16) dma_8rows(src, ld, i, dst);
+}
+
+// MFMA operand fragment of a 128-B-row image: rows r0 + (l & 15), 32-deep half hf of the 64-deep step
+__device__ __forceinline__ bf16x8 frag(const char* img, int r0, int hf) {
+  const int lane = threadIdx.x & 63, r = r0 + (lane & 15), c = hf * 4 + (lane >> 4);
+  return *(const bf16x8*)(img + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+}
+
+// The a rows (16 x 512, row stride ld elements, ns planes at plane stride aL) -> X image [8 k64][ns][16][128 B]
+__device__ __forceinline__ void dma_x(const bf16_t* A, long aL, int ns, int row0, int rows, char* sx,
+                                      long ld = DEC_D) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int lrow = lane >> 2, lchunk = (lane & 3) ^ ((lrow >> 2) & 3);
-  const int r = min(row0 + lrow, rows - 1);
-  for (int q = wave; q < DEC_KS * ns; q += 16) {
-    const int ks = q / ns, pl = q - ks * ns;
-    const bf16_t* src = A + pl * aL + (long)r * DEC_D + ks * 32 + lchunk * 8;
-    __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)(sx + q * 1024), 16, 0, 0);
+  const int lr = lane >> 3, pos = lane & 7;
+  for (int i = wave; i < DEC_K64 * ns * 2; i += 16) {  // 2 instructions (16 rows) per (k64, plane)
+    const int kp = i >> 1, half = i & 1, k64 = kp / ns, pl = kp - k64 * ns;
+    const int r = half * 8 + lr, gr = min(row0 + r, rows - 1);
+    const char* s = (const char*)(A + pl * aL + (long)gr * ld + k64 * 64) + ((pos ^ ((r >> 1) & 7)) << 4);
+    __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)s, (LDS_AS void*)(sx + kp * 2048 + half * 1024), 16, 0, 0);
   }
 }
 
-// B-operand fragment (row m = l & 15, 8 k values of chunk l >> 4) of k-step ks, plane pl
-__device__ __forceinline__ bf16x8 x_frag(const char* sx, int ns, int ks, int pl) {
-  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
-  return *(const bf16x8*)(sx + (ks * ns + pl) * 1024 + fr * 64 + ((fq ^ ((fr >> 2) & 3)) << 4));
-}
-
-// write v (this lane's 4 consecutive columns n0..n0+3 of row m) as bf16 planes into an LDS operand
-// image with k = column: [ks][plane][16 rows][64 B] (same layout as x_frag reads)
+// write v (this lane's 4 consecutive columns n0..n0+3 of row m) as bf16 planes into a 128-B-row operand
+// image with k = column: [k64][ns][16 rows][128 B]
 __device__ __forceinline__ void put_planes(char* img, int ns, int m, int n0, f32x4 v) {
   bf16_t h[4], l[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) split_bf(v[r], h[r], l[r]);
-  const int ks = n0 >> 5, c = (n0 & 31) >> 3;
-  char* dst = img + ks * ns * 1024 + m * 64 + ((c ^ ((m >> 2) & 3)) << 4) + (n0 & 7) * 2;
+  const int k64 = n0 >> 6, c = (n0 & 63) >> 3;
+  char* dst = img + k64 * ns * 2048 + m * 128 + ((c ^ ((m >> 1) & 7)) << 4) + (n0 & 7) * 2;
   *(u32x2*)dst = (u32x2){(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
   if (ns == 2)
-    *(u32x2*)(dst + 1024) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
+    *(u32x2*)(dst + 2048) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
+}
+
+// acc += W-image tile (rows w0.., k64 range) x X-image (16 rows), both planes of X
+__device__ __forceinline__ f32x4 mma_rows(f32x4 acc, const char* wimg, int wrows, int w0, const char* ximg, int ns,
+                                          int k0, int k1) {
+#pragma unroll 2
+  for (int k = k0; k < k1; ++k) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const bf16x8 b = frag(wimg + k * wrows * 128, w0, hf);
+      acc = mfma16(b, frag(ximg + k * ns * 2048, 0, hf), acc);
+      if (ns == 2) acc = mfma16(b, frag(ximg + k * ns * 2048 + 2048, 0, hf), acc);
+    }
+  }
+  return acc;
 }
 
 // ------------------------------------------------------------------------------------------------
-// Self-attention block of one decode step.  LDS: X image 32 KiB (reused for the q|k|v rows after
-// the projection), ctx image 4 KiB.
+// Self-attention block of one decode step.
+//   round 1: X image (32 KiB, region B) + Wq_h, Wk_h images [8 k64][128 rows][128 B] (region A)
+//   round 2: Wv_h [8 k64][64 rows][128 B] + Wo[:, 64h:64h+64] [512 rows][128 B] (region A)
+//   then q|k|v rows fp32 [16][192] + ctx image in region B
 __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sx = smem;                                  // X image, then qkv fp32 [16][192]
-  float* qkv = (float*)smem;
-  char* sc = smem + DEC_KS * 2 * 1024;              // ctx image [2 ks][ns][16][64 B]
+  char* ra = smem;                        // 128 KiB weight region
+  char* sx = smem + 128 * 1024;           // 32 KiB row region
+  float* qkv = (float*)sx;                // after the v projection: [16][192]
+  char* sc = sx + 16 * 192 * 4;           // ctx image [1 k64][ns][16][128 B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int h = blockIdx.x & (DEC_H - 1), row0 = (blockIdx.x >> 3) * DEC_ROWS;
   const int ns = p.nsplit;
+  const char* wq = (const char*)(p.Wqkv + (long)(h * DEC_HD) * DEC_D);
+  const char* wk = (const char*)(p.Wqkv + (long)(DEC_D + h * DEC_HD) * DEC_D);
+  const char* wv = (const char*)(p.Wqkv + (long)(2 * DEC_D + h * DEC_HD) * DEC_D);
 
-  stage_rows(p.A, p.aL, ns, row0, p.rows, sx);
-  // weight fragments: waves 0..11 -> q|k|v column tile (wave >> 2) x 16 + ..., all 16 k-steps
-  bf16x8 wf[DEC_KS];
-  if (wave < 12) {
-    const int which = wave >> 2;  // 0 q, 1 k, 2 v
-    const bf16_t* wr = p.Wqkv + (long)(which * DEC_D + h * DEC_HD + (wave & 3) * 16 + fr) * DEC_D + fq * 8;
-#pragma unroll
-    for (int ks = 0; ks < DEC_KS; ++ks) wf[ks] = *(const bf16x8*)(wr + ks * 32);
+  dma_x(p.A, p.aL, ns, row0, p.rows, sx);
+  for (int k = 0; k < DEC_K64; ++k) {  // Wq_h, Wk_h: image [k64][128 rows] (q rows 0..63, k rows 64..127)
+    dma_rows(wq + k * 128, DEC_D * 2, 64, ra + k * 128 * 128, 8 * (2 * k) + 2);
+    dma_rows(wk + k * 128, DEC_D * 2, 64, ra + k * 128 * 128 + 64 * 128, 8 * (2 * k + 1) + 2);
   }
-  // out-projection fragments: output columns 32 wave + 16 i + (lane & 15), k = this head's 64
-  bf16x8 of[2][2];
+  // the cached keys / values of positions < t0 of this wave's row (it attends for row row0 + wave below) do
+  // not depend on this step: fetch the first 32 positions now, while the projections are staged.  Lane l
+  // holds key / value j = 4 i + (l >> 4), dims 4 (l & 15) ..; 16 lanes read one 256-B row.
+  constexpr int PRE = 8;
+  const int dq = (lane & 15) * 4, jg = lane >> 4;
+  const int brow = row0 + wave, t0 = p.t0;
+  f32x4 kpre[PRE], vpre[PRE];
+  const long own = ((long)brow * DEC_H + h) * p.Lmax * DEC_HD;
+  auto hist = [&](const float* cache, int j) -> f32x4 {  // cached row of position j < t0 (lane's 4 dims)
+    const long rb = p.anc ? ((long)p.anc[(long)brow * p.Lmax + j] * DEC_H + h) * p.Lmax * DEC_HD : own;
+    return *(const f32x4*)(cache + rb + (long)j * DEC_HD + dq);
+  };
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      of[i][ks] = *(const bf16x8*)(p.Wo + (long)(wave * 32 + i * 16 + fr) * DEC_D + h * DEC_HD + ks * 32 + fq * 8);
+  for (int i = 0; i < PRE; ++i) {  // keys now, values at the start of the attention (register budget)
+    const int j = 4 * i + jg;
+    kpre[i] = brow < p.rows && j < t0 ? hist(p.kc, j) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-
-  // ---- q | k | v projection (16 rows x 192 columns of head h)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (wave < 12) {
-#pragma unroll
-    for (int ks = 0; ks < DEC_KS; ++ks) {
-      acc = mfma16(wf[ks], x_frag(sx, ns, ks, 0), acc);
-      if (ns == 2) acc = mfma16(wf[ks], x_frag(sx, ns, ks, 1), acc);
-    }
-    const int which = wave >> 2, n = (wave & 3) * 16 + 4 * fq;
-    acc += *(const f32x4*)(p.bqkv + which * DEC_D + h * DEC_HD + n);
-  }
+  if (wave < 8) acc = mma_rows(acc, ra, 128, wave * 16, sx, ns, 0, DEC_K64);  // q tiles 0..3, k tiles 4..7
+  __syncthreads();  // Wq / Wk no longer read
+  for (int k = 0; k < DEC_K64; ++k) dma_rows(wv + k * 128, DEC_D * 2, 64, ra + k * 64 * 128, 8 * k);
+  dma_rows((const char*)(p.Wo + h * DEC_HD), DEC_D * 2, DEC_D, ra + DEC_K64 * 64 * 128);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wave >= 8 && wave < 12) acc = mma_rows(acc, ra, 64, (wave - 8) * 16, sx, ns, 0, DEC_K64);  // v tiles
   __syncthreads();  // X image no longer read: it becomes the q|k|v rows
-  if (wave < 12) *(f32x4*)(qkv + fr * 192 + wave * 16 + 4 * fq) = acc;
+  if (wave < 12) {
+    const int c = wave * 16 + 4 * fq;  // column in [q | k | v] of this head
+    acc += *(const f32x4*)(p.bqkv + (c >> 6) * DEC_D + h * DEC_HD + (c & 63));
+    *(f32x4*)(qkv + fr * 192 + c) = acc;
+  }
   __syncthreads();
 
-  // ---- attention, one wave per row (torch's causal SDPA of the new position over positions 0..t0)
+  // ---- attention, one wave per row (torch's causal SDPA of the new position over positions 0..t0).
+  // The cached keys / values of a (row, head) are [t0][64] fp32 rows: lane l reads 16-byte chunk
+  // c = l + 64 i, i.e. key j = c >> 4, dims 4 (c & 15) ..; 16 lanes hold one key (1 KiB per instruction).
   {
-    const int r = wave, b = row0 + r;
-    const int t0 = p.t0, nkeys = t0 + 1;
+    const int r = wave, b = brow, nkeys = t0 + 1;
     const float* qr = qkv + r * 192;
-    float ctx = 0.f, l = 1.f;
+    f32x4 ctx = {0.f, 0.f, 0.f, 0.f};
+    float l = 1.f;
     if (b < p.rows) {
-      const long cache = ((long)b * DEC_H + h) * p.Lmax * DEC_HD;
-      p.kc[cache + (long)t0 * DEC_HD + lane] = qr[64 + lane];   // this step's key / value
-      p.vc[cache + (long)t0 * DEC_HD + lane] = qr[128 + lane];
-      float s = -INFINITY;
-      if (lane < nkeys) {
-        const float* kr;
-        if (lane == t0) kr = qr + 64;
-        else if (p.anc) kr = p.kc + ((long)p.anc[(long)b * p.Lmax + lane] * DEC_H + h) * p.Lmax * DEC_HD + (long)lane * DEC_HD;
-        else kr = p.kc + cache + (long)lane * DEC_HD;
-        float a = 0.f;
-#pragma unroll
-        for (int d = 0; d < DEC_HD; d += 4) {
-          const f32x4 kv = *(const f32x4*)(kr + d);
-          a = fmaf(qr[d], kv[0], a);
-          a = fmaf(qr[d + 1], kv[1], a);
-          a = fmaf(qr[d + 2], kv[2], a);
-          a = fmaf(qr[d + 3], kv[3], a);
-        }
-        s = a * p.scale;
+      if (lane < 16) {  // this step's key / value into the cache
+        *(f32x4*)(p.kc + own + (long)t0 * DEC_HD + dq) = *(const f32x4*)(qr + 64 + dq);
+        *(f32x4*)(p.vc + own + (long)t0 * DEC_HD + dq) = *(const f32x4*)(qr + 128 + dq);
       }
-      const float m = wave_max(s);
-      const float e = lane < nkeys ? __expf(s - m) : 0.f;
+#pragma unroll
+      for (int i = 0; i < PRE; ++i) {
+        const int j = 4 * i + jg;
+        vpre[i] = j < t0 ? hist(p.vc, j) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+      const f32x4 q4 = *(const f32x4*)(qr + dq);
+      const f32x4 kcur = *(const f32x4*)(qr + 64 + dq), vcur = *(const f32x4*)(qr + 128 + dq);
+      // scores: lane j of the wave ends up holding score j.  Keys j = 4 i + jg: the first PRE x 4 from the
+      // prefetched registers (unrolled, so they stay in VGPRs), any later ones straight from the cache
+      float s_mine = -INFINITY;
+      auto score = [&](int i, f32x4 k4) {
+        float part = q4[0] * k4[0];
+        part = fmaf(q4[1], k4[1], part);
+        part = fmaf(q4[2], k4[2], part);
+        part = fmaf(q4[3], k4[3], part);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);  // sum over the key's 16 lanes
+        // scores of keys 4i..4i+3 sit in lanes 0, 16, 32, 48: lane j takes key j's
+        const float sc = __shfl(part, ((lane - 4 * i) & 3) * 16, 64);
+        if (lane >= 4 * i && lane < 4 * i + 4) s_mine = lane < nkeys ? sc * p.scale : -INFINITY;
+      };
+      auto pick = [&](int j, f32x4 cur, f32x4 pre) -> f32x4 {
+        return j == t0 ? cur : (j > t0 ? (f32x4){0.f, 0.f, 0.f, 0.f} : pre);
+      };
+#pragma unroll
+      for (int i = 0; i < PRE; ++i)
+        if (4 * i < nkeys) score(i, pick(4 * i + jg, kcur, kpre[i]));
+      for (int i = PRE; 4 * i < nkeys; ++i) {
+        const int j = 4 * i + jg;
+        const f32x4 k4 = j < t0 ? hist(p.kc, j) : kcur;
+        score(i, pick(j, kcur, k4));
+      }
+      const float m = wave_max(s_mine);
+      const float e = lane < nkeys ? __expf(s_mine - m) : 0.f;
       l = wave_sum(e);
-      // context (lane = d): sum_j p_j v_j[d] (p_j from lane j); v of position t0 from LDS, older from the cache
-      for (int j = 0; j < nkeys; ++j) {
-        float v;
-        if (j == t0) v = qr[128 + lane];
-        else if (p.anc) v = p.vc[((long)p.anc[(long)b * p.Lmax + j] * DEC_H + h) * p.Lmax * DEC_HD + (long)j * DEC_HD + lane];
-        else v = p.vc[cache + (long)j * DEC_HD + lane];
-        ctx = fmaf(__shfl(e, j, 64), v, ctx);
+      // context: lane accumulates dims dq..dq+3 over keys j = 4 i + jg, then the 4 key groups are summed
+#pragma unroll
+      for (int i = 0; i < PRE; ++i)
+        if (4 * i < nkeys) {
+          const int j = 4 * i + jg;
+          ctx += __shfl(e, min(j, 63), 64) * pick(j, vcur, vpre[i]);
+        }
+      for (int i = PRE; 4 * i < nkeys; ++i) {
+        const int j = 4 * i + jg;
+        const f32x4 v4 = j < t0 ? hist(p.vc, j) : vcur;
+        ctx += __shfl(e, min(j, 63), 64) * pick(j, vcur, v4);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        ctx[k] += __shfl_xor(ctx[k], 16, 64);
+        ctx[k] += __shfl_xor(ctx[k], 32, 64);
       }
       ctx /= l;
     }
-    // ctx row r (lane = d) -> operand image (k = d); lanes 4g..4g+3 gather 4 consecutive d
-    f32x4 c4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) c4[i] = __shfl(ctx, (lane & ~3) + i, 64);
-    if ((lane & 3) == 0) put_planes(sc, ns, r, lane, c4);
+    if (lane < 16) put_planes(sc, ns, r, dq, ctx);
   }
   __syncthreads();
 
-  // ---- out-projection slab of head h: 16 rows x 512 columns, K = 64
+  // ---- out-projection slab of head h: 16 rows x 512 columns, K = 64 (one k64 step)
+  const char* wo = ra + DEC_K64 * 64 * 128;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      o = mfma16(of[i][ks], x_frag(sc, ns, ks, 0), o);
-      if (ns == 2) o = mfma16(of[i][ks], x_frag(sc, ns, ks, 1), o);
-    }
+    o = mma_rows(o, wo, DEC_D, wave * 32 + i * 16, sc, ns, 0, 1);
     const int row = row0 + fr;
     if (row < p.rows)
       *(f32x4*)(p.part + (long)h * p.part_stride + (long)row * DEC_D + wave * 32 + i * 16 + 4 * fq) = o;
@@ -176,43 +238,32 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Feed-forward block of one decode step.  LDS: X image 32 KiB, k-half reduction 8 KiB, h image 8 KiB.
+// Feed-forward block of one decode step.
+//   round 1: X image (region B) + W1 slice [8 k64][128 rows][128 B] (region A)
+//   round 2: W2 slice [2 k64][512 rows][128 B] (region A); h image + k-half reduction in region B
 __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sx = smem;
-  f32x4* red = (f32x4*)(smem + DEC_KS * 2 * 1024);   // [8 tiles][64 lanes]
-  char* sh = (char*)(red + 8 * 64);                  // h image [4 ks][ns][16][64 B]
+  char* ra = smem;
+  char* sx = smem + 128 * 1024;
+  f32x4* red = (f32x4*)sx;                 // after FFN-1: [8 tiles][64 lanes]
+  char* sh = sx + 8 * 64 * 16;             // h image [2 k64][ns][16][128 B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int nslice = DEC_F / 128;
   const int j = blockIdx.x % nslice, row0 = (blockIdx.x / nslice) * DEC_ROWS;
   const int ns = p.nsplit;
 
-  stage_rows(p.A, p.aL, ns, row0, p.rows, sx);
-  // FFN-1 fragments: tile t = wave & 7 (hidden units 128 j + 16 t ..), k-half kh = wave >> 3
-  const int t = wave & 7, kh = wave >> 3;
-  bf16x8 w1[8];
-  {
-    const bf16_t* wr = p.W1 + (long)(j * 128 + t * 16 + fr) * DEC_D + kh * 256 + fq * 8;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) w1[ks] = *(const bf16x8*)(wr + ks * 32);
-  }
-  // FFN-2 fragments: output columns 32 wave + 16 i + (lane & 15), k = hidden units of slice j
-  bf16x8 w2[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      w2[i][ks] = *(const bf16x8*)(p.W2 + (long)(wave * 32 + i * 16 + fr) * DEC_F + j * 128 + ks * 32 + fq * 8);
+  dma_x(p.A, p.aL, ns, row0, p.rows, sx);
+  const char* w1 = (const char*)(p.W1 + (long)j * 128 * DEC_D);
+  for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 128, ra + k * 128 * 128);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-
+  const int t = wave & 7, kh = wave >> 3;  // FFN-1 tile, k half (4 of the 8 k64 steps)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    acc = mfma16(w1[ks], x_frag(sx, ns, kh * 8 + ks, 0), acc);
-    if (ns == 2) acc = mfma16(w1[ks], x_frag(sx, ns, kh * 8 + ks, 1), acc);
-  }
+  acc = mma_rows(acc, ra, 128, t * 16, sx, ns, kh * 4, kh * 4 + 4);
+  __syncthreads();  // W1 and X no longer read
+  const char* w2 = (const char*)(p.W2 + (long)j * 128);
+  for (int k = 0; k < 2; ++k) dma_rows(w2 + k * 128, DEC_F * 2, DEC_D, ra + k * DEC_D * 128);
   if (kh) red[t * 64 + lane] = acc;
   __syncthreads();
   if (!kh) {
@@ -223,36 +274,119 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
     for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r], 0.f);
     put_planes(sh, ns, fr, n, acc);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      o = mfma16(w2[i][ks], x_frag(sh, ns, ks, 0), o);
-      if (ns == 2) o = mfma16(w2[i][ks], x_frag(sh, ns, ks, 1), o);
-    }
+    o = mma_rows(o, ra, DEC_D, wave * 32 + i * 16, sh, ns, 0, 2);
     const int row = row0 + fr;
     if (row < p.rows)
       *(f32x4*)(p.part + (long)j * p.part_stride + (long)row * DEC_D + wave * 32 + i * 16 + 4 * fq) = o;
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Chained per-head products of the cross-attention block (replaces chain_dec_kernel on the decode path):
+//   Y_h = X_h W1_h^T + b1_h (16 x 64, K = 512), O_h = Y_h W2_h^T (16 x 512, K = 64)
+// block = (16 rows, head h), one DMA round: X image 32 KiB + W1_h [8 k64][64][128 B] 64 KiB +
+// W2_h [512 rows][128 B] 64 KiB.  out = OUT_SPLIT (q~ planes of head h) or OUT_PARTIAL (slab h).
+__global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* w1i = smem;                       // 64 KiB
+  char* w2i = smem + 64 * 1024;           // 64 KiB
+  char* sx = smem + 128 * 1024;           // 32 KiB: X image, then the k-quarter reduction + Y image
+  f32x4* red = (f32x4*)sx;                // [3 quarters][4 tiles][64 lanes]
+  char* sy = sx + 12 * 64 * 16;           // Y image [1 k64][ns][16][128 B]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int h = blockIdx.x % p.H, row0 = (blockIdx.x / p.H) * DEC_ROWS;
+  const int ns = p.nsplit;
+  dma_x(p.X + (long)h * p.x_hstride, p.x_lo, ns, row0, p.M, sx, p.ldx);
+  const char* w1 = (const char*)(p.W1 + (long)h * 64 * DEC_D);
+  for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 64, w1i + k * 64 * 128, 8 * k + 2);
+  dma_rows((const char*)(p.W2 + (long)h * p.w2_hstride), p.ldw2 * 2, DEC_D, w2i, 2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int t = wave & 3, kq = wave >> 2;  // Y tile, k quarter (2 of the 8 k64 steps)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = mma_rows(acc, w1i, 64, t * 16, sx, ns, kq * 2, kq * 2 + 2);
+  __syncthreads();  // X no longer read
+  if (kq) red[((kq - 1) * 4 + t) * 64 + lane] = acc;
+  __syncthreads();
+  if (!kq) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) acc += red[(q * 4 + t) * 64 + lane];
+    const int n = t * 16 + 4 * fq;
+    acc += *(const f32x4*)(p.b1 + h * 64 + n);
+    put_planes(sy, ns, fr, n, acc);
+  }
+  __syncthreads();
+  const int row = row0 + fr;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+    o = mma_rows(o, w2i, DEC_D, wave * 32 + i * 16, sy, ns, 0, 1);
+    const int col = wave * 32 + i * 16 + 4 * fq;
+    if (row >= p.M) continue;
+    if (p.out == OUT_PARTIAL) {
+      *(f32x4*)((float*)p.C + (long)h * p.part_stride + (long)row * p.ldc + col) = o;
+    } else {
+      bf16_t hv[4], lv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) split_bf(o[r], hv[r], lv[r]);
+      bf16_t* dst = (bf16_t*)p.C + (long)row * p.ldc + (long)h * p.c_hstride + col;
+      *(u32x2*)dst = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+      if (ns == 2)
+        *(u32x2*)(dst + p.c_lo) =
+            (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N2 != DEC_D || a.H <= 0 || (a.nsplit != 1 && a.nsplit != 2)) return hipErrorInvalidValue;
+  if (a.out != OUT_PARTIAL && a.out != OUT_SPLIT) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)dec_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             DEC_LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int blocks = (a.M + DEC_ROWS - 1) / DEC_ROWS * a.H;
+  hipLaunchKernelGGL(dec_chain_kernel, dim3(blocks), dim3(1024), DEC_LDS, s, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s) {
   if (a.rows <= 0 || a.t0 < 0 || a.t0 >= a.Lmax || a.t0 >= 64 || (a.nsplit != 1 && a.nsplit != 2))
     return hipErrorInvalidValue;
-  const int lds = DEC_KS * 2 * 1024 + 2 * 2 * 1024;
+  static bool attr = false;
+  if (!attr) {
+    for (const void* f : {(const void*)dec_sa_kernel, (const void*)dec_ffn_kernel}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, DEC_LDS);
+      if (e != hipSuccess) return e;
+    }
+    attr = true;
+  }
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * DEC_H;
-  hipLaunchKernelGGL(dec_sa_kernel, dim3(blocks), dim3(1024), lds, s, a);
+  hipLaunchKernelGGL(dec_sa_kernel, dim3(blocks), dim3(1024), DEC_LDS, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s) {
   if (a.rows <= 0 || (a.nsplit != 1 && a.nsplit != 2)) return hipErrorInvalidValue;
-  const int lds = DEC_KS * 2 * 1024 + 8 * 64 * 16 + 4 * 2 * 1024;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)dec_ffn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             DEC_LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * (DEC_F / 128);
-  hipLaunchKernelGGL(dec_ffn_kernel, dim3(blocks), dim3(1024), lds, s, a);
+  hipLaunchKernelGGL(dec_ffn_kernel, dim3(blocks), dim3(1024), DEC_LDS, s, a);
   return hipGetLastError();
 }

@@ -353,10 +353,11 @@ struct icap_handle {
     const double bytes = 2.0 * batch * ((double)M * K * ns + (double)N * K);
     timed(PROF_GEMM_WAVE, flops, bytes, s, [&] { HIPCHK(launch_gemm_dec(g, s)); });
   }
-  void chain(const ChainArgs& a, hipStream_t s) {
+  void chain(const ChainArgs& a, hipStream_t s, bool fused = false) {
     const double flops = 2.0 * a.M * a.H * (64.0 * 512 + (double)a.N2 * 64);
     const double bytes = 2.0 * a.H * ((double)a.M * 512 * ns + 64.0 * 512 + (double)a.N2 * 64);
-    timed(PROF_GEMM_WAVE, flops, bytes, s, [&] { HIPCHK(launch_chain_dec(a, s)); });
+    if (fused) timed(PROF_DEC_FUSED, flops, bytes, s, [&] { HIPCHK(launch_dec_chain(a, s)); });
+    else timed(PROF_GEMM_WAVE, flops, bytes, s, [&] { HIPCHK(launch_chain_dec(a, s)); });
   }
   void attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, bf16_t* out, long out_ld, long out_lo,
                  hipStream_t s, int head_major = 0) {
@@ -831,7 +832,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.W2 = L.ca_kT; c.ldw2 = 64; c.w2_hstride = (long)D * 64;
       c.C = b.qt; c.ldc = (long)H * D; c.c_lo = b.cL; c.c_hstride = D;
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_SPLIT;
-      h->chain(c, s);
+      h->chain(c, s, fused);
     }
     h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * ns * (double)(rows / n_new) * S * D, s, [&] {
       HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, mem_rpi, S, 0.125f, b.c, b.cL, ns, s,
@@ -846,7 +847,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.W2 = L.ca_out.w; c.ldw2 = D; c.w2_hstride = 64;
       c.C = b.part; c.ldc = D; c.part_stride = PS;
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_PARTIAL;
-      h->chain(c, s);
+      h->chain(c, s, fused);
     }
     HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL, ns,
                                      s));

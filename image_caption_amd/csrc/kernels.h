@@ -141,6 +141,9 @@ struct DecFfnArgs {
   float* part; long part_stride;
 };
 hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s);
+// The chained per-head cross-attention products (ChainArgs as launch_chain_dec, N2 = 512) with 16-row
+// blocks and one full-line DMA round (decode.hip); used by the decode loops.
+hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s);
 
 // LayerNorm over rows of D fp32 values; optional fp32 output (may alias input) and
 // bf16 hi(/lo) planes.  Input row r is read from (r / in_group) * in_stride + in_off + r % in_group.
