@@ -41,7 +41,7 @@ METRIC = "captions/sec (224×224, max_len=30, greedy) at 1/2/4/8 MI355X vs CPU r
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA, MI355X_MICROARCH.md chip table
 PEAK_I8_TOPS = 5000.0      # dense i8 MFMA (2x bf16 per clock: 16x16x64 i8 = cycles of 16x16x32 bf16), same table
 PEAK_HBM_GBS = 8000.0
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")  # collected on the default (f16) bench
 
 
 def pmc_traffic(kernel: str, headline: bool = True):
@@ -126,7 +126,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--max-len", type=int, default=30)
-    ap.add_argument("--precision", default="i8x2", choices=sorted(_lib.PRECISIONS))
+    ap.add_argument("--precision", default="f16", choices=sorted(_lib.PRECISIONS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -340,10 +340,10 @@ def main():
             # products (A1.W1, A1.W2, A2.W1) against the i8 peak - reported as mfma_issue_frac.
             i8 = "i8" in dom["kernel"]
             peak = PEAK_I8_TOPS if i8 else PEAK_BF16_TFLOPS
-            work = 3 if i8 else (1 if args.precision == "bf16" else 2)
+            work = 3 if i8 else (1 if args.precision in ("bf16", "f16") else 2)
             achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
             roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak,
-                    "unit": "TFLOP/s", "peak_dtype": "i8" if i8 else "bf16", "frac": round(achieved / peak, 4),
+                    "unit": "TFLOP/s", "peak_dtype": "i8" if i8 else ("f16" if args.precision == "f16" else "bf16"), "frac": round(achieved / peak, 4),
                     "traffic": pmc_traffic(dom["kernel"], headline),
                     "mfma_products_per_alg_mac": work, "mfma_issue_frac": round(achieved * work / peak, 4)}
         roof.update({"kernel": dom["kernel"], "launches_per_step": dom["launches"] // args.steps,
@@ -351,7 +351,7 @@ def main():
                      "share_of_step": round(dom["ms"] / args.steps / step_ms, 3)})
         cpu = None
         if roof["traffic"] is not None:
-            roof["traffic_unit"] = "bytes/launch (HBM-side, rocprofv3 PMC, profiles/r01/pmc_traffic.json)"
+            roof["traffic_unit"] = "bytes/launch (HBM-side, rocprofv3 PMC, profiles/r02/pmc_traffic.json)"
         if ws == 1 and not args.no_cpu_baseline and args.model == "vit":
             cpu = cpu_baseline(args.cpu_seconds, args.cpu_batch, L)
         line = {
@@ -360,7 +360,7 @@ def main():
             "value": round(value, 2), "unit": "images/s" if args.mode == "scst" else "captions/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None,
-            "dtype": {"bf16": "bf16", "bf16x2": "bf16x2", "i8x2": "i8x2+bf16x2"}[args.precision], "data": "synthetic images N(0,1) + seeded random-init weights",
+            "dtype": {"bf16": "bf16", "bf16x2": "bf16x2", "i8x2": "i8x2+bf16x2", "f16": "f16+bf16x2"}[args.precision], "data": "synthetic images N(0,1) + seeded random-init weights",
             "config": {"workload": ("vit_b16 encoder + 6-layer decoder, greedy, 224x224, max_len=30" if args.model == "vit"
                                     else f"grid resnet101 ({'torch/MIOpen fp32' if args.torch_trunk else 'HIP'}) "
                                          "+ 6-layer encoder + 6-layer decoder, greedy, 224x224, max_len=30")

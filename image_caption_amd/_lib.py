@@ -16,8 +16,8 @@ LIB_PATH = Path(__file__).resolve().parent / "libicap.so"
 ABI_VERSION = 2
 
 KIND_VIT, KIND_GRID = 0, 1
-PREC_BF16, PREC_BF16X2, PREC_I8X2 = 1, 2, 3
-PRECISIONS = {"bf16": PREC_BF16, "bf16x2": PREC_BF16X2, "i8x2": PREC_I8X2}
+PREC_BF16, PREC_BF16X2, PREC_I8X2, PREC_F16 = 1, 2, 3, 4
+PRECISIONS = {"bf16": PREC_BF16, "bf16x2": PREC_BF16X2, "i8x2": PREC_I8X2, "f16": PREC_F16}
 PROF_GEMM_128, PROF_GEMM_64, PROF_ENC_ATTN, PROF_CROSS_ATTN, PROF_GEMM_WAVE, PROF_GEMM_256 = 0, 1, 2, 3, 4, 5
 PROF_GEMM_I8 = 6
 PROF_DEC_FUSED = 7

@@ -295,7 +295,7 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(const float* __restri
 // (image, head)'s K and V rows are contiguous 128-byte rows; else row-major [token][3 D].
 // QPW query tiles per wave: 16 / QPW waves per block (QPW = 2: 8 waves, two blocks per CU).
 
-template <bool SPLIT, bool HM, int QPW>
+template <bool SPLIT, bool HM, int QPW, bool F16 = false>
 __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pipe_kernel(
     const bf16_t* __restrict__ qkv, long ld, long lo, int N, int H, float scale, bf16_t* out, long out_ld,
     long out_lo) {
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
         for (int ks = 0; ks < 2; ++ks) {
           const int off = row * 128 + (((ks * 4 + g) ^ kswz(row)) << 4);
           const bf16x8 kh = *(const bf16x8*)(Kh + off);
-          acc = mfma16(kh, qh[t][ks], acc);
+          acc = mma<F16>(kh, qh[t][ks], acc);
           if (SPLIT) {
             const bf16x8 kl = *(const bf16x8*)(Kl + off);
             acc = mfma16(kl, qh[t][ks], acc);
@@ -422,13 +422,18 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
           l[t] += e;
         }
       bf16x8 ph, pl;
+      if constexpr (F16) {  // probabilities as one fp16 plane
+        const u32x2 p0 = pack16x4<true>(s[0]), p1 = pack16x4<true>(s[1]);
+        ph = __builtin_bit_cast(bf16x8, (u32x4){p0[0], p0[1], p1[0], p1[1]});
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        ph[j] = (__bf16)s[0][j];
-        ph[4 + j] = (__bf16)s[1][j];
-        if (SPLIT) {
-          pl[j] = (__bf16)(s[0][j] - (float)ph[j]);
-          pl[4 + j] = (__bf16)(s[1][j] - (float)ph[4 + j]);
+        for (int j = 0; j < 4; ++j) {
+          ph[j] = (__bf16)s[0][j];
+          ph[4 + j] = (__bf16)s[1][j];
+          if (SPLIT) {
+            pl[j] = (__bf16)(s[0][j] - (float)ph[j]);
+            pl[4 + j] = (__bf16)(s[1][j] - (float)ph[4 + j]);
+          }
         }
       }
       const int key0 = 4 * g + q4;  // and key0 + 16: the same swizzle (vswz has period 8)
@@ -437,7 +442,7 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
         const int off0 = key0 * 128 + (((dt * 2 + (p4 >> 1)) ^ vswz(key0)) << 4) + (p4 & 1) * 8;
         const int off1 = off0 + 16 * 128;
         const bf16x8 vh = tr_pair(Vh + off0, Vh + off1);
-        o[t][dt] = mfma16(vh, ph, o[t][dt]);
+        o[t][dt] = mma<F16>(vh, ph, o[t][dt]);
         if (SPLIT) {
           const bf16x8 vl = tr_pair(Vl + off0, Vl + off1);
           o[t][dt] = mfma16(vl, ph, o[t][dt]);
@@ -459,10 +464,14 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
       bf16_t* dst = out + ((long)b * N + qq) * out_ld + h * 64;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
+        const int d = dt * 16 + 4 * g;
+        if constexpr (F16) {
+          *(u32x2*)(dst + d) = pack16x4<true>(o[t][dt] * inv);
+          continue;
+        }
         bf16_t hv[4], lv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) split_bf(o[t][dt][r] * inv, hv[r], lv[r]);
-        const int d = dt * 16 + 4 * g;
         *(u32x2*)(dst + d) = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
         if (SPLIT)
           *(u32x2*)(dst + out_lo + d) =
@@ -500,6 +509,17 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
   if (N <= 64) {
     return nsplit == 2 ? run_enc<4, true>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s)
                        : run_enc<4, false>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s);
+  }
+  if (nsplit == NS_F16) {  // one fp16 plane (ICAP_PREC_F16 encoder): the pipelined form, one query tile per wave
+    if (N > 256) return hipErrorInvalidValue;
+    const int lds = 4 * 2 * 32 * 128;
+    if (head_major)
+      hipLaunchKernelGGL((enc_attention_pipe_kernel<false, true, 1, true>), dim3(H, B), dim3(1024), lds, s, qkv, ld, lo,
+                         N, H, scale, out, out_ld, out_lo);
+    else
+      hipLaunchKernelGGL((enc_attention_pipe_kernel<false, false, 1, true>), dim3(H, B), dim3(1024), lds, s, qkv, ld,
+                         lo, N, H, scale, out, out_ld, out_lo);
+    return hipGetLastError();
   }
   static const int pipe = icap_knob("ICAP_ENC_ATTN_PIPE", 1);  // 0: the stage-everything form for N > 64
   // ICAP_ENC_ATTN_QPW: query tiles per wave (1: 16 waves, 2: 8 waves, 2 blocks/CU)

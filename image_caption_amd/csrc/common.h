@@ -57,6 +57,35 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// fp16 single-plane operands (ICAP_PREC_F16 encoder): the same 16-bit storage type carries fp16 bits;
+// mma<F16> picks the MFMA, cvt16<F16> / pack16x4<F16> the conversion (both round to nearest even).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+template <bool F16>
+__device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16_t f2h(float f) { return __builtin_bit_cast(bf16_t, (_Float16)f); }
+__device__ __forceinline__ float h2f(bf16_t u) { return (float)__builtin_bit_cast(_Float16, u); }
+template <bool F16>
+__device__ __forceinline__ bf16_t cvt16(float f) {
+  if constexpr (F16) return f2h(f);
+  else return f2bf(f);
+}
+template <bool F16>
+__device__ __forceinline__ u32x2 pack16x4(f32x4 v) {
+  if constexpr (F16) {
+    const f16x2v a = {(_Float16)v[0], (_Float16)v[1]}, b = {(_Float16)v[2], (_Float16)v[3]};
+    return (u32x2){__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b)};
+  } else {
+    return (u32x2){pack_bf2((f32x2){v[0], v[1]}), pack_bf2((f32x2){v[2], v[3]})};
+  }
+}
+
 // GELU(v) = v/2 (1 + erf(v / sqrt 2)) with erfc from the Chebyshev fit of Numerical Recipes §6.2
 // (fractional error < 1.2e-7 everywhere): one rcp, one exp, 10 FMA, no branches - well inside the
 // bf16x2 planes' 2^-17 the value is stored with.  ocml's erff costs several times that in the

@@ -201,6 +201,7 @@ int gemm_tile_class(const GemmArgs& g) {
   // 256 x 256 tiles whenever N allows and there are >= 96 of them (trunk sweep, profiles/r01
   // v6_trunk_class_sweep.txt: even 98-196 tiles beat 4x as many 128 x 128 tiles); 128 x 128 only for
   // N >= 256 (at N = 128 the 64 x 64 kernel is faster)
+  if (g.f16) return PROF_GEMM_256;  // the fp16 forms live in launch_gemm_256
   const long huge_tiles = (long)((g.M + 255) / 256) * (g.N / 256) * g.batch;
   if (g.N % 256 == 0 && g.batch == 1 && huge_tiles >= 96) return PROF_GEMM_256;
   const long big_tiles = (long)((g.M + 127) / 128) * (g.N / 128) * g.batch;
@@ -623,7 +624,7 @@ hipError_t launch_chain_dec(const ChainArgs& a, hipStream_t s) {
 // vmcnt(0) after each load).  Rows >= M load from row M - 1 and are not stored.
 namespace {
 
-template <int TM, int TN>
+template <int TM, int TN, bool F16 = false>
 __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM][TN], int mb, int nb, int fr,
                                              int fq) {
   const int M = p.M;
@@ -728,6 +729,13 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
         for (int i = 0; i < 4; ++i)
           if (orow[i0 + i] >= 0) *(f32x4*)(C + orow[i0 + i] + nb + j * 16 + 4 * fq) = c[i] + acc[i0 + i][j];
       }
+  } else if (F16) {  // one fp16 plane
+    bf16_t* C = (bf16_t*)p.C;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        if (orow[i] >= 0) *(u32x2*)(C + orow[i] + nb + j * 16 + 4 * fq) = pack16x4<true>(acc[i][j]);
   } else {
     bf16_t* C = (bf16_t*)p.C;
     const bool lo_plane = p.out == OUT_SPLIT && p.c_planes == 2;
@@ -773,7 +781,8 @@ namespace {
 // two blocks each, one per K half.  Both halves leave their fp32 partial tile with agent-scope stores,
 // wait for them to complete and take a ticket; the second adds the other's partial (a + b: the same
 // bits whichever finished first) and runs the epilogue.
-template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0, int KSD = 32, int TS = 0>
+template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0, int KSD = 32, int TS = 0,
+          bool F16 = false>
 __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64 ? 3 : 1)) void gemm_256_kernel(
     GemmArgs p) {
   constexpr int WGM = NW / 4;                       // wave grid WGM x 4
@@ -912,7 +921,7 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
           for (int i = 0; i < TM; ++i) {
             const bf16x8 af = *(const bf16x8*)(s0 + pl * OPB + (wm * WM + i * 16) * 128 + fo);
 #pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af, acc[i][j]);
+            for (int j = 0; j < TN; ++j) acc[i][j] = mma<F16>(bfr[j], af, acc[i][j]);
           }
       }
     } else {
@@ -929,7 +938,7 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
             if (NOMFMA) {  // measurement variant: staging pipeline only (keeps the fragment reads live)
               asm volatile("" ::"v"(af), "v"(bfr[j]));
             } else {
-              acc[i][j] = mfma16(bfr[j], af, acc[i][j]);  // D = W·A^T
+              acc[i][j] = mma<F16>(bfr[j], af, acc[i][j]);  // D = W·A^T
             }
           }
         }
@@ -963,7 +972,7 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
           acc[i][j][e] += __hip_atomic_load(other + ((i * TN + j) * 4 + e) * NT + tid, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
   }
-  epilogue_256<TM, TN>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
+  epilogue_256<TM, TN, F16>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
 }
 
 }  // namespace
@@ -985,7 +994,7 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // K-tiles (K' = nsplit K; the W k-tile is re-staged per plane from L2).
 namespace {
 
-template <bool ROW128>
+template <bool ROW128, bool F16 = false>
 __global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs p) {
   constexpr int BM = 256, BK = 64, KH = 16384, BUF = 65536;  // k-half region, buffer bytes
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1068,7 +1077,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qm * 4 + i][qn * 2 + j] = mfma16(rb[j][kh], ra[i][kh], acc[qm * 4 + i][qn * 2 + j]);
+          acc[qm * 4 + i][qn * 2 + j] = mma<F16>(rb[j][kh], ra[i][kh], acc[qm * 4 + i][qn * 2 + j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -1110,7 +1119,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(GemmArgs p) {
     }
   }
 
-  epilogue_256<8, 4>(p, acc, m0 + wr * 128, n0 + wc * 64, fr, fq);
+  epilogue_256<8, 4, F16>(p, acc, m0 + wr * 128, n0 + wc * 64, fr, fq);
 }
 
 }  // namespace
@@ -1156,6 +1165,29 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
   static const int tall_min_k = icap_knob("ICAP_GEMM_TALL_MIN_K", 128);
   // ICAP_GEMM_TALL_BM: 128 (default) or 64 (64 x 256 tiles, 4 waves, 3 blocks per CU)
   static const int tall_bm = icap_knob("ICAP_GEMM_TALL_BM", 128) == 64 ? 64 : 128;
+  if (g.f16) {  // fp16 single plane (ICAP_PREC_F16 encoder)
+    if (g.nsplit != 1 || g.cv || g.res || g.scale || (g.out == OUT_SPLIT && g.c_planes != 1) || g.K < 128)
+      return hipErrorInvalidValue;
+    // ICAP_F16_GEMM: 0 = 128 x 256 tiles, 2-stage ring, 2 blocks per CU; 1 / 2 = 256 x 256 8-phase (64-B / 128-B LDS rows)
+    static const int form = icap_knob("ICAP_F16_GEMM", 0);
+    if ((form == 1 || form == 2) && g.K % 64 == 0) {
+      static bool attr8 = false;
+      if (!attr8) {
+        for (const void* f : {(const void*)gemm_8ph_kernel<false, true>, (const void*)gemm_8ph_kernel<true, true>})
+          if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 131072) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr8 = true;
+      }
+      const int nwg8 = (g.N / 256) * ((g.M + 255) / 256);
+      if (form == 2) hipLaunchKernelGGL((gemm_8ph_kernel<true, true>), dim3(nwg8), dim3(512), 131072, s, g);
+      else hipLaunchKernelGGL((gemm_8ph_kernel<false, true>), dim3(nwg8), dim3(512), 131072, s, g);
+      return hipGetLastError();
+    }
+    const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
+    constexpr int ldsh1 = 2 * (128 * 32 * 2 + 256 * 32 * 2);
+    hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 0, true>), dim3(nwgh), dim3(512), ldsh1, s, g);
+    return hipGetLastError();
+  }
   if (tall_min_k && g.K >= tall_min_k && (nw == 8 || nw == 16) && tall_bm == 64 && !g.cv) {
     const int nwgq = (g.N / 256) * ((g.M + 63) / 64);
     constexpr int ldsq = 2 * (2 * 64 * 32 * 2 + 256 * 32 * 2), ldsq1 = 2 * (64 * 32 * 2 + 256 * 32 * 2);

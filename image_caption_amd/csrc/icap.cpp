@@ -137,6 +137,7 @@ struct icap_handle {
   int ns = 2;  // activation planes (1 = bf16, 2 = hi/lo)
   bool i8 = false;  // ICAP_PREC_I8X2: LayerNorm-fed ViT GEMMs on int8 two-slice operands
   bool i8k = false;  // ... and MLP-2 on the block-scaled int8 GELU output (ICAP_I8_MLP2=1, opt-in)
+  bool f16 = false;  // ICAP_PREC_F16: the ViT encoder on single fp16 planes (fp16 MFMA); the decoder stays bf16x2
   std::vector<void*> owned;
   std::vector<size_t> owned_n;  // bytes of each owned buffer
   // icap_update_weights re-packs into the buffers icap_create allocated, in the same order: alloc()
@@ -246,9 +247,16 @@ struct icap_handle {
     HIPCHK(launch_f32_to_bf16(src, p, (long)n, s));
     return p;
   }
-  Lin lin(const float* w, const float* b, int N, int K, hipStream_t s) {
+  bf16_t* own_f16(const float* src, size_t n, hipStream_t s) {
+    REQUIRE(src != nullptr, "missing parameter pointer");
+    bf16_t* p = (bf16_t*)alloc(n * 2);
+    HIPCHK(launch_f32_to_f16(src, p, (long)n, s));
+    return p;
+  }
+  // nn.Linear packing: bf16 weights, or fp16 (half = true: the ICAP_PREC_F16 encoder)
+  Lin lin(const float* w, const float* b, int N, int K, hipStream_t s, bool half = false) {
     Lin l;
-    l.w = own_bf16(w, (size_t)N * K, s);
+    l.w = half ? own_f16(w, (size_t)N * K, s) : own_bf16(w, (size_t)N * K, s);
     l.b = b ? own_f32(b, N, s) : nullptr;
     l.N = N;
     l.K = K;
@@ -300,6 +308,20 @@ struct icap_handle {
 #ifdef ICAP_TOOLS
     if (out == OUT_F32_RESID) tail_split(g);
 #endif
+    run_gemm(g, s);
+  }
+  // fp16 single-plane GEMM (ICAP_PREC_F16 encoder): A one fp16 plane, W packed by lin(..., half = true);
+  // OUT_SPLIT writes one fp16 plane
+  void gemm16(const bf16_t* A, long lda, const Lin& W, int M, void* C, long ldc, int epi, int out, hipStream_t s,
+              int hm_n = 0) {
+    GemmArgs g = gemm_args();
+    g.hm_n = hm_n;
+    g.A = A; g.lda = lda;
+    g.W = W.w; g.ldw = W.K;
+    g.bias = W.b;
+    g.C = C; g.ldc = ldc;
+    g.M = M; g.N = W.N; g.K = W.K; g.nsplit = 1; g.c_planes = 1; g.f16 = 1;
+    g.epi = epi; g.out = out;
     run_gemm(g, s);
   }
   // residual-output GEMMs (N = 768 / 512: a partial last round of tiles) split their tail tiles in K when
@@ -414,16 +436,17 @@ void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PA
     REQUIRE(d.vit_heads * 64 == V, "ViT heads must be 64 wide");
     h->cls = h->own_f32(d.cls, V, s);
     h->pos = h->own_f32(d.pos, (size_t)(np + 1) * V, s);
-    h->conv = h->lin(d.conv_w, d.conv_b, V, 3 * d.patch * d.patch, s);
+    const bool hf = h->f16;
+    h->conv = h->lin(d.conv_w, d.conv_b, V, 3 * d.patch * d.patch, s, hf);
     for (int i = 0; i < d.vit_layers; ++i) {
       const icap_vit_layer_w& L = d.vit_layers_w[i];
       VitLayer o;
       o.ln1 = h->ln(L.ln_1, V, s);
-      o.qkv = h->lin(L.attn.in_w, L.attn.in_b, 3 * V, V, s);
-      o.out = h->lin(L.attn.out_w, L.attn.out_b, V, V, s);
+      o.qkv = h->lin(L.attn.in_w, L.attn.in_b, 3 * V, V, s, hf);
+      o.out = h->lin(L.attn.out_w, L.attn.out_b, V, V, s, hf);
       o.ln2 = h->ln(L.ln_2, V, s);
-      o.mlp0 = h->lin(L.mlp0_w, L.mlp0_b, d.vit_mlp, V, s);
-      o.mlp3 = h->lin(L.mlp3_w, L.mlp3_b, V, d.vit_mlp, s);
+      o.mlp0 = h->lin(L.mlp0_w, L.mlp0_b, d.vit_mlp, V, s, hf);
+      o.mlp3 = h->lin(L.mlp3_w, L.mlp3_b, V, d.vit_mlp, s, hf);
       if (h->i8) {
         o.qkv8 = h->lin8(L.attn.in_w, L.attn.in_b, 3 * V, V, s);
         o.mlp08 = h->lin8(L.mlp0_w, L.mlp0_b, d.vit_mlp, V, s);
@@ -433,7 +456,7 @@ void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PA
     }
     h->vit_ln_w = h->own_f32(d.vit_ln_w, V, s);
     h->vit_ln_b = h->own_f32(d.vit_ln_b, V, s);
-    h->proj = h->lin(d.proj_w, d.proj_b, D, V, s);
+    h->proj = h->lin(d.proj_w, d.proj_b, D, V, s, hf);
     if (h->i8) h->proj8 = h->lin8(d.proj_w, d.proj_b, D, V, s);
   } else if (d.kind == ICAP_KIND_GRID) {
     h->proj = h->lin(d.proj_w, d.proj_b, D, d.cnn_dim, s);
@@ -478,7 +501,60 @@ void enc_layer_postln(icap_handle* h, const EncLayer& L, int B, int N, float* x,
   HIPCHK(launch_layernorm(x, D, M, D, 0, 0, 0, L.n2.w, L.n2.b, 1e-5f, x, D, a, D, aL, h->ns, s));
 }
 
+// ICAP_PREC_F16 form of encode_vit: every GEMM and the attention on single fp16 planes (fp16 MFMA, fp32
+// accumulate); the residual stream, LayerNorm statistics, softmax and GELU stay fp32.
+void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  const int V = d.vit_dim, g = d.image / d.patch, np = g * g, T = np + 1, M = B * T, Dm = d.d_model;
+  const int Kp = 3 * d.patch * d.patch, F = d.vit_mlp;
+  const int hm = T > 64 && T <= 256 ? T : 0;
+  REQUIRE(hm, "ICAP_PREC_F16 encoder needs 64 < tokens <= 256");
+  h->e_patch.ensure((size_t)B * np * Kp * 2);
+  h->e_x.ensure((size_t)M * V * 4);
+  h->e_a.ensure((size_t)M * V * 2);
+  h->e_qkv.ensure((size_t)M * 3 * V * 2);
+  h->e_h.ensure((size_t)M * F * 2);
+  bf16_t *patch = h->e_patch.as<bf16_t>(), *a = h->e_a.as<bf16_t>(), *qkv = h->e_qkv.as<bf16_t>(),
+         *hb = h->e_h.as<bf16_t>();
+  float* x = h->e_x.as<float>();
+  HIPCHK(launch_im2col_patches(img, B, 3, d.image, d.patch, patch, 0, NS_F16, s));
+  {  // patch-embed GEMM: rows (b, p) -> x[b*T + 1 + p] with conv bias + pos[1 + p]
+    GemmArgs ga = gemm_args();
+    ga.A = patch; ga.lda = Kp;
+    ga.W = h->conv.w; ga.ldw = Kp; ga.bias = h->conv.b;
+    ga.C = x; ga.ldc = V;
+    ga.M = B * np; ga.N = V; ga.K = Kp; ga.nsplit = 1; ga.c_planes = 1; ga.f16 = 1;
+    ga.epi = EPI_NONE; ga.out = OUT_F32;
+    ga.rm_group = np; ga.rm_stride = T; ga.rm_off = 1;
+    ga.addend = h->pos; ga.add_ld = V; ga.add_group = np; ga.add_off = 1;
+    h->run_gemm(ga, s);
+  }
+  HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
+  for (const VitLayer& L : h->vit) {
+    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s));
+    h->gemm16(a, V, L.qkv, M, qkv, 3 * V, EPI_NONE, OUT_SPLIT, s, hm);  // head-major [image][q|k|v x head][token][64]
+    {
+      const double flops = 4.0 * B * d.vit_heads * (double)T * T * 64;
+      const double bytes = 2.0 * B * (double)T * V * 4;
+      h->timed(PROF_ENC_ATTN, flops, bytes, s, [&] {
+        HIPCHK(launch_enc_attention(qkv, 3 * V, 0, B, T, d.vit_heads, 0.125f, a, V, 0, NS_F16, s, 1));
+      });
+    }
+    h->gemm16(a, V, L.out, M, x, V, EPI_NONE, OUT_F32_RESID, s);
+    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s));
+    h->gemm16(a, V, L.mlp0, M, hb, F, EPI_GELU, OUT_SPLIT, s);
+    h->gemm16(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s);
+  }
+  // final LN on patch rows only (drop CLS), then projection 768 -> d_model
+  HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s));
+  h->gemm16(a, V, h->proj, B * np, memory, Dm, EPI_NONE, OUT_F32, s);
+}
+
 void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStream_t s) {
+  if (h->f16) {
+    encode_vit_f16(h, img, B, memory, s);
+    return;
+  }
   const icap_model_desc& d = h->d;
   const int V = d.vit_dim, g = d.image / d.patch, np = g * g, T = np + 1, M = B * T, Dm = d.d_model;
   const int Kp = 3 * d.patch * d.patch, ns = h->ns;
@@ -1084,13 +1160,14 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
                  "unset it or build with `python -m image_caption_amd.build --tools`");
 #endif
     REQUIRE(desc->precision == ICAP_PREC_BF16 || desc->precision == ICAP_PREC_BF16X2 ||
-                desc->precision == ICAP_PREC_I8X2,
+                desc->precision == ICAP_PREC_I8X2 || desc->precision == ICAP_PREC_F16,
             "bad precision");
     icap_handle* h = new icap_handle();
     try {
       h->d = *desc;
       h->ns = desc->precision == ICAP_PREC_BF16 ? 1 : 2;
       h->i8 = desc->precision == ICAP_PREC_I8X2 && desc->kind == ICAP_KIND_VIT;
+      h->f16 = desc->precision == ICAP_PREC_F16 && desc->kind == ICAP_KIND_VIT;
       // measured and rejected as the default: MLP-2 fed by the block-scaled GELU output takes
       // 1211 us (two-step fold: 256 VGPRs, 30 spilled) / 646 us (per-step fold, 64-column blocks) against
       // 467 us for the bf16x2 form
@@ -1337,6 +1414,10 @@ int icap_op_gemm(const uint16_t* A, long lda, long a_lo, int nsplit, const uint1
     g.W = W; g.ldw = K; g.bias = bias;
     g.C = C; g.ldc = ldc; g.c_lo = c_lo;
     g.M = M; g.N = N; g.K = K; g.epi = epi; g.out = out;
+    if (nsplit == NS_F16) {  // fp16 A and W, one fp16 output plane
+      REQUIRE(N % 256 == 0 && K % 32 == 0 && K >= 128, "fp16 GEMM: N % 256 == 0, K % 32 == 0, K >= 128");
+      g.nsplit = 1; g.c_planes = 1; g.f16 = 1;
+    }
     HIPCHK(launch_gemm(g, (hipStream_t)stream));
   });
 }

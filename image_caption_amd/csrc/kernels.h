@@ -21,6 +21,10 @@ inline int icap_knob(const char*, int dflt) { return dflt; }
 // Name of the first knob set in the environment ("" when none); checked by icap_create in a product build.
 extern "C" const char* icap_knobs_set();
 
+// Plane format argument of the row kernels (layernorm, im2col, split): 1 = one bf16 plane, 2 = bf16 hi/lo
+// planes, NS_F16 = one fp16 plane (ICAP_PREC_F16 encoder).
+constexpr int NS_F16 = -1;
+
 // Epilogue / output selectors shared by kernels and the host dispatcher.
 enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RELU = 2 };
 // OUT_I8K (launch_gemm_i8, 128 x 128 tiles only): C as int8 two-slice row images [M][N/64][2][64] with one
@@ -65,6 +69,9 @@ struct GemmArgs {
   // round of split_slots block slots run as two K halves merged by the second finisher; split_ws holds
   // 2 x 128 x 256 fp32 partials per split tile (8 x split_slots tiles), split_cnt its tickets (zero at rest)
   float* split_ws; int* split_cnt; int split_slots;
+  // f16 = 1: A and W are single fp16 planes (nsplit 1), fp16 MFMA; OUT_SPLIT writes one fp16 plane
+  // (launch_gemm_256 128 x 256 path only: the ICAP_PREC_F16 encoder GEMMs)
+  int f16;
 };
 // bytes of split_ws for split_slots block slots per XCD
 inline size_t gemm_split_ws_bytes(int split_slots) { return (size_t)8 * split_slots * 2 * 128 * 256 * 4; }
@@ -196,6 +203,7 @@ hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int 
 // bf16 planes -> fp32 (hi + lo)
 hipError_t launch_planes_to_f32(const bf16_t* src, long lo, long n, int nsplit, float* dst, hipStream_t s);
 hipError_t launch_f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);
+hipError_t launch_f32_to_f16(const float* src, bf16_t* dst, long n, hipStream_t s);
 hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s);
 
 // Encoder self-attention (non-causal) over N tokens, heads of 64, MFMA bf16 (nsplit 1 or 2).

@@ -10,6 +10,10 @@
 namespace {
 
 __device__ __forceinline__ void store_planes(bf16_t* base, long idx, long lo, int nsplit, float v) {
+  if (nsplit == NS_F16) {
+    base[idx] = f2h(v);
+    return;
+  }
   bf16_t hi, l;
   split_bf(v, hi, l);
   base[idx] = hi;
@@ -53,7 +57,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
     for (int k = 0; k < 4; ++k) y[k] = (v[c * 4 + k] - mean) * rstd * wv[k] + bv[k];
     if (out_f32) *(f32x4*)(out_f32 + (long)row * ld_f32 + col) = y;
-    if (out_bf) {
+    if (out_bf && nsplit == NS_F16) {
+      *(u32x2*)(out_bf + (long)row * ld_bf + col) = pack16x4<true>(y);
+    } else if (out_bf) {
       bf16_t h[4], l[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) split_bf(y[k], h[k], l[k]);
@@ -217,6 +223,11 @@ __global__ void im2col_kernel(const float* __restrict__ img, int B, int C, int H
     const float* src = img + (((long)b * C + c) * HW + y) * HW + xx;
     f32x4 a = *(const f32x4*)src, bq = *(const f32x4*)(src + 4);
     float v[8] = {a[0], a[1], a[2], a[3], bq[0], bq[1], bq[2], bq[3]};
+    if (nsplit == NS_F16) {
+      const u32x2 x0 = pack16x4<true>(a), x1 = pack16x4<true>(bq);
+      *(u32x4*)(out + r * K + k0) = (u32x4){x0[0], x0[1], x1[0], x1[1]};
+      continue;
+    }
     bf16_t h[8], l[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) split_bf(v[k], h[k], l[k]);
@@ -407,6 +418,11 @@ hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int 
 
 hipError_t launch_planes_to_f32(const bf16_t* src, long lo, long n, int nsplit, float* dst, hipStream_t s) {
   hipLaunchKernelGGL(planes_to_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, lo, n, nsplit, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_f32_to_f16(const float* src, bf16_t* dst, long n, hipStream_t s) {
+  hipLaunchKernelGGL(split_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, n, dst, 0L, NS_F16);
   return hipGetLastError();
 }
 

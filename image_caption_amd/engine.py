@@ -17,7 +17,7 @@ import torch
 from . import _lib
 from ._lib import (ConvBnW, DecLayerW, EncLayerW, LnW, MhaW, ModelDesc, VitLayerW, check, stream_ptr)
 
-DEFAULT_PRECISION = "i8x2"
+DEFAULT_PRECISION = "f16"
 
 
 def _ln(sd, p):

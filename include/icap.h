@@ -31,6 +31,8 @@ extern "C" {
 #define ICAP_PREC_BF16X2 2 /* activations as hi+lo bf16 pairs (~16 mantissa bits), fp32 acc  */
 #define ICAP_PREC_I8X2 3   /* bf16x2, except the LayerNorm-fed ViT GEMMs (QKV, MLP-1, projection):
                               both operands as two int8 slices (16-bit fixed point per row), int32 acc */
+#define ICAP_PREC_F16 4    /* ViT encoder on single fp16 planes (11-bit significand, fp16 MFMA, fp32 acc);
+                              decoder as bf16x2 */
 
 typedef struct icap_handle icap_handle;
 
@@ -211,7 +213,9 @@ int icap_profile_read(icap_handle* h, int kernel_class, double* total_ms, long* 
 
 /* ---- op-level entry points (kernel parity tests) ---- */
 /* C = epi(A·W^T + bias); A = nsplit bf16 planes (plane stride a_lo); W (N,K) bf16.
- * epi: 0 none, 1 GELU(erf), 2 ReLU.  out: 0 fp32, 1 bf16, 2 split bf16 planes, 3 fp32 +=. */
+ * epi: 0 none, 1 GELU(erf), 2 ReLU.  out: 0 fp32, 1 bf16, 2 split bf16 planes, 3 fp32 +=.
+ * nsplit = -1: A, W and the out = 2 plane are fp16 (ICAP_PREC_F16; N % 256 == 0, K >= 128).
+ * icap_op_layernorm / icap_op_enc_attention take nsplit = -1 for one fp16 plane the same way. */
 int icap_op_gemm(const uint16_t* A, long lda, long a_lo, int nsplit, const uint16_t* W, const float* bias,
                  void* C, long ldc, long c_lo, int M, int N, int K, int epi, int out, void* stream);
 int icap_op_layernorm(const float* x, int rows, int D, const float* w, const float* b, float eps,

@@ -42,7 +42,7 @@ class HipRouted:
 
     _hip_kind = "vit"
 
-    def _hip_setup(self, backend: str = "auto", precision: str = "i8x2") -> None:
+    def _hip_setup(self, backend: str = "auto", precision: str = "f16") -> None:
         if backend not in BACKENDS:
             raise ValueError(f"backend must be one of {BACKENDS}")
         object.__setattr__(self, "hip_backend", backend)

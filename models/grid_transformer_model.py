@@ -73,7 +73,7 @@ class GridTransformerCaptioning(HipRouted, nn.Module):
 
     def __init__(self, vocab_size, d_model=512, nhead=8, num_encoder_layers=6, num_decoder_layers=6,
                  dim_feedforward=2048, dropout=0.1, max_len=100, pretrained_cnn=True, backend="auto",
-                 hip_precision="i8x2"):
+                 hip_precision="f16"):
         super().__init__()
         self._hip_setup(backend, hip_precision)
         self.vocab_size = vocab_size
@@ -134,5 +134,5 @@ def build_model(vocab_size, config):
         max_len=config.get("max_len", 100),
         pretrained_cnn=config.get("pretrained_cnn", True),
         backend=config.get("backend", "auto"),
-        hip_precision=config.get("hip_precision", "i8x2"),
+        hip_precision=config.get("hip_precision", "f16"),
     )

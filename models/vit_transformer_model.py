@@ -3,7 +3,7 @@
 Same classes, constructor arguments, config keys, attribute names and state_dict keys as the
 reference; `generate` / `encoder(...)` / `decoder(...)` on GPU tensors in eval/no-grad run the
 MI355X HIP engine (libicap.so) instead of torch modules.  Extra, build-owned config keys:
-`backend` ("auto" | "hip" | "torch") and `hip_precision` ("i8x2" default, "bf16x2" or "bf16").
+`backend` ("auto" | "hip" | "torch") and `hip_precision` ("f16" default: fp16 encoder operands, bf16x2 decoder; "i8x2", "bf16x2" or "bf16").
 """
 from __future__ import annotations
 
@@ -57,7 +57,7 @@ class ViTTransformerCaptioning(HipRouted, nn.Module):
 
     def __init__(self, vocab_size, d_model=512, nhead=8, num_encoder_layers=6, num_decoder_layers=6,
                  dim_feedforward=2048, dropout=0.1, max_len=100, pretrained_vit=True, backend="auto",
-                 hip_precision="i8x2"):
+                 hip_precision="f16"):
         super().__init__()
         self._hip_setup(backend, hip_precision)
         self.vocab_size = vocab_size
@@ -112,5 +112,5 @@ def build_model(vocab_size, config):
         max_len=config.get("max_len", 100),
         pretrained_vit=config.get("pretrained_vit", True),
         backend=config.get("backend", "auto"),
-        hip_precision=config.get("hip_precision", "i8x2"),
+        hip_precision=config.get("hip_precision", "f16"),
     )

@@ -388,3 +388,78 @@ def test_gemm_tail_split(cuda, M, N, K, slots):
     tiles = (N // 256) * ((M + 127) // 128)
     if (tiles // 8 + 1) > slots:
         assert not torch.equal(outs[0], ref)
+
+
+# ---------------------------------------------------------------- fp16 single-plane encoder (ICAP_PREC_F16)
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (50432, 768, 768), (1000, 3072, 768), (777, 768, 3072)])
+@pytest.mark.parametrize("epi", [0, 1])
+def test_gemm_f16(cuda, M, N, K, epi):
+    """fp16 A / W (nsplit = -1), fp32 accumulate: against fp64 on the same fp16 values; fp32, one fp16
+    plane (rounding of the output: 2^-11 relative) and residual outputs."""
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    a = torch.randn(M, K, generator=g).to(torch.float16).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.float16).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    ref = a.double() @ w.double().t() + bias.double()
+    if epi == 1:
+        ref = torch.nn.functional.gelu(ref)
+    C = torch.empty(M, N, device=cuda)
+    L.check(lib.icap_op_gemm(a.data_ptr(), K, 0, -1, w.data_ptr(), bias.data_ptr(), C.data_ptr(), N, 0,
+                             M, N, K, epi, 0, L.stream_ptr()), "gemm f16")
+    Ch = torch.empty(M, N, device=cuda, dtype=torch.float16)
+    L.check(lib.icap_op_gemm(a.data_ptr(), K, 0, -1, w.data_ptr(), bias.data_ptr(), Ch.data_ptr(), N, 0,
+                             M, N, K, epi, 2, L.stream_ptr()), "gemm f16 plane")
+    R = torch.randn(M, N, generator=g).to(cuda)
+    R0 = R.clone()
+    L.check(lib.icap_op_gemm(a.data_ptr(), K, 0, -1, w.data_ptr(), bias.data_ptr(), R.data_ptr(), N, 0,
+                             M, N, K, epi, 3, L.stream_ptr()), "gemm f16 resid")
+    torch.cuda.synchronize()
+    scale = max(1.0, ref.abs().max().item())
+    assert (C.double() - ref).abs().max().item() < 2e-5 * scale
+    assert torch.equal(Ch, C.to(torch.float16))  # the plane is the fp32 result rounded once
+    assert (R.double() - R0.double() - C.double()).abs().max().item() < 1e-5 * scale
+
+
+def test_gemm_f16_head_major_via_engine_layout(cuda):
+    """Identity A through the fp16 kernel: exact, and not transposed."""
+    L, lib = _lib()
+    n = 256
+    A = torch.eye(n, device=cuda).to(torch.float16).contiguous()
+    w = (torch.arange(n * n, device=cuda, dtype=torch.float32).reshape(n, n) % 251).to(torch.float16)
+    C = torch.empty(n, n, device=cuda)
+    L.check(lib.icap_op_gemm(A.data_ptr(), n, 0, -1, w.data_ptr(), None, C.data_ptr(), n, 0, n, n, n, 0, 0,
+                             L.stream_ptr()), "gemm f16")
+    torch.cuda.synchronize()
+    assert torch.equal(C, w.float().t())
+
+
+def test_layernorm_f16(cuda):
+    L, lib = _lib()
+    rows, D = 333, 768
+    x = (torch.randn(rows, D, device=cuda) * 3 + 1).contiguous()
+    w = torch.randn(D, device=cuda)
+    b = torch.randn(D, device=cuda)
+    y = torch.empty_like(x)
+    yh = torch.empty(rows, D, device=cuda, dtype=torch.float16)
+    L.check(lib.icap_op_layernorm(x.data_ptr(), rows, D, w.data_ptr(), b.data_ptr(), 1e-6, y.data_ptr(),
+                                  yh.data_ptr(), 0, -1, L.stream_ptr()), "ln f16")
+    torch.cuda.synchronize()
+    assert torch.equal(yh, y.to(torch.float16))
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (3, 100, 8)])
+def test_enc_attention_f16(cuda, B, N, H):
+    """One fp16 plane in and out; the probabilities enter the P.V product as fp16 (2^-11 relative)."""
+    L, lib = _lib()
+    D = H * 64
+    g = torch.Generator(device="cpu").manual_seed(B * N + H + 1)
+    qkv = (torch.randn(B * N, 3 * D, generator=g) * 1.5).to(torch.float16).to(cuda)
+    v = qkv.double().view(B, N, 3, H, 64)
+    q, k, vv = v[:, :, 0].transpose(1, 2), v[:, :, 1].transpose(1, 2), v[:, :, 2].transpose(1, 2)
+    ref = torch.softmax(q @ k.transpose(-1, -2) / 8.0, -1) @ vv
+    ref = ref.transpose(1, 2).reshape(B * N, D)
+    out = torch.zeros(B * N, D, device=cuda, dtype=torch.float16)
+    L.check(lib.icap_op_enc_attention(qkv.data_ptr(), 0, B, N, H, out.data_ptr(), 0, -1, L.stream_ptr()), "attn f16")
+    torch.cuda.synchronize()
+    assert (out.double() - ref).abs().max().item() < 4e-3

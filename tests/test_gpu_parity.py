@@ -1,5 +1,5 @@
 """HIP path vs the reference-generated goldens and the CPU oracle, through the C-ABI and through
-the drop-in nn.Module surface.  Tolerances: i8x2 (default) and bf16x2 modes - token ids identical, logits
+the drop-in nn.Module surface.  Tolerances: f16 (default), i8x2 and bf16x2 modes - token ids identical, logits
 within 1e-3 (SURVEY/BASELINE north star); bf16 mode - ids identical wherever the reference
 top-2 margin exceeds 0.2, logits within 0.1."""
 import os
@@ -13,6 +13,9 @@ from oracle import captioner as O
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
+# encoder memory vs the oracle (|memory| <= ~3): fp16 operands (f16, the default) round to 2^-11 relative, the
+# 16-bit forms to ~2^-16; the logits are held to 1e-3 in every mode
+MEM_TOL = {"bf16x2": 1e-3, "i8x2": 1e-3, "f16": 4e-3}
 
 
 def gold(name):
@@ -40,14 +43,14 @@ def test_vit_golden_ids_and_logits(vit_engine, cuda):
     g = gold("vit_b4.npz")
     imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
     mem = vit_engine.encode(imgs)
-    assert np.abs(mem[:, :4, :16].cpu().numpy() - g["memory_head"]).max() < 1e-3
+    assert np.abs(mem[:, :4, :16].cpu().numpy() - g["memory_head"]).max() < MEM_TOL["f16"]  # default precision
     ids = vit_engine.greedy(mem, W.START_TOKEN, W.END_TOKEN, 30).cpu().numpy()
     assert ids.dtype == np.int64 and np.array_equal(ids, g["ids"])
     tf = vit_engine.decoder_forward(torch.from_numpy(g["ids"][:, :-1]).to(cuda), mem, causal=True)
     assert np.abs(tf.cpu().numpy() - g["logits_tf"]).max() < 1e-3
 
 
-@pytest.mark.parametrize("precision", ["bf16x2", "i8x2"])
+@pytest.mark.parametrize("precision", ["bf16x2", "i8x2", "f16"])
 def test_vit_golden_per_precision(vit_sd, cuda, precision):
     """Both parity modes meet the same bar: golden ids identical, logits within 1e-3, ids equal to
     the fp32 oracle's on 24 more images.  i8x2 = the LayerNorm-fed ViT GEMMs on int8 two-slice
@@ -59,7 +62,7 @@ def test_vit_golden_per_precision(vit_sd, cuda, precision):
     g = gold("vit_b4.npz")
     imgs = torch.from_numpy(W.synthetic_images(4, seed=0)).to(cuda)
     mem = eng.encode(imgs)
-    assert np.abs(mem[:, :4, :16].cpu().numpy() - g["memory_head"]).max() < 1e-3
+    assert np.abs(mem[:, :4, :16].cpu().numpy() - g["memory_head"]).max() < MEM_TOL[precision]
     ids = eng.greedy(mem, W.START_TOKEN, W.END_TOKEN, 30).cpu().numpy()
     assert np.array_equal(ids, g["ids"])
     tf = eng.decoder_forward(torch.from_numpy(g["ids"][:, :-1]).to(cuda), mem, causal=True)
@@ -68,7 +71,7 @@ def test_vit_golden_per_precision(vit_sd, cuda, precision):
     imgs = torch.from_numpy(W.synthetic_images(24, seed=7))
     ref_mem = O.vit_encode(vit_sd, imgs)
     mem = eng.encode(imgs.to(cuda))
-    assert (mem.cpu() - ref_mem).abs().max().item() < 2e-3
+    assert (mem.cpu() - ref_mem).abs().max().item() < 2 * MEM_TOL[precision]
     ref = O.greedy_from_memory(vit_sd, ref_mem, W.START_TOKEN, W.END_TOKEN, 30)
     ids = eng.greedy(mem, W.START_TOKEN, W.END_TOKEN, 30).cpu()
     assert torch.equal(ids, ref)
@@ -179,7 +182,7 @@ def test_batch_independence_and_determinism_at_b256(vit_engine, cuda, vit_sd):
     alone, _ = vit_engine.greedy_raw(vit_engine.encode(imgs[pick.to(cuda)]), W.START_TOKEN, W.END_TOKEN, 30)
     assert torch.equal(alone, a[pick.to(cuda)])
     ref_mem = O.vit_encode(vit_sd, imgs[pick.to(cuda)].cpu())
-    assert (mem[pick.to(cuda)].cpu() - ref_mem).abs().max().item() < 1e-3
+    assert (mem[pick.to(cuda)].cpu() - ref_mem).abs().max().item() < MEM_TOL["f16"]  # default precision
     ref = O.greedy_from_memory(vit_sd, ref_mem, W.START_TOKEN, W.END_TOKEN, 30)
     assert np.array_equal(a[pick.to(cuda)].long().cpu().numpy()[:, : ref.shape[1]], ref.numpy())
 

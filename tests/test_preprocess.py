@@ -85,4 +85,4 @@ def test_gpu_preprocess_feeds_encoder(cuda):
     x = preprocess_batch(imgs, "crop", device=cuda)
     mem = Engine(sd, "vit", {}, device=cuda).encode(x)
     ref = O.vit_encode(sd, torch.from_numpy(P.preprocess_batch(imgs, "crop")))
-    assert (mem.cpu() - ref).abs().max().item() < 1e-3
+    assert (mem.cpu() - ref).abs().max().item() < 4e-3  # f16 encoder (default): fp16 operands
