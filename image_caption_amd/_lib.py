@@ -111,6 +111,7 @@ SIGNATURES = {
     "icap_op_layernorm": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_long,
                                   c_int, c_void_p]),
     "icap_op_enc_attention": (c_int, [c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
+    "icap_op_cross_attn": (c_int, [c_void_p, c_long, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
     "icap_stream_create_cu_mask": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
     "icap_stream_destroy": (c_int, [c_void_p]),
     "icap_op_pack_i8": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),

@@ -799,6 +799,183 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
 
 constexpr int XA_RED_BYTES = (8 * 512 + 512) * 4 + 16;  // + the KS = 2 ticket
 
+// Cross-attention over a single fp16 memory plane (the parity precisions' decoder: the memory rounded
+// once to fp16 adds <= 2^-12 relative to the encoder's own error; CPU emulation, DESIGN.md §3: logit error
+// 1.29e-4 -> 1.32e-4 at B = 16, no token changes).  Half the bytes of the bf16 hi/lo planes, so one
+// 64-key chunk is 64 KiB: 4 chunks instead of 7 at S = 196, i.e. half the chunk steps (each costs three
+// block barriers).  q~ arrives as bf16 hi/lo planes (the chain kernel's output) and is re-split into fp16
+// hi/lo fragments once per block; the probabilities are fp16 hi/lo too; every product is
+// mem.hi + mem.lo (2 MFMAs instead of 3).  Roles per 64-key chunk:
+//   scores  wave w: key tile w & 3, d-group w >> 2 (128 = 4 k-steps); the 4 d-partials summed through LDS
+//   context wave w: d in [32w, 32w + 32), keys as 2 k-steps of 32 (key tiles 2s, 2s + 1)
+template <int DUMMY>
+__global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __restrict__ qt, long qt_lo,
+                                                              const bf16_t* __restrict__ mem, int rows_per_image,
+                                                              int S, float scale, bf16_t* out, long out_lo) {
+  constexpr int DM = 512, H = 8, CK = 64;
+  constexpr int BUF = CK * DM * 2;              // 64 KiB per chunk
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = (float*)(smem + 2 * BUF);        // [4 d-groups][4 tiles][4 regs][64 lanes]
+  float* tot = red + 4 * 1024;                  // [4 tiles][4 regs][64 lanes]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int skt = wave & 3, sdg = wave >> 2;
+  const int bpi = (rows_per_image + 1) / 2;
+  const int pb = blockIdx.x;
+  const int img = pb / bpi, pair = pb - img * bpi;
+  const int slot = 2 * pair + (fr >> 3);
+  const bool valid = slot < rows_per_image;
+  const long r = (long)img * rows_per_image + slot;
+  const int hd = fr & 7;
+  const bf16_t* mb = mem + (long)img * S * DM;
+  const int nchunks = (S + CK - 1) / CK;
+
+  // q~ as fp16 hi/lo fragments: column (row, head), d = 128 sdg + 32 ks + 8 fq + j.  (Issuing these loads
+  // behind the first chunks' DMA does not pay: the compiler then waits vmcnt(0) for the DMA as well,
+  // 7.7 -> 9.6 us at S = 1, tools/xattn_time.py.)
+  f16x8 qh[4], ql[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const long off = r * H * DM + hd * DM + sdg * 128 + ks * 32 + fq * 8;
+    bf16x8 a = {}, b = {};
+    if (valid) {
+      a = *(const bf16x8*)(qt + off);
+      b = *(const bf16x8*)(qt + qt_lo + off);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = (float)a[j] + (float)b[j];
+      const _Float16 h = (_Float16)v;
+      qh[ks][j] = h;
+      ql[ks][j] = (_Float16)(v - (float)h);
+    }
+  }
+
+  // chunk staging: wave w loads key rows 4w .. 4w + 3 (1 KiB per instruction), lane-linear LDS
+  // destination, source 16-B chunk pre-swizzled c ^ (key & 15)
+  auto stage = [&](int c, int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = wave * 4 + i;
+      const int g = min(c * CK + key, S - 1);
+      const bf16_t* src = mb + (long)g * DM + (lane ^ (key & 15)) * 8;
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)(smem + buf * BUF + key * 1024), 16,
+                                       0, 0);
+    }
+  };
+  auto mma16h = [](f16x8 a, f16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); };
+
+  f32x4 acc[2];
+  acc[0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  acc[1] = acc[0];
+  float m_run = -INFINITY, l_run = 0.f;
+  const int q4 = fr >> 2, p4 = fr & 3;
+
+  stage(0, 0);
+  if (nchunks > 1) stage(1, 1);
+  for (int c = 0; c < nchunks; ++c) {
+    if (c + 1 < nchunks) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const char* cb = smem + (c & 1) * BUF;
+    {  // partial scores: key tile skt, d-group sdg
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      const int key = skt * 16 + fr;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int ch = (sdg * 128 + ks * 32 + fq * 8) >> 3;
+        const f16x8 mh = *(const f16x8*)(cb + key * 1024 + ((ch ^ (key & 15)) << 4));
+        a = mma16h(mh, qh[ks], a);
+        a = mma16h(mh, ql[ks], a);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[((sdg * 4 + skt) * 4 + j) * 64 + lane] = a[j];
+    }
+    __syncthreads();
+    {
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) v += red[g * 1024 + threadIdx.x];
+      tot[threadIdx.x] = v;
+    }
+    __syncthreads();
+    // total scores (every wave), scale, mask, online softmax per head (= lane & 15)
+    f32x4 sc[4];
+    float cmax = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = c * CK + kt * 16 + fq * 4 + j;
+        const float v = key < S ? tot[(kt * 4 + j) * 64 + lane] * scale : -INFINITY;
+        sc[kt][j] = v;
+        cmax = fmaxf(cmax, v);
+      }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    const float m_new = fmaxf(m_run, cmax);
+    const float alpha = __expf(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = __expf(sc[kt][j] - m_new);
+        sc[kt][j] = e;
+        psum += e;
+      }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    acc[0] *= alpha;
+    acc[1] *= alpha;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      // P^T as the B operand of key tiles 2 s2, 2 s2 + 1 (element j < 4 -> key 4fq + j of the first tile,
+      // j >= 4 -> key 4fq + j - 4 of the second), fp16 hi/lo
+      f16x8 ph, pl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const _Float16 h0 = (_Float16)sc[2 * s2][j], h1 = (_Float16)sc[2 * s2 + 1][j];
+        ph[j] = h0;
+        ph[4 + j] = h1;
+        pl[j] = (_Float16)(sc[2 * s2][j] - (float)h0);
+        pl[4 + j] = (_Float16)(sc[2 * s2 + 1][j] - (float)h1);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int d = wave * 32 + dt * 16 + 4 * p4;
+        const int k0 = 32 * s2 + 4 * fq + q4, k1 = k0 + 16;
+        const int o0 = k0 * 1024 + ((((d >> 3) ^ (k0 & 15))) << 4) + (d & 7) * 2;
+        const int o1 = k1 * 1024 + ((((d >> 3) ^ (k1 & 15))) << 4) + (d & 7) * 2;
+        const f16x8 vh = __builtin_bit_cast(f16x8, tr_pair(cb + o0, cb + o1));
+        acc[dt] = mma16h(vh, ph, acc[dt]);
+        acc[dt] = mma16h(vh, pl, acc[dt]);
+      }
+    }
+    if (c + 2 < nchunks) {
+      __syncthreads();  // every wave is done with buffer c & 1
+      stage(c + 2, c & 1);
+    }
+  }
+  if (valid) {
+    const float inv = 1.f / l_run;
+    bf16_t* dst = out + r * H * DM + hd * DM + wave * 32;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      bf16_t hv[4], lv[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) split_bf(acc[dt][rr] * inv, hv[rr], lv[rr]);
+      const int d = dt * 16 + 4 * fq;
+      *(u32x2*)(dst + d) = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+      *(u32x2*)(dst + out_lo + d) =
+          (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+    }
+  }
+}
+constexpr int XA16_LDS = 2 * 64 * 512 * 2 + (4 * 1024 + 1024) * 4;
+
 }  // namespace
 
 int cross_attn_splits(int S) {
@@ -814,6 +991,22 @@ int cross_attn_splits(int S) {
 }
 
 size_t cross_attn_part_floats(int rows) { return (size_t)rows * 2 * XA_PART_FLOATS; }
+
+hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem16, int rows, int rows_per_image,
+                                 int S, float scale, bf16_t* out, long out_lo, hipStream_t s) {
+  if (S <= 0 || rows <= 0 || rows_per_image <= 0 || rows % rows_per_image) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)cross_attn_f16_kernel<0>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, XA16_LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int pairs = rows / rows_per_image * ((rows_per_image + 1) / 2);
+  hipLaunchKernelGGL(cross_attn_f16_kernel<0>, dim3(pairs), dim3(1024), XA16_LDS, s, qt, qt_lo, mem16,
+                     rows_per_image, S, scale, out, out_lo);
+  return hipGetLastError();
+}
 
 hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* mem, long mem_lo, int rows,
                                   int rows_per_image, int S, float scale, bf16_t* out, long out_lo, int nsplit,

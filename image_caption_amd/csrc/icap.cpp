@@ -856,6 +856,13 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   return b;
 }
 
+// The decoder's copy of the memory for the cross-attention: one fp16 plane in the parity precisions (ns = 2,
+// launch_cross_attn_f16), one bf16 plane in the bf16 mode.
+void mem_planes(icap_handle* h, const float* mem, const DecodeBufs& b, hipStream_t s) {
+  if (h->ns == 2) HIPCHK(launch_f32_to_f16(mem, b.memp, b.memL, s));
+  else HIPCHK(launch_split_f32(mem, b.memL, b.memp, b.memL, h->ns, s));
+}
+
 // One pass of all decoder layers over `rows` query rows (n_new per image, positions t0..t0+n_new).
 // Post-LN layer (torch TransformerDecoderLayer.forward, transformer.py:1144-1153):
 //   x = LN1(x + SA(x)); x = LN2(x + CA(x, mem)); x = LN3(x + W2 relu(W1 x)).
@@ -910,9 +917,12 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_SPLIT;
       h->chain(c, s, fused);
     }
-    h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * ns * (double)(rows / n_new) * S * D, s, [&] {
-      HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, mem_rpi, S, 0.125f, b.c, b.cL, ns, s,
-                                    b.xpart, b.xcnt));
+    h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * (double)(rows / mem_rpi) * S * D, s, [&] {
+      if (ns == 2)
+        HIPCHK(launch_cross_attn_f16(b.qt, b.cL, b.memp, rows, mem_rpi, S, 0.125f, b.c, b.cL, s));
+      else
+        HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, mem_rpi, S, 0.125f, b.c, b.cL, ns, s,
+                                      b.xpart, b.xcnt));
     });
     // per head, one launch: o_h = c_h Wv_h^T + bv_h, then slab h = o_h Wo[:, h*64:(h+1)*64]^T; the
     // residual LN sums the H slabs (the output projection as a split-K over heads)
@@ -956,7 +966,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   const int D = d.d_model, wsi = uniforms ? 1 : 0;
   DecodeBufs b = dec_bufs(h, B, B, max_len, S, 0, wsi);
   const float scale = (float)std::sqrt((double)D);
-  if (mem) HIPCHK(launch_split_f32(mem, b.memL, b.memp, b.memL, h->ns, s));
+  if (mem) mem_planes(h, mem, b, s);
   HIPCHK(launch_fill_col(ids, B, max_len, 0, start, s));
   HIPCHK(launch_embed(nullptr, 0, start, B, 1, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
   uint8_t* fin = nullptr;
@@ -1063,7 +1073,7 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     g.gen = g_ws_generation;
   }
   DecodeBufs b = dec_bufs(h, B, B, max_len, S, 0, mode);  // no allocation: sized at capture
-  HIPCHK(launch_split_f32(mem, b.memL, b.memp, b.memL, h->ns, s));
+  mem_planes(h, mem, b, s);
   if (mode) HIPCHK(hipMemcpyAsync(g.uni.p, uniforms, (size_t)(max_len - 1) * B * 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipGraphLaunch(g.exec, s));
   HIPCHK(hipMemcpyAsync(ids, g.ids.p, (size_t)B * max_len * 4, hipMemcpyDeviceToDevice, s));
@@ -1101,7 +1111,7 @@ void decode_beam(icap_handle* h, const float* mem, int B, int S, int max_len, in
   float* sc[2] = {fb, fb + rows};
   float* best_score = fb + 2 * rows;
   float* logits = best_score + B;
-  HIPCHK(launch_split_f32(mem, b.memL, b.memp, b.memL, h->ns, s));
+  mem_planes(h, mem, b, s);
   HIPCHK(launch_beam_init(B, K, start, max_len, seq[0], seq[1], anc[0], anc[1], sc[0], kcur, done, ncomp, best_score,
                           best_len, s));
   const float scale = (float)std::sqrt((double)D);
@@ -1344,7 +1354,7 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
     hipStream_t s = (hipStream_t)stream;
     const int D = h->d.d_model, rows = B * T;
     DecodeBufs b = dec_bufs(h, rows, B, T, S);
-    HIPCHK(launch_split_f32(memory, b.memL, b.memp, b.memL, h->ns, s));
+    mem_planes(h, memory, b, s);
     const float scale = (float)std::sqrt((double)D);
     HIPCHK(launch_embed(tgt, T, 0, rows, T, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
     decoder_layers(h, b, B, T, 0, T, causal, S, s, nullptr, 0, key_lengths);
@@ -1490,6 +1500,14 @@ int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uin
   return guarded([&] {
     HIPCHK(launch_enc_attention(qkv, 3L * H * 64, lo, B, N, H, 0.125f, out, (long)H * 64, out_lo, nsplit,
                                 (hipStream_t)stream));
+  });
+}
+
+int icap_op_cross_attn(const uint16_t* qt, long qt_lo, const uint16_t* mem16, int rows, int rows_per_image, int S,
+                       uint16_t* out, long out_lo, void* stream) {
+  return guarded([&] {
+    HIPCHK(launch_cross_attn_f16(qt, qt_lo, mem16, rows, rows_per_image, S, 0.125f, out, out_lo,
+                                 (hipStream_t)stream));
   });
 }
 

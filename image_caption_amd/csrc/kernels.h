@@ -221,6 +221,10 @@ hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int 
 hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* mem, long mem_lo, int rows,
                                   int rows_per_image, int S, float scale, bf16_t* out, long out_lo, int nsplit,
                                   hipStream_t s, float* xpart = nullptr, int* xcnt = nullptr);
+// The same over a single fp16 memory plane mem16 [B][S][512] (q~ bf16 hi/lo planes in, context bf16 hi/lo
+// planes out): the decoder's cross-attention in the parity precisions (attention.hip).
+hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem16, int rows, int rows_per_image,
+                                 int S, float scale, bf16_t* out, long out_lo, hipStream_t s);
 int cross_attn_splits(int S);
 size_t cross_attn_part_floats(int rows);
 // Batched beam search (beam.hip): state init, per-step selection, final pick.

@@ -254,6 +254,12 @@ int icap_op_gemm_i8_blocks(const int8_t* A, const float* a_scale, const float* a
 /* qkv planes (B*N, 3*H*64) -> out planes (B*N, H*64), non-causal softmax(QK^T/8)V. */
 int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uint16_t* out, long out_lo,
                           int nsplit, void* stream);
+/* Decoder cross-attention, key-absorbed (the decode loops' form): q~ (rows, 8, 512) as bf16 hi/lo planes
+ * (plane stride qt_lo), memory (rows / rows_per_image, S, 512) as one fp16 plane; row r attends to image
+ * r / rows_per_image: out[r][h] = softmax_s(q~[r][h] . mem[s] / 8) . mem -> (rows, 8, 512) bf16 hi/lo
+ * planes (plane stride out_lo).  The value projection is applied by the caller. */
+int icap_op_cross_attn(const uint16_t* qt, long qt_lo, const uint16_t* mem16, int rows, int rows_per_image, int S,
+                       uint16_t* out, long out_lo, void* stream);
 
 #ifdef __cplusplus
 }

@@ -116,6 +116,29 @@ def test_enc_attention(cuda, B, N, H, nsplit):
     assert (got - ref).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("rows,rpi,S", [(256, 1, 196), (40, 5, 196), (24, 3, 49), (6, 2, 1), (8, 1, 70)])
+def test_cross_attn_f16(cuda, rows, rpi, S):
+    """Key-absorbed decoder cross-attention over one fp16 memory plane (decode loops, beam slots and
+    teacher-forced rows of an image share a block): against fp64 softmax(q~ mem^T / 8) mem on the same
+    rounded operands, ragged last chunks (S = 196, 70, 49, 1) and odd rows per image."""
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(rows * 7 + S)
+    B = rows // rpi
+    mem = (torch.randn(B, S, 512, generator=g)).to(torch.float16)
+    qt = torch.randn(rows, 8, 512, generator=g) * 0.3
+    Q = planes(qt.to(cuda), 2)
+    qv = value(Q, 2).double().cpu()
+    m = mem.double()[torch.arange(rows) // rpi]                       # (rows, S, 512)
+    p = torch.softmax(torch.einsum("rhd,rsd->rhs", qv, m) / 8.0, -1)
+    ref = torch.einsum("rhs,rsd->rhd", p, m)
+    out = torch.zeros(2, rows, 8, 512, device=cuda, dtype=torch.bfloat16)
+    L.check(lib.icap_op_cross_attn(Q.data_ptr(), rows * 8 * 512, mem.to(cuda).data_ptr(), rows, rpi, S,
+                                   out.data_ptr(), rows * 8 * 512, L.stream_ptr()), "cross_attn")
+    torch.cuda.synchronize()
+    got = value(out, 2).double().cpu()
+    assert (got - ref).abs().max().item() < 2e-4
+
+
 def test_full_chip_kernels_repeat_bitwise(cuda):
     """Races between a wave's LDS reads and another wave's LDS-DMA refill of the same ring slot show
     up as run-to-run differences: the 128x256 two-blocks-per-CU GEMM (full chip, M = 50432, K = 768
