@@ -86,6 +86,7 @@ SIGNATURES = {
     "icap_destroy": (c_int, [c_void_p]),
     "icap_update_weights": (c_int, [c_void_p, POINTER(ModelDesc), c_int, c_void_p]),
     "icap_encode_vit": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "icap_encode_vit_features": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "icap_encode_grid_tail": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "icap_encode_grid": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "icap_encode_grid_features": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
@@ -112,6 +113,11 @@ SIGNATURES = {
                                   c_int, c_void_p]),
     "icap_op_enc_attention": (c_int, [c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
     "icap_op_cross_attn": (c_int, [c_void_p, c_long, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
+    "icap_decoder_train_workspace": (ctypes.c_size_t, [c_void_p, c_int, c_int, c_int]),
+    "icap_decoder_train_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                           c_void_p, ctypes.c_size_t, c_void_p]),
+    "icap_decoder_train_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
+                                            c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
     "icap_stream_create_cu_mask": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
     "icap_stream_destroy": (c_int, [c_void_p]),
     "icap_op_pack_i8": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),

@@ -4,6 +4,7 @@
 // cited there.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -503,7 +504,7 @@ void enc_layer_postln(icap_handle* h, const EncLayer& L, int B, int N, float* x,
 
 // ICAP_PREC_F16 form of encode_vit: every GEMM and the attention on single fp16 planes (fp16 MFMA, fp32
 // accumulate); the residual stream, LayerNorm statistics, softmax and GELU stay fp32.
-void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipStream_t s) {
+void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipStream_t s, float* feats = nullptr) {
   const icap_model_desc& d = h->d;
   const int V = d.vit_dim, g = d.image / d.patch, np = g * g, T = np + 1, M = B * T, Dm = d.d_model;
   const int Kp = 3 * d.patch * d.patch, F = d.vit_mlp;
@@ -546,13 +547,14 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
     h->gemm16(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s);
   }
   // final LN on patch rows only (drop CLS), then projection 768 -> d_model
-  HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s));
+  HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, V, a, V, 0, NS_F16, s));
   h->gemm16(a, V, h->proj, B * np, memory, Dm, EPI_NONE, OUT_F32, s);
 }
 
-void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStream_t s) {
+// feats (optional): the final-LayerNorm output of the patch tokens, (B, 196, 768) fp32 - the projection's input
+void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStream_t s, float* feats = nullptr) {
   if (h->f16) {
-    encode_vit_f16(h, img, B, memory, s);
+    encode_vit_f16(h, img, B, memory, s, feats);
     return;
   }
   const icap_model_desc& d = h->d;
@@ -627,6 +629,8 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
   }
   // final LN on patch rows only (drop CLS), then projection 768 -> d_model
   const long a2L = (long)B * np * V;
+  if (feats)
+    HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, V, nullptr, 0, 0, 1, s));
   if (h->i8) {
     HIPCHK(launch_layernorm_i8(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, a8, sa, s));
     h->gemm8(a8, sa, h->proj8, B * np, memory, Dm, 0, EPI_NONE, OUT_F32, s);
@@ -1133,6 +1137,214 @@ void decode_beam(icap_handle* h, const float* mem, int B, int S, int max_len, in
   HIPCHK(launch_beam_finalize(B, K, max_len, seq[cur], sc[cur], kcur, ncomp, best_seq, best_len, ids, lens, s));
 }
 
+// ------------------------------------------------------------------------------------------------
+// Decoder training pass (SCST's teacher-forced recompute with autograd, utils/scst_loss.py:124-128;
+// reference: the autograd graph of SCSTLoss._sample_with_log_probs, scst_loss.py:210-254, and its
+// loss.backward(), scripts/train_vit_transformer_scst_optimized.py:261).  fp32 parameters straight from
+// the caller's tensors (no packing: they change every optimizer step), fp32-accurate products
+// (train.hip).  The forward keeps every activation the backward reads in the caller's workspace.
+struct TrainWS {
+  int B, T, S, D, H, F, V, L, M, MS;
+  struct Layer {
+    float *x, *qkv, *p, *c, *xh1, *rs1, *x1, *q2, *k2, *v2, *p2, *c2, *xh2, *rs2, *x2, *hh, *xh3, *rs3;
+  };
+  std::vector<Layer> lay;
+  float *xL, *logits, *lse;
+  float *dx, *dc, *tmp, *dq, *dqkv, *dp, *dh, *dk, *dv, *dlog, *part, *skpart;
+  static constexpr size_t SK_FLOATS = (size_t)8 << 20;  // split-K partial sums of the weight gradients
+  size_t floats = 0;
+  TrainWS(const icap_model_desc& d, int B_, int T_, int S_, float* base) {
+    B = B_; T = T_; S = S_; D = d.d_model; H = d.nhead; F = d.dim_ff; V = d.vocab; L = d.n_dec_layers;
+    M = B * T; MS = B * S;
+    size_t off = 0;
+    auto take = [&](size_t n) {
+      float* p = base ? base + off : nullptr;
+      off += (n + 63) / 64 * 64;  // 256-B aligned carve-outs
+      return p;
+    };
+    const size_t MD = (size_t)M * D, MSD = (size_t)MS * D;
+    lay.resize(L);
+    for (Layer& y : lay) {
+      y.x = take(MD); y.qkv = take(3 * MD); y.p = take((size_t)B * H * T * T); y.c = take(MD);
+      y.xh1 = take(MD); y.rs1 = take(M); y.x1 = take(MD); y.q2 = take(MD); y.k2 = take(MSD); y.v2 = take(MSD);
+      y.p2 = take((size_t)B * H * T * S); y.c2 = take(MD); y.xh2 = take(MD); y.rs2 = take(M); y.x2 = take(MD);
+      y.hh = take((size_t)M * F); y.xh3 = take(MD); y.rs3 = take(M);
+    }
+    xL = take(MD); logits = take((size_t)M * V); lse = take(M);
+    dx = take(MD); dc = take(MD); tmp = take(MD); dq = take(MD); dqkv = take(3 * MD);
+    dp = take((size_t)B * H * T * std::max(T, S)); dh = take((size_t)M * F); dk = take(MSD); dv = take(MSD);
+    dlog = take((size_t)M * V);
+    part = take(colsum_scratch_floats(std::max(std::max(3 * D, F), std::max(V, D))));
+    skpart = take(SK_FLOATS);
+    floats = off;
+  }
+};
+
+void train_check(const icap_model_desc* d, int B, int T, int S) {
+  REQUIRE(d && d->dec_layers && d->emb && d->pe && d->fc_w && d->fc_b, "null decoder parameters");
+  REQUIRE(d->d_model == 512 && d->nhead == 8, "the training pass needs d_model 512, 8 heads");
+  REQUIRE(B > 0 && T > 0 && S > 0 && T <= d->pe_len, "bad batch / length / memory length");
+}
+
+struct TG {  // strided GEMM call builder (train.hip TGemmArgs)
+  TGemmArgs a{};
+  int nb = 1;
+  TG(const float* A, long sam, long sak, const float* B, long sbn, long sbk, float* C, long scm, long scn, int M, int N,
+     int K) {
+    a.A = A; a.sam = sam; a.sak = sak; a.B = B; a.sbn = sbn; a.sbk = sbk; a.C = C; a.scm = scm; a.scn = scn;
+    a.M = M; a.N = N; a.K = K; a.nb2 = 1; a.alpha = 1.f; a.beta = 0.f;
+  }
+  TG& batch(int nb1, int nb2, long sab1, long sab2, long sbb1, long sbb2, long scb1, long scb2) {
+    nb = nb1 * nb2; a.nb2 = nb2;
+    a.sab1 = sab1; a.sab2 = sab2; a.sbb1 = sbb1; a.sbb2 = sbb2; a.scb1 = scb1; a.scb2 = scb2;
+    return *this;
+  }
+  TG& alpha(float v) { a.alpha = v; return *this; }
+  TG& beta(float v) { a.beta = v; return *this; }
+  TG& bias(const float* b) { a.bias = b; return *this; }
+  TG& relu() { a.relu = 1; return *this; }
+  void run(hipStream_t s) { HIPCHK(launch_tgemm(a, nb, s)); }
+};
+// Y (M x N) = X (M x K) W^T (+ b): nn.Linear
+void t_lin(const float* X, const float* W, const float* b, float* Y, int M, int N, int K, hipStream_t s,
+           bool relu = false) {
+  TG g(X, K, 1, W, K, 1, Y, N, 1, M, N, K);
+  g.bias(b);
+  if (relu) g.relu();
+  g.run(s);
+}
+// dX (M x K) (+)= dY (M x N) W (N x K)
+void t_dx(const float* dY, const float* W, float* dX, int M, int N, int K, hipStream_t s, float beta = 0.f) {
+  TG(dY, N, 1, W, 1, K, dX, K, 1, M, K, N).beta(beta).run(s);
+}
+// dW (N x K) = dY^T (N x M) X (M x K): few output tiles and a long sum over the rows, so the sum is
+// split over blocks (partials in skpart, reduced in split order) until the launch has ~512 blocks
+void t_dw(const float* dY, const float* X, float* dW, int M, int N, int K, hipStream_t s, float* skpart) {
+  TG g(dY, 1, N, X, 1, K, dW, K, 1, N, K, M);
+  const long tiles = (long)((N + 63) / 64) * ((K + 63) / 64);
+  int ks = (int)std::min<long>(16, (512 + tiles - 1) / tiles);
+  while (ks > 1 && ((long)ks * N * K > (long)TrainWS::SK_FLOATS || M / ks < 128)) --ks;
+  if (ks > 1) {
+    g.a.ksplit = ks;
+    g.a.part = skpart;
+  }
+  g.run(s);
+}
+
+void train_forward(const icap_model_desc& d, TrainWS& w, const int32_t* ids, const float* mem, int end,
+                   float* logp, hipStream_t s) {
+  const int B = w.B, T = w.T, S = w.S, D = w.D, H = w.H, F = w.F, V = w.V, M = w.M, MS = w.MS;
+  const long ld = T + 1;
+  HIPCHK(launch_embed_fwd(ids, ld, B, T, d.emb, d.pe, D, (float)std::sqrt((double)D), w.lay[0].x, s));
+  for (int l = 0; l < w.L; ++l) {
+    const icap_dec_layer_w& P = d.dec_layers[l];
+    TrainWS::Layer& y = w.lay[l];
+    float* xnext = l + 1 < w.L ? w.lay[l + 1].x : w.xL;
+    // self-attention (causal): per (image, head) S = q k^T / 8 -> softmax -> P v
+    t_lin(y.x, P.self_attn.in_w, P.self_attn.in_b, y.qkv, M, 3 * D, D, s);
+    TG(y.qkv, 3 * D, 1, y.qkv + D, 3 * D, 1, y.p, T, 1, T, T, 64)
+        .batch(B, H, (long)T * 3 * D, 64, (long)T * 3 * D, 64, (long)H * T * T, (long)T * T).alpha(0.125f).run(s);
+    HIPCHK(launch_softmax_rows(y.p, (long)B * H * T, T, T, 1, s));
+    TG(y.p, T, 1, y.qkv + 2 * D, 1, 3 * D, y.c, D, 1, T, 64, T)
+        .batch(B, H, (long)H * T * T, (long)T * T, (long)T * 3 * D, 64, (long)T * D, 64).run(s);
+    t_lin(y.c, P.self_attn.out_w, P.self_attn.out_b, w.tmp, M, D, D, s);
+    HIPCHK(launch_ln_fwd(y.x, w.tmp, P.norm1.w, P.norm1.b, 1e-5f, M, D, y.x1, y.xh1, y.rs1, s));
+    // cross-attention over the memory
+    t_lin(y.x1, P.cross_attn.in_w, P.cross_attn.in_b, y.q2, M, D, D, s);
+    t_lin(mem, P.cross_attn.in_w + (size_t)D * D, P.cross_attn.in_b + D, y.k2, MS, D, D, s);
+    t_lin(mem, P.cross_attn.in_w + (size_t)2 * D * D, P.cross_attn.in_b + 2 * D, y.v2, MS, D, D, s);
+    TG(y.q2, D, 1, y.k2, D, 1, y.p2, S, 1, T, S, 64)
+        .batch(B, H, (long)T * D, 64, (long)S * D, 64, (long)H * T * S, (long)T * S).alpha(0.125f).run(s);
+    HIPCHK(launch_softmax_rows(y.p2, (long)B * H * T, S, T, 0, s));
+    TG(y.p2, S, 1, y.v2, 1, D, y.c2, D, 1, T, 64, S)
+        .batch(B, H, (long)H * T * S, (long)T * S, (long)S * D, 64, (long)T * D, 64).run(s);
+    t_lin(y.c2, P.cross_attn.out_w, P.cross_attn.out_b, w.tmp, M, D, D, s);
+    HIPCHK(launch_ln_fwd(y.x1, w.tmp, P.norm2.w, P.norm2.b, 1e-5f, M, D, y.x2, y.xh2, y.rs2, s));
+    // feed-forward
+    t_lin(y.x2, P.lin1_w, P.lin1_b, y.hh, M, F, D, s, true);
+    t_lin(y.hh, P.lin2_w, P.lin2_b, w.tmp, M, D, F, s);
+    HIPCHK(launch_ln_fwd(y.x2, w.tmp, P.norm3.w, P.norm3.b, 1e-5f, M, D, xnext, y.xh3, y.rs3, s));
+  }
+  t_lin(w.xL, d.fc_w, d.fc_b, w.logits, M, V, D, s);
+  HIPCHK(launch_logp_fwd(w.logits, V, ids, ld, B, T, end, logp, w.lse, s));
+}
+
+void train_backward(const icap_model_desc& d, const icap_model_desc& g, TrainWS& w, const int32_t* ids,
+                    const float* mem, int end, const float* dlogp, float* dmem, hipStream_t s) {
+  const int B = w.B, T = w.T, S = w.S, D = w.D, H = w.H, F = w.F, V = w.V, M = w.M, MS = w.MS;
+  const long ld = T + 1;
+  auto G = [](const float* p) { return const_cast<float*>(p); };
+  auto colsum = [&](const float* src, int rows, int n, const float* dst) {
+    HIPCHK(launch_colsum(src, n, rows, n, w.part, G(dst), 0, s));
+  };
+  auto ln_back = [&](const float* xh, const float* rs, const icap_ln_w& P, const icap_ln_w& Pg) {
+    colsum(w.dx, M, D, Pg.b);
+    HIPCHK(launch_ln_bwd(w.dx, xh, rs, P.w, M, D, w.tmp, s));
+    colsum(w.tmp, M, D, Pg.w);
+  };
+  HIPCHK(launch_logp_bwd(w.logits, w.lse, dlogp, V, ids, ld, B, T, end, w.dlog, s));
+  t_dw(w.dlog, w.xL, G(g.fc_w), M, V, D, s, w.skpart);
+  colsum(w.dlog, M, V, g.fc_b);
+  t_dx(w.dlog, d.fc_w, w.dx, M, V, D, s);
+  for (int l = w.L - 1; l >= 0; --l) {
+    const icap_dec_layer_w& P = d.dec_layers[l];
+    const icap_dec_layer_w& Pg = g.dec_layers[l];
+    TrainWS::Layer& y = w.lay[l];
+    // x3 = LN3(x2 + W2 relu(W1 x2 + b1) + b2)
+    ln_back(y.xh3, y.rs3, P.norm3, Pg.norm3);
+    t_dw(w.dx, y.hh, G(Pg.lin2_w), M, D, F, s, w.skpart);
+    colsum(w.dx, M, D, Pg.lin2_b);
+    t_dx(w.dx, P.lin2_w, w.dh, M, D, F, s);
+    HIPCHK(launch_relu_bwd(w.dh, y.hh, (long)M * F, s));
+    t_dw(w.dh, y.x2, G(Pg.lin1_w), M, F, D, s, w.skpart);
+    colsum(w.dh, M, F, Pg.lin1_b);
+    t_dx(w.dh, P.lin1_w, w.dx, M, F, D, s, 1.f);
+    // x2 = LN2(x1 + CA(x1, mem))
+    ln_back(y.xh2, y.rs2, P.norm2, Pg.norm2);
+    t_dw(w.dx, y.c2, G(Pg.cross_attn.out_w), M, D, D, s, w.skpart);
+    colsum(w.dx, M, D, Pg.cross_attn.out_b);
+    t_dx(w.dx, P.cross_attn.out_w, w.dc, M, D, D, s);
+    TG(w.dc, D, 1, y.v2, D, 1, w.dp, S, 1, T, S, 64)  // dP2 = dc2 V2^T
+        .batch(B, H, (long)T * D, 64, (long)S * D, 64, (long)H * T * S, (long)T * S).run(s);
+    TG(y.p2, 1, S, w.dc, 1, D, w.dv, D, 1, S, 64, T)  // dV2 = P2^T dc2
+        .batch(B, H, (long)H * T * S, (long)T * S, (long)T * D, 64, (long)S * D, 64).run(s);
+    HIPCHK(launch_softmax_bwd(y.p2, w.dp, (long)B * H * T, S, s));
+    TG(w.dp, S, 1, y.k2, 1, D, w.dq, D, 1, T, 64, S)  // dq2 = dS2 K2 / 8
+        .batch(B, H, (long)H * T * S, (long)T * S, (long)S * D, 64, (long)T * D, 64).alpha(0.125f).run(s);
+    TG(w.dp, 1, S, y.q2, 1, D, w.dk, D, 1, S, 64, T)  // dK2 = dS2^T q2 / 8
+        .batch(B, H, (long)H * T * S, (long)T * S, (long)T * D, 64, (long)S * D, 64).alpha(0.125f).run(s);
+    t_dw(w.dq, y.x1, G(Pg.cross_attn.in_w), M, D, D, s, w.skpart);
+    colsum(w.dq, M, D, Pg.cross_attn.in_b);
+    t_dx(w.dq, P.cross_attn.in_w, w.dx, M, D, D, s, 1.f);
+    t_dw(w.dk, mem, G(Pg.cross_attn.in_w) + (size_t)D * D, MS, D, D, s, w.skpart);
+    colsum(w.dk, MS, D, Pg.cross_attn.in_b + D);
+    t_dw(w.dv, mem, G(Pg.cross_attn.in_w) + (size_t)2 * D * D, MS, D, D, s, w.skpart);
+    colsum(w.dv, MS, D, Pg.cross_attn.in_b + 2 * D);
+    if (dmem) {
+      t_dx(w.dk, P.cross_attn.in_w + (size_t)D * D, dmem, MS, D, D, s, l == w.L - 1 ? 0.f : 1.f);
+      t_dx(w.dv, P.cross_attn.in_w + (size_t)2 * D * D, dmem, MS, D, D, s, 1.f);
+    }
+    // x1 = LN1(x + SA(x))
+    ln_back(y.xh1, y.rs1, P.norm1, Pg.norm1);
+    t_dw(w.dx, y.c, G(Pg.self_attn.out_w), M, D, D, s, w.skpart);
+    colsum(w.dx, M, D, Pg.self_attn.out_b);
+    t_dx(w.dx, P.self_attn.out_w, w.dc, M, D, D, s);
+    TG(w.dc, D, 1, y.qkv + 2 * D, 3 * D, 1, w.dp, T, 1, T, T, 64)  // dP = dc v^T
+        .batch(B, H, (long)T * D, 64, (long)T * 3 * D, 64, (long)H * T * T, (long)T * T).run(s);
+    TG(y.p, 1, T, w.dc, 1, D, w.dqkv + 2 * D, 3 * D, 1, T, 64, T)  // dv = P^T dc
+        .batch(B, H, (long)H * T * T, (long)T * T, (long)T * D, 64, (long)T * 3 * D, 64).run(s);
+    HIPCHK(launch_softmax_bwd(y.p, w.dp, (long)B * H * T, T, s));
+    TG(w.dp, T, 1, y.qkv + D, 1, 3 * D, w.dqkv, 3 * D, 1, T, 64, T)  // dq = dS k / 8
+        .batch(B, H, (long)H * T * T, (long)T * T, (long)T * 3 * D, 64, (long)T * 3 * D, 64).alpha(0.125f).run(s);
+    TG(w.dp, 1, T, y.qkv, 1, 3 * D, w.dqkv + D, 3 * D, 1, T, 64, T)  // dk = dS^T q / 8
+        .batch(B, H, (long)H * T * T, (long)T * T, (long)T * 3 * D, 64, (long)T * 3 * D, 64).alpha(0.125f).run(s);
+    t_dw(w.dqkv, y.x, G(Pg.self_attn.in_w), M, 3 * D, D, s, w.skpart);
+    colsum(w.dqkv, M, 3 * D, Pg.self_attn.in_b);
+    t_dx(w.dqkv, P.self_attn.in_w, w.dx, M, 3 * D, D, s, 1.f);
+  }
+  HIPCHK(launch_embed_bwd(ids, ld, B, T, w.dx, D, V, (float)std::sqrt((double)D), G(g.emb), s));
+}
+
 }  // namespace
 
 // ================================================================================== C ABI
@@ -1270,6 +1482,14 @@ int icap_encode_vit(icap_handle* h, const float* images, int B, float* memory, v
     REQUIRE(h && images && memory && B > 0, "bad arguments");
     REQUIRE(h->d.kind == ICAP_KIND_VIT, "handle is not a ViT model");
     encode_vit(h, images, B, memory, (hipStream_t)stream);
+  });
+}
+
+int icap_encode_vit_features(icap_handle* h, const float* images, int B, float* memory, float* feats, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && images && memory && feats && B > 0, "bad arguments");
+    REQUIRE(h->d.kind == ICAP_KIND_VIT, "handle is not a ViT model");
+    encode_vit(h, images, B, memory, (hipStream_t)stream, feats);
   });
 }
 
@@ -1500,6 +1720,35 @@ int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uin
   return guarded([&] {
     HIPCHK(launch_enc_attention(qkv, 3L * H * 64, lo, B, N, H, 0.125f, out, (long)H * 64, out_lo, nsplit,
                                 (hipStream_t)stream));
+  });
+}
+
+size_t icap_decoder_train_workspace(const icap_model_desc* d, int B, int T, int S) {
+  if (!d) return 0;
+  return TrainWS(*d, B, T, S, nullptr).floats * sizeof(float);
+}
+
+int icap_decoder_train_forward(const icap_model_desc* d, const int32_t* ids, int B, int T, const float* memory, int S,
+                               int end_token, float* logp, void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    train_check(d, B, T, S);
+    REQUIRE(ids && memory && logp && ws, "null argument");
+    TrainWS w(*d, B, T, S, (float*)ws);
+    REQUIRE(ws_bytes >= w.floats * sizeof(float), "workspace too small (icap_decoder_train_workspace)");
+    train_forward(*d, w, ids, memory, end_token, logp, (hipStream_t)stream);
+  });
+}
+
+int icap_decoder_train_backward(const icap_model_desc* d, const icap_model_desc* grad, const int32_t* ids, int B, int T,
+                                const float* memory, int S, int end_token, const float* dlogp, float* dmemory,
+                                void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    train_check(d, B, T, S);
+    REQUIRE(grad && grad->dec_layers && grad->emb && grad->fc_w && grad->fc_b, "null gradient pointers");
+    REQUIRE(ids && memory && dlogp && ws, "null argument");
+    TrainWS w(*d, B, T, S, (float*)ws);
+    REQUIRE(ws_bytes >= w.floats * sizeof(float), "workspace too small (icap_decoder_train_workspace)");
+    train_backward(*d, *grad, w, ids, memory, end_token, dlogp, dmemory, (hipStream_t)stream);
   });
 }
 

@@ -249,3 +249,37 @@ struct HeadArgs {
   const float* emb; const float* pe; int pe_pos; float emb_scale; float* x_next; bf16_t* a_next; long lo; int nsplit;
 };
 hipError_t launch_head(const HeadArgs& h, hipStream_t s);
+
+// ---- decoder training pass (train.hip): fp32-accurate strided GEMM and the row kernels around it ----
+// C[b][m][n] = alpha * sum_k A[b][m][k] B[b][n][k] (+ beta * C) (+ bias[n]) (relu), element strides
+// (sam, sak) / (sbn, sbk) / (scm, scn); batch index z in [0, nbatch): b1 = z / nb2, b2 = z % nb2 with
+// strides sab1 / sab2 etc.  fp32 operands and products (v_mfma_f32_16x16x4_f32).
+struct TGemmArgs {
+  const float* A; long sam, sak, sab1, sab2;
+  const float* B; long sbn, sbk, sbb1, sbb2;
+  float* C; long scm, scn, scb1, scb2;
+  const float* bias;
+  int M, N, K, nb2;
+  float alpha, beta;
+  int relu;
+  int ksplit; float* part;  // ksplit > 1 (unbatched only): K split over blocks, raw sums in part [ksplit][M][N]
+};
+hipError_t launch_tgemm(const TGemmArgs& a, int nbatch, hipStream_t s);
+hipError_t launch_softmax_rows(float* x, long rows, int n, int T, int causal, hipStream_t s);
+hipError_t launch_softmax_bwd(const float* P, float* dP, long rows, int n, hipStream_t s);
+hipError_t launch_ln_fwd(const float* a, const float* b, const float* w, const float* bias, float eps, int rows, int D,
+                         float* y, float* xhat, float* rstd, hipStream_t s);
+hipError_t launch_ln_bwd(float* dy, const float* xhat, const float* rstd, const float* w, int rows, int D, float* prod,
+                         hipStream_t s);
+size_t colsum_scratch_floats(int n);
+hipError_t launch_colsum(const float* src, long ld, int rows, int n, float* part, float* dst, int accumulate,
+                         hipStream_t s);
+hipError_t launch_relu_bwd(float* dh, const float* h, long n, hipStream_t s);
+hipError_t launch_embed_fwd(const int32_t* ids, long ld, int B, int T, const float* emb, const float* pe, int D,
+                            float scale, float* x, hipStream_t s);
+hipError_t launch_embed_bwd(const int32_t* ids, long ld, int B, int T, const float* dx, int D, int V, float scale,
+                            float* dE, hipStream_t s);
+hipError_t launch_logp_fwd(const float* logits, int V, const int32_t* ids, long ld, int B, int T, int end_token,
+                           float* logp, float* lse, hipStream_t s);
+hipError_t launch_logp_bwd(const float* logits, const float* lse, const float* dlogp, int V, const int32_t* ids,
+                           long ld, int B, int T, int end_token, float* dlogits, hipStream_t s);

@@ -150,6 +150,7 @@ class Engine:
             keep.append(vl)
             desc.kind = _lib.KIND_VIT
             desc.vit_dim = conv.shape[0]
+            self.vit_dim = int(conv.shape[0])
             desc.vit_heads = conv.shape[0] // 64
             desc.vit_mlp = sd[f"{P}encoder.layers.encoder_layer_0.mlp.0.weight"].shape[0]
             desc.vit_layers = n_vit
@@ -232,6 +233,19 @@ class Engine:
             check(self.lib.icap_encode_grid_tail(self.handle, x.data_ptr(), B, mem.data_ptr(),
                                                  stream_ptr(self.device)), "icap_encode_grid_tail")
         return mem
+
+    def encode_vit_features(self, images: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """ViT: images (B,3,224,224) -> (memory (B,196,d), trunk output (B,196,vit_dim) = the projection's
+        input) in one pass (icap_encode_vit_features)."""
+        x = images.to(device=self.device, dtype=torch.float32).contiguous()
+        if self.kind != "vit" or tuple(x.shape[1:]) != (3, 224, 224):
+            raise ValueError("encode_vit_features needs a ViT engine and (B,3,224,224) images")
+        B = x.shape[0]
+        mem = torch.empty(B, self.mem_tokens, self.d_model, device=self.device, dtype=torch.float32)
+        feats = torch.empty(B, self.mem_tokens, self.vit_dim, device=self.device, dtype=torch.float32)
+        check(self.lib.icap_encode_vit_features(self.handle, x.data_ptr(), B, mem.data_ptr(), feats.data_ptr(),
+                                                stream_ptr(self.device)), "icap_encode_vit_features")
+        return mem, feats
 
     def encode_grid_features(self, images: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Grid: images (B,3,224,224) -> (memory (B,49,d), trunk features (B,cnn_dim,7,7)) in one pass."""

@@ -9,8 +9,8 @@ Per rank r of R (one process per GPU, torch.distributed over RCCL; gloo in the C
      CIDEr's document frequency over the whole batch it scores (scst_loss.py:179-180);
   3. CIDEr-D rewards of both sets over the global batch (icap_cider_d on a GPU, the ids
      restatement on a CPU), advantage = r(sample) - r(greedy), local slice;
-  4. teacher-forced recompute of the local samples' token log-probs through the PyTorch modules
-     (autograd) inside a DistributedDataParallel wrapper, loss = -mean(adv * sum_t log p)
+  4. teacher-forced recompute of the local samples' token log-probs (on a GPU: the HIP decoder training
+     pass, image_caption_amd/train.py; on a CPU: the PyTorch modules) inside a DistributedDataParallel wrapper, loss = -mean(adv * sum_t log p)
      (scst_loss.py:190-191) over the local shard: DDP's gradient average over ranks equals the
      gradient of the global-batch mean.
 """
@@ -38,6 +38,12 @@ class TeacherForcedLogProbs(nn.Module):
     def forward(self, images: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
         from utils.scst_loss import masked_token_logp
 
+        if images.is_cuda and getattr(self.model, "hip_backend", "torch") != "torch":
+            # HIP decoder forward + backward (train.py); the encoder's trainable part in PyTorch
+            from .train import decoder_token_logp, hip_memory_with_grad
+
+            return decoder_token_logp(self.model.decoder, hip_memory_with_grad(self.model, images), ids,
+                                      self.end_token)
         memory = self.model.encoder(images)
         L = ids.shape[1]
         mask = self.model.decoder.generate_square_subsequent_mask(L - 1, images.device)

@@ -112,6 +112,10 @@ int icap_update_weights(icap_handle* h, const icap_model_desc* desc, int parts, 
 /* images (B,3,224,224) fp32 normalised -> memory (B,196,d_model) fp32.
  * Replaces: VisionTransformerEncoder.forward, models/vit_transformer_model.py:71-100. */
 int icap_encode_vit(icap_handle* h, const float* images, int B, float* memory, void* stream);
+/* The same, also writing the frozen trunk's output feats (B,196,vit_dim) fp32 = the encoder.projection
+ * input (vit:88-100: the final LayerNorm of the patch tokens): the SCST step applies the trainable
+ * projection in PyTorch so its gradient flows (the ViT itself is frozen, vit:64). */
+int icap_encode_vit_features(icap_handle* h, const float* images, int B, float* memory, float* feats, void* stream);
 
 /* ResNet trunk features (B,cnn_dim,7,7) fp32 -> memory (B,49,d_model) fp32.
  * Replaces: GridFeatureEncoder.forward after self.cnn, models/grid_transformer_model.py:97-108. */
@@ -251,6 +255,24 @@ int icap_op_gemm_tail_split(const uint16_t* A, long lda, long a_lo, int nsplit, 
 int icap_op_gemm_i8_blocks(const int8_t* A, const float* a_scale, const float* a_kscale, const int8_t* W,
                            const float* w_scale, const float* bias, void* C, float* c_kscale, int M, int N, int K,
                            int epi, int out, void* stream);
+/* ---- decoder training pass (SCST's teacher-forced log-prob recompute and its backward) ----
+ * Replaces the autograd graph the reference builds while sampling (SCSTLoss._sample_with_log_probs,
+ * utils/scst_loss.py:210-254: decoder forward + log_softmax + gather + masked_fill) and its backward
+ * (loss.backward(), scripts/train_vit_transformer_scst_optimized.py:261), for the TransformerDecoder
+ * (vit:103-182) as torch.autograd.Function (image_caption_amd/train.py).  Eval-mode forward (dropout off).
+ * `d` holds the decoder's CURRENT fp32 parameters (only the decoder fields are read); ids (B, T+1) int32:
+ * inputs ids[:, :T], targets ids[:, 1:]; memory (B, S, d_model) fp32; logp (B, T) = log p(target) with
+ * the steps after a row's first end_token zeroed.  The forward keeps its activations in ws (bytes from
+ * icap_decoder_train_workspace), which the backward of the same call reads: dlogp (B, T) -> gradients of
+ * every decoder parameter written (not accumulated) to the pointers of `grad` (same layout as `d`) and
+ * dmemory (B, S, d_model) (may be NULL).  fp32 products (fp32 MFMA). */
+size_t icap_decoder_train_workspace(const icap_model_desc* d, int B, int T, int S);
+int icap_decoder_train_forward(const icap_model_desc* d, const int32_t* ids, int B, int T, const float* memory, int S,
+                               int end_token, float* logp, void* ws, size_t ws_bytes, void* stream);
+int icap_decoder_train_backward(const icap_model_desc* d, const icap_model_desc* grad, const int32_t* ids, int B, int T,
+                                const float* memory, int S, int end_token, const float* dlogp, float* dmemory,
+                                void* ws, size_t ws_bytes, void* stream);
+
 /* qkv planes (B*N, 3*H*64) -> out planes (B*N, H*64), non-causal softmax(QK^T/8)V. */
 int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uint16_t* out, long out_lo,
                           int nsplit, void* stream);

@@ -23,21 +23,29 @@ VOCAB.update({"<pad>": 0, "<unk>": 106, "<start>": 107, "<end>": 108})
 REFS = [["w1 w2 w3"], ["w4 w5"], ["w6"], ["w7 w8 w9 w10"], ["w3 w3 w9"], ["w11 w2"], ["w5 w6 w7"], ["w8"]]
 
 
-def _vit_model(cuda, backend="auto", dropout=0.0):
+def _vit_model(cuda, backend="auto", dropout=0.0, precision="f16"):
     from models.vit_transformer_model import build_model
 
-    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False, "dropout": dropout, "backend": backend})
+    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False, "dropout": dropout, "backend": backend,
+                                   "hip_precision": precision})
     m.load_state_dict(W.to_torch(W.vit_state_dict(0)))
     return m.to(cuda)
 
 
-def test_scst_grad_step_matches_torch_sampler(cuda):
+@pytest.mark.parametrize("precision", ["f16", "bf16x2"])
+def test_scst_grad_step_matches_torch_sampler(cuda, precision):
+    """Gradients of every trainable parameter (decoder: HIP training pass; projection: autograd on the HIP
+    trunk's output) against the PyTorch model.  The HIP memory carries the trunk's rounding - fp16
+    operands (f16, the default: 4e-3 on the memory) or 16-bit ones (bf16x2: 1e-5) - which the gradients
+    inherit: held to 2e-2 of each tensor's norm with the f16 trunk (whose memory flips a few ReLU / softmax
+    decisions), to 1e-3 of each tensor's maximum with the bf16x2 trunk.  (The
+    backward itself matches fp64 autograd as closely as fp32 autograd does: tests/test_gpu_train.py.)"""
     from utils.scst_loss import SCSTLoss
 
     B, L = 8, 30
     imgs = torch.from_numpy(W.synthetic_images(B, seed=5)).to(cuda)
     uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(17)).to(cuda)
-    hip_m = _vit_model(cuda)
+    hip_m = _vit_model(cuda, precision=precision)
     ref_m = _vit_model(cuda, backend="torch")
     hip_m.train()
     ref_m.train()
@@ -57,16 +65,21 @@ def test_scst_grad_step_matches_torch_sampler(cuda):
     assert abs(loss_h.item() - loss_r.item()) <= 1e-3 * max(1.0, abs(loss_r.item()))
     loss_h.backward()
     loss_r.backward()
-    gh = dict(hip_m.decoder.named_parameters())
+    # the decoder's gradients come from the HIP training pass (image_caption_amd/train.py), the
+    # projection's from PyTorch autograd on the HIP trunk's output
+    gh = dict(hip_m.named_parameters())
     n = 0
-    for name, p in ref_m.decoder.named_parameters():
+    for name, p in ref_m.named_parameters():
         if p.grad is None:
             continue
         n += 1
         a, b = gh[name].grad, p.grad
         assert a is not None, name
-        assert (a - b).abs().max().item() <= 1e-3 * max(b.abs().max().item(), 1e-6), name
-    assert n > 10
+        if precision == "f16":  # a different memory (fp16 trunk): ReLU / softmax flips, so a norm-wise bound
+            assert (a - b).norm().item() <= 2e-2 * max(b.norm().item(), 1e-9), name
+        else:
+            assert (a - b).abs().max().item() <= 1e-3 * max(b.abs().max().item(), 1e-6), name
+    assert n > 10 and gh["encoder.projection.weight"].grad is not None
 
 
 def test_scst_grid_batchnorm_updated_once(cuda):
