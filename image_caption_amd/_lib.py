@@ -98,6 +98,11 @@ SIGNATURES = {
                                    c_void_p]),
     "icap_decode_sample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
+    "icap_op_residual_layernorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_long, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_long, c_float, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "icap_drop_hash_host": (ctypes.c_uint32, [ctypes.c_uint32] * 6),
+    "icap_decode_sample_dropout": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_float,
+                                           ctypes.c_uint32, c_void_p, c_void_p, c_void_p]),
     "icap_decode_beam": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                  c_void_p, c_void_p]),
     "icap_decoder_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
@@ -113,11 +118,11 @@ SIGNATURES = {
                                   c_int, c_void_p]),
     "icap_op_enc_attention": (c_int, [c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
     "icap_op_cross_attn": (c_int, [c_void_p, c_long, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
-    "icap_decoder_train_workspace": (ctypes.c_size_t, [c_void_p, c_int, c_int, c_int]),
-    "icap_decoder_train_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
-                                           c_void_p, ctypes.c_size_t, c_void_p]),
+    "icap_decoder_train_workspace": (ctypes.c_size_t, [c_void_p, c_int, c_int, c_int, c_float]),
+    "icap_decoder_train_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float,
+                                           ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
     "icap_decoder_train_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
-                                            c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
+                                            c_float, c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
     "icap_stream_create_cu_mask": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
     "icap_stream_destroy": (c_int, [c_void_p]),
     "icap_op_pack_i8": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),

@@ -808,10 +808,13 @@ constexpr int XA_RED_BYTES = (8 * 512 + 512) * 4 + 16;  // + the KS = 2 ticket
 // mem.hi + mem.lo (2 MFMAs instead of 3).  Roles per 64-key chunk:
 //   scores  wave w: key tile w & 3, d-group w >> 2 (128 = 4 k-steps); the 4 d-partials summed through LDS
 //   context wave w: d in [32w, 32w + 32), keys as 2 k-steps of 32 (key tiles 2s, 2s + 1)
+// drop (thr != 0, one row per image): train-mode dropout on the probabilities used for the context (the
+// softmax normaliser stays undropped), mask of (row, drop.pos, head * 256 + memory token).
 template <int DUMMY>
 __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __restrict__ qt, long qt_lo,
                                                               const bf16_t* __restrict__ mem, int rows_per_image,
-                                                              int S, float scale, bf16_t* out, long out_lo) {
+                                                              int S, float scale, bf16_t* out, long out_lo,
+                                                              DropCfg drop, float* gsum) {
   constexpr int DM = 512, H = 8, CK = 64;
   constexpr int BUF = CK * DM * 2;              // 64 KiB per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -868,7 +871,7 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
   f32x4 acc[2];
   acc[0] = (f32x4){0.f, 0.f, 0.f, 0.f};
   acc[1] = acc[0];
-  float m_run = -INFINITY, l_run = 0.f;
+  float m_run = -INFINITY, l_run = 0.f, d_run = 0.f;  // d_run: the dropped-probability mass (train mode)
   const int q4 = fr >> 2, p4 = fr & 3;
 
   stage(0, 0);
@@ -930,6 +933,20 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
     m_run = m_new;
     acc[0] *= alpha;
     acc[1] *= alpha;
+    if (drop.thr) {
+      float dsum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = c * CK + kt * 16 + fq * 4 + j;
+          if (valid && key < S) sc[kt][j] *= drop_mul(drop, 3, (int)r, drop.pos, hd * 256 + key);
+          dsum += sc[kt][j];
+        }
+      dsum += __shfl_xor(dsum, 16, 64);
+      dsum += __shfl_xor(dsum, 32, 64);
+      d_run = d_run * alpha + dsum;
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       // P^T as the B operand of key tiles 2 s2, 2 s2 + 1 (element j < 4 -> key 4fq + j of the first tile,
@@ -959,6 +976,7 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
       stage(c + 2, c & 1);
     }
   }
+  if (valid && drop.thr && gsum && wave == 0 && fq == 0) gsum[r * H + hd] = d_run / l_run;
   if (valid) {
     const float inv = 1.f / l_run;
     bf16_t* dst = out + r * H * DM + hd * DM + wave * 32;
@@ -993,8 +1011,10 @@ int cross_attn_splits(int S) {
 size_t cross_attn_part_floats(int rows) { return (size_t)rows * 2 * XA_PART_FLOATS; }
 
 hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem16, int rows, int rows_per_image,
-                                 int S, float scale, bf16_t* out, long out_lo, hipStream_t s) {
+                                 int S, float scale, bf16_t* out, long out_lo, hipStream_t s, DropCfg drop,
+                                 float* gsum) {
   if (S <= 0 || rows <= 0 || rows_per_image <= 0 || rows % rows_per_image) return hipErrorInvalidValue;
+  if (drop.thr && (rows_per_image != 1 || S > 256 || !gsum)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)cross_attn_f16_kernel<0>,
@@ -1004,7 +1024,7 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
   }
   const int pairs = rows / rows_per_image * ((rows_per_image + 1) / 2);
   hipLaunchKernelGGL(cross_attn_f16_kernel<0>, dim3(pairs), dim3(1024), XA16_LDS, s, qt, qt_lo, mem16,
-                     rows_per_image, S, scale, out, out_lo);
+                     rows_per_image, S, scale, out, out_lo, drop, gsum);
   return hipGetLastError();
 }
 

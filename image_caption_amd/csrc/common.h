@@ -144,3 +144,28 @@ __device__ __forceinline__ void q2_pack4(const float* y, float inv, uint32_t& hi
   }
 }
 
+// ---- counter-based dropout masks (train-mode sampling and the training pass) ----
+// keep(seed, site, layer, row, pos, idx) = h >= thr with h a 32-bit hash of the six integers and
+// thr = round(p 2^32); kept elements are scaled by 1 / (1 - p) (torch.nn.Dropout).  The mask of an
+// element depends only on its (image row, query position, index) - not on the decode step - so the
+// KV-cached sampler and the teacher-forced training pass draw the same masks; oracle/dropout.py is the
+// numpy restatement.  Sites: 0 positional-encoding output, 1 self-attention probabilities (idx = head
+// * 128 + key), 2 self-attention output, 3 cross-attention probabilities (idx = head * 256 + memory
+// token), 4 cross-attention output, 5 feed-forward hidden, 6 feed-forward output; layer 0..15.
+__host__ __device__ inline uint32_t icap_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__host__ __device__ inline uint32_t icap_drop_hash(uint32_t seed, uint32_t site, uint32_t layer, uint32_t row,
+                                                   uint32_t pos, uint32_t idx) {
+  uint32_t h = icap_mix32(idx * 0x9E3779B1u + 0x7F4A7C15u);
+  h = icap_mix32(h ^ (pos * 0x85EBCA77u + 0xC2B2AE3Du));
+  h = icap_mix32(h ^ (row * 0x27D4EB2Fu + 0x165667B1u));
+  h = icap_mix32(h ^ ((site * 16u + layer) * 0x94D049BBu + 0x2545F491u));
+  return icap_mix32(h ^ seed);
+}
+

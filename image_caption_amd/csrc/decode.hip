@@ -202,17 +202,19 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
       const float m = wave_max(s_mine);
       const float e = lane < nkeys ? __expf(s_mine - m) : 0.f;
       l = wave_sum(e);
+      // train mode: dropout on the attention probabilities (key = lane), the normaliser stays undropped
+      const float ed = p.drop.thr && lane < nkeys ? e * drop_mul(p.drop, 1, b, t0, h * 128 + lane) : e;
       // context: lane accumulates dims dq..dq+3 over keys j = 4 i + jg, then the 4 key groups are summed
 #pragma unroll
       for (int i = 0; i < PRE; ++i)
         if (4 * i < nkeys) {
           const int j = 4 * i + jg;
-          ctx += __shfl(e, min(j, 63), 64) * pick(j, vcur, vpre[i]);
+          ctx += __shfl(ed, min(j, 63), 64) * pick(j, vcur, vpre[i]);
         }
       for (int i = PRE; 4 * i < nkeys; ++i) {
         const int j = 4 * i + jg;
         const f32x4 v4 = j < t0 ? hist(p.vc, j) : vcur;
-        ctx += __shfl(e, min(j, 63), 64) * pick(j, vcur, v4);
+        ctx += __shfl(ed, min(j, 63), 64) * pick(j, vcur, v4);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -272,6 +274,9 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
     acc += *(const f32x4*)(p.b1 + j * 128 + n);
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r], 0.f);
+    if (p.drop.thr)  // train mode: dropout on the hidden activations
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] *= drop_mul(p.drop, 5, row0 + fr, p.drop.pos, j * 128 + n + r);
     put_planes(sh, ns, fr, n, acc);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -318,7 +323,9 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) acc += red[(q * 4 + t) * 64 + lane];
     const int n = t * 16 + 4 * fq;
-    acc += *(const f32x4*)(p.b1 + h * 64 + n);
+    const f32x4 bv = *(const f32x4*)(p.b1 + h * 64 + n);
+    if (p.b1_scale) acc += bv * p.b1_scale[(long)min(row0 + fr, p.M - 1) * p.H + h];
+    else acc += bv;
     put_planes(sy, ns, fr, n, acc);
   }
   __syncthreads();

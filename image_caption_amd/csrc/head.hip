@@ -86,7 +86,8 @@ __global__ __launch_bounds__(128) void head_kernel(HeadArgs a) {
   if (a.emb) {
     const long base = (long)r * a.Dm;
     for (int d = tid; d < a.Dm; d += 128) {
-      const float v = a.emb[(long)tok * a.Dm + d] * a.emb_scale + a.pe[(long)a.pe_pos * a.Dm + d];
+      float v = a.emb[(long)tok * a.Dm + d] * a.emb_scale + a.pe[(long)a.pe_pos * a.Dm + d];
+      if (a.drop.thr) v *= drop_mul(a.drop, 0, r, a.pe_pos, d);  // PositionalEncoding's dropout
       a.x_next[base + d] = v;
       bf16_t hi, lo;
       split_bf(v, hi, lo);

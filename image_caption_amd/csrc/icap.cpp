@@ -112,6 +112,7 @@ struct DecLayer {
 // Captured decode loop (hipGraph): all max_len-1 steps x ~80 kernels replayed with one launch.
 struct DecodeGraph {
   int B = 0, S = 0, L = 0, mode = -1, start = -1, end = -1, gen = -1;
+  uint32_t drop_thr = 0;
   bool logits = false;
   int calls = 0;
   hipGraph_t graph = nullptr;
@@ -131,6 +132,7 @@ struct icap_handle {
   bool use_graphs = true;
   hipStream_t cap_stream = nullptr;
   int dec_branches = 2;                 // ICAP_DEC_BRANCHES: independent decode chains per batch
+  DevBuf drop_seed;                     // the sampler's dropout seed (device word read by the kernels)
   static constexpr int MAX_BRANCHES = 4;
   hipStream_t aux_stream[MAX_BRANCHES] = {};  // streams of chains 1.. (chain 0 runs on the caller's)
   hipEvent_t ev_fork = nullptr, ev_join[MAX_BRANCHES] = {};
@@ -203,6 +205,7 @@ struct icap_handle {
   // the greedy and sampled graphs of an SCST step can replay concurrently on two streams
   struct DecWS {
     DevBuf x, a, qkv, q, qt, c, o, h, kv, fin, part, memp, xpart, xcnt;  // xpart / xcnt: split cross-attention
+    DevBuf gs;  // train-mode cross-attention value-bias weights
   } dws[2];
   DevBuf d_beam;
 
@@ -805,6 +808,7 @@ struct DecodeBufs {
   long PS;     // split-K slab stride (of the whole buffer)
   float* xpart;  // split cross-attention partial states / tickets
   int* xcnt;
+  float* gs;     // train-mode cross-attention: per (row, head) weight of the value bias [rows][8]
 };
 
 // Rows [r0, r0 + n) of a decode buffer set (every plane / slab / layer stride stays the whole
@@ -816,6 +820,7 @@ DecodeBufs sub_bufs(const DecodeBufs& b, const icap_model_desc& d, int r0, int L
   v.qt += (size_t)r0 * H * D; v.c += (size_t)r0 * H * D; v.o += (size_t)r0 * D; v.hb += (size_t)r0 * d.dim_ff;
   v.kc += (size_t)r0 * H * Lmax * 64; v.vc += (size_t)r0 * H * Lmax * 64;
   v.part += (size_t)r0 * D; v.memp += (size_t)r0 * S * D;
+  v.gs += (size_t)r0 * H;
   if (v.xpart) {
     v.xpart += cross_attn_part_floats(r0);
     v.xcnt += r0;
@@ -840,6 +845,7 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   w.h.ensure((size_t)rows * d.dim_ff * 2 * ns);
   w.kv.ensure((size_t)2 * d.n_dec_layers * kv_rows * H * Lmax * 64 * 4);
   w.part.ensure((size_t)MAX_KSPLIT * rows * D * 4);
+  w.gs.ensure((size_t)rows * H * 4);
   if (cross_attn_splits(S) > 1) w.xpart.ensure(cross_attn_part_floats(rows) * 4);
   if (cross_attn_splits(S) > 1 && w.xcnt.n < (size_t)rows * 4) {  // tickets: zero at rest (each launch resets its own)
     w.xcnt.ensure((size_t)rows * 4);
@@ -852,6 +858,7 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   b.kc = w.kv.as<float>();
   b.xpart = w.xpart.as<float>(); b.xcnt = w.xcnt.as<int>();
   b.part = w.part.as<float>();
+  b.gs = w.gs.as<float>();
   b.vc = b.kc + (size_t)d.n_dec_layers * kv_rows * H * Lmax * 64;
   b.memp = w.memp.as<bf16_t>(); b.memL = (long)B * S * D;
   b.aL = (long)rows * D; b.qL = (long)rows * D; b.cL = (long)rows * H * D; b.hL = (long)rows * d.dim_ff;
@@ -874,9 +881,10 @@ void mem_planes(icap_handle* h, const float* mem, const DecodeBufs& b, hipStream
 // slabs that the residual-LayerNorm kernel reduces together with bias + residual.
 // B here counts KV rows (sequences); mem_rpi = decoder rows per memory image (default n_new; the
 // beam slots of an image for beam search); anc = beam ancestry table for the self-attention.
+// drop (one-token decode only): train-mode dropout masks (DropCfg; row_base = the chain's first row)
 void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int Lmax, int causal,
                     int S, hipStream_t s, const int32_t* anc = nullptr, int mem_rpi = 0,
-                    const int32_t* klen = nullptr) {
+                    const int32_t* klen = nullptr, const DropCfg* drop = nullptr) {
   const icap_model_desc& d = h->d;
   const int D = d.d_model, H = d.nhead, F = d.dim_ff, rows = B * n_new, ns = h->ns;
   if (mem_rpi <= 0) mem_rpi = n_new;
@@ -886,8 +894,15 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
   // one new token per sequence (the decode loops): the fused self-attention and feed-forward blocks
   // (decode.hip); the teacher-forced / padded forms keep the separate GEMM + attention launches
   const bool fused = n_new == 1 && !klen && causal && D == 512 && H == 8 && F == 2048 && t0 < 64 && t0 < Lmax;
+  REQUIRE(!drop || (fused && ns == 2 && !anc), "dropout needs the one-token decode blocks in a parity precision");
   for (int l = 0; l < d.n_dec_layers; ++l) {
     const DecLayer& L = h->dec[l];
+    DropCfg dl{};
+    if (drop) {
+      dl = *drop;
+      dl.layer = l;
+      dl.pos = t0;
+    }
     // self-attention block
     if (fused) {
       DecSaArgs sa{};
@@ -896,10 +911,11 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       sa.kc = b.kc + l * kv_layer; sa.vc = b.vc + l * kv_layer; sa.Lmax = Lmax; sa.t0 = t0; sa.scale = 0.125f;
       sa.anc = anc;
       sa.part = b.part; sa.part_stride = PS;
+      sa.drop = dl;
       h->timed(PROF_DEC_FUSED, 2.0 * rows * (3.0 * D * D + (double)D * D), 2.0 * (4.0 * D * D + (double)rows * D * ns),
                s, [&] { HIPCHK(launch_dec_sa(sa, s)); });
       HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
-                                       ns, s));
+                                       ns, s, dl, 2));
     } else {
       h->wgemm(b.a, D, b.aL, L.sa_qkv.w, D, L.sa_qkv.b, rows, 3 * D, D, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, WAVE_2x2,
                1, 0, s);
@@ -923,7 +939,8 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
     }
     h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * (double)(rows / mem_rpi) * S * D, s, [&] {
       if (ns == 2)
-        HIPCHK(launch_cross_attn_f16(b.qt, b.cL, b.memp, rows, mem_rpi, S, 0.125f, b.c, b.cL, s));
+        HIPCHK(launch_cross_attn_f16(b.qt, b.cL, b.memp, rows, mem_rpi, S, 0.125f, b.c, b.cL, s, dl,
+                                     drop ? b.gs : nullptr));
       else
         HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, mem_rpi, S, 0.125f, b.c, b.cL, ns, s,
                                       b.xpart, b.xcnt));
@@ -937,20 +954,22 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.W2 = L.ca_out.w; c.ldw2 = D; c.w2_hstride = 64;
       c.C = b.part; c.ldc = D; c.part_stride = PS;
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_PARTIAL;
+      if (drop) c.b1_scale = b.gs;  // the value bias weighs sum_s P_s m_s under probability dropout
       h->chain(c, s, fused);
     }
     HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL, ns,
-                                     s));
+                                     s, dl, 4));
     // feed-forward block
     if (fused) {
       DecFfnArgs ff{};
       ff.A = b.a; ff.aL = b.aL; ff.nsplit = ns; ff.rows = rows;
       ff.W1 = L.lin1.w; ff.b1 = L.lin1.b; ff.W2 = L.lin2.w;
       ff.part = b.part; ff.part_stride = PS;
+      ff.drop = dl;
       h->timed(PROF_DEC_FUSED, 4.0 * rows * (double)D * F, 2.0 * (2.0 * D * F + (double)rows * D * ns), s,
                [&] { HIPCHK(launch_dec_ffn(ff, s)); });
       HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, F / 128, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a,
-                                       b.aL, ns, s));
+                                       b.aL, ns, s, dl, 6));
     } else {
       h->wgemm(b.a, D, b.aL, L.lin1.w, D, L.lin1.b, rows, F, D, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, WAVE_2x2, 1, 0, s);
       h->wgemm(b.hb, F, b.hL, L.lin2.w, F, nullptr, rows, D, F, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_F,
@@ -962,7 +981,8 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
 }
 
 void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
-                       float* step_logits, const float* uniforms, float* logp, hipStream_t s) {
+                       float* step_logits, const float* uniforms, float* logp, hipStream_t s,
+                       const DropCfg* drop = nullptr) {
   const icap_model_desc& d = h->d;
   REQUIRE(B > 0 && max_len >= 1, "bad batch / max_len");
   REQUIRE(max_len <= d.pe_len, "max_len exceeds the positional-encoding table (PositionalEncoding max_len)");
@@ -972,7 +992,8 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   const float scale = (float)std::sqrt((double)D);
   if (mem) mem_planes(h, mem, b, s);
   HIPCHK(launch_fill_col(ids, B, max_len, 0, start, s));
-  HIPCHK(launch_embed(nullptr, 0, start, B, 1, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
+  HIPCHK(launch_embed(nullptr, 0, start, B, 1, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s,
+                      drop ? *drop : DropCfg{}));
   uint8_t* fin = nullptr;
   if (uniforms) {
     h->dws[wsi].fin.ensure((size_t)B);
@@ -1002,7 +1023,12 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
       const int r0 = (int)((long)B * part / nb), n = (int)((long)B * (part + 1) / nb) - r0;
       hipStream_t st = part ? h->aux_stream[part] : s;
       DecodeBufs v = sub_bufs(b, d, r0, max_len, S);
-      decoder_layers(h, v, n, 1, t, max_len, 1, S, st);
+      DropCfg dc{};
+      if (drop) {
+        dc = *drop;
+        dc.row_base = r0;
+      }
+      decoder_layers(h, v, n, 1, t, max_len, 1, S, st, nullptr, 0, nullptr, drop ? &dc : nullptr);
       HeadArgs ha{};
       ha.x = v.x; ha.rows = n; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = d.vocab;
       ha.logits = step_logits ? step_logits + ((size_t)t * B + r0) * d.vocab : nullptr;
@@ -1014,6 +1040,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
       if (t + 2 < max_len) {
         ha.emb = h->emb; ha.pe = h->pe; ha.pe_pos = t + 1; ha.emb_scale = scale;
         ha.x_next = v.x; ha.a_next = v.a; ha.lo = v.aL; ha.nsplit = h->ns;
+        if (drop) ha.drop = dc;
       }
       HIPCHK(launch_head(ha, st));
     }
@@ -1027,22 +1054,36 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
 // Graph path: the first call with a new (B, S, max_len, mode) runs eagerly (allocates the
 // workspace, sets kernel attributes); the second captures the whole loop on a private stream into
 // a hipGraph over handle-owned in/out buffers; later calls copy memory in, replay, copy ids out.
+// drop_p > 0 (sampling only): train-mode dropout masks under drop_seed (DropCfg, common.h)
 void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
-                 float* step_logits, const float* uniforms, float* logp, hipStream_t s) {
+                 float* step_logits, const float* uniforms, float* logp, hipStream_t s, float drop_p = 0.f,
+                 uint32_t drop_seed = 0) {
   const int mode = uniforms ? 1 : 0;
   DecodeGraph& g = h->dg[mode];
   const bool wl = step_logits != nullptr;
+  DropCfg drop{};
+  if (drop_p > 0.f) {
+    REQUIRE(mode == 1 && drop_p < 1.f, "dropout applies to sampling, with p in [0, 1)");
+    h->drop_seed.ensure(4 * 2);
+    uint32_t* sp = h->drop_seed.as<uint32_t>() + mode;
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)sp, (int)drop_seed, 1, s));  // outside any captured graph
+    drop.seed = sp;
+    drop.thr = (uint32_t)std::min(4294967295.0, std::floor((double)drop_p * 4294967296.0 + 0.5));
+    drop.scale = 1.0f / (1.0f - drop_p);
+  }
+  const DropCfg* dp = drop.thr ? &drop : nullptr;
   if (!h->use_graphs) {
-    decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s);
+    decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s, dp);
     return;
   }
   if (g.B != B || g.S != S || g.L != max_len || g.mode != mode || g.logits != wl || g.start != start ||
-      g.end != end || (g.exec && g.gen != g_ws_generation)) {
+      g.end != end || g.drop_thr != drop.thr || (g.exec && g.gen != g_ws_generation)) {
     g.reset();
     g.B = B; g.S = S; g.L = max_len; g.mode = mode; g.logits = wl; g.start = start; g.end = end;
+    g.drop_thr = drop.thr;
   }
   if (!g.exec && g.calls++ == 0) {
-    decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s);
+    decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s, dp);
     return;
   }
   const size_t lg_bytes = (size_t)(max_len - 1) * B * h->d.vocab * 4;
@@ -1063,7 +1104,7 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     try {
       decode_loop_eager(h, nullptr, B, S, max_len, start, end, g.ids.as<int32_t>(),
                         wl ? g.lg.as<float>() : nullptr, mode ? g.uni.as<float>() : nullptr,
-                        mode ? g.lp.as<float>() : nullptr, h->cap_stream);
+                        mode ? g.lp.as<float>() : nullptr, h->cap_stream, dp);
     } catch (...) {
       hipGraph_t dead = nullptr;
       (void)hipStreamEndCapture(h->cap_stream, &dead);
@@ -1147,14 +1188,18 @@ struct TrainWS {
   int B, T, S, D, H, F, V, L, M, MS;
   struct Layer {
     float *x, *qkv, *p, *c, *xh1, *rs1, *x1, *q2, *k2, *v2, *p2, *c2, *xh2, *rs2, *x2, *hh, *xh3, *rs3;
+    float *pd, *pd2, *hd;  // dropped attention probabilities / hidden (alias p, p2, hh without dropout)
   };
+  DropCfg drop{};          // thr 0: eval-mode pass
   std::vector<Layer> lay;
   float *xL, *logits, *lse;
-  float *dx, *dc, *tmp, *dq, *dqkv, *dp, *dh, *dk, *dv, *dlog, *part, *skpart;
+  float *dx, *dc, *tmp, *dq, *dqkv, *dp, *dh, *dk, *dv, *dlog, *part, *skpart, *dm;
+  uint32_t* seed;
   static constexpr size_t SK_FLOATS = (size_t)8 << 20;  // split-K partial sums of the weight gradients
   size_t floats = 0;
-  TrainWS(const icap_model_desc& d, int B_, int T_, int S_, float* base) {
+  TrainWS(const icap_model_desc& d, int B_, int T_, int S_, float* base, float drop_p = 0.f) {
     B = B_; T = T_; S = S_; D = d.d_model; H = d.nhead; F = d.dim_ff; V = d.vocab; L = d.n_dec_layers;
+    const bool dr = drop_p > 0.f;
     M = B * T; MS = B * S;
     size_t off = 0;
     auto take = [&](size_t n) {
@@ -1169,6 +1214,9 @@ struct TrainWS {
       y.xh1 = take(MD); y.rs1 = take(M); y.x1 = take(MD); y.q2 = take(MD); y.k2 = take(MSD); y.v2 = take(MSD);
       y.p2 = take((size_t)B * H * T * S); y.c2 = take(MD); y.xh2 = take(MD); y.rs2 = take(M); y.x2 = take(MD);
       y.hh = take((size_t)M * F); y.xh3 = take(MD); y.rs3 = take(M);
+      y.pd = dr ? take((size_t)B * H * T * T) : y.p;
+      y.pd2 = dr ? take((size_t)B * H * T * S) : y.p2;
+      y.hd = dr ? take((size_t)M * F) : y.hh;
     }
     xL = take(MD); logits = take((size_t)M * V); lse = take(M);
     dx = take(MD); dc = take(MD); tmp = take(MD); dq = take(MD); dqkv = take(3 * MD);
@@ -1176,6 +1224,13 @@ struct TrainWS {
     dlog = take((size_t)M * V);
     part = take(colsum_scratch_floats(std::max(std::max(3 * D, F), std::max(V, D))));
     skpart = take(SK_FLOATS);
+    dm = dr ? take(MD) : nullptr;
+    seed = (uint32_t*)take(64);
+    if (dr) {
+      drop.seed = seed;
+      drop.thr = (uint32_t)std::min(4294967295.0, std::floor((double)drop_p * 4294967296.0 + 0.5));
+      drop.scale = 1.0f / (1.0f - drop_p);
+    }
     floats = off;
   }
 };
@@ -1235,19 +1290,29 @@ void train_forward(const icap_model_desc& d, TrainWS& w, const int32_t* ids, con
                    float* logp, hipStream_t s) {
   const int B = w.B, T = w.T, S = w.S, D = w.D, H = w.H, F = w.F, V = w.V, M = w.M, MS = w.MS;
   const long ld = T + 1;
+  const bool dr = w.drop.thr != 0;
+  auto drop_at = [&](int layer) {
+    DropCfg c = w.drop;
+    c.layer = layer;
+    return c;
+  };
   HIPCHK(launch_embed_fwd(ids, ld, B, T, d.emb, d.pe, D, (float)std::sqrt((double)D), w.lay[0].x, s));
+  if (dr) HIPCHK(launch_drop_rows(w.lay[0].x, w.lay[0].x, B, T, D, drop_at(0), 0, s));
   for (int l = 0; l < w.L; ++l) {
     const icap_dec_layer_w& P = d.dec_layers[l];
     TrainWS::Layer& y = w.lay[l];
     float* xnext = l + 1 < w.L ? w.lay[l + 1].x : w.xL;
+    const DropCfg dl = drop_at(l);
     // self-attention (causal): per (image, head) S = q k^T / 8 -> softmax -> P v
     t_lin(y.x, P.self_attn.in_w, P.self_attn.in_b, y.qkv, M, 3 * D, D, s);
     TG(y.qkv, 3 * D, 1, y.qkv + D, 3 * D, 1, y.p, T, 1, T, T, 64)
         .batch(B, H, (long)T * 3 * D, 64, (long)T * 3 * D, 64, (long)H * T * T, (long)T * T).alpha(0.125f).run(s);
     HIPCHK(launch_softmax_rows(y.p, (long)B * H * T, T, T, 1, s));
-    TG(y.p, T, 1, y.qkv + 2 * D, 1, 3 * D, y.c, D, 1, T, 64, T)
+    if (dr) HIPCHK(launch_drop_attn(y.p, y.pd, B, H, T, T, 128, dl, 1, s));
+    TG(y.pd, T, 1, y.qkv + 2 * D, 1, 3 * D, y.c, D, 1, T, 64, T)
         .batch(B, H, (long)H * T * T, (long)T * T, (long)T * 3 * D, 64, (long)T * D, 64).run(s);
     t_lin(y.c, P.self_attn.out_w, P.self_attn.out_b, w.tmp, M, D, D, s);
+    if (dr) HIPCHK(launch_drop_rows(w.tmp, w.tmp, B, T, D, dl, 2, s));
     HIPCHK(launch_ln_fwd(y.x, w.tmp, P.norm1.w, P.norm1.b, 1e-5f, M, D, y.x1, y.xh1, y.rs1, s));
     // cross-attention over the memory
     t_lin(y.x1, P.cross_attn.in_w, P.cross_attn.in_b, y.q2, M, D, D, s);
@@ -1256,13 +1321,17 @@ void train_forward(const icap_model_desc& d, TrainWS& w, const int32_t* ids, con
     TG(y.q2, D, 1, y.k2, D, 1, y.p2, S, 1, T, S, 64)
         .batch(B, H, (long)T * D, 64, (long)S * D, 64, (long)H * T * S, (long)T * S).alpha(0.125f).run(s);
     HIPCHK(launch_softmax_rows(y.p2, (long)B * H * T, S, T, 0, s));
-    TG(y.p2, S, 1, y.v2, 1, D, y.c2, D, 1, T, 64, S)
+    if (dr) HIPCHK(launch_drop_attn(y.p2, y.pd2, B, H, T, S, 256, dl, 3, s));
+    TG(y.pd2, S, 1, y.v2, 1, D, y.c2, D, 1, T, 64, S)
         .batch(B, H, (long)H * T * S, (long)T * S, (long)S * D, 64, (long)T * D, 64).run(s);
     t_lin(y.c2, P.cross_attn.out_w, P.cross_attn.out_b, w.tmp, M, D, D, s);
+    if (dr) HIPCHK(launch_drop_rows(w.tmp, w.tmp, B, T, D, dl, 4, s));
     HIPCHK(launch_ln_fwd(y.x1, w.tmp, P.norm2.w, P.norm2.b, 1e-5f, M, D, y.x2, y.xh2, y.rs2, s));
     // feed-forward
     t_lin(y.x2, P.lin1_w, P.lin1_b, y.hh, M, F, D, s, true);
-    t_lin(y.hh, P.lin2_w, P.lin2_b, w.tmp, M, D, F, s);
+    if (dr) HIPCHK(launch_drop_rows(y.hh, y.hd, B, T, F, dl, 5, s));
+    t_lin(y.hd, P.lin2_w, P.lin2_b, w.tmp, M, D, F, s);
+    if (dr) HIPCHK(launch_drop_rows(w.tmp, w.tmp, B, T, D, dl, 6, s));
     HIPCHK(launch_ln_fwd(y.x2, w.tmp, P.norm3.w, P.norm3.b, 1e-5f, M, D, xnext, y.xh3, y.rs3, s));
   }
   t_lin(w.xL, d.fc_w, d.fc_b, w.logits, M, V, D, s);
@@ -1282,6 +1351,15 @@ void train_backward(const icap_model_desc& d, const icap_model_desc& g, TrainWS&
     HIPCHK(launch_ln_bwd(w.dx, xh, rs, P.w, M, D, w.tmp, s));
     colsum(w.tmp, M, D, Pg.w);
   };
+  const bool dr = w.drop.thr != 0;
+  // do = dropout mask * ds (the sub-layer output's gradient; ds itself stays in dx for the residual)
+  auto masked = [&](int layer, int site) -> const float* {
+    if (!dr) return w.dx;
+    DropCfg c = w.drop;
+    c.layer = layer;
+    HIPCHK(launch_drop_rows(w.dx, w.dm, B, T, D, c, site, s));
+    return w.dm;
+  };
   HIPCHK(launch_logp_bwd(w.logits, w.lse, dlogp, V, ids, ld, B, T, end, w.dlog, s));
   t_dw(w.dlog, w.xL, G(g.fc_w), M, V, D, s, w.skpart);
   colsum(w.dlog, M, V, g.fc_b);
@@ -1290,24 +1368,30 @@ void train_backward(const icap_model_desc& d, const icap_model_desc& g, TrainWS&
     const icap_dec_layer_w& P = d.dec_layers[l];
     const icap_dec_layer_w& Pg = g.dec_layers[l];
     TrainWS::Layer& y = w.lay[l];
-    // x3 = LN3(x2 + W2 relu(W1 x2 + b1) + b2)
+    DropCfg dl = w.drop;
+    dl.layer = l;
+    // x3 = LN3(x2 + drop(W2 drop(relu(W1 x2 + b1)) + b2))
     ln_back(y.xh3, y.rs3, P.norm3, Pg.norm3);
-    t_dw(w.dx, y.hh, G(Pg.lin2_w), M, D, F, s, w.skpart);
-    colsum(w.dx, M, D, Pg.lin2_b);
-    t_dx(w.dx, P.lin2_w, w.dh, M, D, F, s);
+    const float* df = masked(l, 6);
+    t_dw(df, y.hd, G(Pg.lin2_w), M, D, F, s, w.skpart);
+    colsum(df, M, D, Pg.lin2_b);
+    t_dx(df, P.lin2_w, w.dh, M, D, F, s);
+    if (dr) HIPCHK(launch_drop_rows(w.dh, w.dh, B, T, F, dl, 5, s));
     HIPCHK(launch_relu_bwd(w.dh, y.hh, (long)M * F, s));
     t_dw(w.dh, y.x2, G(Pg.lin1_w), M, F, D, s, w.skpart);
     colsum(w.dh, M, F, Pg.lin1_b);
     t_dx(w.dh, P.lin1_w, w.dx, M, F, D, s, 1.f);
     // x2 = LN2(x1 + CA(x1, mem))
     ln_back(y.xh2, y.rs2, P.norm2, Pg.norm2);
-    t_dw(w.dx, y.c2, G(Pg.cross_attn.out_w), M, D, D, s, w.skpart);
-    colsum(w.dx, M, D, Pg.cross_attn.out_b);
-    t_dx(w.dx, P.cross_attn.out_w, w.dc, M, D, D, s);
-    TG(w.dc, D, 1, y.v2, D, 1, w.dp, S, 1, T, S, 64)  // dP2 = dc2 V2^T
+    const float* do2 = masked(l, 4);
+    t_dw(do2, y.c2, G(Pg.cross_attn.out_w), M, D, D, s, w.skpart);
+    colsum(do2, M, D, Pg.cross_attn.out_b);
+    t_dx(do2, P.cross_attn.out_w, w.dc, M, D, D, s);
+    TG(w.dc, D, 1, y.v2, D, 1, w.dp, S, 1, T, S, 64)  // d(dropped P2) = dc2 V2^T
         .batch(B, H, (long)T * D, 64, (long)S * D, 64, (long)H * T * S, (long)T * S).run(s);
-    TG(y.p2, 1, S, w.dc, 1, D, w.dv, D, 1, S, 64, T)  // dV2 = P2^T dc2
+    TG(y.pd2, 1, S, w.dc, 1, D, w.dv, D, 1, S, 64, T)  // dV2 = (dropped P2)^T dc2
         .batch(B, H, (long)H * T * S, (long)T * S, (long)T * D, 64, (long)S * D, 64).run(s);
+    if (dr) HIPCHK(launch_drop_attn(w.dp, w.dp, B, H, T, S, 256, dl, 3, s));
     HIPCHK(launch_softmax_bwd(y.p2, w.dp, (long)B * H * T, S, s));
     TG(w.dp, S, 1, y.k2, 1, D, w.dq, D, 1, T, 64, S)  // dq2 = dS2 K2 / 8
         .batch(B, H, (long)H * T * S, (long)T * S, (long)S * D, 64, (long)T * D, 64).alpha(0.125f).run(s);
@@ -1326,13 +1410,15 @@ void train_backward(const icap_model_desc& d, const icap_model_desc& g, TrainWS&
     }
     // x1 = LN1(x + SA(x))
     ln_back(y.xh1, y.rs1, P.norm1, Pg.norm1);
-    t_dw(w.dx, y.c, G(Pg.self_attn.out_w), M, D, D, s, w.skpart);
-    colsum(w.dx, M, D, Pg.self_attn.out_b);
-    t_dx(w.dx, P.self_attn.out_w, w.dc, M, D, D, s);
-    TG(w.dc, D, 1, y.qkv + 2 * D, 3 * D, 1, w.dp, T, 1, T, T, 64)  // dP = dc v^T
+    const float* do1 = masked(l, 2);
+    t_dw(do1, y.c, G(Pg.self_attn.out_w), M, D, D, s, w.skpart);
+    colsum(do1, M, D, Pg.self_attn.out_b);
+    t_dx(do1, P.self_attn.out_w, w.dc, M, D, D, s);
+    TG(w.dc, D, 1, y.qkv + 2 * D, 3 * D, 1, w.dp, T, 1, T, T, 64)  // d(dropped P) = dc v^T
         .batch(B, H, (long)T * D, 64, (long)T * 3 * D, 64, (long)H * T * T, (long)T * T).run(s);
-    TG(y.p, 1, T, w.dc, 1, D, w.dqkv + 2 * D, 3 * D, 1, T, 64, T)  // dv = P^T dc
+    TG(y.pd, 1, T, w.dc, 1, D, w.dqkv + 2 * D, 3 * D, 1, T, 64, T)  // dv = (dropped P)^T dc
         .batch(B, H, (long)H * T * T, (long)T * T, (long)T * D, 64, (long)T * 3 * D, 64).run(s);
+    if (dr) HIPCHK(launch_drop_attn(w.dp, w.dp, B, H, T, T, 128, dl, 1, s));
     HIPCHK(launch_softmax_bwd(y.p, w.dp, (long)B * H * T, T, s));
     TG(w.dp, T, 1, y.qkv + D, 1, 3 * D, w.dqkv, 3 * D, 1, T, 64, T)  // dq = dS k / 8
         .batch(B, H, (long)H * T * T, (long)T * T, (long)T * 3 * D, 64, (long)T * 3 * D, 64).alpha(0.125f).run(s);
@@ -1341,6 +1427,11 @@ void train_backward(const icap_model_desc& d, const icap_model_desc& g, TrainWS&
     t_dw(w.dqkv, y.x, G(Pg.self_attn.in_w), M, 3 * D, D, s, w.skpart);
     colsum(w.dqkv, M, 3 * D, Pg.self_attn.in_b);
     t_dx(w.dqkv, P.self_attn.in_w, w.dx, M, 3 * D, D, s, 1.f);
+  }
+  if (dr) {
+    DropCfg c = w.drop;
+    c.layer = 0;
+    HIPCHK(launch_drop_rows(w.dx, w.dx, B, T, D, c, 0, s));
   }
   HIPCHK(launch_embed_bwd(ids, ld, B, T, w.dx, D, V, (float)std::sqrt((double)D), G(g.emb), s));
 }
@@ -1556,6 +1647,17 @@ int icap_decode_sample(icap_handle* h, const float* memory, int B, int S, int ma
   });
 }
 
+int icap_decode_sample_dropout(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                               int end_token, const float* uniforms, float p, uint32_t seed, int32_t* ids, float* logp,
+                               void* stream) {
+  return guarded([&] {
+    REQUIRE(h && memory && ids && uniforms && logp, "bad arguments");
+    REQUIRE(p >= 0.f && p < 1.f, "dropout p must be in [0, 1)");
+    decode_loop(h, memory, B, S, max_len, start_token, end_token, ids, nullptr, uniforms, logp, (hipStream_t)stream,
+                p, seed);
+  });
+}
+
 int icap_decode_beam(icap_handle* h, const float* memory, int B, int S, int max_len, int beam_size, int grid_variant,
                      int start_token, int end_token, int32_t* ids, int32_t* lengths, void* stream) {
   return guarded([&] {
@@ -1723,33 +1825,57 @@ int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uin
   });
 }
 
-size_t icap_decoder_train_workspace(const icap_model_desc* d, int B, int T, int S) {
+size_t icap_decoder_train_workspace(const icap_model_desc* d, int B, int T, int S, float drop_p) {
   if (!d) return 0;
-  return TrainWS(*d, B, T, S, nullptr).floats * sizeof(float);
+  return TrainWS(*d, B, T, S, nullptr, drop_p).floats * sizeof(float);
 }
 
 int icap_decoder_train_forward(const icap_model_desc* d, const int32_t* ids, int B, int T, const float* memory, int S,
-                               int end_token, float* logp, void* ws, size_t ws_bytes, void* stream) {
+                               int end_token, float drop_p, uint32_t drop_seed, float* logp, void* ws, size_t ws_bytes,
+                               void* stream) {
   return guarded([&] {
     train_check(d, B, T, S);
     REQUIRE(ids && memory && logp && ws, "null argument");
-    TrainWS w(*d, B, T, S, (float*)ws);
+    REQUIRE(drop_p >= 0.f && drop_p < 1.f && (drop_p == 0.f || (T <= 128 && S <= 256)), "bad dropout p / lengths");
+    TrainWS w(*d, B, T, S, (float*)ws, drop_p);
     REQUIRE(ws_bytes >= w.floats * sizeof(float), "workspace too small (icap_decoder_train_workspace)");
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)w.seed, (int)drop_seed, 1, (hipStream_t)stream));
     train_forward(*d, w, ids, memory, end_token, logp, (hipStream_t)stream);
   });
 }
 
 int icap_decoder_train_backward(const icap_model_desc* d, const icap_model_desc* grad, const int32_t* ids, int B, int T,
-                                const float* memory, int S, int end_token, const float* dlogp, float* dmemory,
-                                void* ws, size_t ws_bytes, void* stream) {
+                                const float* memory, int S, int end_token, float drop_p, const float* dlogp,
+                                float* dmemory, void* ws, size_t ws_bytes, void* stream) {
   return guarded([&] {
     train_check(d, B, T, S);
     REQUIRE(grad && grad->dec_layers && grad->emb && grad->fc_w && grad->fc_b, "null gradient pointers");
     REQUIRE(ids && memory && dlogp && ws, "null argument");
-    TrainWS w(*d, B, T, S, (float*)ws);
+    TrainWS w(*d, B, T, S, (float*)ws, drop_p);  // the seed word the forward left in ws
     REQUIRE(ws_bytes >= w.floats * sizeof(float), "workspace too small (icap_decoder_train_workspace)");
     train_backward(*d, *grad, w, ids, memory, end_token, dlogp, dmemory, (hipStream_t)stream);
   });
+}
+
+int icap_op_residual_layernorm(float* x, int rows, const float* parts, int nparts, long part_stride, const float* bias,
+                               const float* w, const float* b, uint16_t* out, long out_lo, float drop_p,
+                               const uint32_t* seed, int layer, int pos, int site, void* stream) {
+  return guarded([&] {
+    DropCfg d{};
+    if (drop_p > 0.f) {
+      d.seed = seed;
+      d.thr = (uint32_t)std::min(4294967295.0, std::floor((double)drop_p * 4294967296.0 + 0.5));
+      d.scale = 1.0f / (1.0f - drop_p);
+      d.layer = layer;
+      d.pos = pos;
+    }
+    HIPCHK(launch_residual_layernorm(x, rows, 512, parts, nparts, part_stride, bias, w, b, 1e-5f, out, out_lo, 2,
+                                     (hipStream_t)stream, d, site));
+  });
+}
+
+uint32_t icap_drop_hash_host(uint32_t seed, uint32_t site, uint32_t layer, uint32_t row, uint32_t pos, uint32_t idx) {
+  return icap_drop_hash(seed, site, layer, row, pos, idx);
 }
 
 int icap_op_cross_attn(const uint16_t* qt, long qt_lo, const uint16_t* mem16, int rows, int rows_per_image, int S,

@@ -11,6 +11,7 @@ typedef uint16_t bf16_t;
 // while one is set (icap_knobs_set), so no environment can change what the library computes.
 #ifdef ICAP_TOOLS
 #include <stdlib.h>
+
 inline int icap_knob(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
@@ -20,6 +21,18 @@ inline int icap_knob(const char*, int dflt) { return dflt; }
 #endif
 // Name of the first knob set in the environment ("" when none); checked by icap_create in a product build.
 extern "C" const char* icap_knobs_set();
+
+#include "common.h"
+
+// Dropout of the train-mode decoder (common.h icap_drop_hash): thr = round(p 2^32) (0: off), scale = 1/(1-p),
+// the seed read from device memory (so a captured decode graph replays with each call's seed); row_base
+// is added to a kernel's local row index (the chains of a batch), site / layer name the mask.
+struct DropCfg {
+  const uint32_t* seed; uint32_t thr; float scale; int row_base; int layer; int pos;
+};
+__device__ __forceinline__ float drop_mul(const DropCfg& d, int site, int row, int pos, int idx) {
+  return icap_drop_hash(*d.seed, site, d.layer, d.row_base + row, pos, idx) >= d.thr ? d.scale : 0.f;
+}
 
 // Plane format argument of the row kernels (layernorm, im2col, split): 1 = one bf16 plane, 2 = bf16 hi/lo
 // planes, NS_F16 = one fp16 plane (ICAP_PREC_F16 encoder).
@@ -127,6 +140,9 @@ struct ChainArgs {
   const bf16_t* W2; long ldw2; long w2_hstride;
   void* C; long ldc; long c_lo; long c_hstride; long part_stride;
   int M, N2, H, nsplit, out;
+  // dec_chain only: b1 scaled per (row, head) by b1_scale[row * H + h] - the value projection of the
+  // key-absorbed cross-attention under probability dropout, whose bias enters as sum_s P_s m_s (not 1)
+  const float* b1_scale;
 };
 hipError_t launch_chain_dec(const ChainArgs& a, hipStream_t s);
 
@@ -139,6 +155,7 @@ struct DecSaArgs {
   const bf16_t* Wqkv; const float* bqkv; const bf16_t* Wo;
   float *kc, *vc; int Lmax, t0; float scale; const int32_t* anc;
   float* part; long part_stride;
+  DropCfg drop;  // thr 0: no dropout (site 1: the attention probabilities)
 };
 hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s);
 // dec_ffn: slab j of 16 = relu(a W1[128j:128j+128]^T + b1) W2[:, 128j:128j+128]^T -> part[j][rows][512]
@@ -146,6 +163,7 @@ struct DecFfnArgs {
   const bf16_t* A; long aL; int nsplit, rows;
   const bf16_t* W1; const float* b1; const bf16_t* W2;
   float* part; long part_stride;
+  DropCfg drop;  // site 5: the hidden activations (pos = the decode position)
 };
 hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s);
 // The chained per-head cross-attention products (ChainArgs as launch_chain_dec, N2 = 512) with 16-row
@@ -162,7 +180,7 @@ hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_gr
 // x = LN(x + sum_{s<nparts} parts[s*part_stride + row*D + col] + bias) in place (fp32), plus planes.
 hipError_t launch_residual_layernorm(float* x, int rows, int D, const float* parts, int nparts, long part_stride,
                                     const float* bias, const float* w, const float* b, float eps, bf16_t* out_bf,
-                                    long bf_lo, int nsplit, hipStream_t s);
+                                    long bf_lo, int nsplit, hipStream_t s, DropCfg drop = DropCfg{}, int site = 0);
 hipError_t launch_im2col_patches(const float* img, int B, int C, int HW, int P, bf16_t* out, long lo,
                                  int nsplit, hipStream_t s);
 hipError_t launch_cls_rows(const float* cls, const float* pos, float* x, int B, int tokens, int D,
@@ -194,7 +212,8 @@ hipError_t launch_image_nhwc4(const float* img, int B, int HW, int border, bf16_
 hipError_t launch_bn_fold(const float* g, const float* b, const float* mean, const float* var, int C, float eps,
                           float* scale, float* shift, hipStream_t s);
 hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0, const float* emb,
-                        const float* pe, int D, float scale, float* x, bf16_t* a, long lo, int nsplit, hipStream_t s);
+                        const float* pe, int D, float scale, float* x, bf16_t* a, long lo, int nsplit, hipStream_t s,
+                        DropCfg drop = DropCfg{});
 // byte fill as a kernel (captured into decode graphs: a captured small hipMemsetAsync was not
 // re-applied on the second replay of the sampled-decode graph, ROCm 7.2)
 hipError_t launch_fill_u8(uint8_t* p, long n, uint8_t value, hipStream_t s);
@@ -223,8 +242,10 @@ hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* me
                                   hipStream_t s, float* xpart = nullptr, int* xcnt = nullptr);
 // The same over a single fp16 memory plane mem16 [B][S][512] (q~ bf16 hi/lo planes in, context bf16 hi/lo
 // planes out): the decoder's cross-attention in the parity precisions (attention.hip).
+// drop (train mode): gsum [rows][8] receives sum_s P_s m_s / sum_s P_s per (row, head) (the value bias's weight)
 hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem16, int rows, int rows_per_image,
-                                 int S, float scale, bf16_t* out, long out_lo, hipStream_t s);
+                                 int S, float scale, bf16_t* out, long out_lo, hipStream_t s,
+                                 DropCfg drop = DropCfg{}, float* gsum = nullptr);
 int cross_attn_splits(int S);
 size_t cross_attn_part_floats(int rows);
 // Batched beam search (beam.hip): state init, per-step selection, final pick.
@@ -247,6 +268,7 @@ struct HeadArgs {
   const float* uniforms;  // null => argmax
   float* logp; long ld_logp; uint8_t* finished; int end_token;
   const float* emb; const float* pe; int pe_pos; float emb_scale; float* x_next; bf16_t* a_next; long lo; int nsplit;
+  DropCfg drop;  // site 0 on the next step's embedding (positional-encoding dropout)
 };
 hipError_t launch_head(const HeadArgs& h, hipStream_t s);
 
@@ -283,3 +305,6 @@ hipError_t launch_logp_fwd(const float* logits, int V, const int32_t* ids, long 
                            float* logp, float* lse, hipStream_t s);
 hipError_t launch_logp_bwd(const float* logits, const float* lse, const float* dlogp, int V, const int32_t* ids,
                            long ld, int B, int T, int end_token, float* dlogits, hipStream_t s);
+hipError_t launch_drop_rows(const float* x, float* out, int B, int T, int n, DropCfg d, int site, hipStream_t s);
+hipError_t launch_drop_attn(const float* x, float* out, int B, int H, int T, int Tk, int stride, DropCfg d, int site,
+                            hipStream_t s);

@@ -164,7 +164,8 @@ __global__ __launch_bounds__(NT) void residual_layernorm_kernel(float* __restric
                                                                 long part_stride, const float* __restrict__ bias,
                                                                 const float* __restrict__ w,
                                                                 const float* __restrict__ b, float eps,
-                                                                bf16_t* out_bf, long bf_lo, int nsplit) {
+                                                                bf16_t* out_bf, long bf_lo, int nsplit,
+                                                                DropCfg drop, int site) {
   constexpr int D = NT * 4, NW = NT / 64;
   __shared__ float red[2][NW];
   const int row = blockIdx.x, col = threadIdx.x * 4;
@@ -177,9 +178,17 @@ __global__ __launch_bounds__(NT) void residual_layernorm_kernel(float* __restric
   f32x4 v = *(const f32x4*)(xr + col);
   const f32x4 bb = bias ? *(const f32x4*)(bias + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
   const f32x4 wv = *(const f32x4*)(w + col), bv = *(const f32x4*)(b + col);
-  v += bb;
+  if (drop.thr == 0) {
+    v += bb;
 #pragma unroll
-  for (int s = 0; s < RLN_MAX_PARTS; ++s) v += pp[s];
+    for (int s = 0; s < RLN_MAX_PARTS; ++s) v += pp[s];
+  } else {  // x + dropout(sublayer output) (TransformerDecoderLayer dropout1 / 2 / 3)
+    f32x4 o = bb;
+#pragma unroll
+    for (int s = 0; s < RLN_MAX_PARTS; ++s) o += pp[s];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] += o[k] * drop_mul(drop, site, row, drop.pos, col + k);
+  }
   float sm = wave_sum(v[0] + v[1] + v[2] + v[3]);
   if (lane == 0) red[0][wave] = sm;
   __syncthreads();
@@ -265,12 +274,13 @@ __global__ void nchw_to_rows_kernel(const float* __restrict__ f, int B, int C, i
 // x[r] = emb[tok[r]] * scale + pe[t0 + r % T]  (TransformerDecoder.forward, vit:166-169)
 __global__ void embed_kernel(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0,
                              const float* emb, const float* pe, int D, float scale, float* x, bf16_t* a, long lo,
-                             int nsplit) {
+                             int nsplit, DropCfg drop) {
   const long total = (long)rows * D;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int d = (int)(i % D), r = (int)(i / D);
     const int t = tok ? tok[(long)(r / T) * tok_ld + r % T] : fixed_tok;
-    const float v = emb[(long)t * D + d] * scale + pe[(long)(t0 + r % T) * D + d];
+    float v = emb[(long)t * D + d] * scale + pe[(long)(t0 + r % T) * D + d];
+    if (drop.thr) v *= drop_mul(drop, 0, r / T, t0 + r % T, d);  // PositionalEncoding's dropout
     x[i] = v;
     store_planes(a, i, lo, nsplit, v);
   }
@@ -359,15 +369,15 @@ hipError_t launch_pack_i8_rows(const float* w, int N, int K, int8_t* out, float*
 
 hipError_t launch_residual_layernorm(float* x, int rows, int D, const float* parts, int nparts, long part_stride,
                                     const float* bias, const float* w, const float* b, float eps, bf16_t* out_bf,
-                                    long bf_lo, int nsplit, hipStream_t s) {
+                                    long bf_lo, int nsplit, hipStream_t s, DropCfg drop, int site) {
   if (nparts < 0 || nparts > RLN_MAX_PARTS || rows <= 0) return hipErrorInvalidValue;
   dim3 grid(rows);
   if (D == 512)
     hipLaunchKernelGGL(residual_layernorm_kernel<128>, grid, dim3(128), 0, s, x, rows, parts, nparts, part_stride,
-                       bias, w, b, eps, out_bf, bf_lo, nsplit);
+                       bias, w, b, eps, out_bf, bf_lo, nsplit, drop, site);
   else if (D == 768)
     hipLaunchKernelGGL(residual_layernorm_kernel<192>, grid, dim3(192), 0, s, x, rows, parts, nparts, part_stride,
-                       bias, w, b, eps, out_bf, bf_lo, nsplit);
+                       bias, w, b, eps, out_bf, bf_lo, nsplit, drop, site);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -395,9 +405,10 @@ hipError_t launch_nchw_to_rows(const float* feats, int B, int C, int S, bf16_t* 
 }
 
 hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0, const float* emb,
-                        const float* pe, int D, float scale, float* x, bf16_t* a, long lo, int nsplit, hipStream_t s) {
+                        const float* pe, int D, float scale, float* x, bf16_t* a, long lo, int nsplit, hipStream_t s,
+                        DropCfg drop) {
   hipLaunchKernelGGL(embed_kernel, dim3(grid_for((long)rows * D)), dim3(256), 0, s, tok, tok_ld, fixed_tok, rows, T,
-                     t0, emb, pe, D, scale, x, a, lo, nsplit);
+                     t0, emb, pe, D, scale, x, a, lo, nsplit, drop);
   return hipGetLastError();
 }
 

@@ -354,6 +354,25 @@ __global__ __launch_bounds__(256) void logp_bwd_kernel(const float* logits, cons
     dlogits[(long)m * V + j] = g * ((j == tgt ? 1.f : 0.f) - __expf(logits[(long)m * V + j] - l));
 }
 
+// dropout masks of the training pass (common.h): out = x * mask over a (B*T, n) matrix (row m = image
+// m / T, position m % T, index = column) or over attention probabilities (B, H, T, Tk): image, head, query
+// position, key -> index head * stride + key.  out may alias x.
+__global__ void drop_rows_kernel(const float* x, float* out, int T, int n, long total, DropCfg d, int site) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long m = i / n;
+    const int c = (int)(i - m * n);
+    out[i] = x[i] * drop_mul(d, site, (int)(m / T), (int)(m % T), c);
+  }
+}
+__global__ void drop_attn_kernel(const float* x, float* out, int H, int T, int Tk, int stride, long total, DropCfg d,
+                                 int site) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / Tk;
+    const int j = (int)(i - row * Tk), t = (int)(row % T), h = (int)((row / T) % H), b = (int)(row / ((long)T * H));
+    out[i] = x[i] * drop_mul(d, site, b, t, h * stride + j);
+  }
+}
+
 int ew_grid(long n) { return (int)std::min<long>((n + 255) / 256, 8192); }
 
 }  // namespace
@@ -446,5 +465,19 @@ hipError_t launch_logp_bwd(const float* logits, const float* lse, const float* d
                            long ld, int B, int T, int end_token, float* dlogits, hipStream_t s) {
   hipLaunchKernelGGL(logp_bwd_kernel, dim3((B * T + 3) / 4), dim3(256), 0, s, logits, lse, dlogp, V, ids, ld, B, T,
                      end_token, dlogits);
+  return hipGetLastError();
+}
+
+hipError_t launch_drop_rows(const float* x, float* out, int B, int T, int n, DropCfg d, int site, hipStream_t s) {
+  const long total = (long)B * T * n;
+  hipLaunchKernelGGL(drop_rows_kernel, dim3(ew_grid(total)), dim3(256), 0, s, x, out, T, n, total, d, site);
+  return hipGetLastError();
+}
+
+hipError_t launch_drop_attn(const float* x, float* out, int B, int H, int T, int Tk, int stride, DropCfg d, int site,
+                            hipStream_t s) {
+  const long total = (long)B * H * T * Tk;
+  hipLaunchKernelGGL(drop_attn_kernel, dim3(ew_grid(total)), dim3(256), 0, s, x, out, H, T, Tk, stride, total, d,
+                     site);
   return hipGetLastError();
 }

@@ -278,8 +278,9 @@ class Engine:
         return apply_stop_rule(ids.long(), end)
 
     def sample(self, memory: torch.Tensor, uniforms: torch.Tensor, start: int, end: int,
-               max_len: int) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Sampled ids (B,max_len) int32 and per-step log-probs (B,max_len-1), no early stop."""
+               max_len: int, dropout: Optional[Tuple[float, int]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Sampled ids (B,max_len) int32 and per-step log-probs (B,max_len-1), no early stop.
+        dropout = (p, seed): train-mode sampling (icap_decode_sample_dropout)."""
         mem = memory.to(device=self.device, dtype=torch.float32).contiguous()
         B, S = mem.shape[0], mem.shape[1]
         u = uniforms.to(device=self.device, dtype=torch.float32).contiguous()
@@ -287,6 +288,12 @@ class Engine:
             raise ValueError("uniforms must be (max_len-1, B)")
         ids = torch.empty(B, max_len, device=self.device, dtype=torch.int32)
         logp = torch.empty(B, max_len - 1, device=self.device, dtype=torch.float32)
+        if dropout is not None and dropout[0] > 0:
+            check(self.lib.icap_decode_sample_dropout(self.handle, mem.data_ptr(), B, S, max_len, int(start),
+                                                      int(end), u.data_ptr(), float(dropout[0]),
+                                                      int(dropout[1]) & 0xFFFFFFFF, ids.data_ptr(), logp.data_ptr(),
+                                                      stream_ptr(self.device)), "icap_decode_sample_dropout")
+            return ids, logp
         check(self.lib.icap_decode_sample(self.handle, mem.data_ptr(), B, S, max_len, int(start), int(end),
                                           u.data_ptr(), ids.data_ptr(), logp.data_ptr(), stream_ptr(self.device)),
               "icap_decode_sample")

@@ -6,7 +6,8 @@ autograd (projection / Grid tail) see ordinary parameter gradients.
 Reference: the autograd graph SCSTLoss._sample_with_log_probs builds (utils/scst_loss.py:210-254 of the
 reference: decoder forward, log_softmax, gather, masked_fill after <end>) and loss.backward()
 (scripts/train_vit_transformer_scst_optimized.py:261).  Eval-mode forward: no dropout, the same as the HIP
-sampler (so the distribution sampled from is the one differentiated)."""
+sampler; or train mode with the sampler's counter-based dropout masks (p, seed): the same masks, so the
+distribution sampled from is the one differentiated either way."""
 from __future__ import annotations
 
 import ctypes
@@ -56,7 +57,7 @@ def _desc(t: dict, n_layers: int, d_model: int, nhead: int, pe: torch.Tensor):
 class _DecoderLogProbs(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg, memory, ids, *params):
-        lib, n_layers, d_model, nhead, pe, end = cfg
+        lib, n_layers, d_model, nhead, pe, end, drop_p, seed = cfg
         names = decoder_param_names(n_layers)
         t = dict(zip(names, params))
         desc, keep = _desc(t, n_layers, d_model, nhead, pe)
@@ -64,11 +65,12 @@ class _DecoderLogProbs(torch.autograd.Function):
         T, S = L - 1, memory.shape[1]
         mem = memory.detach().float().contiguous()
         ids32 = ids.to(torch.int32).contiguous()
-        nbytes = lib.icap_decoder_train_workspace(ctypes.byref(desc), B, T, S)
+        nbytes = lib.icap_decoder_train_workspace(ctypes.byref(desc), B, T, S, drop_p)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=memory.device)
         logp = torch.empty(B, T, dtype=torch.float32, device=memory.device)
         check(lib.icap_decoder_train_forward(ctypes.byref(desc), ids32.data_ptr(), B, T, mem.data_ptr(), S, end,
-                                             logp.data_ptr(), ws.data_ptr(), nbytes, stream_ptr(memory.device)),
+                                             drop_p, seed, logp.data_ptr(), ws.data_ptr(), nbytes,
+                                             stream_ptr(memory.device)),
               "icap_decoder_train_forward")
         ctx.cfg, ctx.ws, ctx.keep = cfg, ws, keep
         ctx.save_for_backward(mem, ids32, *params)
@@ -77,7 +79,7 @@ class _DecoderLogProbs(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dlogp):
-        lib, n_layers, d_model, nhead, pe, end = ctx.cfg
+        lib, n_layers, d_model, nhead, pe, end, drop_p, _ = ctx.cfg
         mem, ids32, *params = ctx.saved_tensors
         names = decoder_param_names(n_layers)
         t = dict(zip(names, params))
@@ -88,7 +90,7 @@ class _DecoderLogProbs(torch.autograd.Function):
         dmem = torch.empty_like(mem) if ctx.mem_grad else None
         dl = dlogp.float().contiguous()
         check(lib.icap_decoder_train_backward(ctypes.byref(desc), ctypes.byref(gdesc), ids32.data_ptr(), B, L - 1,
-                                              mem.data_ptr(), mem.shape[1], end, dl.data_ptr(),
+                                              mem.data_ptr(), mem.shape[1], end, drop_p, dl.data_ptr(),
                                               None if dmem is None else dmem.data_ptr(), ctx.ws.data_ptr(),
                                               ctx.ws.numel(), stream_ptr(mem.device)),
               "icap_decoder_train_backward")
@@ -96,10 +98,26 @@ class _DecoderLogProbs(torch.autograd.Function):
         return (None, dmem, None) + tuple(grads[k] for k in names)
 
 
-def decoder_token_logp(decoder: nn.Module, memory: torch.Tensor, ids: torch.Tensor, end_token: int) -> torch.Tensor:
+def decoder_dropout(decoder: nn.Module) -> float:
+    """The dropout p of a TransformerDecoder in train mode (PositionalEncoding and every decoder layer share
+    the config's value, vit:103-147), 0 in eval mode."""
+    if not decoder.training:
+        return 0.0
+    ps = {decoder.pos_encoder.dropout.p}
+    for layer in decoder.transformer_decoder.layers:
+        ps |= {layer.dropout.p, layer.dropout1.p, layer.dropout2.p, layer.dropout3.p, layer.self_attn.dropout,
+               layer.multihead_attn.dropout}
+    if len(ps) != 1:
+        raise ValueError(f"the HIP decoder needs one dropout p for every site, got {sorted(ps)}")
+    return float(ps.pop())
+
+
+def decoder_token_logp(decoder: nn.Module, memory: torch.Tensor, ids: torch.Tensor, end_token: int,
+                       dropout: Tuple[float, int] = (0.0, 0)) -> torch.Tensor:
     """(B, L-1) log p(ids[:, t+1] | ids[:, :t+1], memory), zeroed after a row's first <end>: the HIP forward
     and backward of `decoder` (a TransformerDecoder: vit:103-182 / grid's) - the same values as
-    utils.scst_loss.masked_token_logp(decoder(ids[:, :-1], memory, causal mask), ids, end) in eval mode."""
+    utils.scst_loss.masked_token_logp(decoder(ids[:, :-1], memory, causal mask), ids, end) in eval mode;
+    dropout = (p, seed) > 0: train mode with the masks of Engine.sample(..., dropout=(p, seed))."""
     n_layers = len(decoder.transformer_decoder.layers)
     names = decoder_param_names(n_layers)
     named = dict(decoder.named_parameters())
@@ -109,7 +127,8 @@ def decoder_token_logp(decoder: nn.Module, memory: torch.Tensor, ids: torch.Tens
             raise ValueError("the HIP decoder training pass needs contiguous fp32 parameters on the GPU")
     pe = decoder.pos_encoder.pe.detach().float().contiguous()
     nhead = decoder.transformer_decoder.layers[0].self_attn.num_heads
-    cfg = (_lib.load(), n_layers, decoder.d_model, nhead, pe, int(end_token))
+    cfg = (_lib.load(), n_layers, decoder.d_model, nhead, pe, int(end_token), float(dropout[0]),
+           int(dropout[1]) & 0xFFFFFFFF)
     return _DecoderLogProbs.apply(cfg, memory, ids, *params)
 
 

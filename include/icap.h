@@ -177,6 +177,23 @@ int icap_decode_beam(icap_handle* h, const float* memory, int B, int S, int max_
  * inverse CDF on the injected uniforms). */
 int icap_decode_sample(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
                        int end_token, const float* uniforms, int32_t* ids, float* logp, void* stream);
+/* The same in train mode: TransformerDecoder's dropout (p: nn.Dropout of the positional encoding and of
+ * every TransformerDecoderLayer) active, as the reference samples after model.train() (scst_loss.py:161).
+ * Masks are a counter-based hash of (seed, site, layer, image row, position, index) (common.h
+ * icap_drop_hash; oracle/dropout.py restates it): the mask of a position does not depend on the step, so
+ * icap_decoder_train_forward / _backward with the same (p, seed) differentiate exactly the distribution
+ * sampled from.  Needs a parity precision and max_len <= 65. */
+/* The decode loops' residual LayerNorm (d_model 512): x = LN(x + drop(sum of nparts slabs + bias)) in place,
+ * bf16 hi/lo planes of x -> out; drop_p > 0: the train-mode mask of (seed[0] device word, site, layer, row,
+ * pos, column). */
+int icap_op_residual_layernorm(float* x, int rows, const float* parts, int nparts, long part_stride, const float* bias,
+                               const float* w, const float* b, uint16_t* out, long out_lo, float drop_p,
+                               const uint32_t* seed, int layer, int pos, int site, void* stream);
+/* The dropout mask hash itself (host side, no device work): keep <=> hash >= round(p 2^32). */
+uint32_t icap_drop_hash_host(uint32_t seed, uint32_t site, uint32_t layer, uint32_t row, uint32_t pos, uint32_t idx);
+int icap_decode_sample_dropout(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                               int end_token, const float* uniforms, float p, uint32_t seed, int32_t* ids, float* logp,
+                               void* stream);
 
 /* Full-prefix decoder forward: tgt (B,T) int32 -> logits (B,T,vocab) fp32, causal or unmasked.
  * key_lengths (B int32, device, optional): tgt_key_padding_mask as lengths - keys j >= key_lengths[b]
@@ -259,19 +276,22 @@ int icap_op_gemm_i8_blocks(const int8_t* A, const float* a_scale, const float* a
  * Replaces the autograd graph the reference builds while sampling (SCSTLoss._sample_with_log_probs,
  * utils/scst_loss.py:210-254: decoder forward + log_softmax + gather + masked_fill) and its backward
  * (loss.backward(), scripts/train_vit_transformer_scst_optimized.py:261), for the TransformerDecoder
- * (vit:103-182) as torch.autograd.Function (image_caption_amd/train.py).  Eval-mode forward (dropout off).
+ * (vit:103-182) as torch.autograd.Function (image_caption_amd/train.py).  drop_p > 0: train mode, the
+ * dropout masks of icap_decode_sample_dropout under drop_seed (the forward stores the seed in ws; the
+ * backward of the same call takes the same drop_p); drop_p = 0: eval mode.
  * `d` holds the decoder's CURRENT fp32 parameters (only the decoder fields are read); ids (B, T+1) int32:
  * inputs ids[:, :T], targets ids[:, 1:]; memory (B, S, d_model) fp32; logp (B, T) = log p(target) with
  * the steps after a row's first end_token zeroed.  The forward keeps its activations in ws (bytes from
  * icap_decoder_train_workspace), which the backward of the same call reads: dlogp (B, T) -> gradients of
  * every decoder parameter written (not accumulated) to the pointers of `grad` (same layout as `d`) and
  * dmemory (B, S, d_model) (may be NULL).  fp32 products (fp32 MFMA). */
-size_t icap_decoder_train_workspace(const icap_model_desc* d, int B, int T, int S);
+size_t icap_decoder_train_workspace(const icap_model_desc* d, int B, int T, int S, float drop_p);
 int icap_decoder_train_forward(const icap_model_desc* d, const int32_t* ids, int B, int T, const float* memory, int S,
-                               int end_token, float* logp, void* ws, size_t ws_bytes, void* stream);
+                               int end_token, float drop_p, uint32_t drop_seed, float* logp, void* ws, size_t ws_bytes,
+                               void* stream);
 int icap_decoder_train_backward(const icap_model_desc* d, const icap_model_desc* grad, const int32_t* ids, int B, int T,
-                                const float* memory, int S, int end_token, const float* dlogp, float* dmemory,
-                                void* ws, size_t ws_bytes, void* stream);
+                                const float* memory, int S, int end_token, float drop_p, const float* dlogp,
+                                float* dmemory, void* ws, size_t ws_bytes, void* stream);
 
 /* qkv planes (B*N, 3*H*64) -> out planes (B*N, H*64), non-causal softmax(QK^T/8)V. */
 int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uint16_t* out, long out_lo,

@@ -61,10 +61,12 @@ def gelu_erf(x: Tensor) -> Tensor:
 
 
 def mha(q_in: Tensor, kv_in: Tensor, in_w: Tensor, in_b: Tensor, out_w: Tensor,
-        out_b: Tensor, nhead: int, causal: bool, key_pad: Optional[Tensor] = None) -> Tensor:
-    """torch `F.multi_head_attention_forward` semantics (batch_first), no dropout.  key_pad (B,S)
+        out_b: Tensor, nhead: int, causal: bool, key_pad: Optional[Tensor] = None,
+        p_mask: Optional[Tensor] = None) -> Tensor:
+    """torch `F.multi_head_attention_forward` semantics (batch_first).  key_pad (B,S)
     bool masks keys; a query left with no key gets a zero context, which is what the
-    scaled_dot_product_attention path (need_weights=False, the TransformerDecoderLayer call) returns."""
+    scaled_dot_product_attention path (need_weights=False, the TransformerDecoderLayer call) returns.
+    p_mask (B,H,T,S): dropout on the attention probabilities (train mode, oracle/dropout.py)."""
     B, T, D = q_in.shape
     S = kv_in.shape[1]
     hd = D // nhead
@@ -76,7 +78,7 @@ def mha(q_in: Tensor, kv_in: Tensor, in_w: Tensor, in_b: Tensor, out_w: Tensor,
     q = q.reshape(B, T, nhead, hd).transpose(1, 2)
     k = k.reshape(B, S, nhead, hd).transpose(1, 2)
     v = v.reshape(B, S, nhead, hd).transpose(1, 2)
-    if key_pad is None:  # softmax(q k^T / sqrt(hd) [+ causal -inf]) v as one fused CPU primitive
+    if key_pad is None and p_mask is None:  # softmax(q k^T / sqrt(hd) [+ causal -inf]) v as one fused CPU primitive
         causal_mask = None
         if causal:
             causal_mask = torch.ones(T, S, dtype=torch.bool, device=q.device).tril(S - T)
@@ -90,6 +92,8 @@ def mha(q_in: Tensor, kv_in: Tensor, in_w: Tensor, in_b: Tensor, out_w: Tensor,
         s = s.masked_fill(key_pad[:, None, None, :], float("-inf"))
     p = torch.softmax(s, dim=-1)
     p = torch.nan_to_num(p, nan=0.0)  # fully masked rows
+    if p_mask is not None:
+        p = p * p_mask
     o = (p @ v).transpose(1, 2).reshape(B, T, D)
     return linear(o, out_w, out_b)
 
@@ -198,24 +202,32 @@ def training_forward(sd: Dict[str, Tensor], memory: Tensor, captions: Tensor, le
 
 
 def decoder_forward(sd: Dict[str, Tensor], tgt: Tensor, memory: Tensor, causal: bool = True,
-                    nhead: int = 8, key_pad: Optional[Tensor] = None) -> Tensor:
-    """`TransformerDecoder.forward` (vit:155-182): tgt (B,T) int -> logits (B,T,V)."""
+                    nhead: int = 8, key_pad: Optional[Tensor] = None, masks: Optional[dict] = None) -> Tensor:
+    """`TransformerDecoder.forward` (vit:155-182): tgt (B,T) int -> logits (B,T,V).  masks (train mode,
+    oracle/dropout.py decoder_masks over at least T positions): the dropout of PositionalEncoding and of
+    every TransformerDecoderLayer (attention maps, dropout1/2/3, FFN hidden)."""
     emb = sd["decoder.embedding.weight"]
     d = emb.shape[1]
+    T = tgt.shape[1]
+    m = (lambda k: masks[k][:, :T]) if masks is not None else (lambda k: None)
+    ma = (lambda k, S: masks[k][:, :, :T, :S]) if masks is not None else (lambda k, S: None)
+    drop = lambda x, k: x if masks is None else x * m(k)
     x = emb[tgt] * math.sqrt(d)
-    x = x + sd["decoder.pos_encoder.pe"][:, : tgt.shape[1]]
+    x = drop(x + sd["decoder.pos_encoder.pe"][:, : tgt.shape[1]], "pe")
     i = 0
     while f"decoder.transformer_decoder.layers.{i}.norm1.weight" in sd:
         p = f"decoder.transformer_decoder.layers.{i}."
         h = mha(x, x, sd[p + "self_attn.in_proj_weight"], sd[p + "self_attn.in_proj_bias"],
-                sd[p + "self_attn.out_proj.weight"], sd[p + "self_attn.out_proj.bias"], nhead, causal, key_pad)
-        x = layer_norm(x + h, sd[p + "norm1.weight"], sd[p + "norm1.bias"], 1e-5)
+                sd[p + "self_attn.out_proj.weight"], sd[p + "self_attn.out_proj.bias"], nhead, causal, key_pad,
+                p_mask=ma(f"sa_p.{i}", T))
+        x = layer_norm(x + drop(h, f"sa_o.{i}"), sd[p + "norm1.weight"], sd[p + "norm1.bias"], 1e-5)
         h = mha(x, memory, sd[p + "multihead_attn.in_proj_weight"], sd[p + "multihead_attn.in_proj_bias"],
-                sd[p + "multihead_attn.out_proj.weight"], sd[p + "multihead_attn.out_proj.bias"], nhead, False)
-        x = layer_norm(x + h, sd[p + "norm2.weight"], sd[p + "norm2.bias"], 1e-5)
-        f = linear(torch.relu(linear(x, sd[p + "linear1.weight"], sd[p + "linear1.bias"])),
-                   sd[p + "linear2.weight"], sd[p + "linear2.bias"])
-        x = layer_norm(x + f, sd[p + "norm3.weight"], sd[p + "norm3.bias"], 1e-5)
+                sd[p + "multihead_attn.out_proj.weight"], sd[p + "multihead_attn.out_proj.bias"], nhead, False,
+                p_mask=ma(f"ca_p.{i}", memory.shape[1]))
+        x = layer_norm(x + drop(h, f"ca_o.{i}"), sd[p + "norm2.weight"], sd[p + "norm2.bias"], 1e-5)
+        hid = drop(torch.relu(linear(x, sd[p + "linear1.weight"], sd[p + "linear1.bias"])), f"ff_h.{i}")
+        f = linear(hid, sd[p + "linear2.weight"], sd[p + "linear2.bias"])
+        x = layer_norm(x + drop(f, f"ff_o.{i}"), sd[p + "norm3.weight"], sd[p + "norm3.bias"], 1e-5)
         i += 1
     return linear(x, sd["decoder.fc_out.weight"], sd["decoder.fc_out.bias"])
 
@@ -326,15 +338,18 @@ def inverse_cdf_sample(logits: Tensor, u: Tensor) -> Tuple[Tensor, Tensor]:
     return idx, logp
 
 
-def sample_with_log_probs(sd, memory: Tensor, uniforms: Tensor, start: int, end: int, max_len: int):
-    """`_sample_with_log_probs` (scst_loss:202-254) with injected uniforms (max_len-1, B)."""
+def sample_with_log_probs(sd, memory: Tensor, uniforms: Tensor, start: int, end: int, max_len: int,
+                          masks: Optional[dict] = None):
+    """`_sample_with_log_probs` (scst_loss:202-254) with injected uniforms (max_len-1, B); masks: train-mode
+    dropout (oracle/dropout.py decoder_masks over max_len - 1 positions), applied to every full-prefix
+    recompute by position, as the KV-cached HIP sampler does."""
     B = memory.shape[0]
     generated = torch.full((B, 1), start, dtype=torch.long, device=memory.device)
     finished = torch.zeros(B, dtype=torch.bool, device=memory.device)
     lps = []
     with torch.no_grad():
         for step in range(max_len - 1):
-            logits = decoder_forward(sd, generated, memory, causal=True)[:, -1, :]
+            logits = decoder_forward(sd, generated, memory, causal=True, masks=masks)[:, -1, :]
             nxt, lp = inverse_cdf_sample(logits, uniforms[step])
             lps.append(lp.masked_fill(finished, 0.0))
             generated = torch.cat([generated, nxt.unsqueeze(1)], dim=1)

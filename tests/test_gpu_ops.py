@@ -2,6 +2,7 @@
 
 Inputs are hi/lo bf16 planes (the engine's activation format), so the exact value the kernel
 sees is hi+lo; tolerances are written per test."""
+import numpy as np
 import pytest
 import torch
 
@@ -137,6 +138,30 @@ def test_cross_attn_f16(cuda, rows, rpi, S):
     torch.cuda.synchronize()
     got = value(out, 2).double().cpu()
     assert (got - ref).abs().max().item() < 2e-4
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1, 0.5])
+def test_residual_layernorm_dropout(cuda, p):
+    """The decode loops' residual LayerNorm with the train-mode dropout of the sub-layer output
+    (x + drop(sum of slabs + bias)): against torch with the oracle's masks (oracle/dropout.py)."""
+    from oracle import dropout as D
+
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(int(p * 10) + 1)
+    rows, nparts, site, layer, pos, seed = 40, 8, 4, 1, 3, 4242
+    x = torch.randn(rows, 512, generator=g)
+    parts = torch.randn(nparts, rows, 512, generator=g) * 0.3
+    bias, w, b = (torch.randn(512, generator=g) for _ in range(3))
+    m = D._mask(p, seed, site, layer, np.arange(rows)[:, None], pos, np.arange(512)[None, :]) if p else 1.0
+    ref = torch.nn.functional.layer_norm(x + (parts.sum(0) + bias) * m, (512,), w, b, 1e-5)
+    xd, pd, bd, wd, bbd = (t.to(cuda) for t in (x, parts, bias, w, b))  # (kept alive across the call)
+    out = torch.empty(2, rows, 512, device=cuda, dtype=torch.bfloat16)
+    sd = torch.tensor([seed], dtype=torch.int32, device=cuda)
+    L.check(lib.icap_op_residual_layernorm(xd.data_ptr(), rows, pd.data_ptr(), nparts, rows * 512, bd.data_ptr(),
+                                           wd.data_ptr(), bbd.data_ptr(), out.data_ptr(), rows * 512, p,
+                                           sd.data_ptr(), layer, pos, site, L.stream_ptr()), "rln")
+    torch.cuda.synchronize()
+    assert (xd.cpu() - ref).abs().max().item() < 1e-4
 
 
 def test_full_chip_kernels_repeat_bitwise(cuda):

@@ -91,3 +91,79 @@ def test_decoder_train_pass_repeats_bitwise(cuda):
         decoder_token_logp(dec, mem, ids, END).sum().backward()
         out.append([p.grad.clone() for p in dec.parameters()])
     assert all(torch.equal(a, b) for a, b in zip(*out))
+
+
+def test_train_pass_dropout_matches_oracle_autograd(cuda):
+    """Train mode: the HIP training pass with the counter-based dropout masks (p, seed) against PyTorch
+    autograd through the oracle's explicit-op decoder given the same masks (oracle/dropout.py): log-probs
+    within 1e-4, every gradient within 1e-3 relative (norm)."""
+    from image_caption_amd.train import decoder_param_names, decoder_token_logp
+    from oracle import captioner as O
+    from oracle import dropout as D
+
+    B, L, S, p, seed = 6, 14, 49, 0.1, 987654321
+    torch.manual_seed(3)
+    dec = TransformerDecoder(109).to(cuda).train()
+    ids = _ids(B, L, 109, 11).to(cuda)
+    mem0 = torch.randn(B, S, 512, generator=torch.Generator().manual_seed(2)).to(cuda)
+    adv = torch.randn(B, generator=torch.Generator().manual_seed(5)).to(cuda)
+    names = decoder_param_names(6)
+    params = dict(dec.named_parameters())
+    masks = {k: v.to(cuda) for k, v in D.decoder_masks(p, seed, B, L - 1, S).items()}
+    sd = {"decoder." + k: v for k, v in params.items()}
+    sd["decoder.pos_encoder.pe"] = dec.pos_encoder.pe
+    mem = mem0.clone().requires_grad_(True)
+    lp_ref = masked_token_logp(O.decoder_forward(sd, ids[:, :-1], mem, True, masks=masks), ids, END)
+    (-(adv * lp_ref.sum(1)).mean()).backward()
+    g_ref = {k: params[k].grad.clone() for k in names}
+    dmem_ref = mem.grad.clone()
+    dec.zero_grad(set_to_none=True)
+
+    mem2 = mem0.clone().requires_grad_(True)
+    lp = decoder_token_logp(dec, mem2, ids, END, dropout=(p, seed))
+    (-(adv * lp.sum(1)).mean()).backward()
+    torch.cuda.synchronize()
+    assert (lp - lp_ref.detach()).abs().max().item() < 1e-4
+    worst = max((_rel(params[k].grad, g_ref[k]), k) for k in names)
+    assert worst[0] < 1e-3, worst
+    assert _rel(mem2.grad, dmem_ref) < 1e-3
+    # the masks are active: another seed gives other log-probs
+    lp_other = decoder_token_logp(dec, mem0, ids, END, dropout=(p, seed + 1)).detach()
+    assert (lp_other - lp.detach()).abs().max().item() > 1e-2
+
+
+def test_sampler_dropout_matches_oracle_and_training_pass(cuda):
+    """Train-mode sampling (icap_decode_sample_dropout) against the oracle's full-prefix sampler given the
+    same masks: identical ids, log-probs within 1e-3; and the HIP training pass with the same (p, seed)
+    reproduces the sampler's log-probs - the distribution sampled from is the one differentiated."""
+    from image_caption_amd.engine import Engine
+    from image_caption_amd.train import decoder_token_logp
+    from models.vit_transformer_model import ViTTransformerCaptioning
+    from oracle import captioner as O
+    from oracle import dropout as D
+    from image_caption_amd import weights as W
+
+    B, L, S, p, seed = 8, 20, 196, 0.1, 4242
+    sd = W.to_torch(W.vit_state_dict(0))
+    eng = Engine(sd, "vit", {}, device=cuda)
+    mem = torch.from_numpy(np.random.Generator(np.random.PCG64(9)).standard_normal((B, S, 512)).astype(np.float32))
+    uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(12))
+    runs = [eng.sample(mem.to(cuda), uni.to(cuda), W.START_TOKEN, W.END_TOKEN, L, dropout=(p, seed)) for _ in range(3)]
+    ids, lp = runs[0][0].cpu().long(), runs[0][1].cpu()
+    for i2, l2 in runs[1:]:  # eager, capture, replay
+        assert torch.equal(i2.cpu().long(), ids) and torch.equal(l2.cpu(), lp)
+    masks = D.decoder_masks(p, seed, B, L - 1, S)
+    ref_ids, ref_lp = O.sample_with_log_probs(sd, mem, uni, W.START_TOKEN, W.END_TOKEN, L, masks=masks)
+    n = ref_ids.shape[1]
+    assert torch.equal(ids[:, :n], ref_ids)
+    assert (lp[:, : n - 1] - ref_lp).abs().max().item() < 1e-3
+    plain, _ = eng.sample(mem.to(cuda), uni.to(cuda), W.START_TOKEN, W.END_TOKEN, L)
+    assert not torch.equal(plain.cpu().long(), ids)  # dropout changed the draws
+    # the training pass on the sampled ids, same masks
+    m = ViTTransformerCaptioning(W.VOCAB_SIZE, pretrained_vit=False)
+    m.load_state_dict(sd)
+    dec = m.decoder.to(cuda).train()
+    with torch.no_grad():
+        tp = decoder_token_logp(dec, mem.to(cuda), ids.to(cuda), W.END_TOKEN, dropout=(p, seed)).cpu()
+    assert (tp - lp).abs().max().item() < 1e-3
+

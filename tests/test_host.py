@@ -29,6 +29,27 @@ def test_header_symbols_exported():
     assert lib.icap_abi_version() == _lib.ABI_VERSION
 
 
+def test_dropout_hash_oracle_matches_library():
+    """oracle/dropout.py's numpy hash is the library's icap_drop_hash (common.h), bit for bit, and the
+    masks keep 1 - p of the elements."""
+    from image_caption_amd import _lib
+    from oracle import dropout as D
+
+    lib = _lib.load()
+    g = np.random.Generator(np.random.PCG64(0))
+    args = g.integers(0, 2**32, size=(500, 6), dtype=np.uint64)
+    args[:, 1] %= 7
+    args[:, 2] %= 6
+    args[:250, 3:] %= 300  # small rows / positions / indices as the decoder uses them
+    want = [lib.icap_drop_hash_host(*(int(v) for v in a)) for a in args]
+    for a, w in zip(args, want):
+        assert int(D.drop_hash(int(a[0]), int(a[1]), int(a[2]), int(a[3]), int(a[4]), int(a[5]))) == w
+    m = D.decoder_masks(0.1, 7, 4, 29, 196)
+    frac = np.mean([float((v == 0).float().mean()) for v in m.values()])
+    assert abs(frac - 0.1) < 0.005, frac
+    assert set(torch.unique(m["ff_h.3"]).tolist()) == {0.0, float(np.float32(1) / np.float32(0.9))}
+
+
 def test_library_refuses_without_gpu_inputs():
     from image_caption_amd import _lib
 

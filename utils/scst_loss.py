@@ -4,10 +4,11 @@ SCSTLoss.forward = sample captions with their log-probs, greedy baseline via mod
 CIDEr-D rewards, advantage = r(sample) - r(greedy), loss = -mean(advantage * sum(log p)).
 
 Changes on the hot path:
-  * sampling runs as one batched HIP decode (icap_decode_sample): fp32 fc_out + softmax and an
+  * sampling runs as one batched HIP decode (icap_decode_sample[_dropout]): fp32 fc_out + softmax and an
     inverse-CDF draw on uniforms that are INJECTED (default torch.rand on the images' device),
-    replacing torch.multinomial, so CPU and GPU consume identical randomness; the sampler runs
-    without dropout (the reference samples in train mode with dropout 0.1 active, :161);
+    replacing torch.multinomial, so CPU and GPU consume identical randomness; in train mode the
+    decoder's dropout (0.1 in the reference, :161) is active with counter-based masks of (seed, site,
+    layer, image, position, index) (oracle/dropout.py) instead of torch's RNG stream;
   * when autograd is on, the sampled sequence's log-probs are recomputed teacher-forced with their
     backward on HIP (icap_decoder_train_forward / _backward through a torch.autograd.Function, eval-mode
     like the sampler) after the encoder's trainable part in PyTorch (the ViT projection on the HIP
@@ -25,7 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from image_caption_amd import cider as _cider
-from image_caption_amd.train import decoder_token_logp, vit_trunk_frozen
+from image_caption_amd.train import decoder_dropout, decoder_token_logp, vit_trunk_frozen
 
 
 def _split(s: str, word2idx: Optional[dict]) -> List:
@@ -78,12 +79,12 @@ class SCSTLoss(nn.Module):
         self.reward_calculator = CiderRewardCalculator()
 
     def forward(self, model, images, references, vocab, device, sample_method="sample", max_len=50,
-                uniforms: Optional[torch.Tensor] = None):
+                uniforms: Optional[torch.Tensor] = None, dropout_seed: Optional[int] = None):
         start, end, pad = vocab["<start>"], vocab["<end>"], vocab["<pad>"]
         self.reward_calculator.word2idx = vocab
         model.train()
         sample_ids, sample_log_probs = self._sample_with_log_probs(model, images, start, end, max_len, device,
-                                                                   uniforms)
+                                                                   uniforms, dropout_seed)
         with torch.no_grad():
             greedy_ids = model.generate(images, start, end, max_len, method="greedy")
         refs = [[_split(r, vocab) for r in (rs if isinstance(rs, list) else [rs])] for rs in references]
@@ -110,13 +111,19 @@ class SCSTLoss(nn.Module):
                       "advantage": adv.mean().item()}
 
     def _sample_with_log_probs(self, model, images, start_token, end_token, max_len, device,
-                               uniforms: Optional[torch.Tensor] = None):
-        """-> (ids (B, L) int64, log_probs (B, L-1)), L per the reference stop rule."""
+                               uniforms: Optional[torch.Tensor] = None, dropout_seed: Optional[int] = None):
+        """-> (ids (B, L) int64, log_probs (B, L-1)), L per the reference stop rule.  In train mode the HIP
+        sampler and the recompute apply the decoder's dropout with the same counter-based masks (seed drawn
+        from torch's generator unless given)."""
         B = images.size(0)
         if uniforms is None:
             uniforms = torch.rand(max_len - 1, B, device=images.device)
         if images.is_cuda and getattr(model, "hip_backend", "torch") != "torch":
             eng = model.hip_engine(images.device)
+            p = decoder_dropout(model.decoder)
+            if p > 0 and dropout_seed is None:
+                dropout_seed = int(torch.randint(0, 2**31 - 1, (1,)).item())
+            drop = (p, int(dropout_seed or 0))
             feats = None
             if getattr(model, "_hip_kind", "") == "grid" and model.encoder.cnn.training:
                 # the reference encodes once per step, in train mode (scst_loss:161, :213): the trunk's
@@ -137,19 +144,19 @@ class SCSTLoss(nn.Module):
                     mem, vfeats = eng.encode_vit_features(images)
                 else:  # ViT, or a Grid model whose trunk is in eval mode: the whole encoder on HIP
                     mem = eng.encode(images)
-                ids32, logp = eng.sample(mem, uniforms, start_token, end_token, max_len)
+                ids32, logp = eng.sample(mem, uniforms, start_token, end_token, max_len, dropout=drop)
             ids = ids32.long()
             L = sample_stop_length(ids, end_token)
             ids, logp = ids[:, :L], logp[:, : L - 1]
             if want_grad:
                 # the log-probs with a gradient: encoder's trainable part in PyTorch, then the decoder's
-                # forward and backward on HIP (icap_decoder_train_*, image_caption_amd/train.py; eval-mode
-                # forward like the HIP sampler, so the distribution sampled from is the one differentiated)
+                # forward and backward on HIP (icap_decoder_train_*, image_caption_amd/train.py) with the
+                # sampler's dropout masks, so the distribution sampled from is the one differentiated
                 if vfeats is not None:
                     memory = model.encoder.projection(vfeats)
                 else:
                     memory = model.encoder.tail(feats) if feats is not None else model.encoder(images)
-                logp = decoder_token_logp(model.decoder, memory, ids, end_token)
+                logp = decoder_token_logp(model.decoder, memory, ids, end_token, dropout=drop)
             return ids, logp
         return self._sample_torch(model, images, start_token, end_token, max_len, uniforms)
 
