@@ -97,10 +97,120 @@ __global__ __launch_bounds__(128) void head_kernel(HeadArgs a) {
   }
 }
 
+// Vocabularies above 128 (the reference builds its vocabulary from the captions with a min-count rule,
+// utils/deepfashion_dataset.py:76-81, so V is a property of the dataset): the same head with 256 threads,
+// each owning the logits v = tid, tid + 256, ... (exact fp32 dot products in the same order), the logits
+// kept in LDS for the sampler's sequential prefix sum.
+__global__ __launch_bounds__(256) void head_wide_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float hs[];
+  float* xs = hs;             // [Dm]
+  float* lg = hs + a.Dm;      // [V]
+  __shared__ int s_tok;
+  __shared__ float s_red[4], s_lse;
+  __shared__ int s_idx[4];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* x = a.x + (long)r * a.Dm;
+  for (int d = tid; d < a.Dm; d += 256) xs[d] = x[d];
+  __syncthreads();
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int v = tid; v < a.V; v += 256) {
+    const float* wr = a.W + (long)v * a.Dm;
+    float acc = 0.f;
+    for (int d = 0; d < a.Dm; d += 4) {
+      const f32x4 wv = *(const f32x4*)(wr + d);
+      const f32x4 xv = *(const f32x4*)(xs + d);
+      acc = fmaf(xv[0], wv[0], acc);
+      acc = fmaf(xv[1], wv[1], acc);
+      acc = fmaf(xv[2], wv[2], acc);
+      acc = fmaf(xv[3], wv[3], acc);
+    }
+    const float logit = acc + a.bias[v];
+    if (a.logits) a.logits[(long)r * a.ld_logits + v] = logit;
+    lg[v] = logit;
+    if (logit > bv) { bv = logit; bi = v; }  // v increases: the first maximum of this thread's subset
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  if (lane == 0) { s_red[w] = bv; s_idx[w] = bi; }
+  __syncthreads();
+  if (tid == 0) {
+    float m = s_red[0];
+    int t = s_idx[0];
+    for (int k = 1; k < 4; ++k)
+      if (s_red[k] > m || (s_red[k] == m && s_idx[k] < t)) { m = s_red[k]; t = s_idx[k]; }
+    s_red[0] = m;
+    s_tok = t;
+  }
+  __syncthreads();
+  const float mx = s_red[0];
+  if (a.uniforms) {
+    for (int v = tid; v < a.V; v += 256) lg[v] = __expf(lg[v] - mx);
+    __syncthreads();
+    if (tid == 0) {  // sequential prefix, as the 128-wide head (torch.cumsum order)
+      float c = 0.f;
+      for (int v = 0; v < a.V; ++v) { c += lg[v]; lg[v] = c; }
+      const float thr = a.uniforms[r] * c;
+      int idx = 0;
+      for (int v = 0; v < a.V; ++v) idx += (lg[v] <= thr) ? 1 : 0;
+      s_tok = min(idx, a.V - 1);
+      s_lse = logf(c);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const float* wr = a.W + (long)s_tok * a.Dm;  // the chosen token's logit, recomputed in the same order
+      float acc = 0.f;
+      for (int d = 0; d < a.Dm; d += 4) {
+        const f32x4 wv = *(const f32x4*)(wr + d);
+        const f32x4 xv = *(const f32x4*)(xs + d);
+        acc = fmaf(xv[0], wv[0], acc);
+        acc = fmaf(xv[1], wv[1], acc);
+        acc = fmaf(xv[2], wv[2], acc);
+        acc = fmaf(xv[3], wv[3], acc);
+      }
+      const float lp = (acc + a.bias[s_tok] - mx) - s_lse;
+      a.logp[(long)r * a.ld_logp] = a.finished[r] != 0 ? 0.f : lp;
+    }
+  }
+  __syncthreads();
+  const int tok = s_tok;
+  if (tid == 0) {
+    a.ids[(long)r * a.ld_ids + a.id_col] = tok;
+    if (a.finished) a.finished[r] = (uint8_t)(a.finished[r] | (tok == a.end_token));
+  }
+  if (a.emb) {
+    const long base = (long)r * a.Dm;
+    for (int d = tid; d < a.Dm; d += 256) {
+      float v = a.emb[(long)tok * a.Dm + d] * a.emb_scale + a.pe[(long)a.pe_pos * a.Dm + d];
+      if (a.drop.thr) v *= drop_mul(a.drop, 0, r, a.pe_pos, d);
+      a.x_next[base + d] = v;
+      bf16_t hi, lo;
+      split_bf(v, hi, lo);
+      a.a_next[base + d] = hi;
+      if (a.nsplit == 2) a.a_next[base + d + a.lo] = lo;
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_head(const HeadArgs& h, hipStream_t s) {
-  if (h.V > 128 || h.Dm % 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_kernel, dim3(h.rows), dim3(128), (h.Dm + 128) * 4, s, h);
+  if (h.V < 1 || h.V > HEAD_MAX_VOCAB || h.Dm % 4) return hipErrorInvalidValue;
+  if (h.V <= 128) {
+    hipLaunchKernelGGL(head_kernel, dim3(h.rows), dim3(128), (h.Dm + 128) * 4, s, h);
+  } else {
+    static bool attr = false;
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)head_wide_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (1024 + HEAD_MAX_VOCAB) * 4);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(head_wide_kernel, dim3(h.rows), dim3(256), (h.Dm + h.V) * 4, s, h);
+  }
   return hipGetLastError();
 }

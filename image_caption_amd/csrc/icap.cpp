@@ -402,7 +402,7 @@ void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PA
   const icap_model_desc& d = h->d;
   const int D = d.d_model, F = d.dim_ff;
   REQUIRE(d.nhead * 64 == D && d.nhead == 8, "decoder must have 8 heads of 64");
-  REQUIRE(d.vocab <= 128, "vocab > 128 unsupported by the head kernel");
+  REQUIRE(d.vocab >= 1 && d.vocab <= HEAD_MAX_VOCAB, "vocab must be in [1, 32768]");
   if (parts & ICAP_PART_DECODER) {
   h->cursor = 0;
   h->dec.clear();
@@ -1137,6 +1137,7 @@ void decode_beam(icap_handle* h, const float* mem, int B, int S, int max_len, in
   REQUIRE(B > 0 && max_len >= 2 && K >= 1 && K <= 15, "bad batch / max_len / beam size (1..15)");
   REQUIRE(max_len <= d.pe_len, "max_len exceeds the positional-encoding table (PositionalEncoding max_len)");
   REQUIRE(S > 0 && S <= 256, "memory length must be in [1, 256]");
+  REQUIRE(d.vocab <= 512, "beam search supports vocabularies up to 512 (beam_select keeps k x V log-probs in LDS)");
   const int D = d.d_model, rows = B * K, V = d.vocab;
   DecodeBufs b = dec_bufs(h, rows, B, max_len, S, rows);
   // beam state, carved from one buffer: seq[2] + anc[2] (rows x L ints), best_seq (B x L),

@@ -270,6 +270,7 @@ struct HeadArgs {
   const float* emb; const float* pe; int pe_pos; float emb_scale; float* x_next; bf16_t* a_next; long lo; int nsplit;
   DropCfg drop;  // site 0 on the next step's embedding (positional-encoding dropout)
 };
+constexpr int HEAD_MAX_VOCAB = 32768;  // logits of one row in LDS (128 KiB) for the sampler's prefix sum
 hipError_t launch_head(const HeadArgs& h, hipStream_t s);
 
 // ---- decoder training pass (train.hip): fp32-accurate strided GEMM and the row kernels around it ----
