@@ -9,6 +9,64 @@
 
 namespace {
 
+constexpr int HEAD_LN_PARTS = 16;
+
+// Row r of the head's input into xs: x itself, or (a.ln.parts set) the last decoder layer's residual LN3
+// x = LN(x + sum of the FFN's split-K slabs + bias) computed here instead of by its own launch - threads
+// 0..127 own 4 consecutive columns each, the layout and summation order of residual_layernorm_kernel<128>,
+// so xs is bitwise what that kernel would have stored.  Called by every thread of the block (barriers).
+__device__ __forceinline__ void head_row_in(const HeadArgs& a, int r, float* xs, float* red) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* x = a.x + (long)r * a.Dm;
+  if (!a.ln.parts) {
+    for (int d = tid; d < a.Dm; d += blockDim.x) xs[d] = x[d];
+    __syncthreads();
+    return;
+  }
+  const RlnArgs& ln = a.ln;
+  const int col = 4 * tid;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f}, dv = v;
+  if (tid < 128) {
+    f32x4 pp[HEAD_LN_PARTS];
+#pragma unroll
+    for (int s = 0; s < HEAD_LN_PARTS; ++s)
+      pp[s] = s < ln.nparts ? *(const f32x4*)(ln.parts + s * ln.part_stride + (long)r * 512 + col)
+                            : (f32x4){0.f, 0.f, 0.f, 0.f};
+    v = *(const f32x4*)(x + col);
+    const f32x4 bb = ln.bias ? *(const f32x4*)(ln.bias + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (ln.drop.thr == 0) {
+      v += bb;
+#pragma unroll
+      for (int s = 0; s < HEAD_LN_PARTS; ++s) v += pp[s];
+    } else {
+      f32x4 o = bb;
+#pragma unroll
+      for (int s = 0; s < HEAD_LN_PARTS; ++s) o += pp[s];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] += o[k] * drop_mul(ln.drop, ln.site, r, ln.drop.pos, col + k);
+    }
+    const float sm = wave_sum(v[0] + v[1] + v[2] + v[3]);
+    if (lane == 0) red[w] = sm;
+  }
+  __syncthreads();
+  const float mean = (red[0] + red[1]) / 512.f;
+  if (tid < 128) {
+    dv = v - mean;
+    const float q = wave_sum(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2] + dv[3] * dv[3]);
+    if (lane == 0) red[2 + w] = q;
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const float rstd = 1.0f / sqrtf((red[2] + red[3]) / 512.f + ln.eps);
+    const f32x4 wv = *(const f32x4*)(ln.w + col), bv = *(const f32x4*)(ln.b + col);
+    f32x4 y;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) y[k] = dv[k] * rstd * wv[k] + bv[k];
+    *(f32x4*)(xs + col) = y;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(128) void head_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float hs[];
   float* xs = hs;             // [Dm]
@@ -16,10 +74,9 @@ __global__ __launch_bounds__(128) void head_kernel(HeadArgs a) {
   __shared__ int s_tok;
   __shared__ float s_red[4];
   __shared__ int s_idx[2];
+  __shared__ float s_ln[4];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const float* x = a.x + (long)r * a.Dm;
-  for (int d = tid; d < a.Dm; d += 128) xs[d] = x[d];
-  __syncthreads();
+  head_row_in(a, r, xs, s_ln);
   float logit = -INFINITY;
   if (tid < a.V) {
     const float* wr = a.W + (long)tid * a.Dm;
@@ -108,10 +165,9 @@ __global__ __launch_bounds__(256) void head_wide_kernel(HeadArgs a) {
   __shared__ int s_tok;
   __shared__ float s_red[4], s_lse;
   __shared__ int s_idx[4];
+  __shared__ float s_ln[4];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const float* x = a.x + (long)r * a.Dm;
-  for (int d = tid; d < a.Dm; d += 256) xs[d] = x[d];
-  __syncthreads();
+  head_row_in(a, r, xs, s_ln);
   float bv = -INFINITY;
   int bi = 0x7fffffff;
   for (int v = tid; v < a.V; v += 256) {
@@ -200,6 +256,7 @@ __global__ __launch_bounds__(256) void head_wide_kernel(HeadArgs a) {
 
 hipError_t launch_head(const HeadArgs& h, hipStream_t s) {
   if (h.V < 1 || h.V > HEAD_MAX_VOCAB || h.Dm % 4) return hipErrorInvalidValue;
+  if (h.ln.parts && (h.Dm != 512 || h.ln.nparts < 1 || h.ln.nparts > HEAD_LN_PARTS)) return hipErrorInvalidValue;
   if (h.V <= 128) {
     hipLaunchKernelGGL(head_kernel, dim3(h.rows), dim3(128), (h.Dm + 128) * 4, s, h);
   } else {

@@ -225,7 +225,9 @@ struct icap_handle {
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col}) b->release();
     for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt}) b->release();
     for (DecWS& w : dws)
-      for (DevBuf* b : {&w.x, &w.a, &w.qkv, &w.q, &w.qt, &w.c, &w.o, &w.h, &w.kv, &w.fin, &w.part, &w.memp}) b->release();
+      for (DevBuf* b : {&w.x, &w.a, &w.qkv, &w.q, &w.qt, &w.c, &w.o, &w.h, &w.kv, &w.fin, &w.part, &w.memp, &w.xpart,
+                         &w.xcnt, &w.gs})
+        b->release();
   }
 
   void* alloc(size_t bytes) {
@@ -882,9 +884,11 @@ void mem_planes(icap_handle* h, const float* mem, const DecodeBufs& b, hipStream
 // B here counts KV rows (sequences); mem_rpi = decoder rows per memory image (default n_new; the
 // beam slots of an image for beam search); anc = beam ancestry table for the self-attention.
 // drop (one-token decode only): train-mode dropout masks (DropCfg; row_base = the chain's first row)
+// tail_ln (one-token decode only): the caller's head folds the last layer's residual LN3 in (HeadArgs::ln);
+// the layers then leave x = the LN2 output and the FFN slabs for it instead of launching that LN.
 void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int Lmax, int causal,
                     int S, hipStream_t s, const int32_t* anc = nullptr, int mem_rpi = 0,
-                    const int32_t* klen = nullptr, const DropCfg* drop = nullptr) {
+                    const int32_t* klen = nullptr, const DropCfg* drop = nullptr, RlnArgs* tail_ln = nullptr) {
   const icap_model_desc& d = h->d;
   const int D = d.d_model, H = d.nhead, F = d.dim_ff, rows = B * n_new, ns = h->ns;
   if (mem_rpi <= 0) mem_rpi = n_new;
@@ -968,8 +972,12 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       ff.drop = dl;
       h->timed(PROF_DEC_FUSED, 4.0 * rows * (double)D * F, 2.0 * (2.0 * D * F + (double)rows * D * ns), s,
                [&] { HIPCHK(launch_dec_ffn(ff, s)); });
-      HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, F / 128, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a,
-                                       b.aL, ns, s, dl, 6));
+      const RlnArgs ln3{b.x, nullptr, b.part, F / 128, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, dl, 6};
+      if (tail_ln && l + 1 == d.n_dec_layers)
+        *tail_ln = ln3;  // the caller's head normalises
+      else
+        HIPCHK(launch_residual_layernorm(b.x, rows, D, ln3.parts, ln3.nparts, PS, ln3.bias, ln3.w, ln3.b, ln3.eps, b.a,
+                                         b.aL, ns, s, dl, 6));
     } else {
       h->wgemm(b.a, D, b.aL, L.lin1.w, D, L.lin1.b, rows, F, D, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, WAVE_2x2, 1, 0, s);
       h->wgemm(b.hb, F, b.hL, L.lin2.w, F, nullptr, rows, D, F, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_F,
@@ -1028,8 +1036,8 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
         dc = *drop;
         dc.row_base = r0;
       }
-      decoder_layers(h, v, n, 1, t, max_len, 1, S, st, nullptr, 0, nullptr, drop ? &dc : nullptr);
       HeadArgs ha{};
+      decoder_layers(h, v, n, 1, t, max_len, 1, S, st, nullptr, 0, nullptr, drop ? &dc : nullptr, &ha.ln);
       ha.x = v.x; ha.rows = n; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = d.vocab;
       ha.logits = step_logits ? step_logits + ((size_t)t * B + r0) * d.vocab : nullptr;
       ha.ld_logits = d.vocab;

@@ -129,6 +129,17 @@ hipError_t launch_gemm_wave(const WaveGemmArgs& g, hipStream_t s);
 // Same contract, 32 x 32 block tiles with the whole K' range (<= 1024 per split) DMA'd to LDS first.
 hipError_t launch_gemm_dec(const WaveGemmArgs& g, hipStream_t s);
 
+// A residual LayerNorm folded into the kernel that consumes it: y = LN(x + sum_{s<nparts} parts[s] + bias)
+// (dropout `site` on the sublayer output, as launch_residual_layernorm), computed by the consumer for its own
+// rows.  Used by the decode head for the last layer's LN3 (x_out unused); parts == nullptr: off.  (Folding
+// LN1 / LN2 into the 8 / 16 blocks per row tile of dec_chain / dec_ffn was measured and rejected: each
+// block's 288 KB of slab reads cost more than the separate launch)
+struct RlnArgs {
+  const float* x; float* x_out; const float* parts; int nparts; long part_stride;
+  const float* bias; const float* w; const float* b; float eps;
+  DropCfg drop; int site;
+};
+
 // Two chained per-head GEMMs in one launch (decoder cross-attention block), for each head h:
 //   Y_h = X_h W1_h^T + b1_h      X_h: rows x 512 (bf16 planes), W1_h: rows [64h, 64h + 64) of W1 [.][512]
 //   O_h = Y_h W2_h^T             W2_h: N2 x 64 at W2 + h * w2_hstride, row stride ldw2
@@ -269,6 +280,7 @@ struct HeadArgs {
   float* logp; long ld_logp; uint8_t* finished; int end_token;
   const float* emb; const float* pe; int pe_pos; float emb_scale; float* x_next; bf16_t* a_next; long lo; int nsplit;
   DropCfg drop;  // site 0 on the next step's embedding (positional-encoding dropout)
+  RlnArgs ln;    // the last decoder layer's residual LN3 on x first (nparts <= 16; x_out unused), or off
 };
 constexpr int HEAD_MAX_VOCAB = 32768;  // logits of one row in LDS (128 KiB) for the sampler's prefix sum
 hipError_t launch_head(const HeadArgs& h, hipStream_t s);
