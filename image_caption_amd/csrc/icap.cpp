@@ -131,7 +131,7 @@ struct icap_handle {
   icap_model_desc d{};
   bool use_graphs = true;
   hipStream_t cap_stream = nullptr;
-  int dec_branches = 2;                 // ICAP_DEC_BRANCHES: independent decode chains per batch
+  int dec_branches = 3;                 // ICAP_DEC_BRANCHES: independent decode chains per batch
   DevBuf drop_seed;                     // the sampler's dropout seed (device word read by the kernels)
   static constexpr int MAX_BRANCHES = 4;
   hipStream_t aux_stream[MAX_BRANCHES] = {};  // streams of chains 1.. (chain 0 runs on the caller's)
@@ -1008,12 +1008,14 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
     fin = h->dws[wsi].fin.as<uint8_t>();
     HIPCHK(launch_fill_u8(fin, B, 0, s));  // a kernel node: reset on every graph replay
   }
-  // The images are independent: with dec_branches = 2 the two halves of the batch decode as two
-  // independent chains on two streams (two parallel branches of the captured graph), so their
-  // latency-bound launches can overlap.
+  // The images are independent: with dec_branches = n the batch decodes as n independent chains of
+  // consecutive rows on n streams (n parallel branches of the captured graph), so their latency-bound
+  // launches overlap.
   // (two chains pay from 128 rows each: B = 256 +3.4 %, B = 128 -6 %, tools/ab_env.sh)
   // ICAP_DEC_MIN_ROWS: smallest chain (64-row chains measured slower)
-  static const int min_rows = std::max(16, icap_knob("ICAP_DEC_MIN_ROWS", 128));
+  // Round 2 (fused decode blocks, tools/chains_r2.sh, B = 256): 2 chains 13.25 ms/step of decode, 3 chains of
+  // 85 rows 12.73, 4 chains of 64 rows 13.37 - so 3 chains from 80 rows each (B = 128 keeps one chain)
+  static const int min_rows = std::max(16, icap_knob("ICAP_DEC_MIN_ROWS", 80));
   const int nb = std::max(1, std::min(h->dec_branches, B / min_rows));
   if (nb > 1) {
     if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));

@@ -41,9 +41,9 @@ def test_vit_encode_and_greedy(cuda, vit_sd, precision):
 
 
 def test_two_chain_decode_matches_one_chain(cuda, vit_sd):
-    """The batch decoded as two independent graph branches (icap_set_decode_chains 2, the default, from
-    B = 256) gives the same greedy ids, step logits and sampled ids / log-probs as one chain, for an
-    odd batch (uneven halves 128 + 129), eagerly and on graph replay."""
+    """The batch decoded as two or three independent graph branches (icap_set_decode_chains; 3 is the
+    default from B = 240) gives the same greedy ids, step logits and sampled ids / log-probs as one chain,
+    for an odd batch (uneven parts 128 + 129, 85 + 86 + 86), eagerly and on graph replay."""
     from image_caption_amd.engine import Engine
 
     B, L = 257, 12
@@ -51,7 +51,7 @@ def test_two_chain_decode_matches_one_chain(cuda, vit_sd):
     mem = mem.to(cuda)
     uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(3)).to(cuda)
     out = {}
-    for nb in ("1", "2"):
+    for nb in ("1", "2", "3"):
         eng = Engine(vit_sd, "vit", {}, device=cuda)
         eng.set_decode_chains(int(nb))
         runs = []
@@ -62,8 +62,9 @@ def test_two_chain_decode_matches_one_chain(cuda, vit_sd):
         for r in runs[1:]:
             assert all(torch.equal(a, b) for a, b in zip(r, runs[0]))
         out[nb] = runs[0]
-    for a, b in zip(out["1"], out["2"]):
-        assert torch.equal(a, b)
+    for nb in ("2", "3"):
+        for a, b in zip(out["1"], out[nb]):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("B", [8, 256])
