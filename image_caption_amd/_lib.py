@@ -90,6 +90,8 @@ SIGNATURES = {
     "icap_encode_grid_tail": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "icap_encode_grid": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "icap_encode_grid_features": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "icap_encode_grid_train": (c_int, [c_void_p, c_void_p, c_int, POINTER(ConvBnW), ctypes.c_float, c_void_p,
+                                       c_void_p, c_void_p]),
     "icap_cider_workspace_bytes": (ctypes.c_size_t, [c_long, c_int]),
     "icap_cider_d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int,
                              c_void_p, c_void_p, ctypes.c_size_t, c_void_p, c_void_p]),

@@ -201,6 +201,7 @@ struct icap_handle {
   int split_slots = -1;     // block slots per XCD of the 128 x 256 GEMM (2 per CU); 0 = tail split off
   DevBuf e_x, e_a, e_qkv, e_h, e_patch, e_sa, e_hs;  // encoder (e_sa: int8 row scales, e_hs: MLP block scales)
   DevBuf t_x, t_y, t_1, t_2, t_r, t_col;  // ResNet trunk (NHWC planes)
+  DevBuf t_bn;                            // train-mode BatchNorm: partial sums + scale / shift
   // decoder workspaces, one set per decode mode (0: greedy / beam / teacher-forced, 1: sampled), so
   // the greedy and sampled graphs of an SCST step can replay concurrently on two streams
   struct DecWS {
@@ -222,7 +223,7 @@ struct icap_handle {
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
-    for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col}) b->release();
+    for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col, &t_bn}) b->release();
     for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt}) b->release();
     for (DecWS& w : dws)
       for (DevBuf* b : {&w.x, &w.a, &w.qkv, &w.q, &w.qt, &w.c, &w.o, &w.h, &w.kv, &w.fin, &w.part, &w.memp, &w.xpart,
@@ -686,8 +687,16 @@ struct ConvGeom {  // implicit-GEMM input geometry (GemmArgs::cv); cv = 0: A is 
   int cv = 0, H = 0, W = 0, C = 0, OW = 0, OH = 0;
 };
 
+// bn (train mode): the GEMM writes the raw convolution, then launch_bn_train normalises it with the batch
+// statistics (updating bn's running statistics) and applies the residual / ReLU.
+struct BnTrain {
+  const icap_conv_bn_w* bn = nullptr;  // n_trunk entries, desc order; null: eval (folded) BatchNorm
+  float momentum = 0.1f;
+};
+
 void trunk_conv(icap_handle* h, const Conv& c, const bf16_t* A, long a_ld, long a_lo, int M, bf16_t* out, long out_lo,
-                bool relu, const bf16_t* res, long res_lo, hipStream_t s, const ConvGeom& cg = ConvGeom()) {
+                bool relu, const bf16_t* res, long res_lo, hipStream_t s, const ConvGeom& cg = ConvGeom(),
+                const icap_conv_bn_w* bn = nullptr, float momentum = 0.f) {
   GemmArgs g = gemm_args();
   if (cg.cv) {
     g.cv = cg.cv; g.cv_H = cg.H; g.cv_W = cg.W; g.cv_OW = cg.OW; g.cv_OHW = cg.OH * cg.OW;
@@ -697,12 +706,26 @@ void trunk_conv(icap_handle* h, const Conv& c, const bf16_t* A, long a_ld, long 
   }
   g.A = A; g.lda = a_ld; g.a_lo = a_lo;
   g.W = c.w; g.ldw = c.Kp;
-  g.bias = c.shift; g.scale = c.scale;
   g.C = out; g.ldc = c.cout; g.c_lo = out_lo; g.c_planes = 2;
   g.M = M; g.N = c.cout; g.K = c.Kp; g.nsplit = h->ns;
-  g.epi = relu ? EPI_RELU : EPI_NONE; g.out = OUT_SPLIT;
-  g.res = res; g.res_ld = c.cout; g.res_lo = res_lo;
+  g.out = OUT_SPLIT;
+  if (!bn) {
+    g.bias = c.shift; g.scale = c.scale;
+    g.epi = relu ? EPI_RELU : EPI_NONE;
+    g.res = res; g.res_ld = c.cout; g.res_lo = res_lo;
+  }
   h->run_gemm(g, s);
+  if (bn) {
+    h->t_bn.ensure(bn_part_bytes() + (size_t)2 * 2048 * 4);
+    REQUIRE(c.cout <= 2048, "train-mode BatchNorm workspace holds 2048 channels");
+    double* part = h->t_bn.as<double>();
+    float* sc = (float*)((char*)h->t_bn.p + bn_part_bytes());
+    HIPCHK(launch_bn_train(out, out_lo, M, c.cout, bn->bn_w, bn->bn_b, const_cast<float*>(bn->bn_mean),
+                           const_cast<float*>(bn->bn_var), momentum, 1e-5f, res, res_lo, relu ? 1 : 0, part, sc,
+                           sc + 2048, s));
+    // keep the handle's eval-mode fold equal to the module's updated running statistics
+    HIPCHK(launch_bn_fold(bn->bn_w, bn->bn_b, bn->bn_mean, bn->bn_var, c.cout, 1e-5f, c.scale, c.shift, s));
+  }
 }
 
 // ResNet-101 trunk (torchvision Bottleneck, stride on the 3x3) on NHWC bf16 planes, then the tail.
@@ -710,9 +733,13 @@ void trunk_conv(icap_handle* h, const Conv& c, const bf16_t* A, long a_ld, long 
 constexpr int TRUNK_CHUNK = 256;
 
 // feats (optional): the trunk output as fp32 rows (B, 49, cnn_dim) - self.cnn(images).flatten(2).permute(0, 2, 1)
-void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStream_t s, float* feats = nullptr) {
+// bt.bn (train mode): batch-statistics BatchNorm over the whole batch, so B <= TRUNK_CHUNK (one chunk)
+void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStream_t s, float* feats = nullptr,
+                 const BnTrain& bt = BnTrain()) {
   const icap_model_desc& d = h->d;
   REQUIRE(!h->trunk.empty(), "handle was created without the ResNet trunk (n_trunk = 0)");
+  REQUIRE(!bt.bn || B <= TRUNK_CHUNK, "train-mode BatchNorm needs the whole batch in one trunk chunk (B <= 256)");
+  auto bnp = [&](size_t i) { return bt.bn ? bt.bn + i : nullptr; };
   REQUIRE(d.grid_tokens == 49, "the trunk path expects 224x224 images -> 7x7 grids");
   const int ns = h->ns, HW = 224;
   const int H1 = (HW - 1) / 2 + 1, H2 = (H1 - 1) / 2 + 1;  // 112 (stem), 56 (max-pool)
@@ -761,13 +788,15 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
     HIPCHK(launch_image_nhwc4(img + (size_t)b0 * 3 * HW * HW, bc, HW, BORDER, col, cL, ns, s));
     ConvGeom sg;
     sg.cv = 2; sg.H = HP; sg.W = HP; sg.C = 4; sg.OH = H1; sg.OW = H1;
-    trunk_conv(h, stem, col, 0, cL, bc * H1 * H1, T1, aL, true, nullptr, 0, s, sg);
+    trunk_conv(h, stem, col, 0, cL, bc * H1 * H1, T1, aL, true, nullptr, 0, s, sg, bnp(0), bt.momentum);
     HIPCHK(launch_maxpool3s2(T1, aL, bc, H1, H1, stem.cout, H2, H2, X, aL, ns, s));
     int hw = H2;
     size_t ci = 1;
     for (int st = 0; st < 4; ++st)
       for (int j = 0; j < d.trunk_blocks[st]; ++j) {
+        const size_t ids = ci;
         const Conv* ds = j == 0 ? &h->trunk[ci++] : nullptr;
+        const size_t i1 = ci;
         const Conv &c1 = h->trunk[ci], &c2 = h->trunk[ci + 1], &c3 = h->trunk[ci + 2];
         ci += 3;
         const int oh = c2.stride == 2 ? (hw - 1) / 2 + 1 : hw;
@@ -781,14 +810,14 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
             dsA = col;
             dsL = cL;
           }
-          trunk_conv(h, *ds, dsA, ds->cin, dsL, Mout, R, aL, false, nullptr, 0, s);
+          trunk_conv(h, *ds, dsA, ds->cin, dsL, Mout, R, aL, false, nullptr, 0, s, ConvGeom(), bnp(ids), bt.momentum);
           res = R;
         }
-        trunk_conv(h, c1, X, c1.cin, aL, Min, T1, aL, true, nullptr, 0, s);
+        trunk_conv(h, c1, X, c1.cin, aL, Min, T1, aL, true, nullptr, 0, s, ConvGeom(), bnp(i1), bt.momentum);
         ConvGeom g3;  // 3x3 conv2 read straight from T1 (implicit GEMM)
         g3.cv = 1; g3.H = hw; g3.W = hw; g3.C = c1.cout; g3.OH = oh; g3.OW = oh;
-        trunk_conv(h, c2, T1, 0, aL, Mout, T2, aL, true, nullptr, 0, s, g3);
-        trunk_conv(h, c3, T2, c3.cin, aL, Mout, Y, aL, true, res, aL, s);
+        trunk_conv(h, c2, T1, 0, aL, Mout, T2, aL, true, nullptr, 0, s, g3, bnp(i1 + 1), bt.momentum);
+        trunk_conv(h, c3, T2, c3.cin, aL, Mout, Y, aL, true, res, aL, s, ConvGeom(), bnp(i1 + 2), bt.momentum);
         std::swap(X, Y);
         hw = oh;
       }
@@ -1616,6 +1645,22 @@ int icap_encode_grid_features(icap_handle* h, const float* images, int B, float*
     REQUIRE(h && images && memory && feats && B > 0, "bad arguments");
     REQUIRE(h->d.kind == ICAP_KIND_GRID, "not a Grid model");
     encode_grid(h, images, B, memory, (hipStream_t)stream, feats);
+  });
+}
+
+int icap_encode_grid_train(icap_handle* h, const float* images, int B, const icap_conv_bn_w* bn, float momentum,
+                           float* memory, float* feats, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && images && memory && feats && bn && B > 1, "bad arguments (B >= 2 for batch statistics)");
+    REQUIRE(h->d.kind == ICAP_KIND_GRID, "not a Grid model");
+    REQUIRE(momentum >= 0.f && momentum <= 1.f, "momentum must be in [0, 1]");
+    for (size_t i = 0; i < h->trunk.size(); ++i)
+      REQUIRE(bn[i].bn_w && bn[i].bn_b && bn[i].bn_mean && bn[i].bn_var && bn[i].cout == h->trunk[i].cout,
+              "bn entries must match the handle's trunk");
+    BnTrain bt;
+    bt.bn = bn;
+    bt.momentum = momentum;
+    encode_grid(h, images, B, memory, (hipStream_t)stream, feats, bt);
   });
 }
 

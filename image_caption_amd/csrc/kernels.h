@@ -220,6 +220,13 @@ hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int cp, in
 // (B,3,HW,HW) fp32 -> zero-bordered NHWC4 planes [B][HW+2*border][HW+2*border][4] (channel 3 = 0)
 hipError_t launch_image_nhwc4(const float* img, int B, int HW, int border, bf16_t* out, long lo, int nsplit,
                               hipStream_t s);
+// Train-mode BatchNorm over the raw convolution output planes y [M][C] (in place): batch statistics
+// (double sums over all M rows, deterministic), running statistics updated with momentum (unbiased variance),
+// then y = relu?(y * scale + shift (+ res planes)).  part: bn_part_bytes(); scale / shift: C floats each.
+inline size_t bn_part_bytes() { return (size_t)1024 * 64 * 2 * sizeof(double); }
+hipError_t launch_bn_train(bf16_t* y, long lo, long M, int C, const float* gamma, const float* beta, float* run_mean,
+                           float* run_var, float momentum, float eps, const bf16_t* res, long res_lo, int relu,
+                           double* part, float* scale, float* shift, hipStream_t s);
 hipError_t launch_bn_fold(const float* g, const float* b, const float* mean, const float* var, int C, float eps,
                           float* scale, float* shift, hipStream_t s);
 hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows, int T, int t0, const float* emb,

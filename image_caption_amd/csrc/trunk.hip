@@ -142,6 +142,96 @@ __global__ void bn_fold_kernel(const float* g, const float* b, const float* mean
   shift[c] = b[c] - mean[c] * sc;
 }
 
+
+// ---- train-mode BatchNorm (GridFeatureEncoder.cnn under module.train(): the reference's SCST step,
+// scst_loss:161 / :213).  The convolution's GEMM writes its raw output y as planes; bn_stats sums y and y^2
+// per channel over all M = B*H*W rows (double accumulators, fixed reduction order: deterministic),
+// bn_finalize turns them into the batch mean / biased variance, the fp32 scale / shift of
+// y * scale + shift = (y - mean) / sqrt(var + eps) * gamma + beta, and updates the running statistics as
+// torch's BatchNorm2d does (momentum, unbiased variance M / (M - 1)); bn_apply normalises in place, adds
+// the residual planes and applies the ReLU (the eval epilogue's order).
+
+// block = 16 column groups of 4 channels (64 channels) x 16 row lanes; part[chunk][C][2] doubles
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ y, long lo, long M, int C,
+                                                       long rows_per_chunk, double* part) {
+  __shared__ double red[16][64][2];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 64 + tx * 4;
+  const long r0 = blockIdx.y * rows_per_chunk, r1 = min(M, r0 + rows_per_chunk);
+  double s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+  for (long r = r0 + ty; r < r1; r += 16) {
+    const u32x2 h = *(const u32x2*)(y + r * C + c0), l = *(const u32x2*)(y + r * C + c0 + lo);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t wh = h[k >> 1] >> ((k & 1) * 16), wl = l[k >> 1] >> ((k & 1) * 16);
+      const double v = (double)(bf2f((bf16_t)(wh & 0xffff)) + bf2f((bf16_t)(wl & 0xffff)));
+      s[k] += v;
+      q[k] += v * v;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[ty][tx * 4 + k][0] = s[k];
+    red[ty][tx * 4 + k][1] = q[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {  // channel threadIdx.x / 2, sum (0) or squares (1), rows lanes in order
+    const int ch = threadIdx.x >> 1, w = threadIdx.x & 1;
+    double t = 0;
+    for (int i = 0; i < 16; ++i) t += red[i][ch][w];
+    part[((long)blockIdx.y * C + blockIdx.x * 64 + ch) * 2 + w] = t;
+  }
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ part, int nchunks, int C, long M, const float* gamma,
+                                   const float* beta, float* run_mean, float* run_var, float momentum, float eps,
+                                   float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0, q = 0;
+  for (int i = 0; i < nchunks; ++i) {
+    s += part[((long)i * C + c) * 2];
+    q += part[((long)i * C + c) * 2 + 1];
+  }
+  const double mean = s / (double)M, var = fmax(q / (double)M - mean * mean, 0.0);
+  const float invstd = 1.0f / sqrtf((float)var + eps);
+  const float sc = gamma[c] * invstd;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mean * sc;
+  run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+  run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)(var * (double)M / (double)(M - 1));
+}
+
+// in place: y = relu?(y * scale + shift (+ res)), 4 channels per thread
+__global__ void bn_apply_kernel(bf16_t* y, long lo, long M, int C, const float* __restrict__ scale,
+                                const float* __restrict__ shift, const bf16_t* __restrict__ res, long res_lo,
+                                int relu) {
+  const long total = M * C / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * 4) % C);
+    const u32x2 h = *(const u32x2*)(y + i * 4), l = *(const u32x2*)(y + i * 4 + lo);
+    u32x2 rh = {0, 0}, rl = {0, 0};
+    if (res) {
+      rh = *(const u32x2*)(res + i * 4);
+      rl = *(const u32x2*)(res + i * 4 + res_lo);
+    }
+    const f32x4 sc = *(const f32x4*)(scale + c0), sh = *(const f32x4*)(shift + c0);
+    bf16_t oh[4], ol[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int sft = (k & 1) * 16;
+      float v = (bf2f((bf16_t)((h[k >> 1] >> sft) & 0xffff)) + bf2f((bf16_t)((l[k >> 1] >> sft) & 0xffff))) * sc[k] +
+                sh[k];
+      if (res) v += bf2f((bf16_t)((rh[k >> 1] >> sft) & 0xffff)) + bf2f((bf16_t)((rl[k >> 1] >> sft) & 0xffff));
+      if (relu) v = fmaxf(v, 0.f);
+      split_bf(v, oh[k], ol[k]);
+    }
+    *(u32x2*)(y + i * 4) = (u32x2){(uint32_t)oh[0] | ((uint32_t)oh[1] << 16), (uint32_t)oh[2] | ((uint32_t)oh[3] << 16)};
+    *(u32x2*)(y + i * 4 + lo) =
+        (u32x2){(uint32_t)ol[0] | ((uint32_t)ol[1] << 16), (uint32_t)ol[2] | ((uint32_t)ol[3] << 16)};
+  }
+}
+
 }  // namespace
 
 hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int cp, int kwp, int Kp, bf16_t* out,
@@ -163,5 +253,27 @@ hipError_t launch_image_nhwc4(const float* img, int B, int HW, int border, bf16_
 hipError_t launch_bn_fold(const float* g, const float* b, const float* mean, const float* var, int C, float eps,
                           float* scale, float* shift, hipStream_t s) {
   hipLaunchKernelGGL(bn_fold_kernel, dim3((C + 255) / 256), dim3(256), 0, s, g, b, mean, var, C, eps, scale, shift);
+  return hipGetLastError();
+}
+
+int bn_stats_chunks(long M, int C) {
+  // ~1024 blocks over the (64-channel group, row chunk) grid, >= 256 rows per chunk
+  const long groups = C / 64;
+  long n = std::max(1L, 1024 / groups);
+  n = std::min(n, std::max(1L, M / 256));
+  return (int)n;
+}
+
+hipError_t launch_bn_train(bf16_t* y, long lo, long M, int C, const float* gamma, const float* beta, float* run_mean,
+                           float* run_var, float momentum, float eps, const bf16_t* res, long res_lo, int relu,
+                           double* part, float* scale, float* shift, hipStream_t s) {
+  if (M < 2 || C % 64) return hipErrorInvalidValue;
+  const int nch = bn_stats_chunks(M, C);
+  const long rpc = (M + nch - 1) / nch;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(C / 64, nch), dim3(256), 0, s, y, lo, M, C, rpc, part);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, nch, C, M, gamma, beta,
+                     run_mean, run_var, momentum, eps, scale, shift);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(M * C / 4)), dim3(256), 0, s, y, lo, M, C, scale, shift, res,
+                     res_lo, relu);
   return hipGetLastError();
 }

@@ -259,6 +259,34 @@ class Engine:
                                                  stream_ptr(self.device)), "icap_encode_grid_features")
         return mem, rows.permute(0, 2, 1).reshape(B, self.cnn_dim, 7, 7)
 
+    def encode_grid_train(self, images: torch.Tensor, cnn: torch.nn.Module) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Grid: the trunk in TRAINING mode (icap_encode_grid_train): every BatchNorm of `cnn` (the
+        GridFeatureEncoder.cnn whose weights this engine packed) normalises with the batch statistics and
+        updates its running_mean / running_var in place (num_batches_tracked + 1 here), as cnn(images) under
+        cnn.train() does.  -> (memory (B,49,d), trunk features (B,cnn_dim,7,7))."""
+        x = images.to(device=self.device, dtype=torch.float32).contiguous()
+        if self.kind != "grid" or not self.has_trunk or tuple(x.shape[1:]) != (3, 224, 224):
+            raise ValueError("encode_grid_train needs a Grid engine with its trunk and (B,3,224,224) images")
+        sd = {"cnn." + k: v for k, v in cnn.state_dict(keep_vars=True).items()}
+        convs, _ = trunk_convs(sd, prefix="cnn.")
+        for v in sd.values():
+            if not (v.is_cuda and v.device == x.device and v.dtype in (torch.float32, torch.int64) and v.is_contiguous()):
+                raise ValueError("the trunk's parameters and buffers must be contiguous fp32 on the engine's device")
+        bns = [m for m in cnn.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+        moms = {m.momentum for m in bns}
+        if len(moms) != 1 or None in moms or any(not m.track_running_stats or m.eps != 1e-5 for m in bns):
+            raise ValueError("the HIP train-mode trunk needs one fixed BatchNorm momentum, eps 1e-5, running stats")
+        momentum = moms.pop()
+        bn = (ConvBnW * len(convs))(*convs)
+        B = x.shape[0]
+        mem = torch.empty(B, self.mem_tokens, self.d_model, device=self.device, dtype=torch.float32)
+        rows = torch.empty(B, self.mem_tokens, self.cnn_dim, device=self.device, dtype=torch.float32)
+        check(self.lib.icap_encode_grid_train(self.handle, x.data_ptr(), B, bn, float(momentum), mem.data_ptr(),
+                                              rows.data_ptr(), stream_ptr(self.device)), "icap_encode_grid_train")
+        for m in bns:
+            m.num_batches_tracked.add_(1)
+        return mem, rows.permute(0, 2, 1).reshape(B, self.cnn_dim, 7, 7)
+
     # ------------------------------------------------------------------ decoders
     def greedy_raw(self, memory: torch.Tensor, start: int, end: int, max_len: int,
                    want_logits: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:

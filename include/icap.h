@@ -128,6 +128,15 @@ int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, 
 /* As icap_encode_grid, and also the trunk output itself: feats (B, 49, cnn_dim) fp32 =
  * self.cnn(images).flatten(2).permute(0, 2, 1) (grid:94, :100-101), the values the tail consumes. */
 int icap_encode_grid_features(icap_handle* h, const float* images, int B, float* memory, float* feats, void* stream);
+/* As icap_encode_grid_features with the trunk in TRAINING mode, as the reference's SCST step runs it
+ * (model.train() then model.encoder(images), utils/scst_loss.py:161, :213; GridFeatureEncoder.forward,
+ * grid:86-95): every BatchNorm2d normalises with the batch statistics of these B images (biased variance)
+ * and updates its running statistics in place, bn_mean = (1 - momentum) bn_mean + momentum mean,
+ * bn_var likewise with the unbiased variance (torch.nn.BatchNorm2d.forward in training mode; the caller
+ * increments num_batches_tracked).  bn: n_trunk entries in the desc's order (only bn_w, bn_b, bn_mean,
+ * bn_var are read; bn_mean / bn_var are written); the convolution weights are the handle's.  B <= 256. */
+int icap_encode_grid_train(icap_handle* h, const float* images, int B, const icap_conv_bn_w* bn, float momentum,
+                           float* memory, float* feats, void* stream);
 
 /* CIDEr-D rewards on the GPU over token-id rows (pycocoevalcap CiderScorer: n = 1..4, tf-idf with
  * the document frequency over THIS call's reference sets, clipped cosine, Gaussian length penalty,

@@ -10,6 +10,7 @@ forbids them.
 """
 from __future__ import annotations
 
+import copy
 import weakref
 from typing import Optional
 
@@ -63,6 +64,19 @@ class HipRouted:
             return False
         return True
 
+    def __deepcopy__(self, memo):
+        """A copy never shares (or copies) the packed engine - its device handle belongs to this module - and
+        its encoder / decoder route to the COPY's engine, built on first use from the copy's weights."""
+        new = self.__class__.__new__(self.__class__)
+        memo[id(self)] = new
+        for k, v in self.__dict__.items():
+            object.__setattr__(new, k, None if k == "_hip_cache" else copy.deepcopy(v, memo))
+        for name in ("encoder", "decoder"):
+            child = getattr(new, name, None)
+            if isinstance(child, torch.nn.Module):
+                attach_owner(child, new)
+        return new
+
     def hip_engine(self, device: torch.device):
         """The packed engine of this module's current weights.  After an optimizer step only the parts
         whose tensors changed (decoder / encoder, by data_ptr and version) are re-packed in place
@@ -73,8 +87,11 @@ class HipRouted:
         sd = self.state_dict()
 
         def key(prefix_dec: bool):
+            # num_batches_tracked feeds no computation (fixed momentum); the HIP train-mode trunk bumps it
+            # each SCST step while it updates the running statistics and the handle's BatchNorm fold itself
             return tuple((k, t.data_ptr(), t._version) for k, t in sd.items()
-                         if torch.is_tensor(t) and k.startswith("decoder.") == prefix_dec)
+                         if torch.is_tensor(t) and k.startswith("decoder.") == prefix_dec
+                         and not k.endswith("num_batches_tracked"))
 
         base = (str(device), self.hip_precision)
         kd, ke = key(True), key(False)

@@ -100,6 +100,23 @@ def test_dropin_grid_model_state_dict():
     assert set(m.state_dict()) == set(sd)
 
 
+def test_deepcopy_routes_to_the_copy():
+    """copy.deepcopy of a drop-in model: the copy's encoder / decoder route to the copy (not the original's
+    engine), and a packed engine (a device handle) is never copied or shared."""
+    import copy
+
+    from models._hip import owner_of
+    from models.vit_transformer_model import build_model
+
+    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False})
+    object.__setattr__(m, "_hip_cache", ("sentinel",))  # stands in for a packed engine
+    twin = copy.deepcopy(m)
+    assert owner_of(twin.encoder) is twin and owner_of(twin.decoder) is twin
+    assert owner_of(m.encoder) is m
+    assert twin._hip_cache is None and m._hip_cache == ("sentinel",)
+    assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), twin.state_dict().values()))
+
+
 def test_forced_hip_backend_refuses_cpu():
     from models.vit_transformer_model import build_model
 

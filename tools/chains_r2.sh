@@ -1,0 +1,11 @@
+#!/bin/bash
+# Decode chains per batch with the fused round-2 decode blocks: tools build (ICAP_DEC_MIN_ROWS is a tools
+# knob), headline bench at 2 / 3 / 4 chains.  usage: bash tools/chains_r2.sh
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python -m image_caption_amd.build --tools > gpurun_out/chains_build.log 2>&1 || { tail -5 gpurun_out/chains_build.log; exit 1; }
+for cfg in "2 128" "3 64" "4 64" "2 128"; do
+  set -- $cfg
+  echo "== chains=$1 min_rows=$2"
+  ICAP_DEC_MIN_ROWS=$2 timeout -k 10 150 python bench.py --no-cpu-baseline --steps 10 --warmup 2 --decode-chains $1 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); p=d["roofline"]["phases"]; print(d["value"], d["ms_per_step"], p["encoder"]["ms_per_step"], p["decode"]["ms_per_step"])' || exit 1
+done

@@ -1,7 +1,8 @@
 """Time the whole SCST training step of the drop-in model (SCSTLoss.forward: HIP sampler + greedy +
 GPU CIDEr-D + the teacher-forced recompute; loss.backward(); AdamW step) at config 5's per-rank shape
 (B = 128, max_len 30), HIP backend against backend="torch" (the PyTorch modules on the same GPU).
-Measurement tool, not product.  usage: python tools/scst_train_bench.py [B] [steps]"""
+MODEL=grid: the Grid model (train-mode ResNet trunk: icap_encode_grid_train on the HIP backend).
+Measurement tool, not product.  usage: [MODEL=vit|grid] python tools/scst_train_bench.py [B] [steps]"""
 import os
 import sys
 import time
@@ -10,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 from image_caption_amd import weights as W
-from models.vit_transformer_model import build_model
+from models import grid_transformer_model, vit_transformer_model
 from utils.scst_loss import SCSTLoss
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
@@ -21,8 +22,12 @@ vocab.update({"<pad>": 0, "<unk>": 106, "<start>": 107, "<end>": 108})
 refs = [[" ".join(f"w{(i * 7 + j) % 100 + 1}" for j in range(3 + i % 9))] for i in range(B)]
 imgs = torch.from_numpy(W.synthetic_images(B, seed=5)).to(dev)
 for backend in (os.environ.get("BACKENDS", "auto,torch").split(",")):
-    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False, "backend": backend})
-    m.load_state_dict(W.to_torch(W.vit_state_dict(0)))
+    if os.environ.get("MODEL", "vit") == "grid":
+        m = grid_transformer_model.build_model(W.VOCAB_SIZE, {"pretrained_cnn": False, "backend": backend})
+        m.load_state_dict(W.to_torch(W.grid_state_dict(0)))
+    else:
+        m = vit_transformer_model.build_model(W.VOCAB_SIZE, {"pretrained_vit": False, "backend": backend})
+        m.load_state_dict(W.to_torch(W.vit_state_dict(0)))
     m = m.to(dev)
     opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-6)
     loss_fn = SCSTLoss()
@@ -37,5 +42,5 @@ for backend in (os.environ.get("BACKENDS", "auto,torch").split(",")):
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     ms = 1e3 * sum(times[2:]) / steps
-    print(f"backend {backend:5s} B={B}: {ms:8.1f} ms/step  {B / ms * 1e3:8.1f} images/s  loss {loss.item():+.4f}",
+    print(f"{os.environ.get('MODEL', 'vit')} backend {backend:5s} B={B}: {ms:8.1f} ms/step  {B / ms * 1e3:8.1f} images/s  loss {loss.item():+.4f}",
           flush=True)

@@ -125,16 +125,27 @@ class SCSTLoss(nn.Module):
                 dropout_seed = int(torch.randint(0, 2**31 - 1, (1,)).item())
             drop = (p, int(dropout_seed or 0))
             feats = None
+            mem = None
             if getattr(model, "_hip_kind", "") == "grid" and model.encoder.cnn.training:
                 # the reference encodes once per step, in train mode (scst_loss:161, :213): the trunk's
                 # BatchNorm normalises with batch statistics and updates its running statistics ONCE.
-                # The eval-folded HIP trunk cannot do that, so the trunk runs here, once (grad as
-                # enabled); the HIP tail takes it for the sampler and the recompute below reuses it
-                feats = model.encoder.cnn(images.float())
+                # A frozen trunk on 224x224 images runs as the HIP train-mode trunk (icap_encode_grid_train:
+                # batch statistics, running statistics updated in place, memory and trunk features in one
+                # pass); a trainable one (or other sizes) runs here in PyTorch, once, grad as enabled.  The
+                # recompute below reuses the trunk features either way.
+                cnn = model.encoder.cnn
+                if (tuple(images.shape[1:]) == (3, 224, 224) and 2 <= images.size(0) <= 256
+                        and not any(p.requires_grad for p in cnn.parameters())):
+                    with torch.no_grad():
+                        mem, feats = eng.encode_grid_train(images, cnn)
+                else:
+                    feats = model.encoder.cnn(images.float())
             vfeats = None
             want_grad = torch.is_grad_enabled()
             with torch.no_grad():
-                if feats is not None:
+                if mem is not None:
+                    pass  # the HIP train-mode trunk + tail above
+                elif feats is not None:
                     f = feats.detach()
                     mem = eng.encode(f) if f.shape[2] * f.shape[3] == eng.mem_tokens else model.encoder.tail(f)
                 elif getattr(model, "_hip_kind", "") == "grid" and tuple(images.shape[1:]) != (3, 224, 224):
