@@ -1183,6 +1183,33 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       else hipLaunchKernelGGL((gemm_8ph_kernel<false, true>), dim3(nwg8), dim3(512), 131072, s, g);
       return hipGetLastError();
     }
+#ifdef ICAP_TOOLS
+    // 3 / 4: 128 x 256 tiles with 64-deep (full-line) stages, 2 / 3 stages (96 / 144 KiB, one block per CU);
+    // 5: 256 x 256 tiles, 64-deep stages, 2 stages (128 KiB)
+    if (form >= 3 && form <= 5 && g.K % 64 == 0) {
+      static bool attr = false;
+      if (!attr) {
+        if (hipFuncSetAttribute((const void*)gemm_256_kernel<1, 8, 0, 0, 128, 2, 64, 0, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 48 * 1024) != hipSuccess ||
+            hipFuncSetAttribute((const void*)gemm_256_kernel<1, 8, 0, 0, 128, 3, 64, 0, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 3 * 48 * 1024) != hipSuccess ||
+            hipFuncSetAttribute((const void*)gemm_256_kernel<1, 8, 0, 0, 256, 2, 64, 0, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024) != hipSuccess)
+          return hipErrorInvalidValue;
+        attr = true;
+      }
+      if (form == 5)
+        hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 256, 2, 64, 0, true>), dim3((g.N / 256) * ((g.M + 255) / 256)),
+                           dim3(512), 2 * 64 * 1024, s, g);
+      else if (form == 4)
+        hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 3, 64, 0, true>), dim3((g.N / 256) * ((g.M + 127) / 128)),
+                           dim3(512), 3 * 48 * 1024, s, g);
+      else
+        hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 64, 0, true>), dim3((g.N / 256) * ((g.M + 127) / 128)),
+                           dim3(512), 2 * 48 * 1024, s, g);
+      return hipGetLastError();
+    }
+#endif
     const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
     constexpr int ldsh1 = 2 * (128 * 32 * 2 + 256 * 32 * 2);
     hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 0, true>), dim3(nwgh), dim3(512), ldsh1, s, g);
