@@ -975,6 +975,150 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
   epilogue_256<TM, TN, F16>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent fp16 encoder GEMM (ICAP_PREC_F16): 256 x 256 tiles, 8 waves (2 x 4, wave tile 128 x 64),
+// 64-deep stages (every operand row segment one full 128-B line, chunk c of row r at c ^ (r & 7)) in a
+// 2-stage LDS ring (128 KiB, one block per CU), and one block per CU that walks its XCD's tiles.  Why
+// persistent: at M = 50432 a k-step of this tile takes as long as hipBLASLt's (K sweep at N = 2304,
+// tools/f16_ksweep.sh: 188.6 vs 177 us per 768 of K), but every tile of a one-block-per-CU launch pays its
+// dispatch, the first stage's full memory latency and its epilogue with nothing overlapping them - 92 us
+// of the 281 us QKV GEMM (hipBLASLt: 19).  Here the (tile, k-step) sequence of a block is ONE stream of
+// stages: the last k-step of a tile already DMAs the next tile's first stage, whose latency then hides
+// behind that k-step's MFMAs and the epilogue.  Tiles: the XCD-bijective remap of gemm_256_kernel gives
+// XCD x a contiguous range of logical tiles (row-band major), its blocks take every nbx-th of them, so the
+// tiles in flight on one XCD share their A row bands in its L2.
+// SO (store-only epilogues: bias (+ GELU) -> one fp16 plane, optionally head-major; M % 256 == 0, K >= 128):
+// the epilogue's stores must not hold the next tile's k-loop.  VMEM operations retire in issue order (the
+// compiler's own s_waitcnt model on gfx950 counts loads and stores in one in-order counter), so the k-loop
+// waits with counts that leave the previous tile's stores in flight: at a tile seam the next tile's stages
+// 0 AND 1 are issued before the epilogue (its bias was loaded before stage 0, behind the previous tile's
+// MFMAs), k-step 0 waits vmcnt(8 + 32) (stage 0 done; stage 1 and the 32 stores per wave may pend),
+// k-step 1 vmcnt(32); the stores then drain behind two k-steps of MFMAs.
+template <bool SO>
+__global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
+  constexpr int BM = 256, BN = 256, KS = 64, NW = 8, WM = 128, WN = 64, TM = 8, TN = 4;
+  constexpr int OPB = BM * KS * 2, STAGE = 2 * OPB;  // A 32 KiB + W 32 KiB
+  constexpr int IPW = OPB / 1024 / NW;                // 4 DMA instructions per wave per operand
+  constexpr int PER_STAGE = 2 * IPW;                  // 8 per wave per stage
+  constexpr int NSTORE = TM * TN;                     // 32 fp16 stores per wave per tile (SO)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
+  const int xcd = blockIdx.x & 7, q = nwg >> 3, r = nwg & 7;
+  const int xbase = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, xcnt = q + (xcd < r);
+  const int nbx = ((int)gridDim.x - xcd + 7) >> 3, lb = blockIdx.x >> 3;  // blocks on this XCD, rank among them
+  if (lb >= xcnt) return;
+  const int M = p.M, nk = p.K / KS;
+  const int srow = wave * IPW * 8 + (lane >> 3), schunk = (lane & 7) ^ (srow & 7);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  auto stage = [&](int t, int kt, int buf) {  // tile t (logical), k-step kt -> ring buffer buf
+    const int bm = t / nbn, bn = t - bm * nbn, m0 = bm * BM, n0 = bn * BN;
+    char* s0 = smem + buf * STAGE;
+    const bf16_t* Ab = p.A + kt * KS + schunk * 8;
+    const bf16_t* Wb = p.W + (long)(n0 + srow) * p.ldw + kt * KS + schunk * 8;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int row = min(m0 + srow + i * 8, M - 1);
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(Ab + (long)row * p.lda),
+                                       (LDS_AS void*)(s0 + (wave * IPW + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < IPW; ++i)
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(Wb + (long)i * 8 * p.ldw),
+                                       (LDS_AS void*)(s0 + OPB + (wave * IPW + i) * 1024), 16, 0, 0);
+  };
+  // SO: the tile's 256 bias values go to LDS slot (tile count & 1) by one DMA instruction of wave 0, issued
+  // before the tile's first stage (so the counted waits below never count it) - no registers held across
+  // the k-loop (the kernel is at the 256-register limit of two waves per SIMD)
+  float* sbias = (float*)(smem + 2 * STAGE);
+  auto load_bias = [&](int t, int slot) {
+    if (wave == 0 && p.bias) {
+      const int n0 = (t - (t / nbn) * nbn) * BN;
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(p.bias + n0 + lane * 4),
+                                       (LDS_AS void*)(sbias + slot * 256), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  int t = xbase + lb, step = 0, tcount = 0;
+  if (SO) load_bias(t, 0);
+  stage(t, 0, 0);
+  bool seam = false;  // this tile's stages 0 and 1 were issued before the previous tile's epilogue stores
+  for (;;) {
+    const int tn = t + nbx < xbase + xcnt ? t + nbx : -1;  // this block's next tile
+    for (int kt = 0; kt < nk; ++kt, ++step) {
+      // lgkmcnt(0): this wave's reads of the buffer about to be refilled are done before the barrier
+      if (SO && seam && kt == 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE + NSTORE) : "memory");
+      else if (SO && seam && kt == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (SO && seam && kt == 0) {
+        // stage 1 of this tile is already in flight
+      } else if (kt + 1 < nk) {
+        stage(t, kt + 1, (step + 1) & 1);
+      } else if (tn >= 0) {  // the next tile's bias, then its first stage, behind this k-step's MFMAs
+        if (SO) load_bias(tn, (tcount + 1) & 1);
+        stage(tn, 0, (step + 1) & 1);
+      }
+      const char* s0 = smem + (step & 1) * STAGE;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int fo = fr * 128 + (((ks * 4 + fq) ^ (fr & 7)) << 4);
+        bf16x8 bfr[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + OPB + (wn * WN + j * 16) * 128 + fo);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8 af = *(const bf16x8*)(s0 + (wm * WM + i * 16) * 128 + fo);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma<true>(bfr[j], af, acc[i][j]);
+        }
+      }
+    }
+    const int bm = t / nbn, bn = t - bm * nbn, mb = bm * BM + wm * WM, nb = bn * BN + wn * WN;
+    if constexpr (SO) {
+      if (tn >= 0) {  // every wave is done reading the last stage's buffer: stage 1 of the next tile into it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        stage(tn, 1, (step + 1) & 1);  // step = the next tile's k-step 0 here; its k-step 1 reads (step + 1) & 1
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = mb + i * 16 + fr;  // < M: M % 256 == 0
+        const long orow = p.hm_n ? (((long)(m / p.hm_n) * (p.N / 64) + nb / 64) * p.hm_n + m % p.hm_n) * 64 - nb
+                                 : (long)m * p.ldc;
+        bf16_t* C = (bf16_t*)p.C + orow + 4 * fq;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          f32x4 v = acc[i][j];
+          if (p.bias) v += *(const f32x4*)(sbias + (tcount & 1) * 256 + wn * WN + j * 16 + 4 * fq);
+          if (p.epi == EPI_GELU) {
+            const f32x2 lo = gelu_erf_fast2((f32x2){v[0], v[1]}), hi = gelu_erf_fast2((f32x2){v[2], v[3]});
+            v = (f32x4){lo[0], lo[1], hi[0], hi[1]};
+          }
+          *(u32x2*)(C + nb + j * 16) = pack16x4<true>(v);
+        }
+      }
+      seam = true;
+    } else {
+      epilogue_256<TM, TN, true>(p, acc, mb, nb, fr, fq);
+    }
+    if (tn < 0) break;
+    t = tn;
+    ++tcount;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -1181,6 +1325,27 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       const int nwg8 = (g.N / 256) * ((g.M + 255) / 256);
       if (form == 2) hipLaunchKernelGGL((gemm_8ph_kernel<true, true>), dim3(nwg8), dim3(512), 131072, s, g);
       else hipLaunchKernelGGL((gemm_8ph_kernel<false, true>), dim3(nwg8), dim3(512), 131072, s, g);
+      return hipGetLastError();
+    }
+    // store-only epilogues with whole 256-row bands (the ViT QKV and MLP-1 GEMMs): the persistent counted-seam
+    // form by default (QKV 305 -> 265 us, MLP-1 423 -> 342 us at B = 256, tools/f16_forms_r2.sh); form 6 (tools)
+    // also runs the residual GEMMs persistent (slower: the residual epilogue's loads serialise the seam)
+    const bool so = g.out == OUT_SPLIT && !g.addend && !g.rm_group && g.M % 256 == 0 && g.K >= 128 &&
+                    g.K % 64 == 0 && (g.epi == EPI_NONE || g.epi == EPI_GELU);
+    if ((form == 6 && g.K % 64 == 0) || (form == 0 && so)) {
+      static int cus = 0;
+      if (!cus) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0)
+          return hipErrorInvalidValue;
+        for (const void* f : {(const void*)gemm_f16p_kernel<false>, (const void*)gemm_f16p_kernel<true>})
+          if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048) != hipSuccess)
+            return hipErrorInvalidValue;
+      }
+      const int tiles = (g.N / 256) * ((g.M + 255) / 256);
+      if (so)
+        hipLaunchKernelGGL(gemm_f16p_kernel<true>, dim3(std::min(tiles, cus)), dim3(512), 2 * 64 * 1024 + 2048, s, g);
+      else
+        hipLaunchKernelGGL(gemm_f16p_kernel<false>, dim3(std::min(tiles, cus)), dim3(512), 2 * 64 * 1024, s, g);
       return hipGetLastError();
     }
 #ifdef ICAP_TOOLS

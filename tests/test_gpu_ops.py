@@ -439,11 +439,13 @@ def test_gemm_tail_split(cuda, M, N, K, slots):
 
 
 # ---------------------------------------------------------------- fp16 single-plane encoder (ICAP_PREC_F16)
-@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (50432, 768, 768), (1000, 3072, 768), (777, 768, 3072)])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (50432, 768, 768), (1000, 3072, 768), (777, 768, 3072),
+                                   (8192, 2304, 128), (8192, 1024, 192)])
 @pytest.mark.parametrize("epi", [0, 1])
 def test_gemm_f16(cuda, M, N, K, epi):
     """fp16 A / W (nsplit = -1), fp32 accumulate: against fp64 on the same fp16 values; fp32, one fp16
-    plane (rounding of the output: 2^-11 relative) and residual outputs."""
+    plane (rounding of the output: 2^-11 relative) and residual outputs.  M % 256 == 0 with more tiles than
+    CUs runs the persistent plane form across tile seams (2 and 3 k-steps per tile at K = 128 / 192)."""
     L, lib = _lib()
     g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
     a = torch.randn(M, K, generator=g).to(torch.float16).to(cuda)

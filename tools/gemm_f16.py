@@ -15,6 +15,12 @@ TOOLS_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libicap_to
 lib = _lib.load(TOOLS_LIB if os.path.exists(TOOLS_LIB) else None)
 dev = torch.device("cuda", 0)
 SHAPES = {"qkv": (2304, 768, 0, 2), "out": (768, 768, 0, 3), "mlp0": (3072, 768, 1, 2), "mlp3": (768, 3072, 0, 3)}
+if os.environ.get("SHAPE_NK"):  # SHAPE_NK=2304,768: one plain GEMM of M = GEMM_M rows (fp16 out, bias, no epilogue op)
+    _n, _k = map(int, os.environ["SHAPE_NK"].split(","))
+    SHAPES = {f"n{_n}k{_k}": (_n, _k, 0, 2)}
+if os.environ.get("SQUARE"):  # SQUARE=4096: one plain M = N = K GEMM (fp16 out, no epilogue), e.g. against the guide's template
+    _n = int(os.environ["SQUARE"])
+    SHAPES = {f"sq{_n}": (_n, _n, 0, 2)}
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 m = int(os.environ.get("GEMM_M", 256 * 197))
 
