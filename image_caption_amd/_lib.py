@@ -21,11 +21,12 @@ PRECISIONS = {"bf16": PREC_BF16, "bf16x2": PREC_BF16X2, "i8x2": PREC_I8X2, "f16"
 PROF_GEMM_128, PROF_GEMM_64, PROF_ENC_ATTN, PROF_CROSS_ATTN, PROF_GEMM_WAVE, PROF_GEMM_256 = 0, 1, 2, 3, 4, 5
 PROF_GEMM_I8 = 6
 PROF_DEC_FUSED = 7
+PROF_GEMM_F16P = 8
 PART_DECODER, PART_ENCODER = 1, 2
 PROF_NAMES = {PROF_GEMM_128: "gemm_bf16_kernel<128,128,64,64>", PROF_GEMM_64: "gemm_bf16_kernel<64,64,32,32>",
               PROF_ENC_ATTN: "enc_attention_kernel", PROF_CROSS_ATTN: "cross_attn_mfma_kernel",
               PROF_GEMM_WAVE: "gemm_dec_kernel", PROF_GEMM_256: "gemm_256_kernel", PROF_GEMM_I8: "gemm_i8_kernel",
-              PROF_DEC_FUSED: "dec_sa_kernel/dec_ffn_kernel"}
+              PROF_DEC_FUSED: "dec_sa_kernel/dec_ffn_kernel", PROF_GEMM_F16P: "gemm_f16p_kernel"}
 
 
 class LnW(ctypes.Structure):

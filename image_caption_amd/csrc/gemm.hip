@@ -191,6 +191,13 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
+bool gemm_f16_persistent(const GemmArgs& g) {
+  static const int form = icap_knob("ICAP_F16_GEMM", 0);  // tools: 6 = persistent for every fp16 GEMM
+  return g.f16 && (form == 0 || form == 6) && g.out == OUT_SPLIT && !g.addend && !g.rm_group && !g.res &&
+         !g.scale && !g.cv && g.batch == 1 && g.nsplit == 1 && g.c_planes == 1 && g.N % 256 == 0 && g.M % 256 == 0 &&
+         g.K >= 128 && g.K % 64 == 0 && (g.epi == EPI_NONE || g.epi == EPI_GELU);
+}
+
 int gemm_tile_class(const GemmArgs& g) {
   static const int force = icap_knob("ICAP_CONV_CLASS", 0);  // trunk convolutions (GEMMs with a BN scale)
   if (force && g.scale) {
@@ -201,7 +208,7 @@ int gemm_tile_class(const GemmArgs& g) {
   // 256 x 256 tiles whenever N allows and there are >= 96 of them (trunk sweep, profiles/r01
   // v6_trunk_class_sweep.txt: even 98-196 tiles beat 4x as many 128 x 128 tiles); 128 x 128 only for
   // N >= 256 (at N = 128 the 64 x 64 kernel is faster)
-  if (g.f16) return PROF_GEMM_256;  // the fp16 forms live in launch_gemm_256
+  if (g.f16) return gemm_f16_persistent(g) ? PROF_GEMM_F16P : PROF_GEMM_256;  // the fp16 forms live in launch_gemm_256
   const long huge_tiles = (long)((g.M + 255) / 256) * (g.N / 256) * g.batch;
   if (g.N % 256 == 0 && g.batch == 1 && huge_tiles >= 96) return PROF_GEMM_256;
   const long big_tiles = (long)((g.M + 127) / 128) * (g.N / 128) * g.batch;
@@ -215,7 +222,7 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.cv && (g.batch != 1 || !g.cv_zero || (g.cv == 1 && g.cv_cshift < 6) || g.cv_OHW <= 0 || g.cv_OW <= 0))
     return hipErrorInvalidValue;
   const int cls = gemm_tile_class(g);
-  if (cls == PROF_GEMM_256) return launch_gemm_256(g, s);
+  if (cls == PROF_GEMM_256 || cls == PROF_GEMM_F16P) return launch_gemm_256(g, s);
   if (cls == PROF_GEMM_128) return run<128, 128, 64, 64>(g, s);
   return run<64, 64, 32, 32>(g, s);
 }
@@ -1330,9 +1337,8 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     // store-only epilogues with whole 256-row bands (the ViT QKV and MLP-1 GEMMs): the persistent counted-seam
     // form by default (QKV 305 -> 265 us, MLP-1 423 -> 342 us at B = 256, tools/f16_forms_r2.sh); form 6 (tools)
     // also runs the residual GEMMs persistent (slower: the residual epilogue's loads serialise the seam)
-    const bool so = g.out == OUT_SPLIT && !g.addend && !g.rm_group && g.M % 256 == 0 && g.K >= 128 &&
-                    g.K % 64 == 0 && (g.epi == EPI_NONE || g.epi == EPI_GELU);
-    if ((form == 6 && g.K % 64 == 0) || (form == 0 && so)) {
+    const bool so = gemm_f16_persistent(g);
+    if ((form == 6 && g.K % 64 == 0) || so) {
       static int cus = 0;
       if (!cus) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0)

@@ -105,7 +105,9 @@ hipError_t launch_layernorm_i8(const float* x, long ldx, int rows, int D, int in
 // fp32 [N][K] rows -> int8 two-slice row images (same layout, K % 64 == 0) + per-row scale
 hipError_t launch_pack_i8_rows(const float* w, int N, int K, int8_t* out, float* scale, hipStream_t s);
 enum { PROF_GEMM_128 = 0, PROF_GEMM_64 = 1, PROF_ENC_ATTN = 2, PROF_CROSS_ATTN = 3, PROF_GEMM_WAVE = 4, PROF_GEMM_256 = 5,
-       PROF_GEMM_I8 = 6, PROF_DEC_FUSED = 7 };
+       PROF_GEMM_I8 = 6, PROF_DEC_FUSED = 7, PROF_GEMM_F16P = 8 };
+// launch_gemm_256 runs g as the persistent fp16 kernel (gemm_f16p_kernel, store-only epilogue, whole row bands)
+bool gemm_f16_persistent(const GemmArgs& g);
 
 // Decode-step GEMM: each wave streams a (16 TM) x (16 TN) tile's operands into registers (no LDS);
 // block = 4 waves along N.  ksplit > 1 with out = OUT_PARTIAL writes fp32 partial slabs

@@ -231,9 +231,10 @@ int icap_set_decode_chains(icap_handle* h, int chains);
 #define ICAP_PROF_ENC_ATTN 2   /* enc_attention_pipe_kernel / enc_attention_kernel (encoder self-attention) */
 #define ICAP_PROF_CROSS_ATTN 3 /* cross_attn_mfma_kernel (decoder cross-attention)                         */
 #define ICAP_PROF_GEMM_WAVE 4  /* gemm_dec_kernel / chain_dec_kernel (decode-step GEMMs)                   */
-#define ICAP_PROF_GEMM_256 5   /* gemm_256_kernel: bf16 / bf16x2 encoder GEMMs (128x256 or 256x256 tiles)  */
+#define ICAP_PROF_GEMM_256 5   /* gemm_256_kernel: encoder GEMMs (128x256 or 256x256 tiles; fp16 residual ones) */
 #define ICAP_PROF_GEMM_I8 6    /* gemm_i8_kernel: int8 two-slice encoder GEMMs (ICAP_PREC_I8X2)            */
 #define ICAP_PROF_DEC_FUSED 7  /* dec_sa_kernel / dec_ffn_kernel (fused decode-step blocks, eager launches)   */
+#define ICAP_PROF_GEMM_F16P 8  /* gemm_f16p_kernel: persistent fp16 encoder GEMMs (ViT QKV, MLP-1)          */
 /* Enable (1) / disable (0) HIP-event bracketing of every hot-kernel launch; clears records. */
 int icap_profile_enable(icap_handle* h, int enable);
 /* Sum over recorded launches of one class: device ms, launch count, algorithmic flops and bytes
