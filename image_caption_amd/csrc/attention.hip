@@ -810,11 +810,15 @@ constexpr int XA_RED_BYTES = (8 * 512 + 512) * 4 + 16;  // + the KS = 2 ticket
 //   context wave w: d in [32w, 32w + 32), keys as 2 k-steps of 32 (key tiles 2s, 2s + 1)
 // drop (thr != 0, one row per image): train-mode dropout on the probabilities used for the context (the
 // softmax normaliser stays undropped), mask of (row, drop.pos, head * 256 + memory token).
-template <int DUMMY>
+// KS = 2 (no dropout, >= 2 chunks): the chunks of a row pair split over two blocks (chunks [0, c/2) and
+// [c/2, c)); each leaves its unnormalised context and softmax statistics (agent-scope stores), and the second
+// to take the pair's ticket merges them in part order (deterministic) and resets the ticket (xpart / xcnt as
+// cross_attn_mfma_kernel<KS = 2>).
+template <int KS>
 __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __restrict__ qt, long qt_lo,
                                                               const bf16_t* __restrict__ mem, int rows_per_image,
                                                               int S, float scale, bf16_t* out, long out_lo,
-                                                              DropCfg drop, float* gsum) {
+                                                              DropCfg drop, float* gsum, float* xpart, int* xcnt) {
   constexpr int DM = 512, H = 8, CK = 64;
   constexpr int BUF = CK * DM * 2;              // 64 KiB per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -824,7 +828,7 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
   const int fr = lane & 15, fq = lane >> 4;
   const int skt = wave & 3, sdg = wave >> 2;
   const int bpi = (rows_per_image + 1) / 2;
-  const int pb = blockIdx.x;
+  const int pb = blockIdx.x / KS, part = blockIdx.x - pb * KS;
   const int img = pb / bpi, pair = pb - img * bpi;
   const int slot = 2 * pair + (fr >> 3);
   const bool valid = slot < rows_per_image;
@@ -832,6 +836,7 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
   const int hd = fr & 7;
   const bf16_t* mb = mem + (long)img * S * DM;
   const int nchunks = (S + CK - 1) / CK;
+  const int cper = (nchunks + KS - 1) / KS, c0 = part * cper, c1 = min(nchunks, c0 + cper);
 
   // q~ as fp16 hi/lo fragments: column (row, head), d = 128 sdg + 32 ks + 8 fq + j.  (Issuing these loads
   // behind the first chunks' DMA does not pay: the compiler then waits vmcnt(0) for the DMA as well,
@@ -874,13 +879,13 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
   float m_run = -INFINITY, l_run = 0.f, d_run = 0.f;  // d_run: the dropped-probability mass (train mode)
   const int q4 = fr >> 2, p4 = fr & 3;
 
-  stage(0, 0);
-  if (nchunks > 1) stage(1, 1);
-  for (int c = 0; c < nchunks; ++c) {
-    if (c + 1 < nchunks) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  if (c0 < c1) stage(c0, 0);
+  if (c0 + 1 < c1) stage(c0 + 1, 1);
+  for (int c = c0; c < c1; ++c) {
+    if (c + 1 < c1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const char* cb = smem + (c & 1) * BUF;
+    const char* cb = smem + ((c - c0) & 1) * BUF;
     {  // partial scores: key tile skt, d-group sdg
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
       const int key = skt * 16 + fr;
@@ -971,10 +976,50 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
         acc[dt] = mma16h(vh, pl, acc[dt]);
       }
     }
-    if (c + 2 < nchunks) {
-      __syncthreads();  // every wave is done with buffer c & 1
-      stage(c + 2, c & 1);
+    if (c + 2 < c1) {
+      __syncthreads();  // every wave is done with buffer (c - c0) & 1
+      stage(c + 2, (c - c0) & 1);
     }
+  }
+  if (KS == 2) {
+    float* mine = xpart + ((long)pb * 2 + part) * XA_PART_FLOATS;
+    const float* other = xpart + ((long)pb * 2 + (part ^ 1)) * XA_PART_FLOATS;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        __hip_atomic_store(mine + (dt * 4 + rr) * 1024 + threadIdx.x, acc[dt][rr], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 16) {
+      __hip_atomic_store(mine + 8 * 1024 + threadIdx.x, m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(mine + 8 * 1024 + 16 + threadIdx.x, l_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores are complete
+    __syncthreads();                                   // ... and every thread's
+    int* flag = (int*)(tot + 1024);                    // after the score totals
+    if (threadIdx.x == 0)
+      *flag = __hip_atomic_fetch_add(xcnt + pb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag == 0) return;  // the partner block merges
+    if (threadIdx.x == 0) __hip_atomic_store(xcnt + pb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float om = __hip_atomic_load(other + 8 * 1024 + fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float ol = __hip_atomic_load(other + 8 * 1024 + 16 + fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float oa[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      oa[k] = __hip_atomic_load(other + k * 1024 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // part 0's state first whatever the arrival order
+    const float m0 = part ? om : m_run, m1 = part ? m_run : om;
+    const float l0 = part ? ol : l_run, l1 = part ? l_run : ol;
+    const float mn = fmaxf(m0, m1), f0 = __expf(m0 - mn), f1 = __expf(m1 - mn);
+    l_run = __fadd_rn(__fmul_rn(l0, f0), __fmul_rn(l1, f1));
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float x0 = part ? oa[dt * 4 + rr] : acc[dt][rr], x1 = part ? acc[dt][rr] : oa[dt * 4 + rr];
+        acc[dt][rr] = __fadd_rn(__fmul_rn(x0, f0), __fmul_rn(x1, f1));
+      }
   }
   if (valid && drop.thr && gsum && wave == 0 && fq == 0) gsum[r * H + hd] = d_run / l_run;
   if (valid) {
@@ -992,7 +1037,7 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
     }
   }
 }
-constexpr int XA16_LDS = 2 * 64 * 512 * 2 + (4 * 1024 + 1024) * 4;
+constexpr int XA16_LDS = 2 * 64 * 512 * 2 + (4 * 1024 + 1024) * 4 + 16;  // + the KS = 2 ticket flag
 
 }  // namespace
 
@@ -1010,21 +1055,32 @@ int cross_attn_splits(int S) {
 
 size_t cross_attn_part_floats(int rows) { return (size_t)rows * 2 * XA_PART_FLOATS; }
 
+int cross_attn_f16_splits() {
+  // key split of the fp16 cross-attention (tools knob ICAP_XATTN16_KS, default 1)
+  static const int ks = icap_knob("ICAP_XATTN16_KS", 1);
+  return ks == 2 ? 2 : 1;
+}
+
 hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem16, int rows, int rows_per_image,
                                  int S, float scale, bf16_t* out, long out_lo, hipStream_t s, DropCfg drop,
-                                 float* gsum) {
+                                 float* gsum, float* xpart, int* xcnt) {
   if (S <= 0 || rows <= 0 || rows_per_image <= 0 || rows % rows_per_image) return hipErrorInvalidValue;
   if (drop.thr && (rows_per_image != 1 || S > 256 || !gsum)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)cross_attn_f16_kernel<0>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, XA16_LDS);
-    if (e != hipSuccess) return e;
+    for (const void* f : {(const void*)cross_attn_f16_kernel<1>, (const void*)cross_attn_f16_kernel<2>}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, XA16_LDS);
+      if (e != hipSuccess) return e;
+    }
     attr = true;
   }
   const int pairs = rows / rows_per_image * ((rows_per_image + 1) / 2);
-  hipLaunchKernelGGL(cross_attn_f16_kernel<0>, dim3(pairs), dim3(1024), XA16_LDS, s, qt, qt_lo, mem16,
-                     rows_per_image, S, scale, out, out_lo, drop, gsum);
+  if (xpart && xcnt && !drop.thr && S > 64 && cross_attn_f16_splits() == 2)
+    hipLaunchKernelGGL(cross_attn_f16_kernel<2>, dim3(2 * pairs), dim3(1024), XA16_LDS, s, qt, qt_lo, mem16,
+                       rows_per_image, S, scale, out, out_lo, drop, gsum, xpart, xcnt);
+  else
+    hipLaunchKernelGGL(cross_attn_f16_kernel<1>, dim3(pairs), dim3(1024), XA16_LDS, s, qt, qt_lo, mem16,
+                       rows_per_image, S, scale, out, out_lo, drop, gsum, xpart, xcnt);
   return hipGetLastError();
 }
 

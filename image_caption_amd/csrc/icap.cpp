@@ -877,8 +877,9 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   w.kv.ensure((size_t)2 * d.n_dec_layers * kv_rows * H * Lmax * 64 * 4);
   w.part.ensure((size_t)MAX_KSPLIT * rows * D * 4);
   w.gs.ensure((size_t)rows * H * 4);
-  if (cross_attn_splits(S) > 1) w.xpart.ensure(cross_attn_part_floats(rows) * 4);
-  if (cross_attn_splits(S) > 1 && w.xcnt.n < (size_t)rows * 4) {  // tickets: zero at rest (each launch resets its own)
+  const bool xsplit = cross_attn_splits(S) > 1 || (ns == 2 && cross_attn_f16_splits() > 1);
+  if (xsplit) w.xpart.ensure(cross_attn_part_floats(rows) * 4);
+  if (xsplit && w.xcnt.n < (size_t)rows * 4) {  // tickets: zero at rest (each launch resets its own)
     w.xcnt.ensure((size_t)rows * 4);
     HIPCHK(hipMemset(w.xcnt.p, 0, w.xcnt.n));
   }
@@ -973,7 +974,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
     h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * (double)(rows / mem_rpi) * S * D, s, [&] {
       if (ns == 2)
         HIPCHK(launch_cross_attn_f16(b.qt, b.cL, b.memp, rows, mem_rpi, S, 0.125f, b.c, b.cL, s, dl,
-                                     drop ? b.gs : nullptr));
+                                     drop ? b.gs : nullptr, b.xpart, b.xcnt));
       else
         HIPCHK(launch_cross_attn_mfma(b.qt, b.cL, b.memp, b.memL, rows, mem_rpi, S, 0.125f, b.c, b.cL, ns, s,
                                       b.xpart, b.xcnt));

@@ -265,8 +265,11 @@ hipError_t launch_cross_attn_mfma(const bf16_t* qt, long qt_lo, const bf16_t* me
 // drop (train mode): gsum [rows][8] receives sum_s P_s m_s / sum_s P_s per (row, head) (the value bias's weight)
 hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem16, int rows, int rows_per_image,
                                  int S, float scale, bf16_t* out, long out_lo, hipStream_t s,
-                                 DropCfg drop = DropCfg{}, float* gsum = nullptr);
+                                 DropCfg drop = DropCfg{}, float* gsum = nullptr, float* xpart = nullptr,
+                                 int* xcnt = nullptr);
 int cross_attn_splits(int S);
+// blocks per row pair of launch_cross_attn_f16 (2: key split, needs xpart / xcnt as launch_cross_attn_mfma)
+int cross_attn_f16_splits();
 size_t cross_attn_part_floats(int rows);
 // Batched beam search (beam.hip): state init, per-step selection, final pick.
 hipError_t launch_beam_init(int B, int K, int start, int Lmax, int32_t* seq_a, int32_t* seq_b, int32_t* anc_a,
