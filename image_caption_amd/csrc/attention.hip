@@ -513,7 +513,12 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
   if (nsplit == NS_F16) {  // one fp16 plane (ICAP_PREC_F16 encoder): the pipelined form, one query tile per wave
     if (N > 256) return hipErrorInvalidValue;
     const int lds = 4 * 2 * 32 * 128;
-    if (head_major)
+    // ICAP_ENC_ATTN16_QPW (tools): 2 query tiles per wave (8 waves, K/V chunk reads shared by 32 queries)
+    static const int qpw16 = icap_knob("ICAP_ENC_ATTN16_QPW", 1);
+    if (head_major && qpw16 == 2)
+      hipLaunchKernelGGL((enc_attention_pipe_kernel<false, true, 2, true>), dim3(H, B), dim3(512), lds, s, qkv, ld, lo,
+                         N, H, scale, out, out_ld, out_lo);
+    else if (head_major)
       hipLaunchKernelGGL((enc_attention_pipe_kernel<false, true, 1, true>), dim3(H, B), dim3(1024), lds, s, qkv, ld, lo,
                          N, H, scale, out, out_ld, out_lo);
     else
