@@ -510,11 +510,12 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
     return nsplit == 2 ? run_enc<4, true>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s)
                        : run_enc<4, false>(qkv, ld, lo, B, N, H, scale, out, out_ld, out_lo, s);
   }
-  if (nsplit == NS_F16) {  // one fp16 plane (ICAP_PREC_F16 encoder): the pipelined form, one query tile per wave
+  if (nsplit == NS_F16) {  // one fp16 plane (ICAP_PREC_F16 encoder): the pipelined form
     if (N > 256) return hipErrorInvalidValue;
     const int lds = 4 * 2 * 32 * 128;
-    // ICAP_ENC_ATTN16_QPW (tools): 2 query tiles per wave (8 waves, K/V chunk reads shared by 32 queries)
-    static const int qpw16 = icap_knob("ICAP_ENC_ATTN16_QPW", 1);
+    // two query tiles per wave (8 waves, 119 VGPRs, two blocks per CU): every K/V fragment read from LDS serves
+    // 32 queries - 1.57 -> 1.28 ms/step at B = 256 (tools/knob_ab.sh); ICAP_ENC_ATTN16_QPW=1 (tools): 16 waves
+    static const int qpw16 = icap_knob("ICAP_ENC_ATTN16_QPW", 2);
     if (head_major && qpw16 == 2)
       hipLaunchKernelGGL((enc_attention_pipe_kernel<false, true, 2, true>), dim3(H, B), dim3(512), lds, s, qkv, ld, lo,
                          N, H, scale, out, out_ld, out_lo);

@@ -156,6 +156,34 @@ def test_grid_train_trunk_matches_torch(cuda):
     assert eerr < 4e-3, eerr
 
 
+def test_scst_grid_train_mode_sampler_and_recompute_share_memory(cuda):
+    """Grid in train mode with dropout 0.1 everywhere: the tokens are sampled from the same memory the
+    log-probs are differentiated on (one train-mode tail per step, its dropout masks torch's), so with the
+    same torch seed and the same sampler seed the grad-enabled call returns the no-grad call's ids and its
+    recomputed log-probs match the sampler's within the decoder parity tolerance."""
+    from models.grid_transformer_model import build_model
+    from utils.scst_loss import SCSTLoss
+
+    B, L = 4, 12
+    m = build_model(W.VOCAB_SIZE, {"pretrained_cnn": False, "dropout": 0.1})
+    m.load_state_dict(W.to_torch(W.grid_state_dict(0)))
+    m = m.to(cuda).train()
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=2)).to(cuda)
+    uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(4)).to(cuda)
+    loss_fn = SCSTLoss()
+    out = []
+    for grad in (False, True):
+        torch.manual_seed(123)
+        with torch.set_grad_enabled(grad):
+            ids, logp = loss_fn._sample_with_log_probs(m, imgs, W.START_TOKEN, W.END_TOKEN, L, cuda, uniforms=uni,
+                                                       dropout_seed=77)
+        out.append((ids, logp.detach()))
+    assert torch.equal(out[0][0], out[1][0])
+    err = (out[0][1] - out[1][1]).abs().max().item()
+    print(f"sampler vs recompute log-probs: {err:.2e}")
+    assert err < 1e-3, err
+
+
 @pytest.mark.parametrize("part", ["decoder", "encoder"])
 def test_engine_refresh_in_place(cuda, part):
     """model.hip_engine after an in-place weight change re-packs that part into the SAME handle

@@ -126,28 +126,30 @@ class SCSTLoss(nn.Module):
             drop = (p, int(dropout_seed or 0))
             feats = None
             mem = None
+            memory_t = None
+            want_grad = torch.is_grad_enabled()
             if getattr(model, "_hip_kind", "") == "grid" and model.encoder.cnn.training:
                 # the reference encodes once per step, in train mode (scst_loss:161, :213): the trunk's
-                # BatchNorm normalises with batch statistics and updates its running statistics ONCE.
+                # BatchNorm normalises with batch statistics and updates its running statistics ONCE, and the
+                # sampled tokens and the differentiated log-probs see the SAME memory (one forward graph).
                 # A frozen trunk on 224x224 images runs as the HIP train-mode trunk (icap_encode_grid_train:
-                # batch statistics, running statistics updated in place, memory and trunk features in one
-                # pass); a trainable one (or other sizes) runs here in PyTorch, once, grad as enabled.  The
-                # recompute below reuses the trunk features either way.
+                # batch statistics, running statistics updated in place); a trainable one (or other sizes)
+                # runs here in PyTorch, once, grad as enabled.  The tail (projection, PE, encoder layers) then
+                # runs once in PyTorch in the module's mode - with train-mode dropout its masks are torch's -
+                # and its output is both the sampler's memory (detached) and the recompute's (with grad).
                 cnn = model.encoder.cnn
                 if (tuple(images.shape[1:]) == (3, 224, 224) and 2 <= images.size(0) <= 256
                         and not any(p.requires_grad for p in cnn.parameters())):
                     with torch.no_grad():
-                        mem, feats = eng.encode_grid_train(images, cnn)
+                        _, feats = eng.encode_grid_train(images, cnn)
                 else:
                     feats = model.encoder.cnn(images.float())
+                memory_t = model.encoder.tail(feats)
+                mem = memory_t.detach().float().contiguous()
             vfeats = None
-            want_grad = torch.is_grad_enabled()
             with torch.no_grad():
                 if mem is not None:
-                    pass  # the HIP train-mode trunk + tail above
-                elif feats is not None:
-                    f = feats.detach()
-                    mem = eng.encode(f) if f.shape[2] * f.shape[3] == eng.mem_tokens else model.encoder.tail(f)
+                    pass  # the train-mode Grid encoder above
                 elif getattr(model, "_hip_kind", "") == "grid" and tuple(images.shape[1:]) != (3, 224, 224):
                     mem = model.encoder(images)  # eval trunk, other sizes: torch trunk (+ HIP tail on 7x7)
                 elif want_grad and vit_trunk_frozen(model):
@@ -165,8 +167,10 @@ class SCSTLoss(nn.Module):
                 # sampler's dropout masks, so the distribution sampled from is the one differentiated
                 if vfeats is not None:
                     memory = model.encoder.projection(vfeats)
+                elif memory_t is not None:
+                    memory = memory_t  # the memory the tokens were sampled from
                 else:
-                    memory = model.encoder.tail(feats) if feats is not None else model.encoder(images)
+                    memory = model.encoder(images)
                 logp = decoder_token_logp(model.decoder, memory, ids, end_token, dropout=drop)
             return ids, logp
         return self._sample_torch(model, images, start_token, end_token, max_len, uniforms)
