@@ -192,10 +192,15 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 bool gemm_f16_persistent(const GemmArgs& g) {
-  static const int form = icap_knob("ICAP_F16_GEMM", 0);  // tools: 6 = persistent for every fp16 GEMM
-  return g.f16 && (form == 0 || form == 6) && g.out == OUT_SPLIT && !g.addend && !g.rm_group && !g.res &&
-         !g.scale && !g.cv && g.batch == 1 && g.nsplit == 1 && g.c_planes == 1 && g.N % 256 == 0 && g.M % 256 == 0 &&
-         g.K >= 128 && g.K % 64 == 0 && (g.epi == EPI_NONE || g.epi == EPI_GELU);
+  // tools: ICAP_F16_GEMM 6 = persistent for every fp16 GEMM; ICAP_F16_PRES 0 = the residual GEMMs in the
+  // two-block form (out-proj 131 / MLP-2 340 us against 124 / 314 persistent, encoder 15.7 -> 15.0 ms/step)
+  static const int form = icap_knob("ICAP_F16_GEMM", 0), pres = icap_knob("ICAP_F16_PRES", 1);
+  const bool common = g.f16 && (form == 0 || form == 6) && !g.addend && !g.rm_group && !g.res && !g.scale && !g.cv &&
+                      g.batch == 1 && g.nsplit == 1 && g.N % 256 == 0 && g.M % 256 == 0 && g.K >= 128 &&
+                      g.K % 64 == 0;
+  if (!common) return false;
+  if (g.out == OUT_SPLIT) return g.c_planes == 1 && (g.epi == EPI_NONE || g.epi == EPI_GELU);
+  return pres && g.out == OUT_F32_RESID && g.epi == EPI_NONE;
 }
 
 int gemm_tile_class(const GemmArgs& g) {
@@ -1001,8 +1006,14 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // 0 AND 1 are issued before the epilogue (its bias was loaded before stage 0, behind the previous tile's
 // MFMAs), k-step 0 waits vmcnt(8 + 32) (stage 0 done; stage 1 and the 32 stores per wave may pend),
 // k-step 1 vmcnt(32); the stores then drain behind two k-steps of MFMAs.
-template <bool SO>
+// MODE 2 (RES: out = OUT_F32_RESID, C += acc + bias, M % 256 == 0, K >= 128): the residual GEMMs (ViT out-proj,
+// MLP-2).  The epilogue reads the fp32 residual in two halves of 16 loads per lane (registers: acc + 64); the
+// next tile's stage 0 is in flight behind the last k-step, its stage 1 is issued after the epilogue's stores
+// (the residual loads' waits would otherwise wait for it), and k-step 0 needs no vmcnt wait: the residual loads
+// retired after stage 0 (in order).
+template <int MODE>
 __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
+  constexpr bool SO = MODE == 1, RES = MODE == 2;
   constexpr int BM = 256, BN = 256, KS = 64, NW = 8, WM = 128, WN = 64, TM = 8, TN = 4;
   constexpr int OPB = BM * KS * 2, STAGE = 2 * OPB;  // A 32 KiB + W 32 KiB
   constexpr int IPW = OPB / 1024 / NW;                // 4 DMA instructions per wave per operand
@@ -1054,7 +1065,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   int t = xbase + lb, step = 0, tcount = 0;
-  if (SO) load_bias(t, 0);
+  if (SO || RES) load_bias(t, 0);
   stage(t, 0, 0);
   bool seam = false;  // this tile's stages 0 and 1 were issued before the previous tile's epilogue stores
   for (;;) {
@@ -1063,14 +1074,15 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       // lgkmcnt(0): this wave's reads of the buffer about to be refilled are done before the barrier
       if (SO && seam && kt == 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE + NSTORE) : "memory");
       else if (SO && seam && kt == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+      else if (RES && seam && kt == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (SO && seam && kt == 0) {
+      if ((SO || RES) && seam && kt == 0) {
         // stage 1 of this tile is already in flight
       } else if (kt + 1 < nk) {
         stage(t, kt + 1, (step + 1) & 1);
       } else if (tn >= 0) {  // the next tile's bias, then its first stage, behind this k-step's MFMAs
-        if (SO) load_bias(tn, (tcount + 1) & 1);
+        if (SO || RES) load_bias(tn, (tcount + 1) & 1);
         stage(tn, 0, (step + 1) & 1);
       }
       const char* s0 = smem + (step & 1) * STAGE;
@@ -1111,6 +1123,32 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
           }
           *(u32x2*)(C + nb + j * 16) = pack16x4<true>(v);
         }
+      }
+      seam = true;
+    } else if constexpr (RES) {
+      float* Cb = (float*)p.C + nb + 4 * fq;
+      const float* bl = sbias + (tcount & 1) * 256 + wn * WN + 4 * fq;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        f32x4 rv[4][TN];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            rv[i][j] = *(const f32x4*)(Cb + (long)(mb + (h2 * 4 + i) * 16 + fr) * p.ldc + j * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            f32x4 a = acc[h2 * 4 + i][j];
+            if (p.bias) a += *(const f32x4*)(bl + j * 16);
+            *(f32x4*)(Cb + (long)(mb + (h2 * 4 + i) * 16 + fr) * p.ldc + j * 16) = rv[i][j] + a;
+          }
+      }
+      if (tn >= 0) {  // stage 1 of the next tile into the last stage's buffer, after the stores
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        stage(tn, 1, (step + 1) & 1);
       }
       seam = true;
     } else {
@@ -1343,15 +1381,19 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       if (!cus) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0)
           return hipErrorInvalidValue;
-        for (const void* f : {(const void*)gemm_f16p_kernel<false>, (const void*)gemm_f16p_kernel<true>})
+        for (const void* f : {(const void*)gemm_f16p_kernel<0>, (const void*)gemm_f16p_kernel<1>,
+                              (const void*)gemm_f16p_kernel<2>})
           if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048) != hipSuccess)
             return hipErrorInvalidValue;
       }
       const int tiles = (g.N / 256) * ((g.M + 255) / 256);
-      if (so)
-        hipLaunchKernelGGL(gemm_f16p_kernel<true>, dim3(std::min(tiles, cus)), dim3(512), 2 * 64 * 1024 + 2048, s, g);
+      const dim3 grid(std::min(tiles, cus));
+      if (so && g.out == OUT_F32_RESID)
+        hipLaunchKernelGGL(gemm_f16p_kernel<2>, grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+      else if (so)
+        hipLaunchKernelGGL(gemm_f16p_kernel<1>, grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
       else
-        hipLaunchKernelGGL(gemm_f16p_kernel<false>, dim3(std::min(tiles, cus)), dim3(512), 2 * 64 * 1024, s, g);
+        hipLaunchKernelGGL(gemm_f16p_kernel<0>, grid, dim3(512), 2 * 64 * 1024, s, g);
       return hipGetLastError();
     }
 #ifdef ICAP_TOOLS
