@@ -1379,7 +1379,9 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     if ((form == 6 && g.K % 64 == 0) || so) {
       static int cus = 0;
       if (!cus) {
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0)
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
           return hipErrorInvalidValue;
         for (const void* f : {(const void*)gemm_f16p_kernel<0>, (const void*)gemm_f16p_kernel<1>,
                               (const void*)gemm_f16p_kernel<2>})
