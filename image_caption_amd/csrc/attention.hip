@@ -820,19 +820,21 @@ constexpr int XA_RED_BYTES = (8 * 512 + 512) * 4 + 16;  // + the KS = 2 ticket
 // [c/2, c)); each leaves its unnormalised context and softmax statistics (agent-scope stores), and the second
 // to take the pair's ticket merges them in part order (deterministic) and resets the ticket (xpart / xcnt as
 // cross_attn_mfma_kernel<KS = 2>).
-template <int KS>
-__global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __restrict__ qt, long qt_lo,
+template <int KS, int CK>
+__global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* __restrict__ qt, long qt_lo,
                                                               const bf16_t* __restrict__ mem, int rows_per_image,
                                                               int S, float scale, bf16_t* out, long out_lo,
                                                               DropCfg drop, float* gsum, float* xpart, int* xcnt) {
-  constexpr int DM = 512, H = 8, CK = 64;
-  constexpr int BUF = CK * DM * 2;              // 64 KiB per chunk
+  constexpr int DM = 512, H = 8;
+  constexpr int NW = CK / 4, NT = NW * 64;      // waves (4 keys each per chunk), threads
+  constexpr int NKT = CK / 16, NDT = DM / NW / 16, NS2 = CK / 32;  // key tiles, d tiles per wave, key k-steps
+  constexpr int BUF = CK * DM * 2;              // 64 / 32 KiB per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = (float*)(smem + 2 * BUF);        // [4 d-groups][4 tiles][4 regs][64 lanes]
-  float* tot = red + 4 * 1024;                  // [4 tiles][4 regs][64 lanes]
+  float* red = (float*)(smem + 2 * BUF);        // [4 d-groups][NKT tiles][4 regs][64 lanes]
+  float* tot = red + NKT * 1024;                // [NKT tiles][4 regs][64 lanes]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int skt = wave & 3, sdg = wave >> 2;
+  const int skt = wave % NKT, sdg = wave / NKT;
   const int bpi = (rows_per_image + 1) / 2;
   const int pb = blockIdx.x / KS, part = blockIdx.x - pb * KS;
   const int img = pb / bpi, pair = pb - img * bpi;
@@ -879,9 +881,9 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
   };
   auto mma16h = [](f16x8 a, f16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); };
 
-  f32x4 acc[2];
-  acc[0] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  acc[1] = acc[0];
+  f32x4 acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f, d_run = 0.f;  // d_run: the dropped-probability mass (train mode)
   const int q4 = fr >> 2, p4 = fr & 3;
 
@@ -903,21 +905,21 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
         a = mma16h(mh, ql[ks], a);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) red[((sdg * 4 + skt) * 4 + j) * 64 + lane] = a[j];
+      for (int j = 0; j < 4; ++j) red[((sdg * NKT + skt) * 4 + j) * 64 + lane] = a[j];
     }
     __syncthreads();
-    {
+    {  // NT = NKT * 256 threads: one total each
       float v = 0.f;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) v += red[g * 1024 + threadIdx.x];
+      for (int g = 0; g < 4; ++g) v += red[g * NT + threadIdx.x];
       tot[threadIdx.x] = v;
     }
     __syncthreads();
     // total scores (every wave), scale, mask, online softmax per head (= lane & 15)
-    f32x4 sc[4];
+    f32x4 sc[NKT];
     float cmax = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int key = c * CK + kt * 16 + fq * 4 + j;
@@ -931,7 +933,7 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
     const float alpha = __expf(m_run - m_new);
     float psum = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float e = __expf(sc[kt][j] - m_new);
@@ -942,12 +944,12 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
     psum += __shfl_xor(psum, 32, 64);
     l_run = l_run * alpha + psum;
     m_run = m_new;
-    acc[0] *= alpha;
-    acc[1] *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) acc[dt] *= alpha;
     if (drop.thr) {
       float dsum = 0.f;
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int key = c * CK + kt * 16 + fq * 4 + j;
@@ -959,7 +961,7 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
       d_run = d_run * alpha + dsum;
     }
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
+    for (int s2 = 0; s2 < NS2; ++s2) {
       // P^T as the B operand of key tiles 2 s2, 2 s2 + 1 (element j < 4 -> key 4fq + j of the first tile,
       // j >= 4 -> key 4fq + j - 4 of the second), fp16 hi/lo
       f16x8 ph, pl;
@@ -972,8 +974,8 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
         pl[4 + j] = (_Float16)(sc[2 * s2 + 1][j] - (float)h1);
       }
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const int d = wave * 32 + dt * 16 + 4 * p4;
+      for (int dt = 0; dt < NDT; ++dt) {
+        const int d = wave * (16 * NDT) + dt * 16 + 4 * p4;
         const int k0 = 32 * s2 + 4 * fq + q4, k1 = k0 + 16;
         const int o0 = k0 * 1024 + ((((d >> 3) ^ (k0 & 15))) << 4) + (d & 7) * 2;
         const int o1 = k1 * 1024 + ((((d >> 3) ^ (k1 & 15))) << 4) + (d & 7) * 2;
@@ -991,10 +993,10 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
     float* mine = xpart + ((long)pb * 2 + part) * XA_PART_FLOATS;
     const float* other = xpart + ((long)pb * 2 + (part ^ 1)) * XA_PART_FLOATS;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
-        __hip_atomic_store(mine + (dt * 4 + rr) * 1024 + threadIdx.x, acc[dt][rr], __ATOMIC_RELAXED,
+        __hip_atomic_store(mine + (dt * 4 + rr) * NT + threadIdx.x, acc[dt][rr], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x < 16) {
       __hip_atomic_store(mine + 8 * 1024 + threadIdx.x, m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1002,7 +1004,7 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores are complete
     __syncthreads();                                   // ... and every thread's
-    int* flag = (int*)(tot + 1024);                    // after the score totals
+    int* flag = (int*)(tot + NKT * 256);               // after the score totals
     if (threadIdx.x == 0)
       *flag = __hip_atomic_fetch_add(xcnt + pb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
@@ -1010,17 +1012,17 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
     if (threadIdx.x == 0) __hip_atomic_store(xcnt + pb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float om = __hip_atomic_load(other + 8 * 1024 + fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float ol = __hip_atomic_load(other + 8 * 1024 + 16 + fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    float oa[8];
+    float oa[NDT * 4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      oa[k] = __hip_atomic_load(other + k * 1024 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < NDT * 4; ++k)
+      oa[k] = __hip_atomic_load(other + k * NT + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // part 0's state first whatever the arrival order
     const float m0 = part ? om : m_run, m1 = part ? m_run : om;
     const float l0 = part ? ol : l_run, l1 = part ? l_run : ol;
     const float mn = fmaxf(m0, m1), f0 = __expf(m0 - mn), f1 = __expf(m1 - mn);
     l_run = __fadd_rn(__fmul_rn(l0, f0), __fmul_rn(l1, f1));
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const float x0 = part ? oa[dt * 4 + rr] : acc[dt][rr], x1 = part ? acc[dt][rr] : oa[dt * 4 + rr];
@@ -1030,9 +1032,9 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
   if (valid && drop.thr && gsum && wave == 0 && fq == 0) gsum[r * H + hd] = d_run / l_run;
   if (valid) {
     const float inv = 1.f / l_run;
-    bf16_t* dst = out + r * H * DM + hd * DM + wave * 32;
+    bf16_t* dst = out + r * H * DM + hd * DM + wave * (16 * NDT);
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
+    for (int dt = 0; dt < NDT; ++dt) {
       bf16_t hv[4], lv[4];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) split_bf(acc[dt][rr] * inv, hv[rr], lv[rr]);
@@ -1043,7 +1045,9 @@ __global__ __launch_bounds__(1024) void cross_attn_f16_kernel(const bf16_t* __re
     }
   }
 }
-constexpr int XA16_LDS = 2 * 64 * 512 * 2 + (4 * 1024 + 1024) * 4 + 16;  // + the KS = 2 ticket flag
+// LDS of cross_attn_f16_kernel<KS, CK>: 2 chunk buffers + partial and total scores + the KS = 2 ticket flag
+constexpr int xa16_lds(int ck) { return 2 * ck * 512 * 2 + (ck / 16) * (1024 + 256) * 4 + 16; }
+constexpr int XA16_LDS = xa16_lds(64);
 
 }  // namespace
 
@@ -1074,19 +1078,31 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
   if (drop.thr && (rows_per_image != 1 || S > 256 || !gsum)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)cross_attn_f16_kernel<1>, (const void*)cross_attn_f16_kernel<2>}) {
+    for (const void* f : {(const void*)cross_attn_f16_kernel<1, 64>, (const void*)cross_attn_f16_kernel<2, 64>}) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, XA16_LDS);
+      if (e != hipSuccess) return e;
+    }
+    for (const void* f : {(const void*)cross_attn_f16_kernel<1, 32>, (const void*)cross_attn_f16_kernel<2, 32>}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, xa16_lds(32));
       if (e != hipSuccess) return e;
     }
     attr = true;
   }
+  // 32-key chunks, 8 waves, 74 KiB of LDS: two blocks (rows) share a CU, so the three decode chains' cross-
+  // attentions hold half the CUs (decode 12.70 -> 12.47 ms/step, tools/knob_ab.sh); ICAP_XATTN16_CK=64 (tools):
+  // 64-key chunks, 16 waves, 148 KiB (one block per CU)
+  static const int ck = icap_knob("ICAP_XATTN16_CK", 32) == 64 ? 64 : 32;
   const int pairs = rows / rows_per_image * ((rows_per_image + 1) / 2);
-  if (xpart && xcnt && !drop.thr && S > 64 && cross_attn_f16_splits() == 2)
-    hipLaunchKernelGGL(cross_attn_f16_kernel<2>, dim3(2 * pairs), dim3(1024), XA16_LDS, s, qt, qt_lo, mem16,
-                       rows_per_image, S, scale, out, out_lo, drop, gsum, xpart, xcnt);
-  else
-    hipLaunchKernelGGL(cross_attn_f16_kernel<1>, dim3(pairs), dim3(1024), XA16_LDS, s, qt, qt_lo, mem16,
-                       rows_per_image, S, scale, out, out_lo, drop, gsum, xpart, xcnt);
+  const bool ks2 = xpart && xcnt && !drop.thr && S > ck && cross_attn_f16_splits() == 2;
+#define XA16(KS_, CK_)                                                                                          \
+  hipLaunchKernelGGL((cross_attn_f16_kernel<KS_, CK_>), dim3(KS_ * pairs), dim3(CK_ * 16), xa16_lds(CK_), s, qt, \
+                     qt_lo, mem16, rows_per_image, S, scale, out, out_lo, drop, gsum, xpart, xcnt)
+  if (ck == 32) {
+    if (ks2) XA16(2, 32); else XA16(1, 32);
+  } else {
+    if (ks2) XA16(2, 64); else XA16(1, 64);
+  }
+#undef XA16
   return hipGetLastError();
 }
 
