@@ -196,8 +196,7 @@ bool gemm_f16_persistent(const GemmArgs& g) {
   // two-block form (out-proj 131 / MLP-2 340 us against 124 / 314 persistent, encoder 15.7 -> 15.0 ms/step)
   static const int form = icap_knob("ICAP_F16_GEMM", 0), pres = icap_knob("ICAP_F16_PRES", 1);
   const bool common = g.f16 && (form == 0 || form == 6) && !g.addend && !g.rm_group && !g.res && !g.scale && !g.cv &&
-                      g.batch == 1 && g.nsplit == 1 && g.N % 256 == 0 && g.M % 256 == 0 && g.K >= 128 &&
-                      g.K % 64 == 0;
+                      g.batch == 1 && g.nsplit == 1 && g.N % 256 == 0 && g.M >= 256 && g.K >= 128 && g.K % 64 == 0;
   if (!common) return false;
   if (g.out == OUT_SPLIT) return g.c_planes == 1 && (g.epi == EPI_NONE || g.epi == EPI_GELU);
   return pres && g.out == OUT_F32_RESID && g.epi == EPI_NONE;
@@ -999,14 +998,15 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // behind that k-step's MFMAs and the epilogue.  Tiles: the XCD-bijective remap of gemm_256_kernel gives
 // XCD x a contiguous range of logical tiles (row-band major), its blocks take every nbx-th of them, so the
 // tiles in flight on one XCD share their A row bands in its L2.
-// SO (store-only epilogues: bias (+ GELU) -> one fp16 plane, optionally head-major; M % 256 == 0, K >= 128):
+// SO (store-only epilogues: bias (+ GELU) -> one fp16 plane, optionally head-major; K >= 128; a ragged last
+// row band stores only its rows < M and hands the next tile the uncounted vmcnt(0) wait):
 // the epilogue's stores must not hold the next tile's k-loop.  VMEM operations retire in issue order (the
 // compiler's own s_waitcnt model on gfx950 counts loads and stores in one in-order counter), so the k-loop
 // waits with counts that leave the previous tile's stores in flight: at a tile seam the next tile's stages
 // 0 AND 1 are issued before the epilogue (its bias was loaded before stage 0, behind the previous tile's
 // MFMAs), k-step 0 waits vmcnt(8 + 32) (stage 0 done; stage 1 and the 32 stores per wave may pend),
 // k-step 1 vmcnt(32); the stores then drain behind two k-steps of MFMAs.
-// MODE 2 (RES: out = OUT_F32_RESID, C += acc + bias, M % 256 == 0, K >= 128): the residual GEMMs (ViT out-proj,
+// MODE 2 (RES: out = OUT_F32_RESID, C += acc + bias, K >= 128): the residual GEMMs (ViT out-proj,
 // MLP-2).  The epilogue reads the fp32 residual in two halves of 16 loads per lane (registers: acc + 64); the
 // next tile's stage 0 is in flight behind the last k-step, its stage 1 is issued after the epilogue's stores
 // (the residual loads' waits would otherwise wait for it), and k-step 0 needs no vmcnt wait: the residual loads
@@ -1107,12 +1107,14 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         __builtin_amdgcn_s_barrier();
         stage(tn, 1, (step + 1) & 1);  // step = the next tile's k-step 0 here; its k-step 1 reads (step + 1) & 1
       }
+      const bool tail = bm * BM + BM > M;  // the last row band of a ragged M: rows >= M are not stored
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int m = mb + i * 16 + fr;  // < M: M % 256 == 0
+        const int m = min(mb + i * 16 + fr, M - 1);
         const long orow = p.hm_n ? (((long)(m / p.hm_n) * (p.N / 64) + nb / 64) * p.hm_n + m % p.hm_n) * 64 - nb
                                  : (long)m * p.ldc;
         bf16_t* C = (bf16_t*)p.C + orow + 4 * fq;
+        const bool ok = !tail || mb + i * 16 + fr < M;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           f32x4 v = acc[i][j];
@@ -1121,13 +1123,16 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
             const f32x2 lo = gelu_erf_fast2((f32x2){v[0], v[1]}), hi = gelu_erf_fast2((f32x2){v[2], v[3]});
             v = (f32x4){lo[0], lo[1], hi[0], hi[1]};
           }
-          *(u32x2*)(C + nb + j * 16) = pack16x4<true>(v);
+          if (ok) *(u32x2*)(C + nb + j * 16) = pack16x4<true>(v);
         }
       }
-      seam = true;
+      // the counted waits of the next tile assume all 32 stores per wave were issued: not after a ragged tile
+      // (its next tile waits vmcnt(0) and re-issues its stage 1 - the same bytes into the same buffer)
+      seam = !tail;
     } else if constexpr (RES) {
       float* Cb = (float*)p.C + nb + 4 * fq;
       const float* bl = sbias + (tcount & 1) * 256 + wn * WN + 4 * fq;
+      const bool tail = bm * BM + BM > M;  // ragged last row band: rows >= M neither read nor stored
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         f32x4 rv[4][TN];
@@ -1135,21 +1140,26 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            rv[i][j] = *(const f32x4*)(Cb + (long)(mb + (h2 * 4 + i) * 16 + fr) * p.ldc + j * 16);
+            rv[i][j] = *(const f32x4*)(Cb + (long)min(mb + (h2 * 4 + i) * 16 + fr, M - 1) * p.ldc + j * 16);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+          const int m = mb + (h2 * 4 + i) * 16 + fr;
+          if (tail && m >= M) continue;
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             f32x4 a = acc[h2 * 4 + i][j];
             if (p.bias) a += *(const f32x4*)(bl + j * 16);
-            *(f32x4*)(Cb + (long)(mb + (h2 * 4 + i) * 16 + fr) * p.ldc + j * 16) = rv[i][j] + a;
+            *(f32x4*)(Cb + (long)m * p.ldc + j * 16) = rv[i][j] + a;
           }
+        }
       }
       if (tn >= 0) {  // stage 1 of the next tile into the last stage's buffer, after the stores
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         stage(tn, 1, (step + 1) & 1);
       }
+      // k-step 0 of the next tile skips its vmcnt wait because the residual loads retired after its stage 0;
+      // every lane loads (rows clamped), so that holds for ragged tiles too
       seam = true;
     } else {
       epilogue_256<TM, TN, true>(p, acc, mb, nb, fr, fq);
