@@ -100,6 +100,23 @@ def test_dropin_grid_model_state_dict():
     assert set(m.state_dict()) == set(sd)
 
 
+def test_every_knob_is_refused_by_the_product_build():
+    """Every ICAP_* measurement knob the sources read (icap_knob) is in icap_knobs_set's list, so a product
+    build refuses to run with any of them set (no environment can change what the library computes)."""
+    import re
+
+    csrc = os.path.join(ROOT, "image_caption_amd", "csrc")
+    read = set()
+    for f in os.listdir(csrc):
+        with open(os.path.join(csrc, f)) as fh:
+            read |= set(re.findall(r'icap_knob\("(ICAP_[A-Z0-9_]+)"', fh.read()))
+    with open(os.path.join(csrc, "icap.cpp")) as fh:
+        src = fh.read()
+    lst = src[src.index("const char* icap_knobs_set()"):]
+    refused = set(re.findall(r'"(ICAP_[A-Z0-9_]+)"', lst[:lst.index("};")]))
+    assert read and read <= refused, sorted(read - refused)
+
+
 def test_deepcopy_routes_to_the_copy():
     """copy.deepcopy of a drop-in model: the copy's encoder / decoder route to the copy (not the original's
     engine), and a packed engine (a device handle) is never copied or shared."""
