@@ -471,6 +471,35 @@ def test_gemm_f16(cuda, M, N, K, epi):
     assert (R.double() - R0.double() - C.double()).abs().max().item() < 1e-5 * scale
 
 
+@pytest.mark.parametrize("M,N,K", [(50432, 2304, 768), (25216, 768, 3072), (50000, 3072, 768)])
+def test_gemm_f16_persistent_repeat_bitwise(cuda, M, N, K):
+    """The persistent fp16 GEMM at full-chip shapes (ViT B = 256 QKV, B = 128 MLP-2, a ragged 50000-row
+    MLP-1): its tile seams wait with counted vmcnt that leave the previous tile's stores in flight, so a
+    miscounted wait would read a stage before it landed - run to run differences.  Plane (+ GELU) and residual
+    outputs, 6 runs each in one process: bitwise equal, and against fp64 on sampled rows."""
+    L, lib = _lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).to(torch.float16).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.float16).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    rows = torch.arange(0, M, 991, device=cuda)
+    ref = a[rows].double() @ w.double().t() + bias.double()
+    R0 = torch.randn(M, N, generator=g).to(cuda)
+    for epi, out in ((0, 2), (1, 2), (0, 3)):
+        outs = []
+        for _ in range(6):
+            C = R0.clone() if out == 3 else torch.empty(M, N, device=cuda, dtype=torch.float16)
+            L.check(lib.icap_op_gemm(a.data_ptr(), K, 0, -1, w.data_ptr(), bias.data_ptr(), C.data_ptr(), N, 0,
+                                     M, N, K, epi, out, L.stream_ptr()), "gemm f16")
+            outs.append(C)
+        torch.cuda.synchronize()
+        assert all(torch.equal(o, outs[0]) for o in outs[1:]), (epi, out)
+        want = torch.nn.functional.gelu(ref) if epi == 1 else ref
+        got = outs[0][rows].double() - (R0[rows].double() if out == 3 else 0)
+        tol = (2e-5 if out == 3 else 2 ** -10) * max(1.0, want.abs().max().item())
+        assert (got - want).abs().max().item() < tol, (epi, out)
+
+
 def test_gemm_f16_head_major_via_engine_layout(cuda):
     """Identity A through the fp16 kernel: exact, and not transposed."""
     L, lib = _lib()
