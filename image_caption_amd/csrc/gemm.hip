@@ -1011,7 +1011,8 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // next tile's stage 0 is in flight behind the last k-step, its stage 1 is issued after the epilogue's stores
 // (the residual loads' waits would otherwise wait for it), and k-step 0 needs no vmcnt wait: the residual loads
 // retired after stage 0 (in order).
-template <int MODE>
+// ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh)
+template <int MODE, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   constexpr bool SO = MODE == 1, RES = MODE == 2;
   constexpr int BM = 256, BN = 256, KS = 64, NW = 8, WM = 128, WN = 64, TM = 8, TN = 4;
@@ -1080,10 +1081,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       if ((SO || RES) && seam && kt == 0) {
         // stage 1 of this tile is already in flight
       } else if (kt + 1 < nk) {
-        stage(t, kt + 1, (step + 1) & 1);
+        if (ABL != 1) stage(t, kt + 1, (step + 1) & 1);
       } else if (tn >= 0) {  // the next tile's bias, then its first stage, behind this k-step's MFMAs
         if (SO || RES) load_bias(tn, (tcount + 1) & 1);
-        stage(tn, 0, (step + 1) & 1);
+        if (ABL != 1) stage(tn, 0, (step + 1) & 1);
       }
       const char* s0 = smem + (step & 1) * STAGE;
 #pragma unroll
@@ -1096,7 +1097,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         for (int i = 0; i < TM; ++i) {
           const bf16x8 af = *(const bf16x8*)(s0 + (wm * WM + i * 16) * 128 + fo);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mma<true>(bfr[j], af, acc[i][j]);
+          for (int j = 0; j < TN; ++j) {
+            if (ABL == 2) asm volatile("" ::"v"(bfr[j]), "v"(af));
+            else acc[i][j] = mma<true>(bfr[j], af, acc[i][j]);
+          }
         }
       }
     }
@@ -1105,7 +1109,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       if (tn >= 0) {  // every wave is done reading the last stage's buffer: stage 1 of the next tile into it
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        stage(tn, 1, (step + 1) & 1);  // step = the next tile's k-step 0 here; its k-step 1 reads (step + 1) & 1
+        if (ABL != 1) stage(tn, 1, (step + 1) & 1);  // step = the next tile's k-step 0 here; its k-step 1 reads (step + 1) & 1
       }
       const bool tail = bm * BM + BM > M;  // the last row band of a ragged M: rows >= M are not stored
 #pragma unroll
@@ -1156,7 +1160,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       if (tn >= 0) {  // stage 1 of the next tile into the last stage's buffer, after the stores
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        stage(tn, 1, (step + 1) & 1);
+        if (ABL != 1) stage(tn, 1, (step + 1) & 1);
       }
       // k-step 0 of the next tile skips its vmcnt wait because the residual loads retired after its stage 0;
       // every lane loads (rows clamped), so that holds for ragged tiles too
@@ -1173,6 +1177,241 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
 }
+
+#ifdef ICAP_TOOLS
+// ---------------------------------------------------------------------------------------------
+// Persistent fp16 encoder GEMM, ping-pong form (gemm_f16q_kernel): the tile walk, tiles, modes (SO / RES)
+// and epilogues of gemm_f16p_kernel, with a k-loop in which the two waves of each SIMD alternate between
+// LDS reads and MFMAs.  gemm_f16p_kernel runs both waves of a SIMD in the same state (read 2 A fragments,
+// wait, 8 MFMAs): its LDS latency is exposed at ~44 % MFMA issue.  Here waves 0-3 (rows 0-127 of the tile)
+// lead and waves 4-7 (rows 128-255) trail by ONE barrier, and every phase is
+//     R: [odd phase: counted vmcnt] [2 LDS-DMA instructions] [epilogue part] ds_read of the phase's operands
+//     -- s_barrier --  M: 16 MFMA (setprio 1)  -- s_barrier --
+// so a SIMD's leading wave issues its MFMAs while its trailing wave reads, and the other way round.
+// Phases of a 64-deep k-step (rh = 64-row half of the wave tile, h = 32-deep k-half):
+//     (rh0, h0): A 4 + W 4 reads; (rh1, h0): A 4; (rh1, h1): A 4 + W 4; (rh0, h1): A 4
+// so every LDS byte is read once per wave and the h0 half of a k-step is free after its second phase.
+// LDS: a ring of 4 k-half slots (A [256][32] + W [256][32] fp16, 64-B rows, 32 KiB each; 16-B chunk c of
+// row r at c ^ (-(r >> 2) & 3), conflict-free for the ds_read_b128 lane groups of MI355X_MICROARCH.md) plus
+// two 1 KiB bias slots.  Half v (the block's halves in (tile, k) order) is read in phases 2v, 2v + 1.
+// Global phase q: the leading group's R(q) lies between barriers 2q - 1 and 2q, the trailing group's between
+// 2q and 2q + 1, and every wave's reads of phase q are consumed by its MFMAs before barrier 2q + 2.  So
+//   * half v's A rows are DMA'd in R(2v - 5), its W rows in R(2v - 4): after barrier 4v - 12, by which every
+//     read of half v - 4 (same slot) is done;
+//   * R(2v - 1) waits vmcnt(4) (half v + 1's 4 instructions may pend) before barrier 4v - 2 / 4v - 1, and
+//     half v is first read in R(2v), after barrier 4v - 1 / 4v.
+// A tile's epilogue is split over the next tile's first two R segments (rows rh0 before the MFMAs that
+// overwrite acc[0..3], rh1 before acc[4..7]), so one group's stores overlap the other's MFMAs; their 16 + 16
+// stores per wave stay in flight: the following odd waits count 20, then 36 (VMEM retires in issue order;
+// a wait may count fewer operations than were issued after its target, never more - so extra operations
+// such as the RES residual loads or wave 0's bias DMA only make it conservative).  A ragged last row band
+// skips stores, so its successors count 4.  RES issues each half's residual loads before the segment's DMA
+// instructions (the compiler's wait for them then leaves the fresh DMA in flight).
+// Measured (tools/f16q_check.sh, tools build, ICAP_F16_PP=1): correct - all GPU tests pass with it - but slower
+// than gemm_f16p_kernel: QKV 258 -> 305 us, MLP-1 356 -> 457, MLP-2 324 -> 402, encoder 15.2 -> 17.8 ms/step.
+// The k-loop is not held by LDS latency: gemm_f16p_kernel's timing ablations (tools/f16_ablate.sh) put its DMA
+// alone and its LDS reads + MFMAs alone at ~200 us each for QKV, and here the 64-B k-half rows double the
+// cache-line requests of every DMA instruction.  Kept in the tools build only.
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void gemm_f16q_kernel(GemmArgs p) {
+  constexpr bool SO = MODE == 1, RES = MODE == 2;
+  static_assert(SO || RES, "store-only or residual epilogue");
+  constexpr int BM = 256, BN = 256, WM = 128, WN = 64, TN = 4;
+  constexpr int SLOT = 32768, OPH = 16384;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
+  const int xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int xbase = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8, xcnt = q8 + (xcd < r8);
+  const int nbx = ((int)gridDim.x - xcd + 7) >> 3, lb = blockIdx.x >> 3;
+  if (lb >= xcnt) return;
+  const int M = p.M, hpt = p.K / 32;            // k-halves per tile (even, >= 4)
+  const int ntl = (xcnt - lb + nbx - 1) / nbx;  // tiles xbase + lb + j nbx, j < ntl
+  const int nh = ntl * hpt;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int schunk = (lane & 3) ^ ((4 - (lane >> 4)) & 3);  // DMA lane: row lane >> 2 of a 16-row block
+  const int fsw = (fq ^ ((4 - (fr >> 2)) & 3)) << 4;         // fragment lane: row fr of a 16-row tile
+  float* sbias = (float*)(smem + 4 * SLOT);
+
+  auto tile_of = [&](int j) { return xbase + lb + j * nbx; };
+  auto stage = [&](int v, int part) {  // half v, part 0 = its A rows, 1 = its W rows: 2 instructions per wave
+    const int j = v / hpt, hh = v - j * hpt, t = tile_of(j);
+    const int bm = t / nbn, bn = t - bm * nbn;
+    char* dst = smem + (v & 3) * SLOT + part * OPH + wave * 2048;
+    const int r0 = wave * 32 + (lane >> 2);
+    if (part == 0) {
+      const bf16_t* src = p.A + hh * 32 + schunk * 8;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(src + (long)min(bm * BM + r0 + i * 16, M - 1) * p.lda),
+                                         (LDS_AS void*)(dst + i * 1024), 16, 0, 0);
+    } else {
+      const bf16_t* src = p.W + (long)(bn * BN + r0) * p.ldw + hh * 32 + schunk * 8;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(src + (long)i * 16 * p.ldw),
+                                         (LDS_AS void*)(dst + i * 1024), 16, 0, 0);
+    }
+  };
+  auto load_bias = [&](int j) {  // tile j's 256 bias values -> bias slot j & 1 (wave 0, one DMA instruction)
+    if (wave == 0 && p.bias) {
+      const int t = tile_of(j), n0 = (t - (t / nbn) * nbn) * BN;
+      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(p.bias + n0 + lane * 4),
+                                       (LDS_AS void*)(sbias + (j & 1) * 256), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][TN];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 rv[4][TN];  // RES: one row half of the residual
+  // tile je's rows of half rh: RES loads (issued before the segment's DMA), then bias (+ GELU) and stores
+  auto epi_load = [&](int je, int rh) {
+    if constexpr (RES) {
+      const int t = tile_of(je), bm = t / nbn, bn = t - bm * nbn;
+      const int mb = bm * BM + wm * WM, nb = bn * BN + wn * WN;
+      const float* Cb = (const float*)p.C + nb + 4 * fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          rv[i][j] = *(const f32x4*)(Cb + (long)min(mb + (rh * 4 + i) * 16 + fr, M - 1) * p.ldc + j * 16);
+    }
+  };
+  auto epi_store = [&](int je, int rh) {
+    const int t = tile_of(je), bm = t / nbn, bn = t - bm * nbn;
+    const int mb = bm * BM + wm * WM, nb = bn * BN + wn * WN;
+    const bool tail = bm * BM + BM > M;
+    const float* bl = sbias + (je & 1) * 256 + wn * WN + 4 * fq;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ii = rh * 4 + i, mr = mb + ii * 16 + fr;
+      if constexpr (SO) {
+        const int m = min(mr, M - 1);
+        const long orow = p.hm_n ? (((long)(m / p.hm_n) * (p.N / 64) + nb / 64) * p.hm_n + m % p.hm_n) * 64 - nb
+                                 : (long)m * p.ldc;
+        bf16_t* C = (bf16_t*)p.C + orow + 4 * fq;
+        const bool ok = !tail || mr < M;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          f32x4 v = acc[ii][j];
+          if (p.bias) v += *(const f32x4*)(bl + j * 16);
+          if (p.epi == EPI_GELU) {
+            const f32x2 lo = gelu_erf_fast2((f32x2){v[0], v[1]}), hi = gelu_erf_fast2((f32x2){v[2], v[3]});
+            v = (f32x4){lo[0], lo[1], hi[0], hi[1]};
+          }
+          if (ok) *(u32x2*)(C + nb + j * 16) = pack16x4<true>(v);
+        }
+      } else {
+        float* Cb = (float*)p.C + nb + 4 * fq;
+        if (!tail || mr < M) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            f32x4 a = acc[ii][j];
+            if (p.bias) a += *(const f32x4*)(bl + j * 16);
+            *(f32x4*)(Cb + (long)mr * p.ldc + j * 16) = rv[i][j] + a;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[ii][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    return tail;
+  };
+
+  // prologue: halves 0 and 1 and half 2's A rows in flight, half 0 retired
+  load_bias(0);
+  stage(0, 0);
+  stage(0, 1);
+  stage(1, 0);
+  stage(1, 1);
+  stage(2, 0);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wm) __builtin_amdgcn_s_barrier();  // the trailing group runs one barrier behind
+  asm volatile("" ::: "memory");
+
+  bf16x8 af[4], bfr[4];
+  const int nsteps = nh >> 1, kspt = hpt >> 1;  // 64-deep k-steps: in total, per tile
+  int ec = 0;        // odd-phase waits left that count the previous tile's epilogue stores (20, then 36)
+  int je = -1;       // tile whose epilogue runs in this k-step's first two R segments (-1: none)
+  int kt = 0, j = 0;  // k-step within tile j
+  for (int s = 0; s < nsteps; ++s) {
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int q = 4 * s + ph, h = ph >> 1, rh = (ph == 1 || ph == 2) ? 1 : 0;
+      // ---- R segment
+      if (ph & 1) {
+        if ((q + 3) / 2 < nh) {  // half (q + 1) / 2 retired; half (q + 3) / 2 (+ epilogue stores) may pend
+          if (ec == 2) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+          else if (ec == 1) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (ec) --ec;
+      }
+      if (ph <= 1 && je >= 0) epi_load(je, ph);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ph & 1) {
+        const int vs = (q + 5) / 2;
+        if (vs < nh) {
+          if (vs % hpt == 0) load_bias(vs / hpt);
+          stage(vs, 0);
+        }
+      } else {
+        const int vs = (q + 4) / 2;
+        if (vs < nh) stage(vs, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (ph <= 1 && je >= 0) {
+        const bool tail = epi_store(je, ph);
+        if (ph == 0) ec = tail ? 0 : 2;
+        else je = -1;
+      }
+      const char* sb = smem + ((2 * s + h) & 3) * SLOT;
+      if (ph == 0 || ph == 2) {
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) bfr[jj] = *(const bf16x8*)(sb + OPH + (wn * WN + jj * 16 + fr) * 64 + fsw);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(sb + (wm * WM + rh * 64 + i * 16 + fr) * 64 + fsw);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- M segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) acc[rh * 4 + i][jj] = mma<true>(bfr[jj], af[i], acc[rh * 4 + i][jj]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (++kt == kspt) {  // tile j done: its epilogue runs in the next k-step's first two R segments
+      kt = 0;
+      je = j++;
+    }
+  }
+  // the last tile: the leading group matches the trailing group's extra barrier first
+  if (!wm) __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  epi_load(je, 0);
+  epi_store(je, 0);
+  epi_load(je, 1);
+  epi_store(je, 1);
+}
+
+#endif  // ICAP_TOOLS
 
 }  // namespace
 
@@ -1397,9 +1636,44 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
                               (const void*)gemm_f16p_kernel<2>})
           if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048) != hipSuccess)
             return hipErrorInvalidValue;
+#ifdef ICAP_TOOLS
+        for (const void* f : {(const void*)gemm_f16q_kernel<1>, (const void*)gemm_f16q_kernel<2>})
+          if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 32 * 1024 + 2048) != hipSuccess)
+            return hipErrorInvalidValue;
+#endif
       }
       const int tiles = (g.N / 256) * ((g.M + 255) / 256);
       const dim3 grid(std::min(tiles, cus));
+#ifdef ICAP_TOOLS
+      // ICAP_F16P_ABL (tools): gemm_f16p_kernel without its k-loop DMA (1) or without its MFMAs (2) - wrong
+      // results, timing only (tools/f16_ablate.sh)
+      static const int abl = icap_knob("ICAP_F16P_ABL", 0);
+      if (so && (abl == 1 || abl == 2)) {
+        static bool attr = false;
+        if (!attr) {
+          for (const void* f : {(const void*)gemm_f16p_kernel<1, 1>, (const void*)gemm_f16p_kernel<2, 1>,
+                                (const void*)gemm_f16p_kernel<1, 2>, (const void*)gemm_f16p_kernel<2, 2>})
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048) != hipSuccess)
+              return hipErrorInvalidValue;
+          attr = true;
+        }
+        const bool res = g.out == OUT_F32_RESID;
+        if (abl == 1 && res) hipLaunchKernelGGL((gemm_f16p_kernel<2, 1>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else if (abl == 1) hipLaunchKernelGGL((gemm_f16p_kernel<1, 1>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else if (res) hipLaunchKernelGGL((gemm_f16p_kernel<2, 2>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else hipLaunchKernelGGL((gemm_f16p_kernel<1, 2>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        return hipGetLastError();
+      }
+      // ICAP_F16_PP=1 (tools): the ping-pong k-loop (gemm_f16q_kernel; slower)
+      static const int pp = icap_knob("ICAP_F16_PP", 0);
+      if (so && pp) {
+        if (g.out == OUT_F32_RESID)
+          hipLaunchKernelGGL(gemm_f16q_kernel<2>, grid, dim3(512), 4 * 32 * 1024 + 2048, s, g);
+        else
+          hipLaunchKernelGGL(gemm_f16q_kernel<1>, grid, dim3(512), 4 * 32 * 1024 + 2048, s, g);
+        return hipGetLastError();
+      }
+#endif
       if (so && g.out == OUT_F32_RESID)
         hipLaunchKernelGGL(gemm_f16p_kernel<2>, grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
       else if (so)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# persistent fp16 GEMM with the stage DMA spread over the k-step: GEMM op + stress tests (product build), then
+# (tools build) the four ViT shapes and the headline bench, spread (ABL 0) against one burst per stage (ABL 3).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r2
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -m gpu -x -q -k "gemm_f16" --timeout 200 --timeout-method thread > gpurun_out/r2/f16s_tests.log 2>&1 || { tail -30 gpurun_out/r2/f16s_tests.log; exit 1; }
+tail -1 gpurun_out/r2/f16s_tests.log
+timeout -k 10 400 python -m image_caption_amd.build --tools > gpurun_out/r2/ab_build.log 2>&1 || { tail -5 gpurun_out/r2/ab_build.log; exit 1; }
+for a in 0 3; do
+  echo "== ICAP_F16P_ABL=$a"
+  ICAP_F16P_ABL=$a timeout -k 10 120 python tools/gemm_f16.py 20 2>&1 | grep -v amdgpu.ids || exit 1
+done
+for a in 0 3 0 3; do
+  echo "== ICAP_F16P_ABL=$a"
+  ICAP_F16P_ABL=$a timeout -k 10 150 python bench.py --no-cpu-baseline --steps 10 --warmup 2 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); p=d["roofline"]["phases"]; print(d["value"], d["ms_per_step"], p["encoder"]["ms_per_step"], p["decode"]["ms_per_step"])' || exit 1
+done
