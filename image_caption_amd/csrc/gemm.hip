@@ -1011,12 +1011,16 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // next tile's stage 0 is in flight behind the last k-step, its stage 1 is issued after the epilogue's stores
 // (the residual loads' waits would otherwise wait for it), and k-step 0 needs no vmcnt wait: the residual loads
 // retired after stage 0 (in order).
-// ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh)
-template <int MODE, int ABL = 0>
+// ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh).
+// BMT: tile rows, 256 or (RES) 224 - wave tiles 112 x 64, the A stage 224 rows (wave 7 DMAs W rows only): at
+// N = 768 the 256-row tiles are 591 = 2.3 per CU (3 rounds, the last 30 % full), 224-row tiles 678 = 2.65 per CU
+// (3 rounds of 7/8 the work).
+template <int MODE, int ABL = 0, int BMT = 256>
 __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   constexpr bool SO = MODE == 1, RES = MODE == 2;
-  constexpr int BM = 256, BN = 256, KS = 64, NW = 8, WM = 128, WN = 64, TM = 8, TN = 4;
-  constexpr int OPB = BM * KS * 2, STAGE = 2 * OPB;  // A 32 KiB + W 32 KiB
+  static_assert(BMT == 256 || (RES && BMT == 224), "224-row tiles only for the residual form (no counted waits)");
+  constexpr int BM = BMT, BN = 256, KS = 64, NW = 8, WM = BM / 2, WN = 64, TM = WM / 16, TN = 4;
+  constexpr int OPA = BM * KS * 2, OPB = BN * KS * 2, STAGE = OPA + OPB;  // A 32 (28) KiB + W 32 KiB
   constexpr int IPW = OPB / 1024 / NW;                // 4 DMA instructions per wave per operand
   constexpr int PER_STAGE = 2 * IPW;                  // 8 per wave per stage
   constexpr int NSTORE = TM * TN;                     // 32 fp16 stores per wave per tile (SO)
@@ -1039,6 +1043,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
     const bf16_t* Wb = p.W + (long)(n0 + srow) * p.ldw + kt * KS + schunk * 8;
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
+      if (BM < 256 && (wave * IPW + i) * 8 >= BM) break;  // (wave-uniform) rows past the tile's A image
       const int row = min(m0 + srow + i * 8, M - 1);
       __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(Ab + (long)row * p.lda),
                                        (LDS_AS void*)(s0 + (wave * IPW + i) * 1024), 16, 0, 0);
@@ -1046,7 +1051,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < IPW; ++i)
       __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(Wb + (long)i * 8 * p.ldw),
-                                       (LDS_AS void*)(s0 + OPB + (wave * IPW + i) * 1024), 16, 0, 0);
+                                       (LDS_AS void*)(s0 + OPA + (wave * IPW + i) * 1024), 16, 0, 0);
   };
   // SO: the tile's 256 bias values go to LDS slot (tile count & 1) by one DMA instruction of wave 0, issued
   // before the tile's first stage (so the counted waits below never count it) - no registers held across
@@ -1092,7 +1097,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         const int fo = fr * 128 + (((ks * 4 + fq) ^ (fr & 7)) << 4);
         bf16x8 bfr[TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + OPB + (wn * WN + j * 16) * 128 + fo);
+        for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const bf16x8 af = *(const bf16x8*)(s0 + (wm * WM + i * 16) * 128 + fo);
@@ -1138,15 +1143,17 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       const float* bl = sbias + (tcount & 1) * 256 + wn * WN + 4 * fq;
       const bool tail = bm * BM + BM > M;  // ragged last row band: rows >= M neither read nor stored
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
+      for (int h2 = 0; h2 < 2; ++h2) {  // row tiles [4 h2, min(TM, 4 h2 + 4))
         f32x4 rv[4][TN];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            rv[i][j] = *(const f32x4*)(Cb + (long)min(mb + (h2 * 4 + i) * 16 + fr, M - 1) * p.ldc + j * 16);
+            if (h2 * 4 + i < TM)
+              rv[i][j] = *(const f32x4*)(Cb + (long)min(mb + (h2 * 4 + i) * 16 + fr, M - 1) * p.ldc + j * 16);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+          if (h2 * 4 + i >= TM) break;
           const int m = mb + (h2 * 4 + i) * 16 + fr;
           if (tail && m >= M) continue;
 #pragma unroll
@@ -1633,7 +1640,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
           return hipErrorInvalidValue;
         for (const void* f : {(const void*)gemm_f16p_kernel<0>, (const void*)gemm_f16p_kernel<1>,
-                              (const void*)gemm_f16p_kernel<2>})
+                              (const void*)gemm_f16p_kernel<2>, (const void*)gemm_f16p_kernel<2, 0, 224>})
           if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048) != hipSuccess)
             return hipErrorInvalidValue;
 #ifdef ICAP_TOOLS
@@ -1644,6 +1651,14 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       }
       const int tiles = (g.N / 256) * ((g.M + 255) / 256);
       const dim3 grid(std::min(tiles, cus));
+      // residual GEMMs: 224-row tiles (ICAP_F16_RES_BM=256 in the tools build: the 256-row form)
+      static const int res_bm = icap_knob("ICAP_F16_RES_BM", 224);
+      if (so && g.out == OUT_F32_RESID && res_bm == 224) {
+        const int tiles224 = (g.N / 256) * ((g.M + 223) / 224);
+        hipLaunchKernelGGL((gemm_f16p_kernel<2, 0, 224>), dim3(std::min(tiles224, cus)), dim3(512),
+                           2 * (224 * 128 + 256 * 128) + 2048, s, g);
+        return hipGetLastError();
+      }
 #ifdef ICAP_TOOLS
       // ICAP_F16P_ABL (tools): gemm_f16p_kernel without its k-loop DMA (1) or without its MFMAs (2) - wrong
       // results, timing only (tools/f16_ablate.sh)
