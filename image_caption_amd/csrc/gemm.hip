@@ -1011,13 +1011,15 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // next tile's stage 0 is in flight behind the last k-step, its stage 1 is issued after the epilogue's stores
 // (the residual loads' waits would otherwise wait for it), and k-step 0 needs no vmcnt wait: the residual loads
 // retired after stage 0 (in order).
-// ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh).
+// ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh); 3 = the
+// compiler's own fragment-read order, 4 = A fragments read 3 ahead instead of 2.
 // BMT: tile rows, 256 or (RES) 224 - wave tiles 112 x 64, the A stage 224 rows (wave 7 DMAs W rows only): at
 // N = 768 the 256-row tiles are 591 = 2.3 per CU (3 rounds, the last 30 % full), 224-row tiles 678 = 2.65 per CU
 // (3 rounds of 7/8 the work).
 template <int MODE, int ABL = 0, int BMT = 256>
 __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   constexpr bool SO = MODE == 1, RES = MODE == 2;
+  constexpr int PF = ABL == 0 ? 2 : (ABL == 4 ? 3 : 0);  // A-fragment read distance (0: the compiler's order)
   static_assert(BMT == 256 || (RES && BMT == 224), "224-row tiles only for the residual form (no counted waits)");
   constexpr int BM = BMT, BN = 256, KS = 64, NW = 8, WM = BM / 2, WN = 64, TM = WM / 16, TN = 4;
   constexpr int OPA = BM * KS * 2, OPB = BN * KS * 2, STAGE = OPA + OPB;  // A 32 (28) KiB + W 32 KiB
@@ -1098,12 +1100,28 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         bf16x8 bfr[TN];
 #pragma unroll
         for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo);
+        if constexpr (PF > 0) {
+          // A fragments read PF ahead of their MFMAs, the order pinned (the compiler's own order reads 2, waits
+          // for both, runs 8): QKV 265 -> 256 us, MLP-2 302 -> 285 us (tools/f16_pf.sh)
+          bf16x8 a[TM];
+#pragma unroll
+          for (int i = 0; i < PF; ++i) a[i] = *(const bf16x8*)(s0 + (wm * WM + i * 16) * 128 + fo);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            if (i + PF < TM) a[i + PF] = *(const bf16x8*)(s0 + (wm * WM + (i + PF) * 16) * 128 + fo);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mma<true>(bfr[j], a[i], acc[i][j]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          continue;
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const bf16x8 af = *(const bf16x8*)(s0 + (wm * WM + i * 16) * 128 + fo);
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
-            if (ABL == 2) asm volatile("" ::"v"(bfr[j]), "v"(af));
+            if (ABL == 2) asm volatile("" ::"v"(bfr[j]), "v"(af));  // (PF = 0 for the ablations)
             else acc[i][j] = mma<true>(bfr[j], af, acc[i][j]);
           }
         }
@@ -1651,23 +1669,17 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       }
       const int tiles = (g.N / 256) * ((g.M + 255) / 256);
       const dim3 grid(std::min(tiles, cus));
-      // residual GEMMs: 224-row tiles (ICAP_F16_RES_BM=256 in the tools build: the 256-row form)
-      static const int res_bm = icap_knob("ICAP_F16_RES_BM", 224);
-      if (so && g.out == OUT_F32_RESID && res_bm == 224) {
-        const int tiles224 = (g.N / 256) * ((g.M + 223) / 224);
-        hipLaunchKernelGGL((gemm_f16p_kernel<2, 0, 224>), dim3(std::min(tiles224, cus)), dim3(512),
-                           2 * (224 * 128 + 256 * 128) + 2048, s, g);
-        return hipGetLastError();
-      }
 #ifdef ICAP_TOOLS
       // ICAP_F16P_ABL (tools): gemm_f16p_kernel without its k-loop DMA (1) or without its MFMAs (2) - wrong
-      // results, timing only (tools/f16_ablate.sh)
+      // results, timing only (tools/f16_ablate.sh); 3 / 4: the compiler's fragment-read order / reads 3 ahead
       static const int abl = icap_knob("ICAP_F16P_ABL", 0);
-      if (so && (abl == 1 || abl == 2)) {
+      if (so && abl >= 1 && abl <= 4) {
         static bool attr = false;
         if (!attr) {
           for (const void* f : {(const void*)gemm_f16p_kernel<1, 1>, (const void*)gemm_f16p_kernel<2, 1>,
-                                (const void*)gemm_f16p_kernel<1, 2>, (const void*)gemm_f16p_kernel<2, 2>})
+                                (const void*)gemm_f16p_kernel<1, 2>, (const void*)gemm_f16p_kernel<2, 2>,
+                                (const void*)gemm_f16p_kernel<1, 3>, (const void*)gemm_f16p_kernel<2, 3, 224>,
+                                (const void*)gemm_f16p_kernel<1, 4>, (const void*)gemm_f16p_kernel<2, 4, 224>})
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048) != hipSuccess)
               return hipErrorInvalidValue;
           attr = true;
@@ -1675,8 +1687,16 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
         const bool res = g.out == OUT_F32_RESID;
         if (abl == 1 && res) hipLaunchKernelGGL((gemm_f16p_kernel<2, 1>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
         else if (abl == 1) hipLaunchKernelGGL((gemm_f16p_kernel<1, 1>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
-        else if (res) hipLaunchKernelGGL((gemm_f16p_kernel<2, 2>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
-        else hipLaunchKernelGGL((gemm_f16p_kernel<1, 2>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else if (abl == 2 && res) hipLaunchKernelGGL((gemm_f16p_kernel<2, 2>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else if (abl == 2) hipLaunchKernelGGL((gemm_f16p_kernel<1, 2>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else if (res && abl == 3)
+          hipLaunchKernelGGL((gemm_f16p_kernel<2, 3, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
+                             dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
+        else if (res)
+          hipLaunchKernelGGL((gemm_f16p_kernel<2, 4, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
+                             dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
+        else if (abl == 3) hipLaunchKernelGGL((gemm_f16p_kernel<1, 3>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else hipLaunchKernelGGL((gemm_f16p_kernel<1, 4>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
         return hipGetLastError();
       }
       // ICAP_F16_PP=1 (tools): the ping-pong k-loop (gemm_f16q_kernel; slower)
@@ -1689,6 +1709,14 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
         return hipGetLastError();
       }
 #endif
+      // residual GEMMs: 224-row tiles (ICAP_F16_RES_BM=256 in the tools build: the 256-row form)
+      static const int res_bm = icap_knob("ICAP_F16_RES_BM", 224);
+      if (so && g.out == OUT_F32_RESID && res_bm == 224) {
+        const int tiles224 = (g.N / 256) * ((g.M + 223) / 224);
+        hipLaunchKernelGGL((gemm_f16p_kernel<2, 0, 224>), dim3(std::min(tiles224, cus)), dim3(512),
+                           2 * (224 * 128 + 256 * 128) + 2048, s, g);
+        return hipGetLastError();
+      }
       if (so && g.out == OUT_F32_RESID)
         hipLaunchKernelGGL(gemm_f16p_kernel<2>, grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
       else if (so)
