@@ -1012,14 +1012,19 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // (the residual loads' waits would otherwise wait for it), and k-step 0 needs no vmcnt wait: the residual loads
 // retired after stage 0 (in order).
 // ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh); 3 = the
-// compiler's own fragment-read order, 4 = A fragments read 3 ahead instead of 2.
+// compiler's own fragment-read order, 4 = the read pipeline per k-half.
 // BMT: tile rows, 256 or (RES) 224 - wave tiles 112 x 64, the A stage 224 rows (wave 7 DMAs W rows only): at
 // N = 768 the 256-row tiles are 591 = 2.3 per CU (3 rounds, the last 30 % full), 224-row tiles 678 = 2.65 per CU
 // (3 rounds of 7/8 the work).
 template <int MODE, int ABL = 0, int BMT = 256>
 __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   constexpr bool SO = MODE == 1, RES = MODE == 2;
-  constexpr int PF = ABL == 0 ? 2 : (ABL == 4 ? 3 : 0);  // A-fragment read distance (0: the compiler's order)
+  // fragment reads: ABL 0 = one pipeline over the k-step's 16 A fragments, each read 2 MFMA groups ahead (the
+  // second k-half's W fragments with the read 2 ahead of its first group); 4 = the same per k-half (PF = 2);
+  // 3 and the ablations = the compiler's order (reads 2, waits for both, runs 8).  Per ViT layer 1039 -> 1013
+  // (per k-half) -> 997 us (tools/f16_pf.sh)
+  constexpr int PF = ABL == 4 ? 2 : 0;
+  constexpr bool XK = ABL == 0;
   static_assert(BMT == 256 || (RES && BMT == 224), "224-row tiles only for the residual form (no counted waits)");
   constexpr int BM = BMT, BN = 256, KS = 64, NW = 8, WM = BM / 2, WN = 64, TM = WM / 16, TN = 4;
   constexpr int OPA = BM * KS * 2, OPB = BN * KS * 2, STAGE = OPA + OPB;  // A 32 (28) KiB + W 32 KiB
@@ -1094,6 +1099,28 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         if (ABL != 1) stage(tn, 0, (step + 1) & 1);
       }
       const char* s0 = smem + (step & 1) * STAGE;
+      if constexpr (XK) {
+        const int fo0 = fr * 128 + ((fq ^ (fr & 7)) << 4), fo1 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
+        bf16x8 b2[2][TN], a2[2 * TM];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b2[0][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo0);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) a2[g] = *(const bf16x8*)(s0 + (wm * WM + g * 16) * 128 + fo0);
+#pragma unroll
+        for (int g = 0; g < 2 * TM; ++g) {
+          const int nx = g + 2;
+          if (nx == TM) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) b2[1][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo1);
+          }
+          if (nx < 2 * TM) a2[nx] = *(const bf16x8*)(s0 + (wm * WM + (nx % TM) * 16) * 128 + (nx < TM ? fo0 : fo1));
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[g % TM][j] = mma<true>(b2[g / TM][j], a2[g], acc[g % TM][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        continue;
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int fo = fr * 128 + (((ks * 4 + fq) ^ (fr & 7)) << 4);
@@ -1101,8 +1128,6 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo);
         if constexpr (PF > 0) {
-          // A fragments read PF ahead of their MFMAs, the order pinned (the compiler's own order reads 2, waits
-          // for both, runs 8): QKV 265 -> 256 us, MLP-2 302 -> 285 us (tools/f16_pf.sh)
           bf16x8 a[TM];
 #pragma unroll
           for (int i = 0; i < PF; ++i) a[i] = *(const bf16x8*)(s0 + (wm * WM + i * 16) * 128 + fo);
@@ -1671,7 +1696,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       const dim3 grid(std::min(tiles, cus));
 #ifdef ICAP_TOOLS
       // ICAP_F16P_ABL (tools): gemm_f16p_kernel without its k-loop DMA (1) or without its MFMAs (2) - wrong
-      // results, timing only (tools/f16_ablate.sh); 3 / 4: the compiler's fragment-read order / reads 3 ahead
+      // results, timing only (tools/f16_ablate.sh); 3 / 4: the compiler's fragment-read order / the read pipeline per k-half
       static const int abl = icap_knob("ICAP_F16P_ABL", 0);
       if (so && abl >= 1 && abl <= 4) {
         static bool attr = false;

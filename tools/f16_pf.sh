@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r2
 timeout -k 10 400 python -m image_caption_amd.build --tools > gpurun_out/r2/ab_build.log 2>&1 || { tail -5 gpurun_out/r2/ab_build.log; exit 1; }
-for a in 0 3 4 0; do
+for a in ${ABLS:-0 3 4 0}; do
   echo "== ICAP_F16P_ABL=$a"
   ICAP_F16P_ABL=$a timeout -k 10 120 python tools/gemm_f16.py 20 2>&1 | grep -v amdgpu.ids | cut -c1-60 || exit 1
 done
