@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // (the residual loads' waits would otherwise wait for it), and k-step 0 needs no vmcnt wait: the residual loads
 // retired after stage 0 (in order).
 // ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh); 3 = the
-// compiler's own fragment-read order, 4 = the read pipeline per k-half.
+// compiler's own fragment-read order, 4 = the read pipeline per k-half, 5 = the stage DMA before the first reads.
 // BMT: tile rows, 256 or (RES) 224 - wave tiles 112 x 64, the A stage 224 rows (wave 7 DMAs W rows only): at
 // N = 768 the 256-row tiles are 591 = 2.3 per CU (3 rounds, the last 30 % full), 224-row tiles 678 = 2.65 per CU
 // (3 rounds of 7/8 the work).
@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   // 3 and the ablations = the compiler's order (reads 2, waits for both, runs 8).  Per ViT layer 1039 -> 1013
   // (per k-half) -> 997 us (tools/f16_pf.sh)
   constexpr int PF = ABL == 4 ? 2 : 0;
-  constexpr bool XK = ABL == 0;
+  constexpr bool XK = ABL == 0 || ABL == 5, XK_LATE = ABL == 0;
   static_assert(BMT == 256 || (RES && BMT == 224), "224-row tiles only for the residual form (no counted waits)");
   constexpr int BM = BMT, BN = 256, KS = 64, NW = 8, WM = BM / 2, WN = 64, TM = WM / 16, TN = 4;
   constexpr int OPA = BM * KS * 2, OPB = BN * KS * 2, STAGE = OPA + OPB;  // A 32 (28) KiB + W 32 KiB
@@ -1090,14 +1090,19 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       else if (RES && seam && kt == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      int st_t = -1, st_kt = 0;  // the stage this k-step DMAs into the other buffer (-1: none)
       if ((SO || RES) && seam && kt == 0) {
         // stage 1 of this tile is already in flight
       } else if (kt + 1 < nk) {
-        if (ABL != 1) stage(t, kt + 1, (step + 1) & 1);
+        st_t = t, st_kt = kt + 1;
       } else if (tn >= 0) {  // the next tile's bias, then its first stage, behind this k-step's MFMAs
         if (SO || RES) load_bias(tn, (tcount + 1) & 1);
-        if (ABL != 1) stage(tn, 0, (step + 1) & 1);
+        st_t = tn;
       }
+      if (ABL == 1) st_t = -1;
+      // XK (default): the k-step's first fragment reads go out before the stage's 8 DMA instructions, whose
+      // issue then covers their latency (ABL 5: DMA first)
+      if (!XK_LATE && st_t >= 0) stage(st_t, st_kt, (step + 1) & 1);
       const char* s0 = smem + (step & 1) * STAGE;
       if constexpr (XK) {
         const int fo0 = fr * 128 + ((fq ^ (fr & 7)) << 4), fo1 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
@@ -1106,6 +1111,11 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         for (int j = 0; j < TN; ++j) b2[0][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo0);
 #pragma unroll
         for (int g = 0; g < 2; ++g) a2[g] = *(const bf16x8*)(s0 + (wm * WM + g * 16) * 128 + fo0);
+        if constexpr (XK_LATE) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (st_t >= 0) stage(st_t, st_kt, (step + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int g = 0; g < 2 * TM; ++g) {
           const int nx = g + 2;
@@ -1696,15 +1706,17 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       const dim3 grid(std::min(tiles, cus));
 #ifdef ICAP_TOOLS
       // ICAP_F16P_ABL (tools): gemm_f16p_kernel without its k-loop DMA (1) or without its MFMAs (2) - wrong
-      // results, timing only (tools/f16_ablate.sh); 3 / 4: the compiler's fragment-read order / the read pipeline per k-half
+      // results, timing only (tools/f16_ablate.sh); 3 / 4 / 5: the compiler's fragment-read order / the read pipeline per k-half / the stage's DMA
+      // before the first fragment reads
       static const int abl = icap_knob("ICAP_F16P_ABL", 0);
-      if (so && abl >= 1 && abl <= 4) {
+      if (so && abl >= 1 && abl <= 5) {
         static bool attr = false;
         if (!attr) {
           for (const void* f : {(const void*)gemm_f16p_kernel<1, 1>, (const void*)gemm_f16p_kernel<2, 1>,
                                 (const void*)gemm_f16p_kernel<1, 2>, (const void*)gemm_f16p_kernel<2, 2>,
                                 (const void*)gemm_f16p_kernel<1, 3>, (const void*)gemm_f16p_kernel<2, 3, 224>,
-                                (const void*)gemm_f16p_kernel<1, 4>, (const void*)gemm_f16p_kernel<2, 4, 224>})
+                                (const void*)gemm_f16p_kernel<1, 4>, (const void*)gemm_f16p_kernel<2, 4, 224>,
+                                (const void*)gemm_f16p_kernel<1, 5>, (const void*)gemm_f16p_kernel<2, 5, 224>})
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048) != hipSuccess)
               return hipErrorInvalidValue;
           attr = true;
@@ -1717,11 +1729,15 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
         else if (res && abl == 3)
           hipLaunchKernelGGL((gemm_f16p_kernel<2, 3, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
                              dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
-        else if (res)
+        else if (res && abl == 4)
           hipLaunchKernelGGL((gemm_f16p_kernel<2, 4, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
                              dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
+        else if (res)
+          hipLaunchKernelGGL((gemm_f16p_kernel<2, 5, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
+                             dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
         else if (abl == 3) hipLaunchKernelGGL((gemm_f16p_kernel<1, 3>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
-        else hipLaunchKernelGGL((gemm_f16p_kernel<1, 4>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else if (abl == 4) hipLaunchKernelGGL((gemm_f16p_kernel<1, 4>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else hipLaunchKernelGGL((gemm_f16p_kernel<1, 5>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
         return hipGetLastError();
       }
       // ICAP_F16_PP=1 (tools): the ping-pong k-loop (gemm_f16q_kernel; slower)
