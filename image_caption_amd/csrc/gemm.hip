@@ -1012,19 +1012,23 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // (the residual loads' waits would otherwise wait for it), and k-step 0 needs no vmcnt wait: the residual loads
 // retired after stage 0 (in order).
 // ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh); 3 = the
-// compiler's own fragment-read order, 4 = the read pipeline per k-half, 5 = the stage DMA before the first reads.
+// compiler's own fragment-read order, 4 = the read pipeline per k-half, 5 = the stage DMA before the first reads,
+// 6 = reads 3 groups ahead instead of 2 (within box noise, tools/f16x3_check.sh), 7 = s_setprio(1) around each
+// MFMA group (no gain, tools/f16_pf.sh).
 // BMT: tile rows, 256 or (RES) 224 - wave tiles 112 x 64, the A stage 224 rows (wave 7 DMAs W rows only): at
 // N = 768 the 256-row tiles are 591 = 2.3 per CU (3 rounds, the last 30 % full), 224-row tiles 678 = 2.65 per CU
 // (3 rounds of 7/8 the work).
 template <int MODE, int ABL = 0, int BMT = 256>
 __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   constexpr bool SO = MODE == 1, RES = MODE == 2;
-  // fragment reads: ABL 0 = one pipeline over the k-step's 16 A fragments, each read 2 MFMA groups ahead (the
-  // second k-half's W fragments with the read 2 ahead of its first group); 4 = the same per k-half (PF = 2);
+  // fragment reads: ABL 0 = one pipeline over the k-step's 16 A fragments, each read XD MFMA groups ahead (the
+  // second k-half's W fragments with the read XD ahead of its first group); 4 = per k-half (PF = 2);
   // 3 and the ablations = the compiler's order (reads 2, waits for both, runs 8).  Per ViT layer 1039 -> 1013
   // (per k-half) -> 997 us (tools/f16_pf.sh)
   constexpr int PF = ABL == 4 ? 2 : 0;
-  constexpr bool XK = ABL == 0 || ABL == 5, XK_LATE = ABL == 0;
+  constexpr bool XK = ABL == 0 || ABL >= 5, XK_LATE = ABL == 0 || ABL >= 6;
+  constexpr int XD = ABL == 6 ? 3 : 2;  // XK read distance in MFMA groups (tools: 6 = 3 - within noise of 2)
+  constexpr bool XPRIO = ABL == 7;      // tools: s_setprio(1) around each MFMA group
   static_assert(BMT == 256 || (RES && BMT == 224), "224-row tiles only for the residual form (no counted waits)");
   constexpr int BM = BMT, BN = 256, KS = 64, NW = 8, WM = BM / 2, WN = 64, TM = WM / 16, TN = 4;
   constexpr int OPA = BM * KS * 2, OPB = BN * KS * 2, STAGE = OPA + OPB;  // A 32 (28) KiB + W 32 KiB
@@ -1110,7 +1114,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) b2[0][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo0);
 #pragma unroll
-        for (int g = 0; g < 2; ++g) a2[g] = *(const bf16x8*)(s0 + (wm * WM + g * 16) * 128 + fo0);
+        for (int g = 0; g < XD; ++g) a2[g] = *(const bf16x8*)(s0 + (wm * WM + g * 16) * 128 + fo0);
         if constexpr (XK_LATE) {
           __builtin_amdgcn_sched_barrier(0);
           if (st_t >= 0) stage(st_t, st_kt, (step + 1) & 1);
@@ -1118,15 +1122,17 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         }
 #pragma unroll
         for (int g = 0; g < 2 * TM; ++g) {
-          const int nx = g + 2;
+          const int nx = g + XD;
           if (nx == TM) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) b2[1][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo1);
           }
           if (nx < 2 * TM) a2[nx] = *(const bf16x8*)(s0 + (wm * WM + (nx % TM) * 16) * 128 + (nx < TM ? fo0 : fo1));
           __builtin_amdgcn_sched_barrier(0);
+          if (XPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[g % TM][j] = mma<true>(b2[g / TM][j], a2[g], acc[g % TM][j]);
+          if (XPRIO) __builtin_amdgcn_s_setprio(0);
           __builtin_amdgcn_sched_barrier(0);
         }
         continue;
@@ -1709,14 +1715,16 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       // results, timing only (tools/f16_ablate.sh); 3 / 4 / 5: the compiler's fragment-read order / the read pipeline per k-half / the stage's DMA
       // before the first fragment reads
       static const int abl = icap_knob("ICAP_F16P_ABL", 0);
-      if (so && abl >= 1 && abl <= 5) {
+      if (so && abl >= 1 && abl <= 7) {
         static bool attr = false;
         if (!attr) {
           for (const void* f : {(const void*)gemm_f16p_kernel<1, 1>, (const void*)gemm_f16p_kernel<2, 1>,
                                 (const void*)gemm_f16p_kernel<1, 2>, (const void*)gemm_f16p_kernel<2, 2>,
                                 (const void*)gemm_f16p_kernel<1, 3>, (const void*)gemm_f16p_kernel<2, 3, 224>,
                                 (const void*)gemm_f16p_kernel<1, 4>, (const void*)gemm_f16p_kernel<2, 4, 224>,
-                                (const void*)gemm_f16p_kernel<1, 5>, (const void*)gemm_f16p_kernel<2, 5, 224>})
+                                (const void*)gemm_f16p_kernel<1, 5>, (const void*)gemm_f16p_kernel<2, 5, 224>,
+                                (const void*)gemm_f16p_kernel<1, 6>, (const void*)gemm_f16p_kernel<2, 6, 224>,
+                                (const void*)gemm_f16p_kernel<1, 7>, (const void*)gemm_f16p_kernel<2, 7, 224>})
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048) != hipSuccess)
               return hipErrorInvalidValue;
           attr = true;
@@ -1732,12 +1740,20 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
         else if (res && abl == 4)
           hipLaunchKernelGGL((gemm_f16p_kernel<2, 4, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
                              dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
-        else if (res)
+        else if (res && abl == 5)
           hipLaunchKernelGGL((gemm_f16p_kernel<2, 5, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
+                             dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
+        else if (res && abl == 6)
+          hipLaunchKernelGGL((gemm_f16p_kernel<2, 6, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
+                             dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
+        else if (res)
+          hipLaunchKernelGGL((gemm_f16p_kernel<2, 7, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
                              dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
         else if (abl == 3) hipLaunchKernelGGL((gemm_f16p_kernel<1, 3>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
         else if (abl == 4) hipLaunchKernelGGL((gemm_f16p_kernel<1, 4>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
-        else hipLaunchKernelGGL((gemm_f16p_kernel<1, 5>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else if (abl == 5) hipLaunchKernelGGL((gemm_f16p_kernel<1, 5>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else if (abl == 6) hipLaunchKernelGGL((gemm_f16p_kernel<1, 6>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else hipLaunchKernelGGL((gemm_f16p_kernel<1, 7>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
         return hipGetLastError();
       }
       // ICAP_F16_PP=1 (tools): the ping-pong k-loop (gemm_f16q_kernel; slower)
