@@ -820,7 +820,10 @@ constexpr int XA_RED_BYTES = (8 * 512 + 512) * 4 + 16;  // + the KS = 2 ticket
 // [c/2, c)); each leaves its unnormalised context and softmax statistics (agent-scope stores), and the second
 // to take the pair's ticket merges them in part order (deterministic) and resets the ticket (xpart / xcnt as
 // cross_attn_mfma_kernel<KS = 2>).
-template <int KS, int CK>
+// NB: chunk buffers in the LDS ring.  2: chunk c + 2 is issued after chunk c's context (one barrier more);
+// >= 3: chunk c + NB - 1 goes into chunk c - 1's buffer right after chunk c's opening barrier, NB - 1 chunks
+// in flight (tools knob ICAP_XATTN16_NB).
+template <int KS, int CK, int NB = 2>
 __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* __restrict__ qt, long qt_lo,
                                                               const bf16_t* __restrict__ mem, int rows_per_image,
                                                               int S, float scale, bf16_t* out, long out_lo,
@@ -830,7 +833,7 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
   constexpr int NKT = CK / 16, NDT = DM / NW / 16, NS2 = CK / 32;  // key tiles, d tiles per wave, key k-steps
   constexpr int BUF = CK * DM * 2;              // 64 / 32 KiB per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = (float*)(smem + 2 * BUF);        // [4 d-groups][NKT tiles][4 regs][64 lanes]
+  float* red = (float*)(smem + NB * BUF);       // [4 d-groups][NKT tiles][4 regs][64 lanes]
   float* tot = red + NKT * 1024;                // [NKT tiles][4 regs][64 lanes]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
@@ -887,13 +890,25 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
   float m_run = -INFINITY, l_run = 0.f, d_run = 0.f;  // d_run: the dropped-probability mass (train mode)
   const int q4 = fr >> 2, p4 = fr & 3;
 
-  if (c0 < c1) stage(c0, 0);
-  if (c0 + 1 < c1) stage(c0 + 1, 1);
+  if constexpr (NB == 2) {
+    if (c0 < c1) stage(c0, 0);
+    if (c0 + 1 < c1) stage(c0 + 1, 1);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i)
+      if (c0 + i < c1) stage(c0 + i, i);
+  }
   for (int c = c0; c < c1; ++c) {
-    if (c + 1 < c1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    // chunks issued after c (4 DMA instructions each): NB = 2 issued c + 1 after chunk c - 1, NB >= 3 issued
+    // c + NB - 2 at chunk c - 1's opening barrier
+    const int younger = min(NB == 2 ? 1 : NB - 2, c1 - 1 - c);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const char* cb = smem + ((c - c0) & 1) * BUF;
+    // every wave is past chunk c - 1: its buffer takes chunk c + NB - 1
+    if (NB > 2 && c + NB - 1 < c1) stage(c + NB - 1, (c - c0 + NB - 1) % NB);
+    const char* cb = smem + ((c - c0) % NB) * BUF;
     {  // partial scores: key tile skt, d-group sdg
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
       const int key = skt * 16 + fr;
@@ -984,7 +999,7 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
         acc[dt] = mma16h(vh, pl, acc[dt]);
       }
     }
-    if (c + 2 < c1) {
+    if (NB == 2 && c + 2 < c1) {
       __syncthreads();  // every wave is done with buffer (c - c0) & 1
       stage(c + 2, (c - c0) & 1);
     }
@@ -1045,8 +1060,8 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
     }
   }
 }
-// LDS of cross_attn_f16_kernel<KS, CK>: 2 chunk buffers + partial and total scores + the KS = 2 ticket flag
-constexpr int xa16_lds(int ck) { return 2 * ck * 512 * 2 + (ck / 16) * (1024 + 256) * 4 + 16; }
+// LDS of cross_attn_f16_kernel<KS, CK, NB>: NB chunk buffers + partial and total scores + the KS = 2 ticket flag
+constexpr int xa16_lds(int ck, int nb = 2) { return nb * ck * 512 * 2 + (ck / 16) * (1024 + 256) * 4 + 16; }
 constexpr int XA16_LDS = xa16_lds(64);
 
 }  // namespace
@@ -1086,6 +1101,16 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, xa16_lds(32));
       if (e != hipSuccess) return e;
     }
+#ifdef ICAP_TOOLS
+    {
+      hipError_t e = hipFuncSetAttribute((const void*)cross_attn_f16_kernel<1, 32, 3>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, xa16_lds(32, 3));
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)cross_attn_f16_kernel<1, 32, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                xa16_lds(32, 4));
+      if (e != hipSuccess) return e;
+    }
+#endif
     attr = true;
   }
   // 32-key chunks, 8 waves, 74 KiB of LDS: two blocks (rows) share a CU, so the three decode chains' cross-
@@ -1097,6 +1122,19 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
 #define XA16(KS_, CK_)                                                                                          \
   hipLaunchKernelGGL((cross_attn_f16_kernel<KS_, CK_>), dim3(KS_ * pairs), dim3(CK_ * 16), xa16_lds(CK_), s, qt, \
                      qt_lo, mem16, rows_per_image, S, scale, out, out_lo, drop, gsum, xpart, xcnt)
+#ifdef ICAP_TOOLS
+  // ICAP_XATTN16_NB (tools): 3 / 4 chunk buffers (32-key chunks, no key split)
+  static const int nb = icap_knob("ICAP_XATTN16_NB", 2);
+  if (ck == 32 && !ks2 && (nb == 3 || nb == 4)) {
+    if (nb == 3)
+      hipLaunchKernelGGL((cross_attn_f16_kernel<1, 32, 3>), dim3(pairs), dim3(512), xa16_lds(32, 3), s, qt, qt_lo, mem16,
+                         rows_per_image, S, scale, out, out_lo, drop, gsum, xpart, xcnt);
+    else
+      hipLaunchKernelGGL((cross_attn_f16_kernel<1, 32, 4>), dim3(pairs), dim3(512), xa16_lds(32, 4), s, qt, qt_lo, mem16,
+                         rows_per_image, S, scale, out, out_lo, drop, gsum, xpart, xcnt);
+    return hipGetLastError();
+  }
+#endif
   if (ck == 32) {
     if (ks2) XA16(2, 32); else XA16(1, 32);
   } else {

@@ -1492,7 +1492,7 @@ const char* icap_knobs_set() {
       "ICAP_ENC_ATTN_PIPE", "ICAP_ENC_ATTN_QPW", "ICAP_XATTN_KS", "ICAP_POISON", "ICAP_GEMM_TAIL",
       "ICAP_QKV_HEAD_MAJOR", "ICAP_DEC_MIN_ROWS", "ICAP_I8_MLP2", "ICAP_DEC_BRANCHES", "ICAP_F16_GEMM",
       "ICAP_F16_PRES", "ICAP_XATTN16_KS", "ICAP_XATTN16_CK", "ICAP_ENC_ATTN16_QPW", "ICAP_F16_PP",
-      "ICAP_F16P_ABL", "ICAP_F16_RES_BM"};
+      "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB"};
   for (const char* n : names)
     if (getenv(n)) return n;
   return "";
