@@ -1014,7 +1014,7 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 // ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh); 3 = the
 // compiler's own fragment-read order, 4 = the read pipeline per k-half, 5 = the stage DMA before the first reads,
 // 6 = reads 3 groups ahead instead of 2 (within box noise, tools/f16x3_check.sh), 7 = s_setprio(1) around each
-// MFMA group (no gain, tools/f16_pf.sh).
+// MFMA group (no gain, tools/f16_pf.sh), 8 = 8-byte SO stores.
 // BMT: tile rows, 256 or (RES) 224 - wave tiles 112 x 64, the A stage 224 rows (wave 7 DMAs W rows only): at
 // N = 768 the 256-row tiles are 591 = 2.3 per CU (3 rounds, the last 30 % full), 224-row tiles 678 = 2.65 per CU
 // (3 rounds of 7/8 the work).
@@ -1034,7 +1034,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   constexpr int OPA = BM * KS * 2, OPB = BN * KS * 2, STAGE = OPA + OPB;  // A 32 (28) KiB + W 32 KiB
   constexpr int IPW = OPB / 1024 / NW;                // 4 DMA instructions per wave per operand
   constexpr int PER_STAGE = 2 * IPW;                  // 8 per wave per stage
-  constexpr int NSTORE = TM * TN;                     // 32 fp16 stores per wave per tile (SO)
+  // SO stores per wave per tile: WIDE = 16 B per lane (two 4-column groups of a row joined across the lane pair
+  // fq ^ 1: 16 stores), else 8 B (32 stores; tools ABL 8)
+  constexpr bool WIDE = ABL != 8;
+  constexpr int NSTORE = WIDE ? TM * TN / 2 : TM * TN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -1183,6 +1186,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
                                  : (long)m * p.ldc;
         bf16_t* C = (bf16_t*)p.C + orow + 4 * fq;
         const bool ok = !tail || mb + i * 16 + fr < M;
+        u32x2 pk[TN];
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           f32x4 v = acc[i][j];
@@ -1191,10 +1195,24 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
             const f32x2 lo = gelu_erf_fast2((f32x2){v[0], v[1]}), hi = gelu_erf_fast2((f32x2){v[2], v[3]});
             v = (f32x4){lo[0], lo[1], hi[0], hi[1]};
           }
-          if (ok) *(u32x2*)(C + nb + j * 16) = pack16x4<true>(v);
+          pk[j] = pack16x4<true>(v);
+          if (!WIDE && ok) *(u32x2*)(C + nb + j * 16) = pk[j];
+        }
+        if constexpr (WIDE) {
+          // lanes fq (even) and fq + 1 hold columns 4 fq .. 4 fq + 7 of tiles j and j + 1: the even lane keeps
+          // tile j's 8 columns, the odd lane tile j + 1's (the partner is 16 lanes away, same row)
+          const bool odd = fq & 1;
+#pragma unroll
+          for (int j = 0; j < TN; j += 2) {
+            const u32x2 snd = odd ? pk[j] : pk[j + 1];
+            const u32x2 rcv = {(uint32_t)__shfl_xor((int)snd[0], 16, 64), (uint32_t)__shfl_xor((int)snd[1], 16, 64)};
+            const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], pk[j + 1][0], pk[j + 1][1]}
+                                : (u32x4){pk[j][0], pk[j][1], rcv[0], rcv[1]};
+            if (ok) *(u32x4*)(C + nb + (odd ? (j + 1) * 16 - 4 : j * 16)) = w;
+          }
         }
       }
-      // the counted waits of the next tile assume all 32 stores per wave were issued: not after a ragged tile
+      // the counted waits of the next tile assume all NSTORE stores per wave were issued: not after a ragged tile
       // (its next tile waits vmcnt(0) and re-issues its stage 1 - the same bytes into the same buffer)
       seam = !tail;
     } else if constexpr (RES) {
@@ -1715,7 +1733,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       // results, timing only (tools/f16_ablate.sh); 3 / 4 / 5: the compiler's fragment-read order / the read pipeline per k-half / the stage's DMA
       // before the first fragment reads
       static const int abl = icap_knob("ICAP_F16P_ABL", 0);
-      if (so && abl >= 1 && abl <= 7) {
+      if (so && abl >= 1 && abl <= 8) {
         static bool attr = false;
         if (!attr) {
           for (const void* f : {(const void*)gemm_f16p_kernel<1, 1>, (const void*)gemm_f16p_kernel<2, 1>,
@@ -1724,7 +1742,8 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
                                 (const void*)gemm_f16p_kernel<1, 4>, (const void*)gemm_f16p_kernel<2, 4, 224>,
                                 (const void*)gemm_f16p_kernel<1, 5>, (const void*)gemm_f16p_kernel<2, 5, 224>,
                                 (const void*)gemm_f16p_kernel<1, 6>, (const void*)gemm_f16p_kernel<2, 6, 224>,
-                                (const void*)gemm_f16p_kernel<1, 7>, (const void*)gemm_f16p_kernel<2, 7, 224>})
+                                (const void*)gemm_f16p_kernel<1, 7>, (const void*)gemm_f16p_kernel<2, 7, 224>,
+                                (const void*)gemm_f16p_kernel<1, 8>})
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048) != hipSuccess)
               return hipErrorInvalidValue;
           attr = true;
@@ -1746,14 +1765,18 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
         else if (res && abl == 6)
           hipLaunchKernelGGL((gemm_f16p_kernel<2, 6, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
                              dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
-        else if (res)
+        else if (res && abl == 7)
           hipLaunchKernelGGL((gemm_f16p_kernel<2, 7, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
+                             dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
+        else if (res)  // (8: the SO store width; the residual form as built)
+          hipLaunchKernelGGL((gemm_f16p_kernel<2, 0, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)),
                              dim3(512), 2 * (224 * 128 + 256 * 128) + 2048, s, g);
         else if (abl == 3) hipLaunchKernelGGL((gemm_f16p_kernel<1, 3>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
         else if (abl == 4) hipLaunchKernelGGL((gemm_f16p_kernel<1, 4>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
         else if (abl == 5) hipLaunchKernelGGL((gemm_f16p_kernel<1, 5>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
         else if (abl == 6) hipLaunchKernelGGL((gemm_f16p_kernel<1, 6>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
-        else hipLaunchKernelGGL((gemm_f16p_kernel<1, 7>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else if (abl == 7) hipLaunchKernelGGL((gemm_f16p_kernel<1, 7>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        else hipLaunchKernelGGL((gemm_f16p_kernel<1, 8>), grid, dim3(512), 2 * 64 * 1024 + 2048, s, g);
         return hipGetLastError();
       }
       // ICAP_F16_PP=1 (tools): the ping-pong k-loop (gemm_f16q_kernel; slower)
