@@ -460,15 +460,26 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
     lt += __shfl_xor(lt, 32, 64);
     const float inv = 1.f / lt;
     const int qq = qt * 16 + fr;
+    if constexpr (F16) {
+      // 16-byte stores: lanes g (even) and g + 1 (16 lanes apart, same query) hold d = 16 dt + 4 g .. + 7 of
+      // d-tiles dt and dt + 1; the even lane stores d-tile dt's 8 values, the odd lane d-tile dt + 1's
+      const bool odd = g & 1;
+      bf16_t* dst = out + ((long)b * N + qq) * out_ld + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; dt += 2) {
+        const u32x2 p0 = pack16x4<true>(o[t][dt] * inv), p1 = pack16x4<true>(o[t][dt + 1] * inv);
+        const u32x2 snd = odd ? p0 : p1;
+        const u32x2 rcv = {(uint32_t)__shfl_xor((int)snd[0], 16, 64), (uint32_t)__shfl_xor((int)snd[1], 16, 64)};
+        const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], p1[0], p1[1]} : (u32x4){p0[0], p0[1], rcv[0], rcv[1]};
+        if (qq < N) *(u32x4*)(dst + (odd ? (dt + 1) * 16 - 4 : dt * 16)) = w;
+      }
+      continue;
+    }
     if (qq < N) {
       bf16_t* dst = out + ((long)b * N + qq) * out_ld + h * 64;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const int d = dt * 16 + 4 * g;
-        if constexpr (F16) {
-          *(u32x2*)(dst + d) = pack16x4<true>(o[t][dt] * inv);
-          continue;
-        }
         bf16_t hv[4], lv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) split_bf(o[t][dt][r] * inv, hv[r], lv[r]);
