@@ -79,10 +79,13 @@ __global__ __launch_bounds__(128) void head_kernel(HeadArgs a) {
   head_row_in(a, r, xs, s_ln);
   float logit = -INFINITY;
   if (tid < a.V) {
-    const float* wr = a.W + (long)tid * a.Dm;
+    // W4 (when set): fc_out as [Dm / 4][V][4], so the 4 weights a lane needs per step are 16 B and the wave's
+    // loads one contiguous run (the [V][Dm] rows put every lane on its own line); same products, same order
+    const float* wr = a.W4 ? a.W4 + (long)tid * 4 : a.W + (long)tid * a.Dm;
+    const long wstep = a.W4 ? (long)a.V * 4 : 4;
     float acc = 0.f;
-    for (int d = 0; d < a.Dm; d += 4) {
-      const f32x4 wv = *(const f32x4*)(wr + d);
+    for (int d = 0; d < a.Dm; d += 4, wr += wstep) {
+      const f32x4 wv = *(const f32x4*)wr;
       const f32x4 xv = *(const f32x4*)(xs + d);
       acc = fmaf(xv[0], wv[0], acc);
       acc = fmaf(xv[1], wv[1], acc);
@@ -252,7 +255,21 @@ __global__ __launch_bounds__(256) void head_wide_kernel(HeadArgs a) {
   }
 }
 
+__global__ void head_w4_kernel(const float* __restrict__ w, int V, int Dm, float* __restrict__ w4) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 4-weight group
+  if (i >= (long)V * (Dm / 4)) return;
+  const int v = (int)(i % V), d4 = (int)(i / V);
+  *(f32x4*)(w4 + i * 4) = *(const f32x4*)(w + (long)v * Dm + d4 * 4);
+}
+
 }  // namespace
+
+hipError_t launch_head_w4(const float* w, int V, int Dm, float* w4, hipStream_t s) {
+  if (V < 1 || Dm % 4) return hipErrorInvalidValue;
+  const long n = (long)V * (Dm / 4);
+  hipLaunchKernelGGL(head_w4_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, V, Dm, w4);
+  return hipGetLastError();
+}
 
 hipError_t launch_head(const HeadArgs& h, hipStream_t s) {
   if (h.V < 1 || h.V > HEAD_MAX_VOCAB || h.Dm % 4) return hipErrorInvalidValue;

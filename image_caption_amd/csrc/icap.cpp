@@ -149,6 +149,7 @@ struct icap_handle {
   size_t cursor = 0, dec_allocs = 0;  // dec_allocs: buffers of the decoder part (allocated first)
   // decoder
   float *emb = nullptr, *pe = nullptr, *fc_w = nullptr, *fc_b = nullptr;
+  float* fc_w4 = nullptr;  // fc_out as [D / 4][V][4] for the head's coalesced loads (launch_head_w4)
   std::vector<DecLayer> dec;
   // vit
   float *cls = nullptr, *pos = nullptr, *vit_ln_w = nullptr, *vit_ln_b = nullptr;
@@ -399,6 +400,12 @@ struct icap_handle {
 
 namespace {
 
+// the head's fc_out image ([D / 4][V][4], coalesced loads; tools knob ICAP_HEAD_W4=0: the [V][D] rows)
+const float* head_w4(const icap_handle* h) {
+  static const int on = icap_knob("ICAP_HEAD_W4", 1);
+  return on ? h->fc_w4 : nullptr;
+}
+
 // parts: ICAP_PART_DECODER | ICAP_PART_ENCODER.  On create both, allocating; on an update (h->repack)
 // the selected parts are re-packed into the same buffers.
 void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PART_ENCODER) {
@@ -413,6 +420,8 @@ void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PA
   h->pe = h->own_f32(d.pe, (size_t)d.pe_len * D, s);
   h->fc_w = h->own_f32(d.fc_w, (size_t)d.vocab * D, s);
   h->fc_b = h->own_f32(d.fc_b, d.vocab, s);
+  h->fc_w4 = (float*)h->alloc((size_t)d.vocab * D * 4);
+  HIPCHK(launch_head_w4(h->fc_w, d.vocab, D, h->fc_w4, s));
   for (int i = 0; i < d.n_dec_layers; ++i) {
     const icap_dec_layer_w& L = d.dec_layers[i];
     DecLayer o;
@@ -1070,7 +1079,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
       }
       HeadArgs ha{};
       decoder_layers(h, v, n, 1, t, max_len, 1, S, st, nullptr, 0, nullptr, drop ? &dc : nullptr, &ha.ln);
-      ha.x = v.x; ha.rows = n; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = d.vocab;
+      ha.x = v.x; ha.rows = n; ha.Dm = D; ha.W = h->fc_w; ha.W4 = head_w4(h); ha.bias = h->fc_b; ha.V = d.vocab;
       ha.logits = step_logits ? step_logits + ((size_t)t * B + r0) * d.vocab : nullptr;
       ha.ld_logits = d.vocab;
       ha.ids = ids + (size_t)r0 * max_len; ha.ld_ids = max_len; ha.id_col = t + 1;
@@ -1206,7 +1215,7 @@ void decode_beam(icap_handle* h, const float* mem, int B, int S, int max_len, in
     HIPCHK(launch_embed(seq[cur] + t, max_len, 0, rows, 1, t, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
     decoder_layers(h, b, rows, 1, t, max_len, 1, S, s, t > 0 ? anc[cur] : nullptr, K);
     HeadArgs ha{};
-    ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = V;
+    ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.W4 = head_w4(h); ha.bias = h->fc_b; ha.V = V;
     ha.logits = logits; ha.ld_logits = V;
     h->dws[0].fin.ensure((size_t)rows * 4);  // scratch argmax ids
     ha.ids = h->dws[0].fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
@@ -1492,7 +1501,8 @@ const char* icap_knobs_set() {
       "ICAP_ENC_ATTN_PIPE", "ICAP_ENC_ATTN_QPW", "ICAP_XATTN_KS", "ICAP_POISON", "ICAP_GEMM_TAIL",
       "ICAP_QKV_HEAD_MAJOR", "ICAP_DEC_MIN_ROWS", "ICAP_I8_MLP2", "ICAP_DEC_BRANCHES", "ICAP_F16_GEMM",
       "ICAP_F16_PRES", "ICAP_XATTN16_KS", "ICAP_XATTN16_CK", "ICAP_ENC_ATTN16_QPW", "ICAP_F16_PP",
-      "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB"};
+      "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
+      "ICAP_HEAD_W4"};
   for (const char* n : names)
     if (getenv(n)) return n;
   return "";
@@ -1740,7 +1750,7 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
     HIPCHK(launch_embed(tgt, T, 0, rows, T, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s));
     decoder_layers(h, b, B, T, 0, T, causal, S, s, nullptr, 0, key_lengths);
     HeadArgs ha{};
-    ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.bias = h->fc_b; ha.V = h->d.vocab;
+    ha.x = b.x; ha.rows = rows; ha.Dm = D; ha.W = h->fc_w; ha.W4 = head_w4(h); ha.bias = h->fc_b; ha.V = h->d.vocab;
     ha.logits = logits; ha.ld_logits = h->d.vocab;
     h->dws[0].fin.ensure((size_t)rows * 4);  // scratch ids
     ha.ids = h->dws[0].fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;

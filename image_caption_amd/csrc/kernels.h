@@ -293,7 +293,9 @@ struct HeadArgs {
   const float* emb; const float* pe; int pe_pos; float emb_scale; float* x_next; bf16_t* a_next; long lo; int nsplit;
   DropCfg drop;  // site 0 on the next step's embedding (positional-encoding dropout)
   RlnArgs ln;    // the last decoder layer's residual LN3 on x first (nparts <= 16; x_out unused), or off
+  const float* W4 = nullptr;  // optional fc_out image [Dm / 4][V][4] (launch_head_w4) for V <= 128
 };
+hipError_t launch_head_w4(const float* w, int V, int Dm, float* w4, hipStream_t s);
 constexpr int HEAD_MAX_VOCAB = 32768;  // logits of one row in LDS (128 KiB) for the sampler's prefix sum
 hipError_t launch_head(const HeadArgs& h, hipStream_t s);
 
