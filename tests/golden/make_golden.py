@@ -41,6 +41,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 from image_caption_amd import weights as W  # noqa: E402
+from tests.golden.inputs import decoder_ops_memory  # noqa: E402,F401
 
 REF = "/root/reference"
 END_BIAS = 1.4  # <end> logit offset of the beam-search fixtures (makes beams finish early)
@@ -146,9 +147,6 @@ def teacher_forced(dec, memory, ids):
         return dec(ids[:, :-1], memory, tgt_mask=dec.generate_square_subsequent_mask(T, "cpu"))
 
 
-def decoder_ops_memory() -> np.ndarray:
-    """The (3,196,512) memory of decoder_ops.npz, regenerated from its seed (not stored)."""
-    return np.random.Generator(np.random.PCG64(8)).standard_normal((3, 196, 512)).astype(np.float32)
 
 
 def top2(logits):

@@ -78,7 +78,7 @@ def test_vit_golden_per_precision(vit_sd, cuda, precision):
 
 
 def test_decoder_forward_golden(vit_engine, cuda):
-    from tests.golden.make_golden import decoder_ops_memory
+    from tests.golden.inputs import decoder_ops_memory
 
     g = gold("decoder_ops.npz")
     tgt = torch.from_numpy(g["tgt"]).to(cuda)

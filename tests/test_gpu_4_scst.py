@@ -40,7 +40,7 @@ def test_scst_grad_step_matches_torch_sampler(cuda, precision):
     operands (f16, the default: 4e-3 on the memory) or 16-bit ones (bf16x2: 1e-5) - which the gradients
     inherit: held to 2e-2 of each tensor's norm with the f16 trunk (whose memory flips a few ReLU / softmax
     decisions), to 1e-3 of each tensor's maximum with the bf16x2 trunk.  (The
-    backward itself matches fp64 autograd as closely as fp32 autograd does: tests/test_gpu_train.py.)"""
+    backward itself matches fp64 autograd as closely as fp32 autograd does: tests/test_gpu_5_train.py.)"""
     from utils.scst_loss import SCSTLoss
 
     B, L = 8, 30

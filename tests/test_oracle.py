@@ -57,7 +57,7 @@ def test_grid_greedy_matches_reference(grid_sd):
 
 
 def test_decoder_forward_causal_and_unmasked(vit_sd):
-    from tests.golden.make_golden import decoder_ops_memory
+    from tests.golden.inputs import decoder_ops_memory
 
     g = gold("decoder_ops.npz")
     tgt = torch.from_numpy(g["tgt"])

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 T=${1:-x}
 O=gpurun_out/r2
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_engine.py tests/test_gpu_parity.py -m gpu -x -q \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_6_ops.py tests/test_gpu_2_engine.py tests/test_gpu_1_parity.py -m gpu -x -q \
   -k "f16" --timeout 200 --timeout-method thread > $O/${T}_tests.log 2>&1 || { tail -40 $O/${T}_tests.log; exit 1; }
 tail -2 $O/${T}_tests.log
 for p in f16 i8x2; do

@@ -11,7 +11,7 @@ import sys
 from image_caption_amd import _lib
 _lib.load('tools/libicap_tools.so')
 import pytest
-sys.exit(pytest.main(['tests/test_gpu_ops.py','-m','gpu','-x','-q','-k','gemm_f16','-p','no:cacheprovider']))
+sys.exit(pytest.main(['tests/test_gpu_6_ops.py','-m','gpu','-x','-q','-k','gemm_f16','-p','no:cacheprovider']))
 " > $O/f16form_ops$f.log 2>&1 || { tail -30 $O/f16form_ops$f.log; exit 1; }
   echo "== ICAP_F16_GEMM=$f ($(tail -1 $O/f16form_ops$f.log))"
   ICAP_F16_GEMM=$f timeout -k 10 120 python tools/gemm_f16.py 20 2>&1 | grep -v amdgpu.ids || exit 1

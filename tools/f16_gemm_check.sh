@@ -18,7 +18,7 @@ import torch, os
 from image_caption_amd import _lib
 _lib.load('tools/libicap_tools.so')
 import pytest
-sys.exit(pytest.main(['tests/test_gpu_ops.py','-m','gpu','-x','-q','-k','gemm_f16','-p','no:cacheprovider']))
+sys.exit(pytest.main(['tests/test_gpu_6_ops.py','-m','gpu','-x','-q','-k','gemm_f16','-p','no:cacheprovider']))
 " > $O/${T}_ops$f.log 2>&1 || { tail -30 $O/${T}_ops$f.log; exit 1; }
   tail -1 $O/${T}_ops$f.log
 done

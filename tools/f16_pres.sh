@@ -9,7 +9,7 @@ import sys
 from image_caption_amd import _lib
 _lib.load('tools/libicap_tools.so')
 import pytest
-sys.exit(pytest.main(['tests/test_gpu_ops.py','-m','gpu','-x','-q','-k','gemm_f16','-p','no:cacheprovider']))
+sys.exit(pytest.main(['tests/test_gpu_6_ops.py','-m','gpu','-x','-q','-k','gemm_f16','-p','no:cacheprovider']))
 " > $O/pres_ops.log 2>&1 || { tail -30 $O/pres_ops.log; exit 1; }
 tail -1 $O/pres_ops.log
 for v in 0 1; do

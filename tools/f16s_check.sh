@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r2
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -m gpu -x -q -k "gemm_f16" --timeout 200 --timeout-method thread > gpurun_out/r2/f16s_tests.log 2>&1 || { tail -30 gpurun_out/r2/f16s_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_6_ops.py -m gpu -x -q -k "gemm_f16" --timeout 200 --timeout-method thread > gpurun_out/r2/f16s_tests.log 2>&1 || { tail -30 gpurun_out/r2/f16s_tests.log; exit 1; }
 tail -1 gpurun_out/r2/f16s_tests.log
 timeout -k 10 400 python -m image_caption_amd.build --tools > gpurun_out/r2/ab_build.log 2>&1 || { tail -5 gpurun_out/r2/ab_build.log; exit 1; }
 for a in 0 3; do

@@ -4,7 +4,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-ICAP_GEMM_TALL_MIN_K=1 timeout -k 10 600 python -m pytest tests/test_gpu_ops.py tests/test_gpu_parity.py -m gpu -x -q -k "gemm or grid or golden" > gpurun_out/hk_t.log 2>&1 || { tail -30 gpurun_out/hk_t.log; exit 1; }
+ICAP_GEMM_TALL_MIN_K=1 timeout -k 10 600 python -m pytest tests/test_gpu_6_ops.py tests/test_gpu_1_parity.py -m gpu -x -q -k "gemm or grid or golden" > gpurun_out/hk_t.log 2>&1 || { tail -30 gpurun_out/hk_t.log; exit 1; }
 tail -2 gpurun_out/hk_t.log
 cd /tmp && export TMPDIR=/tmp
 for H in 0 1 128 512; do

@@ -3,9 +3,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -v --timeout 120 --timeout-method thread -k "block_scaled or gemm_i8" > gpurun_out/i8k_ops.log 2>&1 || { tail -40 gpurun_out/i8k_ops.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_6_ops.py -x -v --timeout 120 --timeout-method thread -k "block_scaled or gemm_i8" > gpurun_out/i8k_ops.log 2>&1 || { tail -40 gpurun_out/i8k_ops.log; exit 1; }
 tail -2 gpurun_out/i8k_ops.log
-ICAP_I8_MLP2=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_engine.py -x -q --timeout 120 --timeout-method thread -k i8x2 > gpurun_out/i8k_parity.log 2>&1 || { tail -40 gpurun_out/i8k_parity.log; exit 1; }
+ICAP_I8_MLP2=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_1_parity.py tests/test_gpu_2_engine.py -x -q --timeout 120 --timeout-method thread -k i8x2 > gpurun_out/i8k_parity.log 2>&1 || { tail -40 gpurun_out/i8k_parity.log; exit 1; }
 tail -2 gpurun_out/i8k_parity.log
 for r in 1 2; do
 timeout -k 10 200 env ICAP_I8_MLP2=0 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/i8k_off_$r.json 2>gpurun_out/i8k_off.err || exit 1

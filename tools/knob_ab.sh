@@ -5,7 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r2
 timeout -k 10 400 python -m image_caption_amd.build --tools > gpurun_out/r2/ab_build.log 2>&1 || { tail -5 gpurun_out/r2/ab_build.log; exit 1; }
-env $KNOB=$VAL timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_parity.py tests/test_gpu_ops.py} -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r2/ab_tests.log 2>&1 || { tail -30 gpurun_out/r2/ab_tests.log; exit 1; }
+env $KNOB=$VAL timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_1_parity.py tests/test_gpu_6_ops.py} -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r2/ab_tests.log 2>&1 || { tail -30 gpurun_out/r2/ab_tests.log; exit 1; }
 tail -1 gpurun_out/r2/ab_tests.log
 for v in default $VAL default $VAL; do
   echo "== $KNOB=$v"

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -v --timeout 120 --timeout-method thread -k tail_split > gpurun_out/tail_ops.log 2>&1 || { tail -40 gpurun_out/tail_ops.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_6_ops.py -x -v --timeout 120 --timeout-method thread -k tail_split > gpurun_out/tail_ops.log 2>&1 || { tail -40 gpurun_out/tail_ops.log; exit 1; }
 tail -2 gpurun_out/tail_ops.log
 timeout -k 10 600 ICAP_GEMM_TAIL=1 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/tail_tests.log 2>&1 || { tail -40 gpurun_out/tail_tests.log; exit 1; }
 tail -2 gpurun_out/tail_tests.log

@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r2
 timeout -k 10 400 python -m image_caption_amd.build --tools > gpurun_out/r2/ab_build.log 2>&1 || { tail -5 gpurun_out/r2/ab_build.log; exit 1; }
 for v in 3 4; do
-  ICAP_XATTN16_NB=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_engine.py tests/test_gpu_scst.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r2/nb_tests_$v.log 2>&1 || { tail -30 gpurun_out/r2/nb_tests_$v.log; exit 1; }
+  ICAP_XATTN16_NB=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_1_parity.py tests/test_gpu_2_engine.py tests/test_gpu_4_scst.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r2/nb_tests_$v.log 2>&1 || { tail -30 gpurun_out/r2/nb_tests_$v.log; exit 1; }
   echo "NB=$v: $(tail -1 gpurun_out/r2/nb_tests_$v.log)"
 done
 for v in 2 3 4 2 3 4; do
