@@ -13,7 +13,7 @@ from pathlib import Path
 import torch  # noqa: F401  (load torch's HIP runtime before libicap)
 
 LIB_PATH = Path(__file__).resolve().parent / "libicap.so"
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 KIND_VIT, KIND_GRID = 0, 1
 PREC_BF16, PREC_BF16X2, PREC_I8X2, PREC_F16 = 1, 2, 3, 4
@@ -75,6 +75,7 @@ class ModelDesc(ctypes.Structure):
         ("enc_layers", POINTER(EncLayerW)),
         ("n_trunk", c_int), ("trunk_blocks", c_int * 4),
         ("trunk", POINTER(ConvBnW)),
+        ("dec_weight_planes", c_int),
     ]
 
 
@@ -112,6 +113,7 @@ SIGNATURES = {
                                      c_void_p, c_void_p]),
     "icap_set_graphs": (c_int, [c_void_p, c_int]),
     "icap_set_decode_chains": (c_int, [c_void_p, c_int]),
+    "icap_range_check": (c_int, [c_void_p, c_void_p, POINTER(c_int)]),
     "icap_profile_enable": (c_int, [c_void_p, c_int]),
     "icap_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(c_long),
                                   POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),

@@ -50,6 +50,35 @@ __global__ void beam_init_kernel(int B, int K, int start, int Lmax, int32_t* seq
   }
 }
 
+// (value desc, index asc) maximum over a wave / a 256-thread block; the result is in every lane / thread
+__device__ __forceinline__ void wave_best(float& bv, int& bi) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+}
+__device__ __forceinline__ void block_best(float& bv, int& bi, float* rv, int* ri, int lane, int wave) {
+  wave_best(bv, bi);
+  if (lane == 0) {
+    rv[wave] = bv;
+    ri[wave] = bi;
+  }
+  __syncthreads();
+  bv = rv[0];
+  bi = ri[0];
+  for (int w = 1; w < 4; ++w)
+    if (rv[w] > bv || (rv[w] == bv && ri[w] < bi)) {
+      bv = rv[w];
+      bi = ri[w];
+    }
+  __syncthreads();  // rv / ri are reused by the next call
+}
+
 // One 256-thread block per image.
 __global__ __launch_bounds__(256) void beam_select_kernel(const float* __restrict__ logits, int V, int K, int t,
                                                           int Lmax, int grid_variant, int end_tok,
@@ -75,58 +104,100 @@ __global__ __launch_bounds__(256) void beam_select_kernel(const float* __restric
     return;
   }
   const int nrows = t == 0 ? 1 : k;
-  // log_softmax per live row (one wave per row)
-  for (int j = wave; j < nrows; j += 4) {
-    const float* lg = logits + (long)(r0 + j) * V;
-    float m = -INFINITY;
-    for (int v = lane; v < V; v += 64) m = fmaxf(m, lg[v]);
-    m = wave_max(m);
-    float s = 0.f;
-    for (int v = lane; v < V; v += 64) s += __expf(lg[v] - m);
-    const float lse = m + __logf(wave_sum(s));
-    const float base = t == 0 ? 0.f : sc_c[r0 + j];
-    for (int v = lane; v < V; v += 64) lp[j * V + v] = base + (lg[v] - lse);
-  }
-  __syncthreads();
-  // top-k over nrows*V candidates: k rounds of a block argmax (value desc, index asc)
-  const int ncand = nrows * V;
-  for (int b = 0; b < k; ++b) {
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int c = tid; c < ncand; c += 256) {
-      const float v = lp[c];
-      if (v > bv || (v == bv && c < bi)) {
-        bv = v;
-        bi = c;
-      }
-    }
-#pragma unroll
-    for (int o = 32; o; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) {
-        bv = ov;
-        bi = oi;
-      }
-    }
-    if (lane == 0) {
-      rv[wave] = bv;
-      ri[wave] = bi;
+  if (V <= VMAX) {
+    // log_softmax per live row (one wave per row)
+    for (int j = wave; j < nrows; j += 4) {
+      const float* lg = logits + (long)(r0 + j) * V;
+      float m = -INFINITY;
+      for (int v = lane; v < V; v += 64) m = fmaxf(m, lg[v]);
+      m = wave_max(m);
+      float s = 0.f;
+      for (int v = lane; v < V; v += 64) s += __expf(lg[v] - m);
+      const float lse = m + __logf(wave_sum(s));
+      const float base = t == 0 ? 0.f : sc_c[r0 + j];
+      for (int v = lane; v < V; v += 64) lp[j * V + v] = base + (lg[v] - lse);
     }
     __syncthreads();
-    if (tid == 0) {
-      float v = rv[0];
-      int ix = ri[0];
-      for (int w = 1; w < 4; ++w)
-        if (rv[w] > v || (rv[w] == v && ri[w] < ix)) {
-          v = rv[w];
-          ix = ri[w];
+    // top-k over nrows*V candidates: k rounds of a block argmax (value desc, index asc)
+    const int ncand = nrows * V;
+    for (int b = 0; b < k; ++b) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int c = tid; c < ncand; c += 256) {
+        const float v = lp[c];
+        if (v > bv || (v == bv && c < bi)) {
+          bv = v;
+          bi = c;
         }
-      sel_idx[b] = ix;
-      sel_val[b] = v;
-      lp[ix] = -INFINITY;  // exclude (the candidate array is private to this step)
+      }
+      block_best(bv, bi, rv, ri, lane, wave);
+      if (tid == 0) {
+        sel_idx[b] = bi;
+        sel_val[b] = bv;
+        lp[bi] = -INFINITY;  // exclude (the candidate array is private to this step)
+      }
+      __syncthreads();
+    }
+  } else {
+    // Vocabularies above VMAX: the k*V log-probs do not fit LDS.  The global top-k (value desc, flattened
+    // index asc) is contained in the union of the rows' own top-k (a candidate beaten by fewer than k
+    // candidates overall is beaten by fewer than k of its own row), so each row's top-k is found by k
+    // passes over its logits (pass r: the best candidate ordered after pass r-1's pick), then the
+    // global top-k over those nrows*k candidates.  Log-probs are the same expression as above.
+    __shared__ float cv[BEAM_MAX * BEAM_MAX];
+    __shared__ int ci[BEAM_MAX * BEAM_MAX];
+    for (int j = wave; j < nrows; j += 4) {
+      const float* lg = logits + (long)(r0 + j) * V;
+      float m = -INFINITY;
+      for (int v = lane; v < V; v += 64) m = fmaxf(m, lg[v]);
+      m = wave_max(m);
+      float s = 0.f;
+      for (int v = lane; v < V; v += 64) s += __expf(lg[v] - m);
+      const float lse = m + __logf(wave_sum(s));
+      const float base = t == 0 ? 0.f : sc_c[r0 + j];
+      float pv = INFINITY;
+      int pi = -1;
+      for (int r = 0; r < k; ++r) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int v = lane; v < V; v += 64) {
+          const float x = base + (lg[v] - lse);
+          const bool after = x < pv || (x == pv && v > pi);
+          if (after && (x > bv || (x == bv && v < bi))) {
+            bv = x;
+            bi = v;
+          }
+        }
+        wave_best(bv, bi);
+        if (lane == 0) {
+          cv[j * k + r] = bv;
+          ci[j * k + r] = bi == 0x7fffffff ? 0x7fffffff : j * V + bi;
+        }
+        pv = bv;
+        pi = bi;
+      }
     }
     __syncthreads();
+    const int ncand = nrows * k;
+    for (int b = 0; b < k; ++b) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int c = tid; c < ncand; c += 256) {
+        const float v = cv[c];
+        const int ix = ci[c];
+        if (ix != -1 && (v > bv || (v == bv && ix < bi))) {
+          bv = v;
+          bi = ix;
+        }
+      }
+      block_best(bv, bi, rv, ri, lane, wave);
+      if (tid < ncand && ci[tid] == bi) ci[tid] = -1;  // exclude (flattened indices are unique)
+      if (tid == 0) {
+        sel_idx[b] = bi;
+        sel_val[b] = bv;
+      }
+      __syncthreads();
+    }
   }
   // bookkeeping (thread 0: at most BEAM_MAX beams)
   __shared__ int s_kn, s_stop;
@@ -233,7 +304,7 @@ hipError_t launch_beam_select(const float* logits, int V, int B, int K, int t, i
                               const int32_t* seq_c, int32_t* seq_n, const int32_t* anc_c, int32_t* anc_n,
                               const float* sc_c, float* sc_n, int* kcur, int* done, int* ncomp, float* best_score,
                               int32_t* best_seq, int* best_len, hipStream_t s) {
-  if (K < 1 || K >= BEAM_MAX || V > VMAX || V < 1) return hipErrorInvalidValue;
+  if (K < 1 || K >= BEAM_MAX || V < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(beam_select_kernel, dim3(B), dim3(256), 0, s, logits, V, K, t, Lmax, grid_variant, end_tok, seq_c,
                      seq_n, anc_c, anc_n, sc_c, sc_n, kcur, done, ncomp, best_score, best_seq, best_len);
   return hipGetLastError();

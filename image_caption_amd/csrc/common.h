@@ -76,6 +76,15 @@ __device__ __forceinline__ bf16_t cvt16(float f) {
   if constexpr (F16) return f2h(f);
   else return f2bf(f);
 }
+// fp16 range guard (ICAP_PREC_F16): a packed pair holds an infinity or NaN (exponent field all ones), i.e. a value
+// that overflowed 65504 on conversion or was already non-finite
+__device__ __forceinline__ bool f16_pair_nonfinite(uint32_t u) {
+  return (u & 0x7c00u) == 0x7c00u || (u & 0x7c000000u) == 0x7c000000u;
+}
+// set the handle's sticky range word (one vector store from one lane; never the scalar path)
+__device__ __forceinline__ void range_flag_set(unsigned* flag) {
+  __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <bool F16>
 __device__ __forceinline__ u32x2 pack16x4(f32x4 v) {
   if constexpr (F16) {

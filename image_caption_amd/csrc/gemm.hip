@@ -396,7 +396,9 @@ __global__ __launch_bounds__(NWV * 64) void gemm_dec_kernel(WaveGemmArgs p) {
   const int batch = blockIdx.z / p.ksplit, split = blockIdx.z % p.ksplit;
   const bf16_t* A = p.A + (long)batch * p.a_batch;
   const bf16_t* W = p.W + (long)batch * p.w_batch;
-  const int ns = p.nsplit, nops = ns + 1, step_bytes = nops * 2048;
+  const bf16_t* Wl = p.W_lo ? p.W_lo + (long)batch * p.w_batch : nullptr;
+  // operands per k-step: ns activation planes, W, and (hi/lo weights) W_lo
+  const int ns = p.nsplit, nops = ns + 1 + (Wl ? 1 : 0), step_bytes = nops * 2048;
   const int nks = p.K / 32 / p.ksplit, kbeg = split * nks;
 
   // staging: instruction q in [0, 2 * nops * nks): k-step q / (2 nops), operand, row half
@@ -406,8 +408,9 @@ __global__ __launch_bounds__(NWV * 64) void gemm_dec_kernel(WaveGemmArgs p) {
     const int ks = q / (2 * nops), rem = q - ks * 2 * nops, opnd = rem >> 1, half = rem & 1;
     const int kg = (kbeg + ks) * 32 + lchunk * 8;
     const int r = half * 16 + lrow;
-    const bf16_t* src = opnd < ns ? A + opnd * p.a_lo + (long)min(m0 + r, p.M - 1) * p.lda + kg
-                                  : W + (long)min(n0 + r, p.N - 1) * p.ldw + kg;
+    const bf16_t* src = opnd < ns    ? A + opnd * p.a_lo + (long)min(m0 + r, p.M - 1) * p.lda + kg
+                        : opnd == ns ? W + (long)min(n0 + r, p.N - 1) * p.ldw + kg
+                                     : Wl + (long)min(n0 + r, p.N - 1) * p.ldw + kg;
     __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
                                      (LDS_AS void*)(smem + ks * step_bytes + opnd * 2048 + half * 1024), 16, 0, 0);
   }
@@ -430,6 +433,7 @@ __global__ __launch_bounds__(NWV * 64) void gemm_dec_kernel(WaveGemmArgs p) {
       const bf16x8 al = *(const bf16x8*)(pa + 2048 + ks * step_bytes);
       acc = mfma16(b, al, acc);
     }
+    if (Wl) acc = mfma16(*(const bf16x8*)(pb + 2048 + ks * step_bytes), a, acc);  // W_lo . X_hi
   }
   if (KGRPS > 1) {
     __syncthreads();  // staging area is reused for the reduction
@@ -485,19 +489,19 @@ hipError_t launch_gemm_dec(const WaveGemmArgs& g, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     for (const void* f : {(const void*)gemm_dec_kernel<4>, (const void*)gemm_dec_kernel<16>}) {
-      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, DEC_MAX_KSTEPS * 3 * 2048);
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, DEC_MAX_KSTEPS * 4 * 2048);
       if (e != hipSuccess) return e;
     }
     attr = true;
   }
   // few k-steps per block: 4 waves (one per quadrant, no reduction, up to 8 blocks per CU);
   // otherwise 16 waves so that enough waves issue the LDS-DMA of the larger slice
-  const int nks = steps / g.ksplit;
+  const int nks = steps / g.ksplit, nops = g.nsplit + 1 + (g.W_lo ? 1 : 0);
   dim3 grid((g.N + 31) / 32, (g.M + 31) / 32, g.batch * g.ksplit);
   if (nks <= 4) {
-    hipLaunchKernelGGL(gemm_dec_kernel<4>, grid, dim3(256), nks * (g.nsplit + 1) * 2048, s, g);
+    hipLaunchKernelGGL(gemm_dec_kernel<4>, grid, dim3(256), nks * nops * 2048, s, g);
   } else {
-    const int lds = std::max(nks * (g.nsplit + 1) * 2048, DEC_RED_BYTES);
+    const int lds = std::max(nks * nops * 2048, DEC_RED_BYTES);
     hipLaunchKernelGGL(gemm_dec_kernel<16>, grid, dim3(1024), lds, s, g);
   }
   return hipGetLastError();
@@ -1088,6 +1092,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   if (SO || RES) load_bias(t, 0);
   stage(t, 0, 0);
   bool seam = false;  // this tile's stages 0 and 1 were issued before the previous tile's epilogue stores
+  bool range_bad = false;  // SO: some stored fp16 value is not finite (p.range_flag set once, after the last tile)
   for (;;) {
     const int tn = t + nbx < xbase + xcnt ? t + nbx : -1;  // this block's next tile
     for (int kt = 0; kt < nk; ++kt, ++step) {
@@ -1196,6 +1201,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
             v = (f32x4){lo[0], lo[1], hi[0], hi[1]};
           }
           pk[j] = pack16x4<true>(v);
+          if (ok && (f16_pair_nonfinite(pk[j][0]) || f16_pair_nonfinite(pk[j][1]))) range_bad = true;
           if (!WIDE && ok) *(u32x2*)(C + nb + j * 16) = pk[j];
         }
         if constexpr (WIDE) {
@@ -1260,6 +1266,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
+  // after the tile loop: no counted wait follows, so this store cannot disturb the seams' vmcnt arithmetic
+  if (SO && p.range_flag && __any(range_bad) && lane == 0) range_flag_set(p.range_flag);
 }
 
 #ifdef ICAP_TOOLS

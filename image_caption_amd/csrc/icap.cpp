@@ -72,8 +72,9 @@ struct DevBuf {
   T* as() const { return (T*)p; }
 };
 
-struct Lin {  // packed nn.Linear: bf16 W [N][K] + fp32 bias
+struct Lin {  // packed nn.Linear: bf16 W [N][K] + fp32 bias (+ the lo plane bf16(W - W_hi) of hi/lo weights)
   bf16_t* w = nullptr;
+  bf16_t* wl = nullptr;
   float* b = nullptr;
   int N = 0, K = 0;
 };
@@ -141,6 +142,10 @@ struct icap_handle {
   bool i8 = false;  // ICAP_PREC_I8X2: LayerNorm-fed ViT GEMMs on int8 two-slice operands
   bool i8k = false;  // ... and MLP-2 on the block-scaled int8 GELU output (ICAP_I8_MLP2=1, opt-in)
   bool f16 = false;  // ICAP_PREC_F16: the ViT encoder on single fp16 planes (fp16 MFMA); the decoder stays bf16x2
+  // hi/lo decoder weights (icap_model_desc.dec_weight_planes = 2: fp32 checkpoints that are not bf16-exact): every
+  // decoder GEMM weight is packed as hi = bf16(W) and lo = bf16(W - hi) and the decode runs the unfused launches,
+  // whose GEMMs add W_lo . X_hi; the train-mode dropout sampler keeps the fused blocks (W_hi only)
+  bool wlo = false;
   std::vector<void*> owned;
   std::vector<size_t> owned_n;  // bytes of each owned buffer
   // icap_update_weights re-packs into the buffers icap_create allocated, in the same order: alloc()
@@ -210,6 +215,16 @@ struct icap_handle {
     DevBuf gs;  // train-mode cross-attention value-bias weights
   } dws[2];
   DevBuf d_beam;
+  // ICAP_PREC_F16 range guard: one sticky device word, set by the fp16 encoder's LayerNorm and store-only GEMM
+  // kernels when a value they write is not finite in fp16; read and cleared by icap_range_check
+  DevBuf rflag;
+  unsigned* range_word() {
+    if (!rflag.p) {
+      rflag.ensure(16);
+      HIPCHK(hipMemset(rflag.p, 0, 16));
+    }
+    return rflag.as<unsigned>();
+  }
 
   ~icap_handle() {
     for (DecodeGraph& g : dg) {
@@ -225,7 +240,7 @@ struct icap_handle {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col, &t_bn}) b->release();
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt}) b->release();
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt, &rflag}) b->release();
     for (DecWS& w : dws)
       for (DevBuf* b : {&w.x, &w.a, &w.qkv, &w.q, &w.qt, &w.c, &w.o, &w.h, &w.kv, &w.fin, &w.part, &w.memp, &w.xpart,
                          &w.xcnt, &w.gs})
@@ -269,6 +284,23 @@ struct icap_handle {
     l.N = N;
     l.K = K;
     return l;
+  }
+  // decoder nn.Linear, hi/lo weights when the handle has them: W_hi at w, W_lo at wl = w + N K
+  Lin dlin(const float* w, const float* b, int N, int K, hipStream_t s) {
+    if (!wlo) return lin(w, b, N, K, s);
+    Lin l;
+    l.w = own_bf16_hl(w, (size_t)N * K, s);
+    l.wl = l.w + (size_t)N * K;
+    l.b = b ? own_f32(b, N, s) : nullptr;
+    l.N = N;
+    l.K = K;
+    return l;
+  }
+  bf16_t* own_bf16_hl(const float* src, size_t n, hipStream_t s) {  // [hi n][lo n]
+    REQUIRE(src != nullptr, "missing parameter pointer");
+    bf16_t* p = (bf16_t*)alloc(n * 4);
+    HIPCHK(launch_split_f32(src, (long)n, p, (long)n, 2, s));
+    return p;
   }
   Lin8 lin8(const float* w, const float* b, int N, int K, hipStream_t s) {
     REQUIRE(w != nullptr, "missing parameter pointer");
@@ -330,6 +362,7 @@ struct icap_handle {
     g.C = C; g.ldc = ldc;
     g.M = M; g.N = W.N; g.K = W.K; g.nsplit = 1; g.c_planes = 1; g.f16 = 1;
     g.epi = epi; g.out = out;
+    g.range_flag = range_word();
     run_gemm(g, s);
   }
   // residual-output GEMMs (N = 768 / 512: a partial last round of tiles) split their tail tiles in K when
@@ -371,10 +404,11 @@ struct icap_handle {
   // decode-step GEMM (wave tiles, optional split-K into fp32 partial slabs)
   void wgemm(const bf16_t* A, long lda, long a_lo, const bf16_t* W, long ldw, const float* bias, int M, int N, int K,
              void* C, long ldc, long c_lo, int epi, int out, int tile, int ksplit, long part_stride, hipStream_t s,
-             int batch = 1, long a_batch = 0, long w_batch = 0, long bias_batch = 0, long c_batch = 0) {
+             int batch = 1, long a_batch = 0, long w_batch = 0, long bias_batch = 0, long c_batch = 0,
+             const bf16_t* W_lo = nullptr) {
     WaveGemmArgs g = wave_args();
     g.A = A; g.lda = lda; g.a_lo = a_lo; g.a_batch = a_batch;
-    g.W = W; g.ldw = ldw; g.w_batch = w_batch;
+    g.W = W; g.ldw = ldw; g.w_batch = w_batch; g.W_lo = W_lo;
     g.bias = bias; g.bias_batch = bias_batch;
     g.C = C; g.ldc = ldc; g.c_lo = c_lo; g.c_batch = c_batch; g.c_planes = ns;
     g.M = M; g.N = N; g.K = K; g.nsplit = ns; g.batch = batch; g.ksplit = ksplit; g.part_stride = part_stride;
@@ -425,16 +459,21 @@ void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PA
   for (int i = 0; i < d.n_dec_layers; ++i) {
     const icap_dec_layer_w& L = d.dec_layers[i];
     DecLayer o;
-    o.sa_qkv = h->lin(L.self_attn.in_w, L.self_attn.in_b, 3 * D, D, s);
-    o.sa_out = h->lin(L.self_attn.out_w, L.self_attn.out_b, D, D, s);
-    o.ca_q = h->lin(L.cross_attn.in_w, L.cross_attn.in_b, D, D, s);
-    o.ca_kT = (bf16_t*)h->alloc((size_t)D * D * 2);
+    o.sa_qkv = h->dlin(L.self_attn.in_w, L.self_attn.in_b, 3 * D, D, s);
+    o.sa_out = h->dlin(L.self_attn.out_w, L.self_attn.out_b, D, D, s);
+    o.ca_q = h->dlin(L.cross_attn.in_w, L.cross_attn.in_b, D, D, s);
+    // hi/lo: the lo plane of each of W_k^T / W_v follows its hi plane (+ D * D)
+    o.ca_kT = (bf16_t*)h->alloc((size_t)D * D * 2 * (h->wlo ? 2 : 1));
     HIPCHK(launch_transpose_heads_bf16(L.cross_attn.in_w + (size_t)D * D, d.nhead, 64, D, o.ca_kT, s));
-    o.ca_v = h->own_bf16(L.cross_attn.in_w + (size_t)2 * D * D, (size_t)D * D, s);
+    if (h->wlo)
+      HIPCHK(launch_transpose_heads_bf16(L.cross_attn.in_w + (size_t)D * D, d.nhead, 64, D, o.ca_kT + (size_t)D * D, s,
+                                         1));
+    o.ca_v = h->wlo ? h->own_bf16_hl(L.cross_attn.in_w + (size_t)2 * D * D, (size_t)D * D, s)
+                    : h->own_bf16(L.cross_attn.in_w + (size_t)2 * D * D, (size_t)D * D, s);
     o.ca_vb = h->own_f32(L.cross_attn.in_b + 2 * D, D, s);
-    o.ca_out = h->lin(L.cross_attn.out_w, L.cross_attn.out_b, D, D, s);
-    o.lin1 = h->lin(L.lin1_w, L.lin1_b, F, D, s);
-    o.lin2 = h->lin(L.lin2_w, L.lin2_b, D, F, s);
+    o.ca_out = h->dlin(L.cross_attn.out_w, L.cross_attn.out_b, D, D, s);
+    o.lin1 = h->dlin(L.lin1_w, L.lin1_b, F, D, s);
+    o.lin2 = h->dlin(L.lin2_w, L.lin2_b, D, F, s);
     o.n1 = h->ln(L.norm1, D, s);
     o.n2 = h->ln(L.norm2, D, s);
     o.n3 = h->ln(L.norm3, D, s);
@@ -533,6 +572,9 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
   bf16_t *patch = h->e_patch.as<bf16_t>(), *a = h->e_a.as<bf16_t>(), *qkv = h->e_qkv.as<bf16_t>(),
          *hb = h->e_h.as<bf16_t>();
   float* x = h->e_x.as<float>();
+  // range guard (DESIGN.md §3, f16 range contract): every LayerNorm and store-only GEMM output is fp16; a value
+  // that overflows (or a non-finite residual row, which any earlier overflow becomes) sets the sticky word
+  unsigned* rf = h->range_word();
   HIPCHK(launch_im2col_patches(img, B, 3, d.image, d.patch, patch, 0, NS_F16, s));
   {  // patch-embed GEMM: rows (b, p) -> x[b*T + 1 + p] with conv bias + pos[1 + p]
     GemmArgs ga = gemm_args();
@@ -547,7 +589,7 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
   }
   HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
   for (const VitLayer& L : h->vit) {
-    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s));
+    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s, rf));
     h->gemm16(a, V, L.qkv, M, qkv, 3 * V, EPI_NONE, OUT_SPLIT, s, hm);  // head-major [image][q|k|v x head][token][64]
     {
       const double flops = 4.0 * B * d.vit_heads * (double)T * T * 64;
@@ -557,12 +599,13 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
       });
     }
     h->gemm16(a, V, L.out, M, x, V, EPI_NONE, OUT_F32_RESID, s);
-    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s));
+    HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s, rf));
     h->gemm16(a, V, L.mlp0, M, hb, F, EPI_GELU, OUT_SPLIT, s);
     h->gemm16(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s);
   }
   // final LN on patch rows only (drop CLS), then projection 768 -> d_model
-  HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, V, a, V, 0, NS_F16, s));
+  HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, V, a, V, 0, NS_F16, s,
+                          rf));
   h->gemm16(a, V, h->proj, B * np, memory, Dm, EPI_NONE, OUT_F32, s);
 }
 
@@ -936,7 +979,11 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
   const int KS_D = 4, KS_F = 8;    // split-K of the K=512 and K=dim_ff residual GEMMs
   // one new token per sequence (the decode loops): the fused self-attention and feed-forward blocks
   // (decode.hip); the teacher-forced / padded forms keep the separate GEMM + attention launches
-  const bool fused = n_new == 1 && !klen && causal && D == 512 && H == 8 && F == 2048 && t0 < 64 && t0 < Lmax;
+  // hi/lo decoder weights run the unfused launches (whose GEMMs take W_lo), except for the train-mode dropout
+  // sampler, which keeps the fused blocks on W_hi (the differentiated log-probs use the fp32 weights themselves)
+  const bool fused = n_new == 1 && !klen && causal && D == 512 && H == 8 && F == 2048 && t0 < 64 && t0 < Lmax &&
+                     (!h->wlo || drop);
+  const bool wl = h->wlo && !fused;  // GEMMs add W_lo . X_hi
   REQUIRE(!drop || (fused && ns == 2 && !anc), "dropout needs the one-token decode blocks in a parity precision");
   for (int l = 0; l < d.n_dec_layers; ++l) {
     const DecLayer& L = h->dec[l];
@@ -961,17 +1008,22 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
                                        ns, s, dl, 2));
     } else {
       h->wgemm(b.a, D, b.aL, L.sa_qkv.w, D, L.sa_qkv.b, rows, 3 * D, D, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, WAVE_2x2,
-               1, 0, s);
+               1, 0, s, 1, 0, 0, 0, 0, wl ? L.sa_qkv.wl : nullptr);
       HIPCHK(launch_dec_self_attn(b.qkv, B, n_new, t0, H, b.kc + l * kv_layer, b.vc + l * kv_layer, Lmax, causal,
                                   0.125f, b.o, b.aL, ns, s, anc, klen));
       h->wgemm(b.o, D, b.aL, L.sa_out.w, D, nullptr, rows, D, D, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_D,
-               PS, s);
+               PS, s, 1, 0, 0, 0, 0, wl ? L.sa_out.wl : nullptr);
       HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_D, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
                                        ns, s));
     }
     // cross-attention block (key-absorbed)
     // per head, one launch: q_h = a Wq_h^T + bq_h, then qt[:, h*D:(h+1)*D] = q_h Wk_h (bf16 planes)
-    {
+    if (wl) {  // hi/lo weights: the same two products as two decode-GEMM launches (the second batched over heads)
+      h->wgemm(b.a, D, b.aL, L.ca_q.w, D, L.ca_q.b, rows, D, D, b.q, D, b.qL, EPI_NONE, OUT_SPLIT, WAVE_2x2, 1, 0, s,
+               1, 0, 0, 0, 0, L.ca_q.wl);
+      h->wgemm(b.q, D, b.qL, L.ca_kT, 64, nullptr, rows, D, 64, b.qt, (long)H * D, b.cL, EPI_NONE, OUT_SPLIT,
+               WAVE_2x2, 1, 0, s, H, 64, (long)D * 64, 0, D, L.ca_kT + (size_t)D * D);
+    } else {
       ChainArgs c{};
       c.X = b.a; c.ldx = D; c.x_lo = b.aL; c.x_hstride = 0;
       c.W1 = L.ca_q.w; c.b1 = L.ca_q.b;
@@ -990,7 +1042,12 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
     });
     // per head, one launch: o_h = c_h Wv_h^T + bv_h, then slab h = o_h Wo[:, h*64:(h+1)*64]^T; the
     // residual LN sums the H slabs (the output projection as a split-K over heads)
-    {
+    if (wl) {  // hi/lo weights: the value projection batched over heads into o, then a split-K out-projection
+      h->wgemm(b.c, (long)H * D, b.cL, L.ca_v, D, L.ca_vb, rows, 64, D, b.o, D, b.aL, EPI_NONE, OUT_SPLIT, WAVE_2x2,
+               1, 0, s, H, D, 64L * D, 64, 64, L.ca_v + (size_t)D * D);
+      h->wgemm(b.o, D, b.aL, L.ca_out.w, D, nullptr, rows, D, D, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_D,
+               PS, s, 1, 0, 0, 0, 0, L.ca_out.wl);
+    } else {
       ChainArgs c{};
       c.X = b.c; c.ldx = (long)H * D; c.x_lo = b.cL; c.x_hstride = D;
       c.W1 = L.ca_v; c.b1 = L.ca_vb;
@@ -1000,8 +1057,8 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       if (drop) c.b1_scale = b.gs;  // the value bias weighs sum_s P_s m_s under probability dropout
       h->chain(c, s, fused);
     }
-    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL, ns,
-                                     s, dl, 4));
+    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, wl ? KS_D : H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a,
+                                     b.aL, ns, s, dl, 4));
     // feed-forward block
     if (fused) {
       DecFfnArgs ff{};
@@ -1018,9 +1075,10 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
         HIPCHK(launch_residual_layernorm(b.x, rows, D, ln3.parts, ln3.nparts, PS, ln3.bias, ln3.w, ln3.b, ln3.eps, b.a,
                                          b.aL, ns, s, dl, 6));
     } else {
-      h->wgemm(b.a, D, b.aL, L.lin1.w, D, L.lin1.b, rows, F, D, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, WAVE_2x2, 1, 0, s);
+      h->wgemm(b.a, D, b.aL, L.lin1.w, D, L.lin1.b, rows, F, D, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, WAVE_2x2, 1, 0, s,
+               1, 0, 0, 0, 0, wl ? L.lin1.wl : nullptr);
       h->wgemm(b.hb, F, b.hL, L.lin2.w, F, nullptr, rows, D, F, b.part, D, 0, EPI_NONE, OUT_PARTIAL, WAVE_2x2, KS_F,
-               PS, s);
+               PS, s, 1, 0, 0, 0, 0, wl ? L.lin2.wl : nullptr);
       HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, KS_F, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a, b.aL,
                                        ns, s));
     }
@@ -1186,7 +1244,6 @@ void decode_beam(icap_handle* h, const float* mem, int B, int S, int max_len, in
   REQUIRE(B > 0 && max_len >= 2 && K >= 1 && K <= 15, "bad batch / max_len / beam size (1..15)");
   REQUIRE(max_len <= d.pe_len, "max_len exceeds the positional-encoding table (PositionalEncoding max_len)");
   REQUIRE(S > 0 && S <= 256, "memory length must be in [1, 256]");
-  REQUIRE(d.vocab <= 512, "beam search supports vocabularies up to 512 (beam_select keeps k x V log-probs in LDS)");
   const int D = d.d_model, rows = B * K, V = d.vocab;
   DecodeBufs b = dec_bufs(h, rows, B, max_len, S, rows);
   // beam state, carved from one buffer: seq[2] + anc[2] (rows x L ints), best_seq (B x L),
@@ -1534,6 +1591,8 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
       h->ns = desc->precision == ICAP_PREC_BF16 ? 1 : 2;
       h->i8 = desc->precision == ICAP_PREC_I8X2 && desc->kind == ICAP_KIND_VIT;
       h->f16 = desc->precision == ICAP_PREC_F16 && desc->kind == ICAP_KIND_VIT;
+      REQUIRE(desc->dec_weight_planes >= 0 && desc->dec_weight_planes <= 2, "dec_weight_planes must be 0, 1 or 2");
+      h->wlo = desc->dec_weight_planes == 2;
       // measured and rejected as the default: MLP-2 fed by the block-scaled GELU output takes
       // 1211 us (two-step fold: 256 VGPRs, 30 spilled) / 646 us (per-step fold, 64-column blocks) against
       // 467 us for the bf16x2 form
@@ -1755,6 +1814,19 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
     h->dws[0].fin.ensure((size_t)rows * 4);  // scratch ids
     ha.ids = h->dws[0].fin.as<int32_t>(); ha.ld_ids = 1; ha.id_col = 0;
     HIPCHK(launch_head(ha, s));
+  });
+}
+
+int icap_range_check(icap_handle* h, void* stream, int* overflowed) {
+  return guarded([&] {
+    REQUIRE(h && overflowed, "null handle / output");
+    hipStream_t s = (hipStream_t)stream;
+    unsigned* w = h->range_word();
+    unsigned v = 0;
+    HIPCHK(hipMemcpyAsync(&v, w, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (v) HIPCHK(hipMemsetAsync(w, 0, 16, s));
+    *overflowed = v ? 1 : 0;
   });
 }
 

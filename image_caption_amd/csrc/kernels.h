@@ -85,6 +85,9 @@ struct GemmArgs {
   // f16 = 1: A and W are single fp16 planes (nsplit 1), fp16 MFMA; OUT_SPLIT writes one fp16 plane
   // (launch_gemm_256 128 x 256 path only: the ICAP_PREC_F16 encoder GEMMs)
   int f16;
+  // fp16 range guard (gemm_f16p_kernel store-only fp16 outputs): set to 1 when a stored value is not finite in
+  // fp16 (|v| >= 65520 before rounding, or NaN); nullptr = unchecked
+  unsigned* range_flag;
 };
 // bytes of split_ws for split_slots block slots per XCD
 inline size_t gemm_split_ws_bytes(int split_slots) { return (size_t)8 * split_slots * 2 * 128 * 256 * 4; }
@@ -121,6 +124,9 @@ struct WaveGemmArgs {
   int M, N, K, nsplit, batch, ksplit;
   long part_stride;
   int epi, out, tile;
+  // hi/lo weights (launch_gemm_dec only): W_lo = bf16(W - W_hi), same layout and batch stride as W; the
+  // product then adds W_lo . X_hi, so the weight enters with 16 significand bits (fp32 checkpoints)
+  const bf16_t* W_lo;
 };
 inline WaveGemmArgs wave_args() {
   WaveGemmArgs g{};
@@ -188,7 +194,7 @@ hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s);
 hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_group, long in_stride,
                             long in_off, const float* w, const float* b, float eps, float* out_f32,
                             long ld_f32, bf16_t* out_bf, long ld_bf, long bf_lo, int nsplit,
-                            hipStream_t s);
+                            hipStream_t s, unsigned* range_flag = nullptr);
 
 // x = LN(x + sum_{s<nparts} parts[s*part_stride + row*D + col] + bias) in place (fp32), plus planes.
 hipError_t launch_residual_layernorm(float* x, int rows, int D, const float* parts, int nparts, long part_stride,
@@ -243,7 +249,8 @@ hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int 
 hipError_t launch_planes_to_f32(const bf16_t* src, long lo, long n, int nsplit, float* dst, hipStream_t s);
 hipError_t launch_f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);
 hipError_t launch_f32_to_f16(const float* src, bf16_t* dst, long n, hipStream_t s);
-hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s);
+hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s,
+                                       int lo_plane = 0);
 
 // Encoder self-attention (non-causal) over N tokens, heads of 64, MFMA bf16 (nsplit 1 or 2).
 // head_major: qkv written with GemmArgs::hm_n = N (N in (64, 256])

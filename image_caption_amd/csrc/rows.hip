@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
                                                         const float* __restrict__ w,
                                                         const float* __restrict__ b, float eps,
                                                         float* out_f32, long ld_f32, bf16_t* out_bf,
-                                                        long ld_bf, long bf_lo, int nsplit) {
+                                                        long ld_bf, long bf_lo, int nsplit, unsigned* range_flag) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -50,6 +50,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   for (int i = 0; i < PER; ++i) { const float d = v[i] - mean; q += d * d; }
   const float var = wave_sum(q) / (float)D;
   const float rstd = 1.0f / sqrtf(var + eps);
+  bool bad = false;  // fp16 outputs: a value that is not finite in fp16 (a non-finite residual row included)
 #pragma unroll
   for (int c = 0; c < PER / 4; ++c) {
     const int col = c * 256 + lane * 4;
@@ -58,7 +59,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     for (int k = 0; k < 4; ++k) y[k] = (v[c * 4 + k] - mean) * rstd * wv[k] + bv[k];
     if (out_f32) *(f32x4*)(out_f32 + (long)row * ld_f32 + col) = y;
     if (out_bf && nsplit == NS_F16) {
-      *(u32x2*)(out_bf + (long)row * ld_bf + col) = pack16x4<true>(y);
+      const u32x2 pk = pack16x4<true>(y);
+      bad |= f16_pair_nonfinite(pk[0]) || f16_pair_nonfinite(pk[1]);
+      *(u32x2*)(out_bf + (long)row * ld_bf + col) = pk;
     } else if (out_bf) {
       bf16_t h[4], l[4];
 #pragma unroll
@@ -69,6 +72,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
         *(u32x2*)(o + bf_lo) = (u32x2){(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
     }
   }
+  if (range_flag && __any(bad) && lane == 0) range_flag_set(range_flag);
 }
 
 // layernorm_kernel's row statistics, output as int8 two-slice planes + the row scale (one wave per row)
@@ -311,13 +315,17 @@ __global__ void f32_to_bf16_kernel(const float* src, bf16_t* dst, long n) {
 }
 
 // wk rows [h*hd + i][d] (i < hd, d < D)  ->  dst[h][d][i]   (W_h^T packing for the key absorption)
-__global__ void transpose_heads_kernel(const float* wk, int H, int hd, int D, bf16_t* dst) {
+// lo_plane: write bf16(w - bf16(w)) instead (the low plane of hi/lo decoder weights)
+__global__ void transpose_heads_kernel(const float* wk, int H, int hd, int D, bf16_t* dst, int lo_plane) {
   const long total = (long)H * hd * D;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int ii = (int)(i % hd);
     const long r = i / hd;
     const int d = (int)(r % D), h = (int)(r / D);
-    dst[i] = f2bf(wk[((long)h * hd + ii) * D + d]);
+    const float w = wk[((long)h * hd + ii) * D + d];
+    bf16_t hi, lo;
+    split_bf(w, hi, lo);
+    dst[i] = lo_plane ? lo : hi;
   }
 }
 
@@ -331,17 +339,17 @@ inline int grid_for(long n, int block = 256) {
 hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_group, long in_stride,
                             long in_off, const float* w, const float* b, float eps, float* out_f32,
                             long ld_f32, bf16_t* out_bf, long ld_bf, long bf_lo, int nsplit,
-                            hipStream_t s) {
+                            hipStream_t s, unsigned* range_flag) {
   dim3 grid((rows + 3) / 4);
   if (D == 512)
     hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off,
-                       w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit);
+                       w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit, range_flag);
   else if (D == 768)
     hipLaunchKernelGGL(layernorm_kernel<12>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off,
-                       w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit);
+                       w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit, range_flag);
   else if (D == 256)
     hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, s, x, ldx, rows, in_group, in_stride, in_off,
-                       w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit);
+                       w, b, eps, out_f32, ld_f32, out_bf, ld_bf, bf_lo, nsplit, range_flag);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -442,7 +450,9 @@ hipError_t launch_f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t
   return hipGetLastError();
 }
 
-hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s) {
-  hipLaunchKernelGGL(transpose_heads_kernel, dim3(grid_for((long)H * hd * D)), dim3(256), 0, s, wk, H, hd, D, dst);
+hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s,
+                                       int lo_plane) {
+  hipLaunchKernelGGL(transpose_heads_kernel, dim3(grid_for((long)H * hd * D)), dim3(256), 0, s, wk, H, hd, D, dst,
+                     lo_plane);
   return hipGetLastError();
 }

@@ -72,7 +72,8 @@ class Engine:
     """One packed model on one device.  Not thread-safe (a handle per thread)."""
 
     def __init__(self, state_dict: Dict[str, torch.Tensor], kind: str, config: dict,
-                 precision: str = DEFAULT_PRECISION, device: torch.device | str | None = None):
+                 precision: str = DEFAULT_PRECISION, device: torch.device | str | None = None,
+                 decoder_weight_planes: Optional[int] = None):
         self.lib = _lib.load()
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}")
@@ -85,12 +86,23 @@ class Engine:
         self.precision = precision
         self.d_model = int(config.get("d_model", 512))
         self.nhead = int(config.get("nhead", 8))
+        # decoder GEMM weights as bf16 (1) or bf16 hi/lo (2); None = 2 exactly when some decoder
+        # GEMM weight is not bf16-representable (an fp32 checkpoint), so the logits keep the 1e-3 bar.  Fixed at
+        # creation: update_weights re-packs into the same layout.
+        self.dec_weight_planes = decoder_weight_planes
         desc, keep = self._desc(state_dict)
         handle = ctypes.c_void_p()
         with torch.cuda.device(device):
             check(self.lib.icap_create(ctypes.byref(desc), stream_ptr(device), ctypes.byref(handle)), "icap_create")
         self.handle = handle
         del keep
+
+    def dropout_sampling_ok(self, max_len: int) -> bool:
+        """Whether `sample(..., dropout=...)` can run: the train-mode masks live in the fused one-token decode
+        blocks (csrc/decode.hip), which serve d_model 512 / 8 heads / dim_feedforward 2048, a parity precision
+        (two activation planes: not "bf16") and decode positions below 64 (max_len <= 65)."""
+        return (self.precision != "bf16" and self.d_model == 512 and self.nhead == 8 and self.dim_ff == 2048
+                and 2 <= max_len <= min(65, self.pe_len))
 
     def update_weights(self, state_dict: Dict[str, torch.Tensor], decoder: bool = True, encoder: bool = True) -> None:
         """Re-pack the decoder and/or encoder weights of `state_dict` (same shapes) into this handle's
@@ -125,9 +137,18 @@ class Engine:
                                sd[p + ".linear2.weight"].data_ptr(), sd[p + ".linear2.bias"].data_ptr(),
                                _ln(sd, p + ".norm1"), _ln(sd, p + ".norm2"), _ln(sd, p + ".norm3"))
         dim_ff = sd["decoder.transformer_decoder.layers.0.linear1.weight"].shape[0]
+        if self.dec_weight_planes is None:
+            gemm_w = [v for k, v in sd.items() if k.startswith("decoder.transformer_decoder.")
+                      and k.endswith(("in_proj_weight", "out_proj.weight", "linear1.weight", "linear2.weight"))]
+            exact = all(torch.equal(w, w.to(torch.bfloat16).float()) for w in gemm_w)
+            self.dec_weight_planes = 1 if exact else 2
+        if self.dec_weight_planes not in (1, 2):
+            raise ValueError("decoder_weight_planes must be 1 (bf16) or 2 (bf16 hi/lo)")
         desc = ModelDesc()
+        desc.dec_weight_planes = self.dec_weight_planes
         desc.precision = _lib.PRECISIONS[self.precision]
         desc.d_model, desc.nhead, desc.dim_ff = self.d_model, self.nhead, dim_ff
+        self.dim_ff = dim_ff
         desc.n_dec_layers, desc.vocab, desc.pe_len = n_dec, self.vocab, self.pe_len
         desc.emb = emb.data_ptr()
         desc.pe = sd["decoder.pos_encoder.pe"].data_ptr()
@@ -209,6 +230,17 @@ class Engine:
             except Exception:
                 pass
             self.handle = None
+
+    def range_overflowed(self) -> bool:
+        """fp16 range guard of the f16 ViT encoder (icap_range_check): True when a LayerNorm /
+        Q,K,V / GELU output stored as fp16 since the last check was not finite (|v| >= 65520 or NaN), i.e. the
+        memory of those encodes is not trustworthy and must be recomputed in bf16x2.  Synchronises the
+        engine's current stream; always False for precisions without fp16 activations."""
+        if self.precision != "f16" or self.kind != "vit":
+            return False
+        out = ctypes.c_int(0)
+        check(self.lib.icap_range_check(self.handle, stream_ptr(self.device), ctypes.byref(out)), "icap_range_check")
+        return bool(out.value)
 
     # ------------------------------------------------------------------ encoders
     def encode(self, images: torch.Tensor) -> torch.Tensor:

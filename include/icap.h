@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define ICAP_ABI_VERSION 2
+#define ICAP_ABI_VERSION 3
 
 #define ICAP_KIND_VIT 0   /* ViTTransformerCaptioning  (models/vit_transformer_model.py:185)  */
 #define ICAP_KIND_GRID 1  /* GridTransformerCaptioning (models/grid_transformer_model.py:161) */
@@ -87,6 +87,10 @@ typedef struct {
    * conv2+bn2 (3x3, the stage stride on j == 0), conv3+bn3 (1x1); trunk_blocks = blocks per stage. */
   int n_trunk, trunk_blocks[4];
   const icap_conv_bn_w* trunk;
+  /* decoder GEMM weight planes: 0 or 1 = bf16 (exact for bf16-representable weights), 2 = bf16 hi/lo
+   * (hi = bf16(W), lo = bf16(W - hi): 16 significand bits, for fp32 checkpoints whose weights are not
+   * bf16-exact; the decode then runs the unfused launches, each GEMM adding W_lo . X_hi - DESIGN.md §3) */
+  int dec_weight_planes;
 } icap_model_desc;
 
 int icap_abi_version(void);
@@ -218,6 +222,14 @@ int icap_decoder_forward(icap_handle* h, const int32_t* tgt, int B, int T, const
  * steps into one graph that later calls replay (kernel timing via icap_profile_* is recorded on
  * the eager calls only). */
 int icap_set_graphs(icap_handle* h, int enable);
+
+/* fp16 range guard of ICAP_PREC_F16.  The reference encoder computes in fp32
+ * (models/vit_transformer_model.py:71-100); the f16 precision stores LayerNorm outputs, Q/K/V and the GELU
+ * output as fp16 (max 65504).  Those kernels set a sticky device word when a value they store is not finite
+ * in fp16 (an overflow, or a non-finite residual row that an earlier overflow turned into); this call
+ * synchronises `stream`, returns the word in *overflowed (0/1) and clears it.  On 1 the memory of the encodes
+ * since the last check is not trustworthy: re-encode with a 16-bit-significand precision (bf16x2). */
+int icap_range_check(icap_handle* h, void* stream, int* overflowed);
 
 /* Number of independent decode chains a batch is split into (1..4, default 2; used from 128 rows
  * per chain): the chains are parallel branches of the captured decode graph. */

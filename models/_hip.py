@@ -49,6 +49,7 @@ class HipRouted:
         object.__setattr__(self, "hip_backend", backend)
         object.__setattr__(self, "hip_precision", precision)
         object.__setattr__(self, "_hip_cache", None)
+        object.__setattr__(self, "_hip_cache_fb", None)
 
     def use_hip(self, x: torch.Tensor, *, grad_ok: bool = False) -> bool:
         if self.hip_backend == "torch":
@@ -70,18 +71,35 @@ class HipRouted:
         new = self.__class__.__new__(self.__class__)
         memo[id(self)] = new
         for k, v in self.__dict__.items():
-            object.__setattr__(new, k, None if k == "_hip_cache" else copy.deepcopy(v, memo))
+            object.__setattr__(new, k, None if k in ("_hip_cache", "_hip_cache_fb") else copy.deepcopy(v, memo))
         for name in ("encoder", "decoder"):
             child = getattr(new, name, None)
             if isinstance(child, torch.nn.Module):
                 attach_owner(child, new)
         return new
 
-    def hip_engine(self, device: torch.device):
+    def hip_engine(self, device: torch.device, precision: Optional[str] = None):
         """The packed engine of this module's current weights.  After an optimizer step only the parts
         whose tensors changed (decoder / encoder, by data_ptr and version) are re-packed in place
         (icap_update_weights): frozen encoder weights are not re-packed and the captured decode graphs
-        survive, so an SCST training loop keeps replaying them."""
+        survive, so an SCST training loop keeps replaying them.  `precision` other than the model's
+        hip_precision: a second engine kept beside it (the f16 range guard's bf16x2 re-encode)."""
+        if precision is None or precision == self.hip_precision:
+            return self._engine_slot("_hip_cache", self.hip_precision, device)
+        return self._engine_slot("_hip_cache_fb", precision, device)
+
+    def checked_encode(self, images: torch.Tensor):
+        """(engine, memory) of `images`; if the f16 encoder's range guard fired (an fp16 activation overflowed,
+        DESIGN.md §3) the memory is recomputed by a bf16x2 engine of the same weights, which is returned
+        instead.  Synchronises the stream once (f16 only)."""
+        eng = self.hip_engine(images.device)
+        mem = eng.encode(images)
+        if eng.range_overflowed():
+            eng = self.hip_engine(images.device, precision="bf16x2")
+            mem = eng.encode(images)
+        return eng, mem
+
+    def _engine_slot(self, attr: str, precision: str, device: torch.device):
         from image_caption_amd.engine import Engine
 
         sd = self.state_dict()
@@ -93,16 +111,16 @@ class HipRouted:
                          if torch.is_tensor(t) and k.startswith("decoder.") == prefix_dec
                          and not k.endswith("num_batches_tracked"))
 
-        base = (str(device), self.hip_precision)
+        base = (str(device), precision)
         kd, ke = key(True), key(False)
-        cache = self._hip_cache
+        cache = getattr(self, attr, None)
         if cache is not None and cache[0] == base:
             eng = cache[3]
             dec, enc = cache[1] != kd, cache[2] != ke
             if dec or enc:
                 eng.update_weights(sd, decoder=dec, encoder=enc)
-                object.__setattr__(self, "_hip_cache", (base, kd, ke, eng))
+                object.__setattr__(self, attr, (base, kd, ke, eng))
             return eng
-        eng = Engine(sd, self._hip_kind, {"d_model": self.d_model}, precision=self.hip_precision, device=device)
-        object.__setattr__(self, "_hip_cache", (base, kd, ke, eng))
+        eng = Engine(sd, self._hip_kind, {"d_model": self.d_model}, precision=precision, device=device)
+        object.__setattr__(self, attr, (base, kd, ke, eng))
         return eng

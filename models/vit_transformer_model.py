@@ -43,7 +43,7 @@ class VisionTransformerEncoder(nn.Module):
     def forward(self, images):
         owner = owner_of(self)
         if owner is not None and not self.training and owner.use_hip(images):
-            return owner.hip_engine(images.device).encode(images)
+            return owner.checked_encode(images)[1]  # f16 range guard: bf16x2 re-encode on overflow
         x = self.vit._process_input(images)
         x = torch.cat([self.vit.class_token.expand(x.shape[0], -1, -1), x], dim=1)
         x = self.vit.encoder(x)
@@ -92,7 +92,11 @@ class ViTTransformerCaptioning(HipRouted, nn.Module):
         with torch.no_grad():
             if self.use_hip(images):
                 eng = self.hip_engine(images.device)
-                return eng.greedy(eng.encode(images), start_token, end_token, max_len)
+                ids = eng.greedy(eng.encode(images), start_token, end_token, max_len)
+                if eng.range_overflowed():  # an fp16 encoder activation overflowed: bf16x2 again
+                    eng = self.hip_engine(images.device, precision="bf16x2")
+                    ids = eng.greedy(eng.encode(images), start_token, end_token, max_len)
+                return ids
             return greedy_torch(self, images, start_token, end_token, max_len)
 
     def _beam_search(self, images, start_token, end_token, max_len, beam_size=5):

@@ -53,29 +53,120 @@ def test_large_vocabulary(cuda, vocab):
 
 
 def test_fp32_weights_not_bf16_exact(cuda):
-    """The engine packs decoder / encoder GEMM weights to bf16 once: with fp32 weights that are not
-    bf16-exact (a real checkpoint) the logits carry that rounding (2^-9 relative per weight).  Measured
-    against the fp32 oracle on the same weights: see DESIGN.md §3 for the bound asserted here."""
+    """A real fp32 checkpoint's decoder weights are not bf16-exact: the engine then packs them as bf16 hi/lo planes
+    (dec_weight_planes = 2, chosen automatically) and every decoder GEMM adds W_lo . X_hi, so the logits meet the
+    1e-3 north-star bar against the fp32 oracle on the same weights (bf16 weights alone: 1.1e-2).
+    The f16 encoder's memory keeps its fp16-operand bound (4e-3)."""
     from image_caption_amd.engine import Engine
 
+    assert Engine(W.to_torch(W.vit_state_dict(0)), "vit", {}, device=cuda).dec_weight_planes == 1
     sd = W.to_torch(W.vit_state_dict(1, bf16_exact=False))
     imgs = torch.from_numpy(W.synthetic_images(4, seed=6))
     eng = Engine(sd, "vit", {}, device=cuda)
+    assert eng.dec_weight_planes == 2
     mem = eng.encode(imgs.to(cuda)).cpu()
     ref_mem = O.vit_encode(sd, imgs)
     ids = eng.greedy(ref_mem.to(cuda), W.START_TOKEN, W.END_TOKEN, 30).cpu()
     ref_ids, tr = O.greedy_from_memory(sd, ref_mem, W.START_TOKEN, W.END_TOKEN, 30, return_trace=True)
     tf = eng.decoder_forward(ref_ids[:, :-1].to(cuda), ref_mem.to(cuda), causal=True).cpu()
     lerr = (tf - O.teacher_forced_logits(sd, ref_mem, ref_ids)).abs().max().item()
+    raw, lg = eng.greedy_raw(ref_mem.to(cuda), W.START_TOKEN, W.END_TOKEN, 30, want_logits=True)
+    L = min(raw.shape[1], ref_ids.shape[1])
+    diff = np.nonzero((raw.cpu().long()[:, :L] != ref_ids[:, :L]).any(0).numpy())[0]
+    n = min(int(diff[0]) if len(diff) else L, lg.shape[0], tr.shape[0])  # steps whose prefixes agree
+    serr = (lg.cpu()[:n] - tr[:n]).abs().max().item()  # the KV-cached decode's own step logits
     merr = (mem - ref_mem).abs().max().item()
-    L = min(ids.shape[1], ref_ids.shape[1])
-    agree = (ids[:, :L].long() == ref_ids[:, :L]).float().mean().item()
     margin = O.top2_margin(tr).min().item()
-    print(f"fp32 weights: memory err {merr:.2e}, decoder logit err {lerr:.2e}, token agreement {agree:.3f}, "
+    print(f"fp32 weights: memory err {merr:.2e}, teacher-forced logit err {lerr:.2e}, step logit err {serr:.2e}, "
           f"min reference margin {margin:.2e}")
-    assert merr < 5e-2 and lerr < 5e-2
-    # ids identical up to the first step whose reference top-2 margin is within the error band
+    assert merr < 4e-3 and lerr < 1e-3 and serr < 1e-3
+    # ids identical up to the first step whose reference top-2 margin is within twice the logit tolerance
     for r in range(ids.shape[0]):
-        close = np.nonzero(O.top2_margin(tr[:, r]).numpy() < 4 * lerr)[0]
+        close = np.nonzero(O.top2_margin(tr[:, r]).numpy() < 2e-3)[0]
         upto = (close[0] if len(close) else tr.shape[0]) + 1
         assert torch.equal(ids[r, :upto].long(), ref_ids[r, :upto]), r
+    # beam search and sampling run on the same hi/lo weights
+    bids, blens = eng.beam(ref_mem.to(cuda), W.START_TOKEN, W.END_TOKEN, 12, 3)
+    for i in range(2):
+        ref, bm = O.beam_from_memory(sd, ref_mem[i:i + 1], W.START_TOKEN, W.END_TOKEN, 12, 3, False,
+                                     return_margins=True)
+        if bm > 2e-3:
+            assert int(blens[i]) == ref.shape[1] and np.array_equal(bids[i, :ref.shape[1]].cpu().numpy(),
+                                                                   ref[0].numpy()), i
+
+
+@pytest.mark.parametrize("grid_variant", [False, True])
+def test_beam_search_large_vocabulary(cuda, grid_variant):
+    """Beam search with V = 1000 (above the 512 the k x V LDS candidate array holds): beam_select takes each live
+    row's top-k by k passes over its logits, then the top-k of those k x k candidates (the global top-k lies in
+    their union).  Against the oracle's per-image beam search (vit:327-420 / grid:253-322), with an <end>-biased
+    head so beams finish and are pruned; exact wherever the oracle's selection margin exceeds 1e-4.  The ViT
+    case runs through the drop-in model.generate(method='beam_search')."""
+    from models.vit_transformer_model import build_model
+
+    V = 1000
+    sd = W.to_torch(W.vit_state_dict(2, vocab_size=V))
+    b = sd["decoder.fc_out.bias"].clone()
+    b[W.END_TOKEN] += 1.5
+    sd["decoder.fc_out.bias"] = b
+    m = build_model(V, {"pretrained_vit": False})
+    m.load_state_dict(sd)
+    m = m.to(cuda)
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=11)).to(cuda)
+    eng = m.hip_engine(cuda)
+    with torch.no_grad():
+        mem = eng.encode(imgs)
+    ids, lens = eng.beam(mem, W.START_TOKEN, W.END_TOKEN, 20, 4, grid_variant=grid_variant)
+    checked = 0
+    for i in range(4):
+        ref, margin = O.beam_from_memory(sd, mem[i:i + 1].cpu(), W.START_TOKEN, W.END_TOKEN, 20, 4, grid_variant,
+                                         return_margins=True)
+        if margin > 1e-4:
+            n = ref.shape[1]
+            assert int(lens[i]) == n and np.array_equal(ids[i, :n].cpu().numpy(), ref[0].numpy()), i
+            checked += 1
+    assert checked >= 2
+    if not grid_variant:  # the drop-in surface: ViT generate() searches with beam 5, one image per call (vit:287)
+        out = m.generate(imgs[:1], W.START_TOKEN, W.END_TOKEN, max_len=20, method="beam_search")
+        one, ln = eng.beam(mem[:1], W.START_TOKEN, W.END_TOKEN, 20, 5)
+        assert out.is_cuda and out.dtype == torch.long and out.shape == (1, int(ln[0]))
+        assert np.array_equal(out[0].cpu().numpy(), one[0, :int(ln[0])].cpu().numpy())
+
+
+@pytest.mark.parametrize("site", ["gelu", "layernorm"])
+def test_f16_range_guard(cuda, site):
+    """The f16 encoder stores LayerNorm outputs, Q/K/V and the GELU output as fp16 (max 65504); the reference
+    is fp32 (vit:71-100).  Weights scaled so that one layer's GELU output (mlp.0 x 1e5) or LayerNorm output
+    (ln_1 x 2e4) passes 65504 must set the range word (icap_range_check); the drop-in generate() then
+    re-encodes in bf16x2, whose output it returns, and the guard stays silent on ordinary weights."""
+    from image_caption_amd.engine import Engine
+    from models.vit_transformer_model import build_model
+
+    base = W.to_torch(W.vit_state_dict(0))
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=4)).to(cuda)
+    clean = Engine(base, "vit", {}, device=cuda)
+    clean.encode(imgs)
+    assert not clean.range_overflowed()
+    sd = dict(base)
+    key, f = (("encoder.vit.encoder.layers.encoder_layer_5.mlp.0.weight", 1e5) if site == "gelu"
+              else ("encoder.vit.encoder.layers.encoder_layer_5.ln_1.weight", 2e4))
+    sd[key] = sd[key] * f
+    eng = Engine(sd, "vit", {}, device=cuda)
+    mem16 = eng.encode(imgs)
+    assert eng.range_overflowed()
+    assert not eng.range_overflowed()  # read-and-clear
+    safe = Engine(sd, "vit", {}, precision="bf16x2", device=cuda)
+    mem2 = safe.encode(imgs)
+    assert torch.isfinite(mem2).all() and not safe.range_overflowed()
+    ref_ids = safe.greedy(mem2, W.START_TOKEN, W.END_TOKEN, 20)
+    m = build_model(W.VOCAB_SIZE, {"pretrained_vit": False})
+    m.load_state_dict(sd)
+    m = m.to(cuda)
+    out = m.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=20)
+    assert m._hip_cache_fb is not None and torch.equal(out, ref_ids)  # the bf16x2 re-encode's result
+    with torch.no_grad():
+        assert torch.equal(m.encoder(imgs), mem2)
+    if site == "gelu":  # the bf16x2 memory against the fp32 oracle (huge but finite residual stream)
+        ref_mem = O.vit_encode(sd, imgs.cpu())
+        assert (mem2.cpu() - ref_mem).abs().max().item() < 1e-2 * max(1.0, ref_mem.abs().max().item())
+    del mem16

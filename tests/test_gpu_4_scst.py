@@ -206,7 +206,9 @@ def test_engine_refresh_in_place(cuda, part):
         assert eng2 is eng
         got = m.generate(imgs, 107, 108, 30)
         mem = eng.encode(imgs)
-        fresh = Engine(m.state_dict(), "vit", {}, device=cuda)
+        # the refreshed handle keeps the weight layout it was created with (bf16 decoder weights): compare with a
+        # fresh engine of the same layout (left to itself it would pick hi/lo planes for these non-bf16 weights)
+        fresh = Engine(m.state_dict(), "vit", {}, device=cuda, decoder_weight_planes=eng.dec_weight_planes)
         mem_f = fresh.encode(imgs)
         assert torch.equal(mem, mem_f)
         want = fresh.greedy(mem_f, 107, 108, 30)
@@ -214,3 +216,24 @@ def test_engine_refresh_in_place(cuda, part):
         lg = eng.decoder_forward(want[:, :-1], mem, causal=True)
         lg_f = fresh.decoder_forward(want[:, :-1], mem_f, causal=True)
         assert torch.equal(lg, lg_f)
+
+
+def test_scst_dropout_outside_fused_blocks_uses_reference_loop(cuda):
+    """train-mode dropout sampling needs the fused one-token decode blocks (max_len <= 65, d 512,
+    8 heads, dim_ff 2048, a parity precision).  Outside them SCSTLoss samples with the reference's own
+    PyTorch loop (torch dropout) instead of failing mid-decode; backend='hip' says so up front."""
+    from utils.scst_loss import SCSTLoss
+
+    B, L = 2, 70
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=2)).to(cuda)
+    uni = torch.rand(L - 1, B, generator=torch.Generator().manual_seed(3)).to(cuda)
+    m = _vit_model(cuda, dropout=0.1)
+    m.train()
+    assert not m.hip_engine(cuda).dropout_sampling_ok(L) and m.hip_engine(cuda).dropout_sampling_ok(30)
+    ids, lp = SCSTLoss()._sample_with_log_probs(m, imgs, 107, 108, L, cuda, uni)
+    assert ids.shape[0] == B and lp.shape == (B, ids.shape[1] - 1) and lp.requires_grad
+    assert torch.isfinite(lp).all()
+    mh = _vit_model(cuda, backend="hip", dropout=0.1)
+    mh.train()
+    with pytest.raises(ValueError):
+        SCSTLoss()._sample_with_log_probs(mh, imgs, 107, 108, L, cuda, uni)

@@ -121,6 +121,13 @@ class SCSTLoss(nn.Module):
         if images.is_cuda and getattr(model, "hip_backend", "torch") != "torch":
             eng = model.hip_engine(images.device)
             p = decoder_dropout(model.decoder)
+            if p > 0 and not eng.dropout_sampling_ok(max_len):
+                # train-mode dropout outside what the fused HIP decode blocks serve (other decoder widths,
+                # precision "bf16", max_len > 65): the reference's own PyTorch loop with torch's dropout
+                if getattr(model, "hip_backend", "auto") == "hip":
+                    raise ValueError("backend='hip': train-mode dropout sampling needs d_model 512, 8 heads, "
+                                     "dim_feedforward 2048, a parity precision and max_len <= 65")
+                return self._sample_torch(model, images, start_token, end_token, max_len, uniforms)
             if p > 0 and dropout_seed is None:
                 dropout_seed = int(torch.randint(0, 2**31 - 1, (1,)).item())
             drop = (p, int(dropout_seed or 0))
@@ -155,8 +162,11 @@ class SCSTLoss(nn.Module):
                 elif want_grad and vit_trunk_frozen(model):
                     # the frozen ViT's output too: the recompute below applies only the trainable projection
                     mem, vfeats = eng.encode_vit_features(images)
+                    if eng.range_overflowed():  # f16 range guard: bf16x2 re-encode
+                        eng = model.hip_engine(images.device, precision="bf16x2")
+                        mem, vfeats = eng.encode_vit_features(images)
                 else:  # ViT, or a Grid model whose trunk is in eval mode: the whole encoder on HIP
-                    mem = eng.encode(images)
+                    eng, mem = model.checked_encode(images)  # f16 range guard: bf16x2 re-encode on overflow
                 ids32, logp = eng.sample(mem, uniforms, start_token, end_token, max_len, dropout=drop)
             ids = ids32.long()
             L = sample_stop_length(ids, end_token)
