@@ -76,6 +76,7 @@ class ModelDesc(ctypes.Structure):
         ("n_trunk", c_int), ("trunk_blocks", c_int * 4),
         ("trunk", POINTER(ConvBnW)),
         ("dec_weight_planes", c_int),
+        ("enc_pe_len", c_int),
     ]
 
 
@@ -114,6 +115,9 @@ SIGNATURES = {
     "icap_set_graphs": (c_int, [c_void_p, c_int]),
     "icap_set_decode_chains": (c_int, [c_void_p, c_int]),
     "icap_range_check": (c_int, [c_void_p, c_void_p, POINTER(c_int)]),
+    "icap_grid_tokens": (c_int, [c_void_p, c_int, c_int, POINTER(c_int)]),
+    "icap_encode_grid_hw": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "icap_encode_grid_tail_n": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "icap_profile_enable": (c_int, [c_void_p, c_int]),
     "icap_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(c_long),
                                   POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),

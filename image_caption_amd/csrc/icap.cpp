@@ -163,6 +163,7 @@ struct icap_handle {
   std::vector<VitLayer> vit;
   // grid
   float* enc_pe = nullptr;
+  int enc_pe_rows = 0;  // rows of the packed encoder PE table: the most grid tokens an image may have
   std::vector<EncLayer> enc;
   std::vector<Conv> trunk;  // stem, then per bottleneck block [downsample] conv1 conv2 conv3
   bf16_t* zero = nullptr;   // 256 zero bytes: the implicit-GEMM source of out-of-image taps
@@ -525,7 +526,8 @@ void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PA
       HIPCHK(hipMemsetAsync(h->zero, 0, 256, s));
       REQUIRE(h->trunk.back().cout == d.cnn_dim, "trunk output channels != projection input");
     }
-    h->enc_pe = h->own_f32(d.enc_pe, (size_t)d.grid_tokens * D, s);
+    h->enc_pe_rows = std::max(d.grid_tokens, d.enc_pe_len);
+    h->enc_pe = h->own_f32(d.enc_pe, (size_t)h->enc_pe_rows * D, s);
     for (int i = 0; i < d.n_enc_layers; ++i) {
       const icap_enc_layer_w& L = d.enc_layers[i];
       EncLayer o;
@@ -700,9 +702,11 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
 
 // Grid tail over trunk features given as row planes [B*49][C] (row = b*49 + h*7 + w, i.e. the
 // flatten(2).permute(0, 2, 1) order of grid:100-101): 1x1 projection + PE, 6 post-LN layers.
-void encode_grid_rows(icap_handle* h, const bf16_t* rows, long rL, int B, float* memory, hipStream_t s) {
+// N: tokens per image (the trunk's output grid h x w; 49 at 224 x 224), at most the packed PE table's rows
+void encode_grid_rows(icap_handle* h, const bf16_t* rows, long rL, int B, int N, float* memory, hipStream_t s) {
   const icap_model_desc& d = h->d;
-  const int D = d.d_model, N = d.grid_tokens, M = B * N, C = d.cnn_dim, ns = h->ns;
+  REQUIRE(N >= 1 && N <= h->enc_pe_rows, "grid tokens exceed the encoder's positional-encoding table (max_len)");
+  const int D = d.d_model, M = B * N, C = d.cnn_dim, ns = h->ns;
   h->e_a.ensure((size_t)M * D * 2 * ns);
   h->e_qkv.ensure((size_t)M * 3 * D * 2 * ns);
   h->e_h.ensure((size_t)M * d.dim_ff * 2 * ns);
@@ -723,14 +727,14 @@ void encode_grid_rows(icap_handle* h, const bf16_t* rows, long rL, int B, float*
     enc_layer_postln(h, L, B, N, memory, a, h->e_qkv.as<bf16_t>(), h->e_h.as<bf16_t>(), s);
 }
 
-void encode_grid_tail(icap_handle* h, const float* feats, int B, float* memory, hipStream_t s) {
+void encode_grid_tail(icap_handle* h, const float* feats, int B, int N, float* memory, hipStream_t s) {
   const icap_model_desc& d = h->d;
-  const int N = d.grid_tokens, M = B * N, C = d.cnn_dim, ns = h->ns;
+  const int M = B * N, C = d.cnn_dim, ns = h->ns;
   h->e_patch.ensure((size_t)M * C * 2 * ns);
   bf16_t* rows = h->e_patch.as<bf16_t>();
   const long rL = (long)M * C;
   HIPCHK(launch_nchw_to_rows(feats, B, C, N, rows, rL, ns, s));
-  encode_grid_rows(h, rows, rL, B, memory, s);
+  encode_grid_rows(h, rows, rL, B, N, memory, s);
 }
 
 // One trunk convolution as a GEMM: rows = output pixels (NHWC), out = 2 bf16 planes of
@@ -784,51 +788,83 @@ void trunk_conv(icap_handle* h, const Conv& c, const bf16_t* A, long a_ld, long 
 // Images go through in chunks of TRUNK_CHUNK so the stem GEMM grid and the workspaces stay bounded.
 constexpr int TRUNK_CHUNK = 256;
 
-// feats (optional): the trunk output as fp32 rows (B, 49, cnn_dim) - self.cnn(images).flatten(2).permute(0, 2, 1)
-// bt.bn (train mode): batch-statistics BatchNorm over the whole batch, so B <= TRUNK_CHUNK (one chunk)
-void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStream_t s, float* feats = nullptr,
-                 const BnTrain& bt = BnTrain()) {
+// Trunk output grid of an IH x IW image (torchvision ResNet: 7x7/2 stem pad 3, 3x3/2 max-pool pad 1, one stride-2
+// 3x3 per later stage): each halving is (x - 1) / 2 + 1.
+inline void trunk_grid(const icap_handle* h, int IH, int IW, int& OH, int& OW) {
+  auto half = [](int x) { return (x - 1) / 2 + 1; };
+  OH = half(half(IH));
+  OW = half(half(IW));
+  size_t ci = 1;
+  for (int st = 0; st < 4; ++st)
+    for (int j = 0; j < h->d.trunk_blocks[st]; ++j) {
+      if (j == 0) ++ci;
+      if (h->trunk[ci + 1].stride == 2) {
+        OH = half(OH);
+        OW = half(OW);
+      }
+      ci += 3;
+    }
+}
+
+// images (B,3,IH,IW) -> memory (B, OH*OW, d_model).  feats (optional): the trunk output as fp32 rows (B, OH*OW,
+// cnn_dim) - self.cnn(images).flatten(2).permute(0, 2, 1).  Any image size (grid:86-110 takes whatever the
+// trunk returns), up to the encoder PE table's rows of tokens.
+// bt.bn (train mode): batch-statistics BatchNorm over the whole batch, so B <= the chunk (one chunk)
+void encode_grid(icap_handle* h, const float* img, int B, int IH, int IW, float* memory, hipStream_t s,
+                 float* feats = nullptr, const BnTrain& bt = BnTrain()) {
   const icap_model_desc& d = h->d;
   REQUIRE(!h->trunk.empty(), "handle was created without the ResNet trunk (n_trunk = 0)");
-  REQUIRE(!bt.bn || B <= TRUNK_CHUNK, "train-mode BatchNorm needs the whole batch in one trunk chunk (B <= 256)");
+  REQUIRE(IH >= 1 && IW >= 1 && IH <= 4096 && IW <= 4096, "image size must be in [1, 4096]");
   auto bnp = [&](size_t i) { return bt.bn ? bt.bn + i : nullptr; };
-  REQUIRE(d.grid_tokens == 49, "the trunk path expects 224x224 images -> 7x7 grids");
-  const int ns = h->ns, HW = 224;
-  const int H1 = (HW - 1) / 2 + 1, H2 = (H1 - 1) / 2 + 1;  // 112 (stem), 56 (max-pool)
+  int GH, GW;
+  trunk_grid(h, IH, IW, GH, GW);
+  const int N = GH * GW;
+  REQUIRE(N <= h->enc_pe_rows, "the trunk's output grid exceeds the encoder's positional-encoding table (max_len)");
+  const int ns = h->ns;
+  auto half = [](int x) { return (x - 1) / 2 + 1; };
+  const int H1 = half(IH), W1 = half(IW), H2 = half(H1), W2 = half(W1);  // stem, max-pool
   const long act_per_img = [&] {  // largest NHWC activation of one image (elements of one plane)
-    long m = (long)H1 * H1 * h->trunk[0].cout;
-    int hw = H2;
+    long m = (long)H1 * W1 * h->trunk[0].cout;
+    int hh = H2, ww = W2;
     size_t ci = 1;
     for (int st = 0; st < 4; ++st)
       for (int j = 0; j < d.trunk_blocks[st]; ++j) {
         if (j == 0) ++ci;
         const Conv& c1 = h->trunk[ci];
-        m = std::max(m, (long)hw * hw * std::max(c1.cin, c1.cout));
-        if (j == 0 && h->trunk[ci + 1].stride == 2) hw = (hw - 1) / 2 + 1;
-        m = std::max(m, (long)hw * hw * h->trunk[ci + 2].cout);
+        m = std::max(m, (long)hh * ww * std::max(c1.cin, c1.cout));
+        if (h->trunk[ci + 1].stride == 2) {
+          hh = half(hh);
+          ww = half(ww);
+        }
+        m = std::max(m, (long)hh * ww * h->trunk[ci + 2].cout);
         ci += 3;
       }
     return m;
   }();
   constexpr int BORDER = 3;
-  const int HP = HW + 2 * BORDER;                     // the stem's bordered NHWC4 image
+  const int HP = IH + 2 * BORDER, WP = IW + 2 * BORDER;  // the stem's bordered NHWC4 image
   const long col_per_img = [&] {  // stem image / stride-2 subsample of a downsample's input
-    long m = (long)HP * HP * 4;
-    int hw = H2;
+    long m = (long)HP * WP * 4;
+    int hh = H2, ww = W2;
     size_t ci = 1;
     for (int st = 0; st < 4; ++st)
       for (int j = 0; j < d.trunk_blocks[st]; ++j) {
         const bool ds = j == 0;
         if (ds) ++ci;
         const Conv& c2 = h->trunk[ci + 1];
-        const int oh = c2.stride == 2 ? (hw - 1) / 2 + 1 : hw;
-        if (ds) m = std::max(m, (long)oh * oh * h->trunk[ci - 1].cin);
-        hw = oh;
+        const int oh = c2.stride == 2 ? half(hh) : hh, ow = c2.stride == 2 ? half(ww) : ww;
+        if (ds) m = std::max(m, (long)oh * ow * h->trunk[ci - 1].cin);
+        hh = oh;
+        ww = ow;
         ci += 3;
       }
     return m;
   }();
-  const int bc_max = std::min(B, TRUNK_CHUNK);
+  // images per chunk: 256 at 224 x 224, fewer for larger images (the workspaces stay at the 224 size)
+  const long per224 = 112L * 112 * h->trunk[0].cout;
+  const int chunk = (int)std::max<long>(1, std::min<long>(TRUNK_CHUNK, TRUNK_CHUNK * per224 / act_per_img));
+  REQUIRE(!bt.bn || B <= chunk, "train-mode BatchNorm needs the whole batch in one trunk chunk (B <= 256 at 224)");
+  const int bc_max = std::min(B, chunk);
   const long aL = act_per_img * bc_max, cL = col_per_img * bc_max;
   for (DevBuf* b : {&h->t_x, &h->t_y, &h->t_1, &h->t_2, &h->t_r}) b->ensure((size_t)aL * 2 * 2);
   h->t_col.ensure((size_t)cL * 2 * ns);
@@ -837,12 +873,12 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
   for (int b0 = 0; b0 < B; b0 += bc_max) {
     const int bc = std::min(bc_max, B - b0);
     const Conv& stem = h->trunk[0];
-    HIPCHK(launch_image_nhwc4(img + (size_t)b0 * 3 * HW * HW, bc, HW, BORDER, col, cL, ns, s));
+    HIPCHK(launch_image_nhwc4(img + (size_t)b0 * 3 * IH * IW, bc, IH, IW, BORDER, col, cL, ns, s));
     ConvGeom sg;
-    sg.cv = 2; sg.H = HP; sg.W = HP; sg.C = 4; sg.OH = H1; sg.OW = H1;
-    trunk_conv(h, stem, col, 0, cL, bc * H1 * H1, T1, aL, true, nullptr, 0, s, sg, bnp(0), bt.momentum);
-    HIPCHK(launch_maxpool3s2(T1, aL, bc, H1, H1, stem.cout, H2, H2, X, aL, ns, s));
-    int hw = H2;
+    sg.cv = 2; sg.H = HP; sg.W = WP; sg.C = 4; sg.OH = H1; sg.OW = W1;
+    trunk_conv(h, stem, col, 0, cL, bc * H1 * W1, T1, aL, true, nullptr, 0, s, sg, bnp(0), bt.momentum);
+    HIPCHK(launch_maxpool3s2(T1, aL, bc, H1, W1, stem.cout, H2, W2, X, aL, ns, s));
+    int hh = H2, ww = W2;
     size_t ci = 1;
     for (int st = 0; st < 4; ++st)
       for (int j = 0; j < d.trunk_blocks[st]; ++j) {
@@ -851,14 +887,14 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
         const size_t i1 = ci;
         const Conv &c1 = h->trunk[ci], &c2 = h->trunk[ci + 1], &c3 = h->trunk[ci + 2];
         ci += 3;
-        const int oh = c2.stride == 2 ? (hw - 1) / 2 + 1 : hw;
-        const int Min = bc * hw * hw, Mout = bc * oh * oh;
+        const int oh = c2.stride == 2 ? half(hh) : hh, ow = c2.stride == 2 ? half(ww) : ww;
+        const int Min = bc * hh * ww, Mout = bc * oh * ow;
         const bf16_t* res = X;
         if (ds) {  // identity branch: 1x1 conv (stride = the block's) + BN, no ReLU
           const bf16_t* dsA = X;
           long dsL = aL;
           if (ds->stride == 2) {
-            HIPCHK(launch_subsample2(X, aL, bc, hw, hw, ds->cin, col, cL, ns, s));
+            HIPCHK(launch_subsample2(X, aL, bc, hh, ww, ds->cin, col, cL, ns, s));
             dsA = col;
             dsL = cL;
           }
@@ -867,17 +903,17 @@ void encode_grid(icap_handle* h, const float* img, int B, float* memory, hipStre
         }
         trunk_conv(h, c1, X, c1.cin, aL, Min, T1, aL, true, nullptr, 0, s, ConvGeom(), bnp(i1), bt.momentum);
         ConvGeom g3;  // 3x3 conv2 read straight from T1 (implicit GEMM)
-        g3.cv = 1; g3.H = hw; g3.W = hw; g3.C = c1.cout; g3.OH = oh; g3.OW = oh;
+        g3.cv = 1; g3.H = hh; g3.W = ww; g3.C = c1.cout; g3.OH = oh; g3.OW = ow;
         trunk_conv(h, c2, T1, 0, aL, Mout, T2, aL, true, nullptr, 0, s, g3, bnp(i1 + 1), bt.momentum);
         trunk_conv(h, c3, T2, c3.cin, aL, Mout, Y, aL, true, res, aL, s, ConvGeom(), bnp(i1 + 2), bt.momentum);
         std::swap(X, Y);
-        hw = oh;
+        hh = oh;
+        ww = ow;
       }
-    REQUIRE(hw * hw == d.grid_tokens, "trunk output grid != grid_tokens");
+    REQUIRE(hh == GH && ww == GW, "trunk output grid mismatch");
     if (feats)  // trunk features (both planes: the values the tail consumes)
-      HIPCHK(launch_planes_to_f32(X, aL, (long)bc * d.grid_tokens * d.cnn_dim, 2,
-                                  feats + (size_t)b0 * d.grid_tokens * d.cnn_dim, s));
-    encode_grid_rows(h, X, aL, bc, memory + (size_t)b0 * d.grid_tokens * d.d_model, s);
+      HIPCHK(launch_planes_to_f32(X, aL, (long)bc * N * d.cnn_dim, 2, feats + (size_t)b0 * N * d.cnn_dim, s));
+    encode_grid_rows(h, X, aL, bc, N, memory + (size_t)b0 * N * d.d_model, s);
   }
 }
 
@@ -1700,7 +1736,34 @@ int icap_encode_grid_tail(icap_handle* h, const float* feats, int B, float* memo
   return guarded([&] {
     REQUIRE(h && feats && memory && B > 0, "bad arguments");
     REQUIRE(h->d.kind == ICAP_KIND_GRID, "handle is not a Grid model");
-    encode_grid_tail(h, feats, B, memory, (hipStream_t)stream);
+    encode_grid_tail(h, feats, B, h->d.grid_tokens, memory, (hipStream_t)stream);
+  });
+}
+
+int icap_encode_grid_tail_n(icap_handle* h, const float* feats, int B, int N, float* memory, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && feats && memory && B > 0 && N > 0, "bad arguments");
+    REQUIRE(h->d.kind == ICAP_KIND_GRID, "handle is not a Grid model");
+    encode_grid_tail(h, feats, B, N, memory, (hipStream_t)stream);
+  });
+}
+
+int icap_grid_tokens(icap_handle* h, int H, int W, int* tokens) {
+  return guarded([&] {
+    REQUIRE(h && tokens && H > 0 && W > 0, "bad arguments");
+    REQUIRE(h->d.kind == ICAP_KIND_GRID && !h->trunk.empty(), "not a Grid model with its trunk");
+    int gh, gw;
+    trunk_grid(h, H, W, gh, gw);
+    *tokens = gh * gw;
+  });
+}
+
+int icap_encode_grid_hw(icap_handle* h, const float* images, int B, int H, int W, float* memory, float* feats,
+                        void* stream) {
+  return guarded([&] {
+    REQUIRE(h && images && memory && B > 0, "bad arguments");
+    REQUIRE(h->d.kind == ICAP_KIND_GRID, "not a Grid model");
+    encode_grid(h, images, B, H, W, memory, (hipStream_t)stream, feats);
   });
 }
 
@@ -1708,7 +1771,7 @@ int icap_encode_grid(icap_handle* h, const float* images, int B, float* memory, 
   return guarded([&] {
     REQUIRE(h && images && memory && B > 0, "bad arguments");
     REQUIRE(h->d.kind == ICAP_KIND_GRID, "icap_encode_grid on a non-Grid model");
-    encode_grid(h, images, B, memory, (hipStream_t)stream);
+    encode_grid(h, images, B, 224, 224, memory, (hipStream_t)stream);
   });
 }
 
@@ -1716,7 +1779,7 @@ int icap_encode_grid_features(icap_handle* h, const float* images, int B, float*
   return guarded([&] {
     REQUIRE(h && images && memory && feats && B > 0, "bad arguments");
     REQUIRE(h->d.kind == ICAP_KIND_GRID, "not a Grid model");
-    encode_grid(h, images, B, memory, (hipStream_t)stream, feats);
+    encode_grid(h, images, B, 224, 224, memory, (hipStream_t)stream, feats);
   });
 }
 
@@ -1732,7 +1795,7 @@ int icap_encode_grid_train(icap_handle* h, const float* images, int B, const ica
     BnTrain bt;
     bt.bn = bn;
     bt.momentum = momentum;
-    encode_grid(h, images, B, memory, (hipStream_t)stream, feats, bt);
+    encode_grid(h, images, B, 224, 224, memory, (hipStream_t)stream, feats, bt);
   });
 }
 

@@ -226,7 +226,7 @@ hipError_t launch_preprocess(const uint8_t* px, const int64_t* offs, const int32
 hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int cp, int kwp, int Kp, bf16_t* out,
                             hipStream_t s);
 // (B,3,HW,HW) fp32 -> zero-bordered NHWC4 planes [B][HW+2*border][HW+2*border][4] (channel 3 = 0)
-hipError_t launch_image_nhwc4(const float* img, int B, int HW, int border, bf16_t* out, long lo, int nsplit,
+hipError_t launch_image_nhwc4(const float* img, int B, int IH, int IW, int border, bf16_t* out, long lo, int nsplit,
                               hipStream_t s);
 // Train-mode BatchNorm over the raw convolution output planes y [M][C] (in place): batch statistics
 // (double sums over all M rows, deterministic), running statistics updated with momentum (unbiased variance),

@@ -108,18 +108,18 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, int cout, int cin,
   }
 }
 
-// (B,3,HW,HW) fp32 -> [B][HP][HP][4] planes, HP = HW + 2*border, zero border and channel 3
-__global__ void image_nhwc4_kernel(const float* __restrict__ img, int B, int HW, int border, bf16_t* out, long lo,
-                                   int nsplit) {
-  const int HP = HW + 2 * border;
-  const long total = (long)B * HP * HP;
+// (B,3,IH,IW) fp32 -> [B][IH + 2 border][IW + 2 border][4] planes, zero border and channel 3
+__global__ void image_nhwc4_kernel(const float* __restrict__ img, int B, int IH, int IW, int border, bf16_t* out,
+                                   long lo, int nsplit) {
+  const int HP = IH + 2 * border, WP = IW + 2 * border;
+  const long total = (long)B * HP * WP;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int x = (int)(i % HP) - border, y = (int)((i / HP) % HP) - border;
-    const long b = i / ((long)HP * HP);
+    const int x = (int)(i % WP) - border, y = (int)((i / WP) % HP) - border;
+    const long b = i / ((long)HP * WP);
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (y >= 0 && y < HW && x >= 0 && x < HW)
+    if (y >= 0 && y < IH && x >= 0 && x < IW)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) v[c] = img[((b * 3 + c) * HW + y) * HW + x];
+      for (int c = 0; c < 3; ++c) v[c] = img[((b * 3 + c) * IH + y) * IW + x];
     bf16_t h[4], l[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) split_bf(v[c], h[c], l[c]);
@@ -242,10 +242,10 @@ hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int cp, in
   return hipGetLastError();
 }
 
-hipError_t launch_image_nhwc4(const float* img, int B, int HW, int border, bf16_t* out, long lo, int nsplit,
+hipError_t launch_image_nhwc4(const float* img, int B, int IH, int IW, int border, bf16_t* out, long lo, int nsplit,
                               hipStream_t s) {
-  const long HP = HW + 2 * border;
-  hipLaunchKernelGGL(image_nhwc4_kernel, dim3(grid_for(B * HP * HP)), dim3(256), 0, s, img, B, HW, border, out, lo,
+  const long HP = IH + 2 * border, WP = IW + 2 * border;
+  hipLaunchKernelGGL(image_nhwc4_kernel, dim3(grid_for(B * HP * WP)), dim3(256), 0, s, img, B, IH, IW, border, out, lo,
                      nsplit);
   return hipGetLastError();
 }

@@ -207,6 +207,8 @@ class Engine:
             desc.grid_tokens = 49
             desc.n_enc_layers = n_enc
             desc.enc_pe = sd["encoder.pos_encoder.pe"].data_ptr()
+            desc.enc_pe_len = int(sd["encoder.pos_encoder.pe"].shape[1])
+            self.enc_pe_len = desc.enc_pe_len
             desc.enc_layers = ctypes.cast(el, ctypes.POINTER(EncLayerW))
             trunk = trunk_convs(sd)
             if trunk is not None:
@@ -259,12 +261,29 @@ class Engine:
                 raise _lib.IcapError("this Grid engine was built without the encoder.cnn weights")
             check(self.lib.icap_encode_grid(self.handle, x.data_ptr(), B, mem.data_ptr(), stream_ptr(self.device)),
                   "icap_encode_grid")
+        elif x.dim() == 4 and x.shape[1] == 3 and self.has_trunk:
+            # any other image size on the HIP trunk (grid:86-110): the memory has the trunk grid's h x w tokens
+            n = self.grid_tokens(x.shape[2], x.shape[3])
+            mem = torch.empty(B, n, self.d_model, device=self.device, dtype=torch.float32)
+            check(self.lib.icap_encode_grid_hw(self.handle, x.data_ptr(), B, x.shape[2], x.shape[3], mem.data_ptr(),
+                                               None, stream_ptr(self.device)), "icap_encode_grid_hw")
         else:
-            if x.dim() != 4 or x.shape[2] * x.shape[3] != self.mem_tokens:
-                raise ValueError(f"expected (B,3,224,224) images or (B,C,7,7) trunk features, got {tuple(x.shape)}")
-            check(self.lib.icap_encode_grid_tail(self.handle, x.data_ptr(), B, mem.data_ptr(),
-                                                 stream_ptr(self.device)), "icap_encode_grid_tail")
+            if x.dim() != 4 or x.shape[1] != self.cnn_dim:
+                raise ValueError(f"expected (B,3,H,W) images or (B,{self.cnn_dim},h,w) trunk features, "
+                                 f"got {tuple(x.shape)}")
+            n = x.shape[2] * x.shape[3]
+            if n > self.enc_pe_len:
+                raise ValueError(f"{n} grid tokens exceed the encoder's positional encoding ({self.enc_pe_len})")
+            mem = torch.empty(B, n, self.d_model, device=self.device, dtype=torch.float32)
+            check(self.lib.icap_encode_grid_tail_n(self.handle, x.data_ptr(), B, n, mem.data_ptr(),
+                                                   stream_ptr(self.device)), "icap_encode_grid_tail_n")
         return mem
+
+    def grid_tokens(self, height: int, width: int) -> int:
+        """Tokens of the memory of an (height, width) image: the ResNet trunk's output grid h x w."""
+        out = ctypes.c_int(0)
+        check(self.lib.icap_grid_tokens(self.handle, int(height), int(width), ctypes.byref(out)), "icap_grid_tokens")
+        return int(out.value)
 
     def encode_vit_features(self, images: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """ViT: images (B,3,224,224) -> (memory (B,196,d), trunk output (B,196,vit_dim) = the projection's

@@ -91,6 +91,8 @@ typedef struct {
    * (hi = bf16(W), lo = bf16(W - hi): 16 significand bits, for fp32 checkpoints whose weights are not
    * bf16-exact; the decode then runs the unfused launches, each GEMM adding W_lo . X_hi - DESIGN.md §3) */
   int dec_weight_planes;
+  /* rows of enc_pe (the Grid encoder's PositionalEncoding table, max_len 100 in grid:74); 0 = grid_tokens */
+  int enc_pe_len;
 } icap_model_desc;
 
 int icap_abi_version(void);
@@ -139,6 +141,15 @@ int icap_encode_grid_features(icap_handle* h, const float* images, int B, float*
  * bn_var likewise with the unbiased variance (torch.nn.BatchNorm2d.forward in training mode; the caller
  * increments num_batches_tracked).  bn: n_trunk entries in the desc's order (only bn_w, bn_b, bn_mean,
  * bn_var are read; bn_mean / bn_var are written); the convolution weights are the handle's.  B <= 256. */
+/* Any image size (reference: GridFeatureEncoder.forward, grid:86-110, takes whatever grid the trunk returns):
+ * images (B,3,H,W) -> memory (B, N, d_model), N = the trunk's output grid h x w (icap_grid_tokens), at most the
+ * encoder positional-encoding table's rows (PositionalEncoding(max_len=100), grid:74).  feats: optional trunk
+ * output (B, N, cnn_dim) fp32 or NULL. */
+int icap_grid_tokens(icap_handle* h, int H, int W, int* tokens);
+int icap_encode_grid_hw(icap_handle* h, const float* images, int B, int H, int W, float* memory, float* feats,
+                        void* stream);
+/* The tail over trunk features (B, cnn_dim, N) of any grid (N tokens, row-major h x w). */
+int icap_encode_grid_tail_n(icap_handle* h, const float* feats, int B, int N, float* memory, void* stream);
 int icap_encode_grid_train(icap_handle* h, const float* images, int B, const icap_conv_bn_w* bn, float momentum,
                            float* memory, float* feats, void* stream);
 

@@ -50,13 +50,11 @@ class GridFeatureEncoder(nn.Module):
         owner = owner_of(self)
         if owner is not None and not self.training and owner.use_hip(images):
             eng = owner.hip_engine(images.device)
-            if tuple(images.shape[1:]) == (3, 224, 224):
-                return eng.encode(images)  # HIP trunk + tail
-            with torch.no_grad():  # other image sizes: torch trunk, then the HIP tail when the map is 7x7
-                feats = self.cnn(images.float())
-                if feats.shape[2] * feats.shape[3] == eng.mem_tokens:
-                    return eng.encode(feats)
-                return self.tail(feats)
+            if eng.has_trunk and images.dim() == 4 and images.shape[1] == 3:
+                h, w = images.shape[2], images.shape[3]
+                if eng.grid_tokens(h, w) <= eng.enc_pe_len:
+                    return eng.encode(images)  # HIP trunk + tail, any image size
+            # grids larger than the PE table: the reference's own modules (the PE add raises there as well)
         return self.tail(self.cnn(images))
 
     def tail(self, feats):

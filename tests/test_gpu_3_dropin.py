@@ -170,3 +170,38 @@ def test_f16_range_guard(cuda, site):
         ref_mem = O.vit_encode(sd, imgs.cpu())
         assert (mem2.cpu() - ref_mem).abs().max().item() < 1e-2 * max(1.0, ref_mem.abs().max().item())
     del mem16
+
+
+@pytest.mark.parametrize("hw", [(160, 192), (256, 256), (288, 320)])
+def test_grid_any_image_size_on_hip_trunk(cuda, hw):
+    """GridFeatureEncoder.forward (grid:86-110) takes any image size: the trunk's output grid h x w becomes the
+    memory's tokens (up to the PE table's 100).  The drop-in Grid model runs such images through the HIP trunk
+    (icap_encode_grid_hw: rectangular implicit-GEMM geometry, workspaces chunked to the 224 budget) and the HIP
+    tail; memory against the oracle's fp32 trunk + tail at the config-3 bound, greedy ids margin-gated."""
+    from models.grid_transformer_model import build_model
+
+    sd = W.to_torch(W.grid_state_dict(0))
+    m = build_model(W.VOCAB_SIZE, {"pretrained_cnn": False})
+    m.load_state_dict(sd)
+    m = m.to(cuda).eval()
+    g = torch.Generator().manual_seed(hw[0] * 1000 + hw[1])
+    imgs = torch.randn(3, 3, *hw, generator=g).to(cuda)
+    eng = m.hip_engine(cuda)
+    seen = []
+    orig = eng.lib.icap_encode_grid_hw
+    eng.lib.icap_encode_grid_hw = lambda *a: seen.append(a[3:5]) or orig(*a)
+    with torch.no_grad():
+        mem = m.encoder(imgs)
+    eng.lib.icap_encode_grid_hw = orig
+    assert seen == [hw]  # the HIP trunk ran, at this size
+    sdd = {k: v.to(cuda) for k, v in sd.items()}
+    with torch.no_grad():
+        mem_o = O.grid_encode_tail(sdd, O.resnet101_trunk(sdd, imgs))
+    assert mem.shape == mem_o.shape and mem.shape[1] == eng.grid_tokens(*hw)
+    assert (mem - mem_o).abs().max().item() < 1e-3
+    out = m.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=20)
+    ref, tr = O.greedy_from_memory(sdd, mem_o, W.START_TOKEN, W.END_TOKEN, 20, return_trace=True)
+    for r in range(imgs.shape[0]):
+        close = np.nonzero(O.top2_margin(tr[:, r].cpu()).numpy() < 2e-3)[0]
+        upto = (close[0] if len(close) else tr.shape[0]) + 1
+        assert torch.equal(out[r, :upto].cpu(), ref[r, :upto].cpu()), r
