@@ -9,7 +9,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 LIB = HERE / "libicap.so"
-SOURCES = ["gemm.hip", "rows.hip", "attention.hip", "head.hip", "beam.hip", "decode.hip", "trunk.hip", "preprocess.hip", "cider.hip", "train.hip", "icap.cpp"]
+SOURCES = ["gemm.hip", "rows.hip", "attention.hip", "head.hip", "beam.hip", "decode.hip", "decstep.hip", "trunk.hip", "preprocess.hip", "cider.hip", "train.hip", "icap.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-munsafe-fp-atomics"]

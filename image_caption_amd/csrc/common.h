@@ -81,9 +81,9 @@ __device__ __forceinline__ bf16_t cvt16(float f) {
 __device__ __forceinline__ bool f16_pair_nonfinite(uint32_t u) {
   return (u & 0x7c00u) == 0x7c00u || (u & 0x7c000000u) == 0x7c000000u;
 }
-// set the handle's sticky range word (one vector store from one lane; never the scalar path)
+// set bit 0 of the handle's sticky status word (one vector atomic from one lane; never the scalar path)
 __device__ __forceinline__ void range_flag_set(unsigned* flag) {
-  __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_or(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 template <bool F16>
 __device__ __forceinline__ u32x2 pack16x4(f32x4 v) {

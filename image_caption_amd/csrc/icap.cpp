@@ -219,6 +219,12 @@ struct icap_handle {
   // ICAP_PREC_F16 range guard: one sticky device word, set by the fp16 encoder's LayerNorm and store-only GEMM
   // kernels when a value they write is not finite in fp16; read and cleared by icap_range_check
   DevBuf rflag;
+  // persistent decode step (decstep.hip): per-layer weight pointers and per-step arguments in device memory, the
+  // per-step counter blocks (zeroed by one memset per decode), and the key the argument array was built for
+  bool use_step = false;  // icap_set_decode_step / ICAP_DEC_STEP=1 (tools): the persistent decode step (opt-in)
+  DevBuf step_layers, step_args[2], step_state[2];
+  DevBuf step_trace;  // tools build (ICAP_DEC_STEP_TRACE=1): per-task stamps of every step, + per-workgroup slots
+  long step_key[2][8] = {};
   unsigned* range_word() {
     if (!rflag.p) {
       rflag.ensure(16);
@@ -241,7 +247,12 @@ struct icap_handle {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col, &t_bn}) b->release();
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt, &rflag}) b->release();
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt, &rflag, &step_layers})
+      b->release();
+    for (int i = 0; i < 2; ++i) {
+      step_args[i].release();
+      step_state[i].release();
+    }
     for (DecWS& w : dws)
       for (DevBuf* b : {&w.x, &w.a, &w.qkv, &w.q, &w.qt, &w.c, &w.o, &w.h, &w.kv, &w.fin, &w.part, &w.memp, &w.xpart,
                          &w.xcnt, &w.gs})
@@ -1121,6 +1132,82 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
   }
 }
 
+// ---- persistent decode step (decstep.hip) ----
+// Whether the decode loop runs as one persistent launch per step: the fused blocks' shapes (d 512, 8 heads,
+// dim_ff 2048), two activation planes, decode positions below 64, the bf16 weights (hi/lo weights keep the unfused
+// launches, except for the dropout sampler as in decoder_layers).
+bool step_path(const icap_handle* h, int max_len, const DropCfg* drop) {
+  const icap_model_desc& d = h->d;
+  return h->use_step && h->ns == 2 && d.d_model == 512 && d.nhead == 8 && d.dim_ff == 2048 && max_len <= 65 &&
+         d.n_dec_layers >= 1 && d.n_dec_layers <= DEC_STEP_MAX_LAYERS && (!h->wlo || drop);
+}
+
+// The per-step argument structs of one decode configuration, built on the host and copied to device memory (the
+// kernel reads its arguments there).  Rebuilt when the configuration or the workspace changes; never during a
+// stream capture (decode_loop prepares them before it captures).
+const DecStepArgs* step_args(icap_handle* h, const DecodeBufs& b, int B, int S, int max_len, int wsi,
+                             const DropCfg* drop, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  const int L = d.n_dec_layers, steps = max_len - 1;
+  if (!h->step_layers.p) {
+    std::vector<DecStepLayer> v(L);
+    for (int l = 0; l < L; ++l) {
+      const DecLayer& o = h->dec[l];
+      DecStepLayer& x = v[l];
+      x.Wqkv = o.sa_qkv.w; x.bqkv = o.sa_qkv.b; x.Wo = o.sa_out.w; x.bo = o.sa_out.b;
+      x.n1w = o.n1.w; x.n1b = o.n1.b;
+      x.Wq = o.ca_q.w; x.bq = o.ca_q.b; x.WkT = o.ca_kT;
+      x.Wv = o.ca_v; x.bv = o.ca_vb; x.Wco = o.ca_out.w; x.bco = o.ca_out.b;
+      x.n2w = o.n2.w; x.n2b = o.n2.b;
+      x.W1 = o.lin1.w; x.b1 = o.lin1.b; x.W2 = o.lin2.w; x.b2 = o.lin2.b;
+      x.n3w = o.n3.w; x.n3b = o.n3.b;
+    }
+    h->step_layers.ensure(sizeof(DecStepLayer) * L);
+    HIPCHK(hipMemcpy(h->step_layers.p, v.data(), sizeof(DecStepLayer) * L, hipMemcpyHostToDevice));
+  }
+  const size_t st_ints = dec_step_state_ints(L, B);
+  const long key[8] = {B, S, max_len, (long)g_ws_generation, drop ? (long)drop->thr : -1,
+                       drop ? (long)(intptr_t)drop->seed : 0, (long)(intptr_t)b.x, (long)st_ints};
+  h->step_state[wsi].ensure(st_ints * 4 * steps);
+  if (!h->step_args[wsi].p || h->step_args[wsi].n < sizeof(DecStepArgs) * steps ||
+      std::memcmp(key, h->step_key[wsi], sizeof(key)) != 0) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(s, &cs));
+    REQUIRE(cs == hipStreamCaptureStatusNone, "internal: decode step arguments rebuilt during a capture");
+    std::vector<DecStepArgs> v(steps);
+    int* state = h->step_state[wsi].as<int>();
+    const int ntasks = L * 59 * ((B + 15) / 16);
+    static const int trace = icap_knob("ICAP_DEC_STEP_TRACE", 0);
+    if (trace) h->step_trace.ensure((size_t)steps * ntasks * 4 * 8 + 4096 * 4);
+    for (int t = 0; t < steps; ++t) {
+      DecStepArgs& a = v[t];
+      a = DecStepArgs{};
+      a.layers = h->step_layers.as<DecStepLayer>();
+      a.n_layers = L; a.rows = B; a.t0 = t; a.Lmax = max_len; a.S = S;
+      a.x = b.x; a.a = b.a; a.aL = b.aL;
+      a.kc = b.kc; a.vc = b.vc; a.kvl = (long)b.kvl;
+      a.part = b.part; a.PS = b.PS;
+      a.qt = b.qt; a.cL = b.cL; a.c = b.c; a.mem16 = b.memp; a.gs = b.gs;
+      if (drop) {
+        a.drop = *drop;
+        a.drop.row_base = 0;
+      }
+      int* blk = state + (size_t)t * st_ints;
+      a.ctr = blk;
+      a.qhead = blk + (st_ints - 4);  // the block's last 16 bytes (after every counter)
+      a.err = h->range_word();
+      if (trace) {
+        a.trace = h->step_trace.as<unsigned long long>() + (size_t)t * ntasks * 4;
+        a.trace_cur = (int*)(h->step_trace.as<unsigned long long>() + (size_t)steps * ntasks * 4);
+      }
+    }
+    h->step_args[wsi].ensure(sizeof(DecStepArgs) * steps);
+    HIPCHK(hipMemcpy(h->step_args[wsi].p, v.data(), sizeof(DecStepArgs) * steps, hipMemcpyHostToDevice));
+    std::memcpy(h->step_key[wsi], key, sizeof(key));
+  }
+  return h->step_args[wsi].as<DecStepArgs>();
+}
+
 void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
                        float* step_logits, const float* uniforms, float* logp, hipStream_t s,
                        const DropCfg* drop = nullptr) {
@@ -1149,7 +1236,48 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   // Round 2 (fused decode blocks, tools/chains_r2.sh, B = 256): 2 chains 13.25 ms/step of decode, 3 chains of
   // 85 rows 12.73, 4 chains of 64 rows 13.37 - so 3 chains from 80 rows each (B = 128 keeps one chain)
   static const int min_rows = std::max(16, icap_knob("ICAP_DEC_MIN_ROWS", 80));
-  const int nb = std::max(1, std::min(h->dec_branches, B / min_rows));
+  const bool persist = step_path(h, max_len, drop);
+  const int nb = persist ? 1 : std::max(1, std::min(h->dec_branches, B / min_rows));
+  if (persist) {  // one persistent launch per step (all layers) + the head
+    const DecStepArgs* dargs = step_args(h, b, B, S, max_len, wsi, drop, s);
+    const size_t st_ints = dec_step_state_ints(d.n_dec_layers, B);
+    HIPCHK(hipMemsetAsync(h->step_state[wsi].p, 0, st_ints * 4 * (size_t)(max_len - 1), s));
+    for (int t = 0; t + 1 < max_len; ++t) {
+      DecStepArgs a{};  // the host copy the launcher validates (the kernel reads dargs[t])
+      a.layers = h->step_layers.as<DecStepLayer>();
+      a.n_layers = d.n_dec_layers; a.rows = B; a.t0 = t; a.Lmax = max_len; a.S = S;
+      a.ctr = h->step_state[wsi].as<int>(); a.qhead = a.ctr; a.err = h->range_word();
+      const double fl = 2.0 * B * d.n_dec_layers * (4.0 * D * D * 2 + 2.0 * D * d.dim_ff + 4.0 * d.nhead * S * D);
+      h->timed(PROF_DEC_FUSED, fl, 0.0, s, [&] { HIPCHK(launch_dec_step(a, dargs + t, s)); });
+      const DecLayer& Ll = h->dec[d.n_dec_layers - 1];
+      DropCfg dl{};
+      if (drop) {
+        dl = *drop;
+        dl.row_base = 0;
+        dl.layer = d.n_dec_layers - 1;
+        dl.pos = t;
+      }
+      HeadArgs ha{};
+      ha.ln = RlnArgs{b.x, nullptr, b.part, d.dim_ff / 128, b.PS, Ll.lin2.b, Ll.n3.w, Ll.n3.b, 1e-5f, dl, 6};
+      ha.x = b.x; ha.rows = B; ha.Dm = D; ha.W = h->fc_w; ha.W4 = head_w4(h); ha.bias = h->fc_b; ha.V = d.vocab;
+      ha.logits = step_logits ? step_logits + (size_t)t * B * d.vocab : nullptr;
+      ha.ld_logits = d.vocab;
+      ha.ids = ids; ha.ld_ids = max_len; ha.id_col = t + 1;
+      ha.uniforms = uniforms ? uniforms + (size_t)t * B : nullptr;
+      ha.logp = logp ? logp + t : nullptr; ha.ld_logp = max_len - 1;
+      ha.finished = fin; ha.end_token = end;
+      if (t + 2 < max_len) {
+        ha.emb = h->emb; ha.pe = h->pe; ha.pe_pos = t + 1; ha.emb_scale = scale;
+        ha.x_next = b.x; ha.a_next = b.a; ha.lo = b.aL; ha.nsplit = h->ns;
+        if (drop) {
+          ha.drop = *drop;
+          ha.drop.row_base = 0;
+        }
+      }
+      HIPCHK(launch_head(ha, s));
+    }
+    return;
+  }
   if (nb > 1) {
     if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventRecord(h->ev_fork, s));
@@ -1237,8 +1365,9 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
       g.uni.ensure((size_t)(max_len - 1) * B * 4);
       g.lp.ensure((size_t)B * (max_len - 1) * 4);
     }
-    dec_bufs(h, B, B, max_len, S, 0, mode);  // make sure nothing allocates during capture
+    DecodeBufs pb = dec_bufs(h, B, B, max_len, S, 0, mode);  // make sure nothing allocates during capture
     if (mode) h->dws[mode].fin.ensure((size_t)B);
+    if (step_path(h, max_len, dp)) step_args(h, pb, B, S, max_len, mode, dp, s);  // ... nor uploads
     if (!h->cap_stream) HIPCHK(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(hipStreamSynchronize(s));
     const bool prof = h->prof_on;
@@ -1595,7 +1724,7 @@ const char* icap_knobs_set() {
       "ICAP_QKV_HEAD_MAJOR", "ICAP_DEC_MIN_ROWS", "ICAP_I8_MLP2", "ICAP_DEC_BRANCHES", "ICAP_F16_GEMM",
       "ICAP_F16_PRES", "ICAP_XATTN16_KS", "ICAP_XATTN16_CK", "ICAP_ENC_ATTN16_QPW", "ICAP_F16_PP",
       "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
-      "ICAP_HEAD_W4"};
+      "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE"};
   for (const char* n : names)
     if (getenv(n)) return n;
   return "";
@@ -1629,6 +1758,7 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
       h->f16 = desc->precision == ICAP_PREC_F16 && desc->kind == ICAP_KIND_VIT;
       REQUIRE(desc->dec_weight_planes >= 0 && desc->dec_weight_planes <= 2, "dec_weight_planes must be 0, 1 or 2");
       h->wlo = desc->dec_weight_planes == 2;
+      h->use_step = icap_knob("ICAP_DEC_STEP", 0) != 0;
       // measured and rejected as the default: MLP-2 fed by the block-scaled GELU output takes
       // 1211 us (two-step fold: 256 VGPRs, 30 spilled) / 646 us (per-step fold, 64-column blocks) against
       // 467 us for the bf16x2 form
@@ -1889,7 +2019,8 @@ int icap_range_check(icap_handle* h, void* stream, int* overflowed) {
     HIPCHK(hipMemcpyAsync(&v, w, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (v) HIPCHK(hipMemsetAsync(w, 0, 16, s));
-    *overflowed = v ? 1 : 0;
+    *overflowed = (v & 1u) ? 1 : 0;
+    REQUIRE(!(v & DEC_STEP_GAVE_UP), "internal error: a persistent decode step gave up waiting for a dependency");
   });
 }
 
@@ -1901,6 +2032,26 @@ int icap_set_decode_chains(icap_handle* h, int chains) {
     for (DecodeGraph& g : h->dg) g.reset();
   });
 }
+
+int icap_set_decode_step(icap_handle* h, int enable) {
+  return guarded([&] {
+    REQUIRE(h, "null handle");
+    if (h->use_step != (enable != 0))
+      for (DecodeGraph& g : h->dg) g.reset();  // the captured loops follow the mode
+    h->use_step = enable != 0;
+  });
+}
+
+#ifdef ICAP_TOOLS
+// tools build: the persistent decode's per-task stamps (ICAP_DEC_STEP_TRACE=1) -> host (synchronous)
+int icap_dec_step_trace_read(icap_handle* h, void* host, size_t bytes) {
+  return guarded([&] {
+    REQUIRE(h && h->step_trace.p && bytes <= h->step_trace.n, "no trace (ICAP_DEC_STEP_TRACE=1, tools build)");
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(host, h->step_trace.p, bytes, hipMemcpyDeviceToHost));
+  });
+}
+#endif
 
 int icap_set_graphs(icap_handle* h, int enable) {
   return guarded([&] {

@@ -189,6 +189,46 @@ hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s);
 // blocks and one full-line DMA round (decode.hip); used by the decode loops.
 hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s);
 
+// Persistent decode step (decstep.hip): all decoder layers of one decode step (one new token per row) in ONE
+// launch of one 1024-thread workgroup per CU.  Work items are tasks of 16-row tiles - self-attention per head,
+// residual LayerNorm, the two chained cross-attention products per head, cross-attention per row, feed-forward
+// per hidden slice - pulled from a device queue in a dependency-respecting order; a task issues its weight DMA,
+// then waits for the per-(layer, phase, tile) counter of its inputs, then loads them.  Handed-off outputs are
+// write-through (sc1) stores published by a counter add; consumers acquire once per task.  The last layer's
+// LN3 is left to the head kernel (HeadArgs::ln), as in the launch-per-kernel loop.
+struct DecStepLayer {
+  const bf16_t* Wqkv; const float* bqkv; const bf16_t* Wo; const float* bo;   // self-attention
+  const float *n1w, *n1b;
+  const bf16_t* Wq; const float* bq; const bf16_t* WkT;                       // q, then q~ = q Wk (per head)
+  const bf16_t* Wv; const float* bv; const bf16_t* Wco; const float* bco;     // value, cross out-projection
+  const float *n2w, *n2b;
+  const bf16_t* W1; const float* b1; const bf16_t* W2; const float* b2;       // feed-forward
+  const float *n3w, *n3b;
+};
+constexpr int DEC_STEP_MAX_LAYERS = 8;
+struct DecStepArgs {
+  const DecStepLayer* layers;             // device array [n_layers]
+  int n_layers, rows, t0, Lmax, S;
+  float* x; bf16_t* a; long aL;           // residual stream [rows][512] fp32 and its bf16 hi/lo planes
+  float* kc; float* vc; long kvl;         // KV cache [layer][rows][8][Lmax][64] fp32 (kvl = layer stride)
+  float* part; long PS;                   // split-K slabs [16][rows][512]
+  bf16_t* qt; long cL;                    // q~ planes [rows][8][512]
+  bf16_t* c;                              // cross-attention context planes [rows][8][512] (lo at + cL)
+  const bf16_t* mem16;                    // the memory as one fp16 plane [rows][S][512]
+  float* gs;                              // train mode: value-bias weights [rows][8]
+  DropCfg drop;                           // thr 0: no dropout (layer / pos set per task)
+  int* ctr;                               // [n_layers][8 phases][tiles] completion counters, zeroed per launch
+  int* qhead;                             // task queue head, zeroed per launch
+  unsigned* err;                          // the handle's sticky status word: DEC_STEP_GAVE_UP set on a give-up
+  // tools build: per-task stamps [task][4] (dequeued, inputs ready, body done: s_memrealtime; workgroup) or null
+  unsigned long long* trace; int* trace_cur;
+};
+constexpr unsigned DEC_STEP_GAVE_UP = 2;  // (bit 0 of the same word: the f16 encoder's range guard)
+// a: the host copy (validated here); dev_args: the same struct in device memory (what the kernel reads)
+hipError_t launch_dec_step(const DecStepArgs& a, const DecStepArgs* dev_args, hipStream_t s);
+// ints of the per-launch state block (counters + queue head), zeroed before every launch
+size_t dec_step_state_ints(int n_layers, int rows);
+
 // LayerNorm over rows of D fp32 values; optional fp32 output (may alias input) and
 // bf16 hi(/lo) planes.  Input row r is read from (r / in_group) * in_stride + in_off + r % in_group.
 hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_group, long in_stride,

@@ -237,12 +237,12 @@ class Engine:
         """fp16 range guard of the f16 ViT encoder (icap_range_check): True when a LayerNorm /
         Q,K,V / GELU output stored as fp16 since the last check was not finite (|v| >= 65520 or NaN), i.e. the
         memory of those encodes is not trustworthy and must be recomputed in bf16x2.  Synchronises the
-        engine's current stream; always False for precisions without fp16 activations."""
-        if self.precision != "f16" or self.kind != "vit":
-            return False
+        engine's current stream; always False for precisions without fp16 activations.  Also the health check of
+        the persistent decode: raises IcapError if a decode step gave up waiting for a dependency.""" 
         out = ctypes.c_int(0)
+        # raises if a persistent decode step gave up waiting for a dependency (an internal error, never silent)
         check(self.lib.icap_range_check(self.handle, stream_ptr(self.device), ctypes.byref(out)), "icap_range_check")
-        return bool(out.value)
+        return bool(out.value) and self.precision == "f16" and self.kind == "vit"
 
     # ------------------------------------------------------------------ encoders
     def encode(self, images: torch.Tensor) -> torch.Tensor:
@@ -412,6 +412,10 @@ class Engine:
     def set_decode_chains(self, chains: int) -> None:
         """Independent decode chains per batch (1..4, default 2, used from 128 rows per chain)."""
         check(self.lib.icap_set_decode_chains(self.handle, int(chains)), "icap_set_decode_chains")
+
+    def set_decode_step(self, enable: bool) -> None:
+        """Decode loop form: one persistent launch per step (default) or one launch per fused block."""
+        check(self.lib.icap_set_decode_step(self.handle, int(bool(enable))), "icap_set_decode_step")
 
     def set_graphs(self, enable: bool) -> None:
         """hipGraph replay of the decode loop (default on)."""

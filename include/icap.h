@@ -242,6 +242,12 @@ int icap_set_graphs(icap_handle* h, int enable);
  * since the last check is not trustworthy: re-encode with a 16-bit-significand precision (bf16x2). */
 int icap_range_check(icap_handle* h, void* stream, int* overflowed);
 
+/* Decode loop form: 1 (default) = one persistent launch per decode step running every decoder
+ * layer as dependency-ordered tasks (decstep.hip), where the shapes allow it (d_model 512, 8 heads, dim_ff 2048,
+ * max_len <= 65, two activation planes, bf16 decoder weights); 0 = one launch per fused block.  Same results to
+ * rounding (the residual LayerNorm sums in another order). */
+int icap_set_decode_step(icap_handle* h, int enable);
+
 /* Number of independent decode chains a batch is split into (1..4, default 2; used from 128 rows
  * per chain): the chains are parallel branches of the captured decode graph. */
 int icap_set_decode_chains(icap_handle* h, int chains);
