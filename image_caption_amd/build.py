@@ -10,6 +10,8 @@ HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 LIB = HERE / "libicap.so"
 SOURCES = ["gemm.hip", "rows.hip", "attention.hip", "head.hip", "beam.hip", "decode.hip", "decstep.hip", "trunk.hip", "preprocess.hip", "cider.hip", "train.hip", "icap.cpp"]
+# measured-and-rejected kernel forms: compiled into the tools build only
+TOOLS_SOURCES = ["gemm_tools.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-munsafe-fp-atomics"]
@@ -24,7 +26,7 @@ def _stale(tools: bool = False) -> bool:
     if not FLAVOR.exists() or FLAVOR.read_text().strip() != ("tools" if tools else "product"):
         return True
     t = LIB.stat().st_mtime
-    deps = [CSRC / s for s in SOURCES] + list(CSRC.glob("*.h")) + [HERE.parent / "include" / "icap.h"]
+    deps = [CSRC / s for s in SOURCES + (TOOLS_SOURCES if tools else [])] + list(CSRC.glob("*.h")) + [HERE.parent / "include" / "icap.h"]
     return any(p.stat().st_mtime > t for p in deps)
 
 
@@ -37,7 +39,7 @@ def build(force: bool = False, verbose: bool = True, tools: bool = False) -> Pat
     obj_dir = HERE / "build"
     obj_dir.mkdir(exist_ok=True)
     procs = []
-    for src in SOURCES:
+    for src in SOURCES + (TOOLS_SOURCES if tools else []):
         obj = obj_dir / (src + ".o")
         objs.append(obj)
         cmd = [HIPCC, *FLAGS, *(["-DICAP_TOOLS"] if tools else []), "-x", "hip", "-c", str(CSRC / src), "-o", str(obj)]

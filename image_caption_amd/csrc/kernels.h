@@ -97,6 +97,10 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
 int gemm_tile_class(const GemmArgs& g);
 // 256 x 256-tile, 8-wave encoder GEMM (batch 1, N % 256 == 0).
 hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s);
+#ifdef ICAP_TOOLS
+// gemm_tools.hip (tools build only): takes the launch when a measurement knob selects a rejected form
+bool launch_gemm_256_tools(const GemmArgs& g, hipStream_t s, int cus, hipError_t* err);
+#endif
 // int8 two-slice GEMM (batch 1, N % 256 == 0, K % 64 == 0): acc = 65536 A1.W1 + 256 (A1.W2 + A2.W1)
 // in int32, then * a_scale[m] * w_scale[n] and the gemm_256 epilogue (bias, GELU, head-major, ...)
 hipError_t launch_gemm_i8(const GemmArgs& g, hipStream_t s);
