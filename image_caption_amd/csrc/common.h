@@ -71,6 +71,12 @@ __device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
 }
 __device__ __forceinline__ bf16_t f2h(float f) { return __builtin_bit_cast(bf16_t, (_Float16)f); }
 __device__ __forceinline__ float h2f(bf16_t u) { return (float)__builtin_bit_cast(_Float16, u); }
+// fp16 hi/lo split (the Grid trunk's residual stream in ICAP_PREC_F16): hi = fp16(v), lo = fp16(v - hi), ~22 bits
+__device__ __forceinline__ void split_h(float v, bf16_t& hi, bf16_t& lo) {
+  const _Float16 h = (_Float16)v;
+  hi = __builtin_bit_cast(bf16_t, h);
+  lo = f2h(v - (float)h);
+}
 template <bool F16>
 __device__ __forceinline__ bf16_t cvt16(float f) {
   if constexpr (F16) return f2h(f);

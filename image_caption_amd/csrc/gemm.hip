@@ -16,7 +16,8 @@
 
 namespace {
 
-template <int BM, int BN, int WM, int WN, int CONV = 0>
+// F16: fp16 operands (A planes, W) and fp16 output / residual planes (the ICAP_PREC_F16 Grid trunk)
+template <int BM, int BN, int WM, int WN, int CONV = 0, bool F16 = false>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
   constexpr int WAVES_N = BN / WN;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mma<F16>(af[i], bfr[j], acc[i][j]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -113,6 +114,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
 
   // epilogue: C/D layout of 16x16 MFMA: col = lane & 15, row = 4*(lane >> 4) + r
   const float* bias = p.bias ? p.bias + (long)bz * p.bias_batch : nullptr;
+  bool bad = false;  // F16: a stored value that is not finite in fp16 (range guard)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn * WN + j * 16 + fr;
@@ -128,7 +130,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
         if (p.addend) v += p.addend[(long)((row % p.add_group) + p.add_off) * p.add_ld + col];
         if (p.res) {
           const long ro = (long)row * p.res_ld + col;
-          v += bf2f(p.res[ro]) + bf2f(p.res[ro + p.res_lo]);
+          if constexpr (F16) v += h2f(p.res[ro]) + (p.res_planes == 2 ? h2f(p.res[ro + p.res_lo]) : 0.f);
+          else v += bf2f(p.res[ro]) + bf2f(p.res[ro + p.res_lo]);
         }
         if (p.epi == EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
         else if (p.epi == EPI_RELU) v = fmaxf(v, 0.f);
@@ -144,13 +147,19 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
           ((bf16_t*)p.C)[o] = f2bf(v);
         } else {
           bf16_t hi, lo;
-          split_bf(v, hi, lo);
+          if constexpr (F16) {
+            split_h(v, hi, lo);
+            bad |= (hi & 0x7c00) == 0x7c00;
+          } else {
+            split_bf(v, hi, lo);
+          }
           ((bf16_t*)p.C)[o] = hi;
           if (p.c_planes == 2) ((bf16_t*)p.C)[o + p.c_lo] = lo;
         }
       }
     }
   }
+  if (F16 && p.range_flag && __any(bad) && lane == 0) range_flag_set(p.range_flag);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -158,7 +167,11 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
   constexpr int lds = 2 * (BM + BN) * BK * 2;
   dim3 grid(g.N / BN, (g.M + BM - 1) / BM, g.batch);
   if (grid.y > 65535) return hipErrorInvalidValue;
-  if (g.cv == 1) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), lds, s, g);
+  if (g.f16) {
+    if (g.cv == 1) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, 1, true>), grid, dim3(256), lds, s, g);
+    else if (g.cv == 2) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, 2, true>), grid, dim3(256), lds, s, g);
+    else hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, 0, true>), grid, dim3(256), lds, s, g);
+  } else if (g.cv == 1) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, 1>), grid, dim3(256), lds, s, g);
   else if (g.cv == 2) hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, 2>), grid, dim3(256), lds, s, g);
   else hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN>), grid, dim3(256), lds, s, g);
   return hipGetLastError();
@@ -187,7 +200,8 @@ int gemm_tile_class(const GemmArgs& g) {
   // 256 x 256 tiles whenever N allows and there are >= 96 of them (trunk sweep, profiles/r01
   // v6_trunk_class_sweep.txt: even 98-196 tiles beat 4x as many 128 x 128 tiles); 128 x 128 only for
   // N >= 256 (at N = 128 the 64 x 64 kernel is faster)
-  if (g.f16) return gemm_f16_persistent(g) ? PROF_GEMM_F16P : PROF_GEMM_256;  // the fp16 forms live in launch_gemm_256
+  // the ViT's fp16 forms live in launch_gemm_256; the fp16 trunk convolutions (with a BN scale) pick as bf16 does
+  if (g.f16 && !g.scale) return gemm_f16_persistent(g) ? PROF_GEMM_F16P : PROF_GEMM_256;
   const long huge_tiles = (long)((g.M + 255) / 256) * (g.N / 256) * g.batch;
   if (g.N % 256 == 0 && g.batch == 1 && huge_tiles >= 96) return PROF_GEMM_256;
   const long big_tiles = (long)((g.M + 127) / 128) * (g.N / 128) * g.batch;
@@ -616,12 +630,63 @@ hipError_t launch_gemm_256(const GemmArgs& g0, hipStream_t s) {
 // Product forms of the 256-wide encoder GEMM.  The measured-and-rejected forms (8-phase template, staging-only
 // ablations, 64-row and 64-deep two-block forms, tail split, ping-pong fp16 k-loop, ...) live in gemm_tools.hip,
 // which only the tools build compiles; launch_gemm_256_tools takes the launch when one of its knobs asks for it.
+namespace {
+
+// The bf16 / bf16x2 encoder and trunk GEMMs, and (F16) the ICAP_PREC_F16 Grid trunk's convolutions on fp16 planes.
+template <bool F16>
+hipError_t run_256(const GemmArgs& g, hipStream_t s) {
+  static bool attr = false;
+  constexpr int lds2 = 3 * 3 * 256 * 32 * 2, lds1 = 4 * 2 * 256 * 32 * 2;
+  if (!attr) {
+    hipError_t e = hipSuccess;
+    for (const void* f : {(const void*)gemm_256_kernel<2, 16, 0, 0, 256, 0, 32, 0, F16>,
+                          (const void*)gemm_256_kernel<2, 16, 0, 1, 256, 0, 32, 0, F16>})
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
+    for (const void* f : {(const void*)gemm_256_kernel<1, 16, 0, 0, 256, 0, 32, 0, F16>,
+                          (const void*)gemm_256_kernel<1, 16, 0, 1, 256, 0, 32, 0, F16>})
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  if (g.cv && g.cv != 1) return hipErrorInvalidValue;
+  if (g.split_slots) return hipErrorNotSupported;  // the tail split is a tools-build form
+  // 128 x 256 tiles, 2-stage ring, 2 blocks per CU for K >= 128: ViT 42.9 -> 41.8 ms/step (MLP-out's 591 tiles
+  // become 1182: 4.6 instead of 2.3 rounds), trunk conv3 203 -> 177 us; at K = 64 the 3-stage 256 x 256 ring
+  // stays ahead (tools/halfk_sweep.sh)
+  if (g.K >= 128) {
+    const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
+    constexpr int ldsh = 2 * (2 * 128 * 32 * 2 + 256 * 32 * 2), ldsh1 = 2 * (128 * 32 * 2 + 256 * 32 * 2);
+    if (g.nsplit == 2) {
+      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 1, 128, 2, 32, 0, F16>), dim3(nwgh), dim3(512), ldsh, s, g);
+      else hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 0, 128, 2, 32, 0, F16>), dim3(nwgh), dim3(512), ldsh, s, g);
+    } else {
+      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 1, 128, 2, 32, 0, F16>), dim3(nwgh), dim3(512), ldsh1, s, g);
+      else hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 0, F16>), dim3(nwgh), dim3(512), ldsh1, s, g);
+    }
+    return hipGetLastError();
+  }
+  // K < 128: 256 x 256 tiles, 16 waves, 3-stage (two planes) / 4-stage ring
+  const int nwg = (g.N / 256) * ((g.M + 255) / 256);
+  if (g.nsplit == 2) {
+    if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 16, 0, 1, 256, 0, 32, 0, F16>), dim3(nwg), dim3(1024), lds2, s, g);
+    else hipLaunchKernelGGL((gemm_256_kernel<2, 16, 0, 0, 256, 0, 32, 0, F16>), dim3(nwg), dim3(1024), lds2, s, g);
+  } else {
+    if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 16, 0, 1, 256, 0, 32, 0, F16>), dim3(nwg), dim3(1024), lds1, s, g);
+    else hipLaunchKernelGGL((gemm_256_kernel<1, 16, 0, 0, 256, 0, 32, 0, F16>), dim3(nwg), dim3(1024), lds1, s, g);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
 hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N % 256 || g.K % 32 || g.batch != 1 || (g.nsplit != 1 && g.nsplit != 2))
     return hipErrorInvalidValue;
   const long last_row = g.rm_group ? (long)((g.M - 1) / g.rm_group) * g.rm_stride + g.rm_off + g.rm_group : g.M;
   if (last_row * g.ldc >= (1L << 31)) return hipErrorInvalidValue;  // epilogue uses 32-bit row offsets
-  if (g.f16 && (g.nsplit != 1 || g.cv || g.res || g.scale || (g.out == OUT_SPLIT && g.c_planes != 1) || g.K < 128))
+  // f16 without a BN scale: the ViT encoder's single-plane GEMMs; with one: the Grid trunk's convolutions
+  const bool vit16 = g.f16 && !g.scale;
+  if (vit16 && (g.nsplit != 1 || g.cv || g.res || (g.out == OUT_SPLIT && g.c_planes != 1) || g.K < 128))
     return hipErrorInvalidValue;
   static int cus = 0;
   if (!cus) {
@@ -629,12 +694,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       return hipErrorInvalidValue;
-    constexpr int lds2 = 3 * 3 * 256 * 32 * 2, lds1 = 4 * 2 * 256 * 32 * 2;
     hipError_t e = hipSuccess;
-    for (const void* f : {(const void*)gemm_256_kernel<2, 16>, (const void*)gemm_256_kernel<2, 16, 0, 1>})
-      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
-    for (const void* f : {(const void*)gemm_256_kernel<1, 16>, (const void*)gemm_256_kernel<1, 16, 0, 1>})
-      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
     for (const void* f : {(const void*)gemm_f16p_kernel<1>, (const void*)gemm_f16p_kernel<2>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048);
     if (e == hipSuccess)
@@ -646,12 +706,12 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     }
   }
 #ifdef ICAP_TOOLS
-  {
+  if (!g.f16 || vit16) {
     hipError_t e = hipSuccess;
     if (launch_gemm_256_tools(g, s, cus, &e)) return e;
   }
 #endif
-  if (g.f16) {  // fp16 single plane (ICAP_PREC_F16 encoder)
+  if (vit16) {  // fp16 single plane (ICAP_PREC_F16 encoder)
     if (gemm_f16_persistent(g)) {
       // store-only epilogues with whole 256-row bands (the ViT QKV and MLP-1 GEMMs): the persistent counted-seam
       // form (QKV 305 -> 265 us, MLP-1 423 -> 342 us at B = 256, tools/f16_forms_r2.sh); the residual GEMMs on
@@ -672,36 +732,8 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 0, true>), dim3(nwgh), dim3(512), ldsh1, s, g);
     return hipGetLastError();
   }
-  if (g.cv && g.cv != 1) return hipErrorInvalidValue;
-  if (g.split_slots) return hipErrorNotSupported;  // the tail split is a tools-build form
-  // 128 x 256 tiles, 2-stage ring, 2 blocks per CU for K >= 128: ViT 42.9 -> 41.8 ms/step (MLP-out's 591 tiles
-  // become 1182: 4.6 instead of 2.3 rounds), trunk conv3 203 -> 177 us; at K = 64 the 3-stage 256 x 256 ring
-  // stays ahead (tools/halfk_sweep.sh)
-  if (g.K >= 128) {
-    const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
-    constexpr int ldsh = 2 * (2 * 128 * 32 * 2 + 256 * 32 * 2), ldsh1 = 2 * (128 * 32 * 2 + 256 * 32 * 2);
-    if (g.nsplit == 2) {
-      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 1, 128, 2>), dim3(nwgh), dim3(512), ldsh, s, g);
-      else hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 0, 128, 2>), dim3(nwgh), dim3(512), ldsh, s, g);
-    } else {
-      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 1, 128, 2>), dim3(nwgh), dim3(512), ldsh1, s, g);
-      else hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2>), dim3(nwgh), dim3(512), ldsh1, s, g);
-    }
-    return hipGetLastError();
-  }
-  // K < 128: 256 x 256 tiles, 16 waves, 3-stage (bf16x2) / 4-stage ring
-  constexpr int lds2 = 3 * 3 * 256 * 32 * 2, lds1 = 4 * 2 * 256 * 32 * 2;
-  const int nwg = (g.N / 256) * ((g.M + 255) / 256);
-  if (g.nsplit == 2) {
-    if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 16, 0, 1>), dim3(nwg), dim3(1024), lds2, s, g);
-    else hipLaunchKernelGGL((gemm_256_kernel<2, 16>), dim3(nwg), dim3(1024), lds2, s, g);
-  } else {
-    if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 16, 0, 1>), dim3(nwg), dim3(1024), lds1, s, g);
-    else hipLaunchKernelGGL((gemm_256_kernel<1, 16>), dim3(nwg), dim3(1024), lds1, s, g);
-  }
-  return hipGetLastError();
+  return g.f16 ? run_256<true>(g, s) : run_256<false>(g, s);
 }
-
 
 // ---------------------------------------------------------------------------------------------
 // int8 two-slice encoder GEMM for the LayerNorm-fed projections (ViT QKV, MLP-1, final projection

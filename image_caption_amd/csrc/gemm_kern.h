@@ -87,14 +87,17 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
       for (int i = 0; i < TM; ++i) {
         const long ro = (long)min(mb + i * 16 + fr, M - 1) * p.res_ld + nb + j * 16 + 4 * fq;
         rh[i] = *(const u32x2*)(p.res + ro);
-        rl[i] = *(const u32x2*)(p.res + ro + p.res_lo);
+        rl[i] = F16 && p.res_planes == 1 ? (u32x2){0u, 0u} : *(const u32x2*)(p.res + ro + p.res_lo);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const uint32_t wh = rh[i][r >> 1] >> ((r & 1) * 16), wl = rl[i][r >> 1] >> ((r & 1) * 16);
-          acc[i][j][r] += bf2f((bf16_t)(wh & 0xffff)) + bf2f((bf16_t)(wl & 0xffff));
+          if constexpr (F16)  // fp16 planes (the ICAP_PREC_F16 Grid trunk's residual stream)
+            acc[i][j][r] += h2f((bf16_t)(wh & 0xffff)) + h2f((bf16_t)(wl & 0xffff));
+          else
+            acc[i][j][r] += bf2f((bf16_t)(wh & 0xffff)) + bf2f((bf16_t)(wl & 0xffff));
         }
     }
   }
@@ -149,13 +152,29 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
         for (int i = 0; i < 4; ++i)
           if (orow[i0 + i] >= 0) *(f32x4*)(C + orow[i0 + i] + nb + j * 16 + 4 * fq) = c[i] + acc[i0 + i][j];
       }
-  } else if (F16) {  // one fp16 plane
+  } else if (F16) {  // one fp16 plane, or hi / lo fp16 planes (c_planes == 2: the Grid trunk's residual stream)
     bf16_t* C = (bf16_t*)p.C;
+    const bool lo_plane = p.out == OUT_SPLIT && p.c_planes == 2;
+    bool bad = false;  // fp16 range guard: a stored value that is not finite in fp16
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        if (orow[i] >= 0) *(u32x2*)(C + orow[i] + nb + j * 16 + 4 * fq) = pack16x4<true>(acc[i][j]);
+      for (int j = 0; j < TN; ++j) {
+        if (orow[i] < 0) continue;
+        const u32x2 hv = pack16x4<true>(acc[i][j]);
+        bad |= f16_pair_nonfinite(hv[0]) || f16_pair_nonfinite(hv[1]);
+        *(u32x2*)(C + orow[i] + nb + j * 16 + 4 * fq) = hv;
+        if (lo_plane) {
+          f32x4 lo;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t w = hv[r >> 1] >> ((r & 1) * 16);
+            lo[r] = acc[i][j][r] - h2f((bf16_t)(w & 0xffff));
+          }
+          *(u32x2*)(C + orow[i] + nb + j * 16 + 4 * fq + p.c_lo) = pack16x4<true>(lo);
+        }
+      }
+    if (p.range_flag && __any(bad) && (threadIdx.x & 63) == 0) range_flag_set(p.range_flag);
   } else {
     bf16_t* C = (bf16_t*)p.C;
     const bool lo_plane = p.out == OUT_SPLIT && p.c_planes == 2;

@@ -97,6 +97,7 @@ struct EncLayer {
 };
 struct Conv {  // packed Conv2d + eval BatchNorm: bf16 W [cout][Kp] in (kh, kw, c) order, fp32 scale/shift
   bf16_t* w = nullptr;
+  bf16_t* w16 = nullptr;  // the same in fp16 (ICAP_PREC_F16 Grid: the eval trunk on fp16 planes)
   float *scale = nullptr, *shift = nullptr;
   int cout = 0, cin = 0, k = 1, stride = 1, Kp = 0;
 };
@@ -142,6 +143,11 @@ struct icap_handle {
   bool i8 = false;  // ICAP_PREC_I8X2: LayerNorm-fed ViT GEMMs on int8 two-slice operands
   bool i8k = false;  // ... and MLP-2 on the block-scaled int8 GELU output (ICAP_I8_MLP2=1, opt-in)
   bool f16 = false;  // ICAP_PREC_F16: the ViT encoder on single fp16 planes (fp16 MFMA); the decoder stays bf16x2
+  // ICAP_PREC_F16 on a Grid model: the eval ResNet trunk on fp16 planes - the residual stream as one fp16 plane in
+  // layer1-2 and as fp16 hi/lo planes (~22 bits) in layer3-4, the bottleneck branch (conv1 / conv2 outputs) as one
+  // fp16 plane, fp16 weights and MFMA (encode_grid); the tail and the decoder stay bf16x2, train-mode
+  // BatchNorm stays on the bf16x2 trunk
+  bool t16 = false;
   // hi/lo decoder weights (icap_model_desc.dec_weight_planes = 2: fp32 checkpoints that are not bf16-exact): every
   // decoder GEMM weight is packed as hi = bf16(W) and lo = bf16(W - hi) and the decode runs the unfused launches,
   // whose GEMMs add W_lo . X_hi; the train-mode dropout sampler keeps the fused blocks (W_hi only)
@@ -340,6 +346,10 @@ struct icap_handle {
     o.Kp = stem ? 8 * 8 * 4 : (c.cin * c.k * c.k + 63) / 64 * 64;
     o.w = (bf16_t*)alloc((size_t)o.cout * o.Kp * 2);
     HIPCHK(launch_pack_conv(c.w, c.cout, c.cin, c.k, cp, kwp, o.Kp, o.w, s));
+    if (t16) {
+      o.w16 = (bf16_t*)alloc((size_t)o.cout * o.Kp * 2);
+      HIPCHK(launch_pack_conv(c.w, c.cout, c.cin, c.k, cp, kwp, o.Kp, o.w16, s, true));
+    }
     o.scale = (float*)alloc((size_t)c.cout * 4);
     o.shift = (float*)alloc((size_t)c.cout * 4);
     HIPCHK(launch_bn_fold(c.bn_w, c.bn_b, c.bn_mean, c.bn_var, c.cout, 1e-5f, o.scale, o.shift, s));
@@ -761,9 +771,16 @@ struct BnTrain {
   float momentum = 0.1f;
 };
 
+// f16 (ICAP_PREC_F16 eval trunk): A is a_planes fp16 planes, the output out_planes fp16 planes (the residual planes,
+// when given, fp16 hi/lo), fp16 weights (Conv::w16); stored values that overflow fp16 set the range guard word
+struct Trunk16 {
+  bool on = false;
+  int a_planes = 1, out_planes = 1, res_planes = 2;
+};
+
 void trunk_conv(icap_handle* h, const Conv& c, const bf16_t* A, long a_ld, long a_lo, int M, bf16_t* out, long out_lo,
                 bool relu, const bf16_t* res, long res_lo, hipStream_t s, const ConvGeom& cg = ConvGeom(),
-                const icap_conv_bn_w* bn = nullptr, float momentum = 0.f) {
+                const icap_conv_bn_w* bn = nullptr, float momentum = 0.f, const Trunk16& t16 = Trunk16()) {
   GemmArgs g = gemm_args();
   if (cg.cv) {
     g.cv = cg.cv; g.cv_H = cg.H; g.cv_W = cg.W; g.cv_OW = cg.OW; g.cv_OHW = cg.OH * cg.OW;
@@ -776,6 +793,11 @@ void trunk_conv(icap_handle* h, const Conv& c, const bf16_t* A, long a_ld, long 
   g.C = out; g.ldc = c.cout; g.c_lo = out_lo; g.c_planes = 2;
   g.M = M; g.N = c.cout; g.K = c.Kp; g.nsplit = h->ns;
   g.out = OUT_SPLIT;
+  if (t16.on) {
+    REQUIRE(c.w16 && !bn, "fp16 trunk: eval BatchNorm on a handle packed with fp16 weights");
+    g.f16 = 1; g.W = c.w16; g.nsplit = t16.a_planes; g.c_planes = t16.out_planes; g.res_planes = t16.res_planes;
+    g.range_flag = h->range_word();
+  }
   if (!bn) {
     g.bias = c.shift; g.scale = c.scale;
     g.epi = relu ? EPI_RELU : EPI_NONE;
@@ -881,14 +903,26 @@ void encode_grid(icap_handle* h, const float* img, int B, int IH, int IW, float*
   h->t_col.ensure((size_t)cL * 2 * ns);
   bf16_t *X = h->t_x.as<bf16_t>(), *Y = h->t_y.as<bf16_t>(), *T1 = h->t_1.as<bf16_t>(), *T2 = h->t_2.as<bf16_t>(),
          *R = h->t_r.as<bf16_t>(), *col = h->t_col.as<bf16_t>();
+  // fp16 eval trunk (ICAP_PREC_F16): the image and the bottleneck branch as one fp16 plane; the residual stream (stem /
+  // max-pool output, block and downsample outputs) as one fp16 plane in layer1-2, where it is largest (the HBM-bound
+  // stage: 802k / 401k elements per image), and as fp16 hi/lo planes in layer3-4, which hold 26 of the 33 roundings
+  // (CPU emulation, DESIGN.md §3: trunk features 3.2e-4 relative, memory 1.1e-3, logits 1.1e-4)
+  const bool f16 = h->t16 && !bt.bn;
+  auto xpl = [&](int st) { return f16 ? (st < 2 ? 1 : 2) : ns; };  // residual-stream planes of stage st
+  auto t16 = [&](int a_planes, int out_planes, int res_planes = 2) {
+    Trunk16 t;
+    t.on = f16; t.a_planes = a_planes; t.out_planes = out_planes; t.res_planes = res_planes;
+    return t;
+  };
   for (int b0 = 0; b0 < B; b0 += bc_max) {
     const int bc = std::min(bc_max, B - b0);
     const Conv& stem = h->trunk[0];
-    HIPCHK(launch_image_nhwc4(img + (size_t)b0 * 3 * IH * IW, bc, IH, IW, BORDER, col, cL, ns, s));
+    HIPCHK(launch_image_nhwc4(img + (size_t)b0 * 3 * IH * IW, bc, IH, IW, BORDER, col, cL, f16 ? 1 : ns, s, f16));
     ConvGeom sg;
     sg.cv = 2; sg.H = HP; sg.W = WP; sg.C = 4; sg.OH = H1; sg.OW = W1;
-    trunk_conv(h, stem, col, 0, cL, bc * H1 * W1, T1, aL, true, nullptr, 0, s, sg, bnp(0), bt.momentum);
-    HIPCHK(launch_maxpool3s2(T1, aL, bc, H1, W1, stem.cout, H2, W2, X, aL, ns, s));
+    trunk_conv(h, stem, col, 0, cL, bc * H1 * W1, T1, aL, true, nullptr, 0, s, sg, bnp(0), bt.momentum,
+               t16(1, xpl(0)));
+    HIPCHK(launch_maxpool3s2(T1, aL, bc, H1, W1, stem.cout, H2, W2, X, aL, xpl(0), s, f16));
     int hh = H2, ww = W2;
     size_t ci = 1;
     for (int st = 0; st < 4; ++st)
@@ -900,30 +934,41 @@ void encode_grid(icap_handle* h, const float* img, int B, int IH, int IW, float*
         ci += 3;
         const int oh = c2.stride == 2 ? half(hh) : hh, ow = c2.stride == 2 ? half(ww) : ww;
         const int Min = bc * hh * ww, Mout = bc * oh * ow;
+        const int pin = xpl(j == 0 && st > 0 ? st - 1 : st), pout = xpl(st);  // planes of X and of the output
         const bf16_t* res = X;
+        int rpl = pin;
         if (ds) {  // identity branch: 1x1 conv (stride = the block's) + BN, no ReLU
           const bf16_t* dsA = X;
           long dsL = aL;
           if (ds->stride == 2) {
-            HIPCHK(launch_subsample2(X, aL, bc, hh, ww, ds->cin, col, cL, ns, s));
+            HIPCHK(launch_subsample2(X, aL, bc, hh, ww, ds->cin, col, cL, pin, s));
             dsA = col;
             dsL = cL;
           }
-          trunk_conv(h, *ds, dsA, ds->cin, dsL, Mout, R, aL, false, nullptr, 0, s, ConvGeom(), bnp(ids), bt.momentum);
+          trunk_conv(h, *ds, dsA, ds->cin, dsL, Mout, R, aL, false, nullptr, 0, s, ConvGeom(), bnp(ids), bt.momentum,
+                     t16(pin, pout));
           res = R;
+          rpl = pout;
         }
-        trunk_conv(h, c1, X, c1.cin, aL, Min, T1, aL, true, nullptr, 0, s, ConvGeom(), bnp(i1), bt.momentum);
+        trunk_conv(h, c1, X, c1.cin, aL, Min, T1, aL, true, nullptr, 0, s, ConvGeom(), bnp(i1), bt.momentum,
+                   t16(pin, 1));
         ConvGeom g3;  // 3x3 conv2 read straight from T1 (implicit GEMM)
         g3.cv = 1; g3.H = hh; g3.W = ww; g3.C = c1.cout; g3.OH = oh; g3.OW = ow;
-        trunk_conv(h, c2, T1, 0, aL, Mout, T2, aL, true, nullptr, 0, s, g3, bnp(i1 + 1), bt.momentum);
-        trunk_conv(h, c3, T2, c3.cin, aL, Mout, Y, aL, true, res, aL, s, ConvGeom(), bnp(i1 + 2), bt.momentum);
+        trunk_conv(h, c2, T1, 0, aL, Mout, T2, aL, true, nullptr, 0, s, g3, bnp(i1 + 1), bt.momentum, t16(1, 1));
+        trunk_conv(h, c3, T2, c3.cin, aL, Mout, Y, aL, true, res, aL, s, ConvGeom(), bnp(i1 + 2), bt.momentum,
+                   t16(1, pout, rpl));
         std::swap(X, Y);
         hh = oh;
         ww = ow;
       }
     REQUIRE(hh == GH && ww == GW, "trunk output grid mismatch");
-    if (feats)  // trunk features (both planes: the values the tail consumes)
-      HIPCHK(launch_planes_to_f32(X, aL, (long)bc * N * d.cnn_dim, 2, feats + (size_t)b0 * N * d.cnn_dim, s));
+    float* fb = feats ? feats + (size_t)b0 * N * d.cnn_dim : nullptr;
+    if (f16) {  // the tail reads bf16 hi/lo planes: re-split the fp16 pair (and write the fp32 features)
+      HIPCHK(launch_f16planes_to_bf16(X, aL, (long)bc * N * d.cnn_dim, Y, aL, fb, s));
+      std::swap(X, Y);
+    } else if (fb) {  // trunk features (both planes: the values the tail consumes)
+      HIPCHK(launch_planes_to_f32(X, aL, (long)bc * N * d.cnn_dim, 2, fb, s));
+    }
     encode_grid_rows(h, X, aL, bc, N, memory + (size_t)b0 * N * d.d_model, s);
   }
 }
@@ -1756,6 +1801,7 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
       h->ns = desc->precision == ICAP_PREC_BF16 ? 1 : 2;
       h->i8 = desc->precision == ICAP_PREC_I8X2 && desc->kind == ICAP_KIND_VIT;
       h->f16 = desc->precision == ICAP_PREC_F16 && desc->kind == ICAP_KIND_VIT;
+      h->t16 = desc->precision == ICAP_PREC_F16 && desc->kind == ICAP_KIND_GRID;
       REQUIRE(desc->dec_weight_planes >= 0 && desc->dec_weight_planes <= 2, "dec_weight_planes must be 0, 1 or 2");
       h->wlo = desc->dec_weight_planes == 2;
       h->use_step = icap_knob("ICAP_DEC_STEP", 0) != 0;

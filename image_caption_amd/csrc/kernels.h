@@ -59,6 +59,7 @@ struct GemmArgs {
   // convolution epilogue (ResNet trunk): v = acc * scale[n] + bias[n] (+ res planes) before the
   // activation; res = bf16 hi plane at res[row * res_ld + n], lo plane at + res_lo
   const float* scale; const bf16_t* res; long res_ld; long res_lo;
+  int res_planes;  // 2 (default): hi + lo; 1: the hi plane only (the fp16 trunk's one-plane residual stream)
   // implicit-GEMM convolution (A is not materialised; rows = output pixels (b, oh, ow)):
   //   cv = 1: 3x3 / pad 1 / stride cv_stride over NHWC planes A [B][cv_H][cv_W][C], C = 1 << cv_cshift
   //           (>= 64), k = (kh*3 + kw)*C + c; taps outside the image read cv_zero (>= 16 zero bytes)
@@ -91,7 +92,7 @@ struct GemmArgs {
 };
 // bytes of split_ws for split_slots block slots per XCD
 inline size_t gemm_split_ws_bytes(int split_slots) { return (size_t)8 * split_slots * 2 * 128 * 256 * 4; }
-inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; return g; }
+inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; g.res_planes = 2; return g; }
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
 // Which kernel launch_gemm picks (PROF_GEMM_256 / PROF_GEMM_128 / PROF_GEMM_64).
 int gemm_tile_class(const GemmArgs& g);
@@ -254,8 +255,9 @@ hipError_t launch_nchw_to_rows(const float* feats, int B, int C, int S, bf16_t* 
 // ResNet trunk (trunk.hip): gathers into GEMM A operands (NHWC bf16 planes), max-pool, packing
 hipError_t launch_subsample2(const bf16_t* x, long xlo, int B, int H, int W, int C, bf16_t* out, long lo, int nsplit,
                              hipStream_t s);
+// (f16: fp16 planes, the ICAP_PREC_F16 trunk; subsample2 copies bits and serves both)
 hipError_t launch_maxpool3s2(const bf16_t* x, long xlo, int B, int H, int W, int C, int OH, int OW, bf16_t* out,
-                             long lo, int nsplit, hipStream_t s);
+                             long lo, int nsplit, hipStream_t s, bool f16 = false);
 // [Cout][Kp] bf16 with k = (kh*kwp + kw)*cp + c (cp >= cin, kwp >= k; padding taps/channels are 0)
 // CIDEr-D on token-id rows (cider.hip): hypothesis k belongs to image k % B; image i's references
 // are rows ref_off[i] .. ref_off[i+1]; rows are raw ids (<start>/<pad> dropped, cut at <end>)
@@ -268,10 +270,10 @@ hipError_t launch_cider(const int32_t* hyp, int n_hyp, int Lh, int B, const int3
 hipError_t launch_preprocess(const uint8_t* px, const int64_t* offs, const int32_t* geom, int B, int S, int max_rows,
                              uint8_t* tmp, float* out, hipStream_t s);
 hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int cp, int kwp, int Kp, bf16_t* out,
-                            hipStream_t s);
+                            hipStream_t s, bool f16 = false);
 // (B,3,HW,HW) fp32 -> zero-bordered NHWC4 planes [B][HW+2*border][HW+2*border][4] (channel 3 = 0)
 hipError_t launch_image_nhwc4(const float* img, int B, int IH, int IW, int border, bf16_t* out, long lo, int nsplit,
-                              hipStream_t s);
+                              hipStream_t s, bool f16 = false);
 // Train-mode BatchNorm over the raw convolution output planes y [M][C] (in place): batch statistics
 // (double sums over all M rows, deterministic), running statistics updated with momentum (unbiased variance),
 // then y = relu?(y * scale + shift (+ res planes)).  part: bn_part_bytes(); scale / shift: C floats each.
@@ -291,6 +293,9 @@ hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hip
 hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int nsplit, hipStream_t s);
 // bf16 planes -> fp32 (hi + lo)
 hipError_t launch_planes_to_f32(const bf16_t* src, long lo, long n, int nsplit, float* dst, hipStream_t s);
+// fp16 hi/lo planes -> bf16 hi/lo planes of the same values (+ their fp32 sum when f32 != nullptr); n % 4 == 0
+hipError_t launch_f16planes_to_bf16(const bf16_t* src, long slo, long n, bf16_t* dst, long dlo, float* f32,
+                                   hipStream_t s);
 hipError_t launch_f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);
 hipError_t launch_f32_to_f16(const float* src, bf16_t* dst, long n, hipStream_t s);
 hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf16_t* dst, hipStream_t s,

@@ -309,6 +309,26 @@ __global__ void planes_to_f32_kernel(const bf16_t* src, long lo, long n, int nsp
     dst[i] = nsplit == 2 ? bf2f(src[i]) + bf2f(src[i + lo]) : bf2f(src[i]);
 }
 
+// fp16 hi/lo planes (the ICAP_PREC_F16 trunk output) -> bf16 hi/lo planes of the same values (the bf16x2 Grid
+// tail's input), and optionally their fp32 sum (the trunk features); 4 elements per thread
+__global__ void f16planes_to_bf16_kernel(const bf16_t* src, long slo, long n4, bf16_t* dst, long dlo, float* f32) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const u32x2 h = *(const u32x2*)(src + 4 * i), l = *(const u32x2*)(src + 4 * i + slo);
+    f32x4 v;
+    bf16_t oh[4], ol[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sh = (r & 1) * 16;
+      v[r] = h2f((bf16_t)((h[r >> 1] >> sh) & 0xffff)) + h2f((bf16_t)((l[r >> 1] >> sh) & 0xffff));
+      split_bf(v[r], oh[r], ol[r]);
+    }
+    *(u32x2*)(dst + 4 * i) = (u32x2){(uint32_t)oh[0] | ((uint32_t)oh[1] << 16), (uint32_t)oh[2] | ((uint32_t)oh[3] << 16)};
+    *(u32x2*)(dst + 4 * i + dlo) =
+        (u32x2){(uint32_t)ol[0] | ((uint32_t)ol[1] << 16), (uint32_t)ol[2] | ((uint32_t)ol[3] << 16)};
+    if (f32) *(f32x4*)(f32 + 4 * i) = v;
+  }
+}
+
 __global__ void f32_to_bf16_kernel(const float* src, bf16_t* dst, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     dst[i] = f2bf(src[i]);
@@ -432,6 +452,13 @@ hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hip
 
 hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int nsplit, hipStream_t s) {
   hipLaunchKernelGGL(split_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, n, dst, lo, nsplit);
+  return hipGetLastError();
+}
+
+hipError_t launch_f16planes_to_bf16(const bf16_t* src, long slo, long n, bf16_t* dst, long dlo, float* f32,
+                                   hipStream_t s) {
+  if (n % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(f16planes_to_bf16_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, src, slo, n / 4, dst, dlo, f32);
   return hipGetLastError();
 }
 

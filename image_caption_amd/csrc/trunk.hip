@@ -27,7 +27,8 @@ __global__ void subsample2_kernel(const bf16_t* __restrict__ x, long xlo, int B,
 }
 
 // 3x3 / stride 2 / pad 1 max-pool on planes (the value is hi + lo; -inf padding like torch);
-// 8 channels per thread, 16-byte loads of each plane
+// 8 channels per thread, 16-byte loads of each plane.  F16: fp16 planes (the ICAP_PREC_F16 trunk)
+template <bool F16>
 __global__ void maxpool3s2_kernel(const bf16_t* __restrict__ x, long xlo, int B, int H, int W, int C, int OH, int OW,
                                   bf16_t* out, long lo, int nsplit) {
   const int C8 = C / 8;
@@ -52,8 +53,8 @@ __global__ void maxpool3s2_kernel(const bf16_t* __restrict__ x, long xlo, int B,
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t hw = hv[e >> 1], lw = lv[e >> 1];
-          const float v = __uint_as_float((e & 1 ? hw >> 16 : hw & 0xffffu) << 16) +
-                          __uint_as_float((e & 1 ? lw >> 16 : lw & 0xffffu) << 16);
+          const bf16_t hb = (bf16_t)(e & 1 ? hw >> 16 : hw & 0xffffu), lb = (bf16_t)(e & 1 ? lw >> 16 : lw & 0xffffu);
+          const float v = F16 ? h2f(hb) + (nsplit == 2 ? h2f(lb) : 0.f) : bf2f(hb) + bf2f(lb);
           m[e] = fmaxf(m[e], v);
         }
       }
@@ -62,8 +63,13 @@ __global__ void maxpool3s2_kernel(const bf16_t* __restrict__ x, long xlo, int B,
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       bf16_t h0, l0, h1, l1;
-      split_bf(m[2 * e], h0, l0);
-      split_bf(m[2 * e + 1], h1, l1);
+      if (F16) {
+        split_h(m[2 * e], h0, l0);
+        split_h(m[2 * e + 1], h1, l1);
+      } else {
+        split_bf(m[2 * e], h0, l0);
+        split_bf(m[2 * e + 1], h1, l1);
+      }
       ho[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
       lo4[e] = (uint32_t)l0 | ((uint32_t)l1 << 16);
     }
@@ -85,16 +91,20 @@ hipError_t launch_subsample2(const bf16_t* x, long xlo, int B, int H, int W, int
 }
 
 hipError_t launch_maxpool3s2(const bf16_t* x, long xlo, int B, int H, int W, int C, int OH, int OW, bf16_t* out,
-                             long lo, int nsplit, hipStream_t s) {
+                             long lo, int nsplit, hipStream_t s, bool f16) {
   if (C % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid_for((long)B * OH * OW * (C / 8))), dim3(256), 0, s, x, xlo, B, H,
-                     W, C, OH, OW, out, lo, nsplit);
+  const dim3 grid(grid_for((long)B * OH * OW * (C / 8)));
+  if (f16)
+    hipLaunchKernelGGL(maxpool3s2_kernel<true>, grid, dim3(256), 0, s, x, xlo, B, H, W, C, OH, OW, out, lo, nsplit);
+  else
+    hipLaunchKernelGGL(maxpool3s2_kernel<false>, grid, dim3(256), 0, s, x, xlo, B, H, W, C, OH, OW, out, lo, nsplit);
   return hipGetLastError();
 }
 
 namespace {
 
-// torch conv weight [Cout][Cin][kh][kw] fp32 -> [Cout][Kp] bf16, k = (kh*kwp + kw)*cp + c, 0 on padding
+// torch conv weight [Cout][Cin][kh][kw] fp32 -> [Cout][Kp] bf16 (F16: fp16), k = (kh*kwp + kw)*cp + c, 0 on padding
+template <bool F16>
 __global__ void pack_conv_kernel(const float* __restrict__ w, int cout, int cin, int k, int cp, int kwp, int Kp,
                                  bf16_t* out) {
   const long total = (long)cout * Kp;
@@ -104,11 +114,12 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, int cout, int cin,
     const int c = kk % cp, tap = kk / cp, kh = tap / kwp, kw = tap % kwp;
     float v = 0.f;
     if (c < cin && kw < k && kh < k) v = w[((o * cin + c) * k + kh) * k + kw];
-    out[i] = f2bf(v);
+    out[i] = cvt16<F16>(v);
   }
 }
 
-// (B,3,IH,IW) fp32 -> [B][IH + 2 border][IW + 2 border][4] planes, zero border and channel 3
+// (B,3,IH,IW) fp32 -> [B][IH + 2 border][IW + 2 border][4] planes, zero border and channel 3 (F16: fp16 planes)
+template <bool F16>
 __global__ void image_nhwc4_kernel(const float* __restrict__ img, int B, int IH, int IW, int border, bf16_t* out,
                                    long lo, int nsplit) {
   const int HP = IH + 2 * border, WP = IW + 2 * border;
@@ -122,7 +133,10 @@ __global__ void image_nhwc4_kernel(const float* __restrict__ img, int B, int IH,
       for (int c = 0; c < 3; ++c) v[c] = img[((b * 3 + c) * IH + y) * IW + x];
     bf16_t h[4], l[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) split_bf(v[c], h[c], l[c]);
+    for (int c = 0; c < 4; ++c) {
+      if (F16) split_h(v[c], h[c], l[c]);
+      else split_bf(v[c], h[c], l[c]);
+    }
     u32x2 hv = {(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
     *(u32x2*)(out + i * 4) = hv;
     if (nsplit == 2) {
@@ -235,18 +249,22 @@ __global__ void bn_apply_kernel(bf16_t* y, long lo, long M, int C, const float* 
 }  // namespace
 
 hipError_t launch_pack_conv(const float* w, int cout, int cin, int k, int cp, int kwp, int Kp, bf16_t* out,
-                            hipStream_t s) {
+                            hipStream_t s, bool f16) {
   if (cp < cin || kwp < k || Kp < k * kwp * cp) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pack_conv_kernel, dim3(grid_for((long)cout * Kp)), dim3(256), 0, s, w, cout, cin, k, cp, kwp,
-                     Kp, out);
+  const dim3 grid(grid_for((long)cout * Kp));
+  if (f16) hipLaunchKernelGGL(pack_conv_kernel<true>, grid, dim3(256), 0, s, w, cout, cin, k, cp, kwp, Kp, out);
+  else hipLaunchKernelGGL(pack_conv_kernel<false>, grid, dim3(256), 0, s, w, cout, cin, k, cp, kwp, Kp, out);
   return hipGetLastError();
 }
 
 hipError_t launch_image_nhwc4(const float* img, int B, int IH, int IW, int border, bf16_t* out, long lo, int nsplit,
-                              hipStream_t s) {
+                              hipStream_t s, bool f16) {
   const long HP = IH + 2 * border, WP = IW + 2 * border;
-  hipLaunchKernelGGL(image_nhwc4_kernel, dim3(grid_for(B * HP * WP)), dim3(256), 0, s, img, B, IH, IW, border, out, lo,
-                     nsplit);
+  const dim3 grid(grid_for(B * HP * WP));
+  if (f16)
+    hipLaunchKernelGGL(image_nhwc4_kernel<true>, grid, dim3(256), 0, s, img, B, IH, IW, border, out, lo, nsplit);
+  else
+    hipLaunchKernelGGL(image_nhwc4_kernel<false>, grid, dim3(256), 0, s, img, B, IH, IW, border, out, lo, nsplit);
   return hipGetLastError();
 }
 

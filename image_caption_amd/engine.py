@@ -234,15 +234,16 @@ class Engine:
             self.handle = None
 
     def range_overflowed(self) -> bool:
-        """fp16 range guard of the f16 ViT encoder (icap_range_check): True when a LayerNorm /
-        Q,K,V / GELU output stored as fp16 since the last check was not finite (|v| >= 65520 or NaN), i.e. the
+        """fp16 range guard of the f16 encoders (icap_range_check): True when a ViT LayerNorm /
+        Q,K,V / GELU output or a Grid trunk activation stored as fp16 since the last check was not finite
+        (|v| >= 65520 or NaN), i.e. the
         memory of those encodes is not trustworthy and must be recomputed in bf16x2.  Synchronises the
         engine's current stream; always False for precisions without fp16 activations.  Also the health check of
         the persistent decode: raises IcapError if a decode step gave up waiting for a dependency.""" 
         out = ctypes.c_int(0)
         # raises if a persistent decode step gave up waiting for a dependency (an internal error, never silent)
         check(self.lib.icap_range_check(self.handle, stream_ptr(self.device), ctypes.byref(out)), "icap_range_check")
-        return bool(out.value) and self.precision == "f16" and self.kind == "vit"
+        return bool(out.value) and self.precision == "f16"
 
     # ------------------------------------------------------------------ encoders
     def encode(self, images: torch.Tensor) -> torch.Tensor:

@@ -53,7 +53,8 @@ class GridFeatureEncoder(nn.Module):
             if eng.has_trunk and images.dim() == 4 and images.shape[1] == 3:
                 h, w = images.shape[2], images.shape[3]
                 if eng.grid_tokens(h, w) <= eng.enc_pe_len:
-                    return eng.encode(images)  # HIP trunk + tail, any image size
+                    # HIP trunk + tail, any image size; the f16 trunk's range guard re-encodes in bf16x2 on overflow
+                    return owner.checked_encode(images)[1]
             # grids larger than the PE table: the reference's own modules (the PE add raises there as well)
         return self.tail(self.cnn(images))
 

@@ -10,7 +10,8 @@ The oracle (oracle/captioner.py, fp32) runs on the GPU here - the same device-ag
 has no TF32, so torch fp32 is fp32 - and is tied to its CPU run on a few rows of each workload.
 
 Checks and tolerances (north star: logits within 1e-3, token ids identical):
-  * memory (B, S, 512): max |HIP - oracle| < 4e-3 (ViT, fp16 encoder) / 1e-3 (Grid) over all rows; Grid trunk features relative 1e-3,
+  * memory (B, S, 512): max |HIP - oracle| < 4e-3 over all rows (the default precision f16: ViT encoder and Grid
+    trunk on fp16 operands, |memory| <= ~3); Grid trunk features relative 1e-3,
     and every image's error is < 1/10 of its distance to the nearest other image (an image mix-up
     cannot pass);
   * greedy: the oracle's teacher-forced logits on the HIP ids (every row, every step) within 1e-3 of
@@ -34,6 +35,9 @@ L = 30
 # ViT memory vs the oracle in the default precision (f16: fp16 encoder operands, 2^-11 relative rounding;
 # |memory| <= ~3); the logits stay within 1e-3
 VIT_MEM_TOL = 4e-3
+# Grid memory in the default precision (f16: the ResNet trunk on fp16 planes - the residual stream as fp16 hi/lo, the
+# bottleneck branch as one fp16 plane; CPU emulation: trunk features 2.3e-4 relative, memory 8.9e-4, logits 8e-5)
+GRID_MEM_TOL = 4e-3
 
 
 def _dev_sd(sd, dev):
@@ -112,7 +116,7 @@ def test_config3_grid_b256_trunk_and_every_row(cuda, grid_sd):
     assert bool((per_img * 10 < d.amin(1)).all())
     with torch.no_grad():
         mem_o = O.grid_encode_tail(sdd, feats_o)
-    assert (mem - mem_o).abs().max().item() < 1e-3
+    assert (mem - mem_o).abs().max().item() < GRID_MEM_TOL
     rows = [0, 255]
     with torch.no_grad():
         cpu = O.grid_encode(grid_sd, imgs[rows].cpu())

@@ -141,7 +141,7 @@ def test_grid_golden(cuda):
     with torch.no_grad():
         mem = m.encoder(imgs)
     assert np.allclose(mem.double().sum(dim=(1, 2)).cpu().numpy(), g["memory_sum"], rtol=1e-4, atol=0.5)
-    assert np.abs(mem[:, :4, :16].cpu().numpy() - g["memory_head"]).max() < 1e-3
+    assert np.abs(mem[:, :4, :16].cpu().numpy() - g["memory_head"]).max() < MEM_TOL["f16"]  # default: fp16 trunk
     ids = m.generate(imgs, W.START_TOKEN, W.END_TOKEN, max_len=30)
     assert np.array_equal(ids.cpu().numpy(), g["ids"])
     eng = m.hip_engine(imgs.device)
@@ -165,9 +165,9 @@ def test_grid_trunk_vs_oracle_across_chunks(cuda):
     with torch.no_grad():
         feats = O.resnet101_trunk(sd, sub)
         ref = O.grid_encode_tail(sd, feats)
-    assert (mem[pick.to(cuda)].cpu() - ref).abs().max().item() < 1e-3
+    assert (mem[pick.to(cuda)].cpu() - ref).abs().max().item() < MEM_TOL["f16"]  # default precision: fp16 trunk
     tail = eng.encode(feats.to(cuda))
-    assert (tail.cpu() - ref).abs().max().item() < 1e-3
+    assert (tail.cpu() - ref).abs().max().item() < 1e-3  # the tail alone stays bf16x2
 
 
 def test_batch_independence_and_determinism_at_b256(vit_engine, cuda, vit_sd):
