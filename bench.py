@@ -133,6 +133,9 @@ def main():
     ap.add_argument("--no-graphs", action="store_true", help="launch the decode loop eagerly (no hipGraph)")
     ap.add_argument("--decode-chains", type=int, default=0,
                     help="independent decode chains per batch (icap_set_decode_chains; 0 = library default)")
+    ap.add_argument("--decode-step", type=int, default=-1, choices=[-1, 0, 1, 2],
+                    help="decode loop form (icap_set_decode_step: 0 launch per block, 1 task step, 2 group step; "
+                         "-1 = library default)")
     ap.add_argument("--model", default="vit", choices=["vit", "grid"])
     ap.add_argument("--torch-trunk", action="store_true", help="grid: ResNet trunk via PyTorch/MIOpen fp32")
     ap.add_argument("--mode", default="greedy", choices=["greedy", "scst", "beam"])
@@ -162,6 +165,8 @@ def main():
         eng.set_graphs(False)
     if args.decode_chains:
         eng.set_decode_chains(args.decode_chains)
+    if args.decode_step >= 0:
+        eng.set_decode_step(args.decode_step)
     B = args.batch
     total = B * ws
     imgs = torch.from_numpy(W.synthetic_images(B, seed=1 + rank)).to(dev)

@@ -227,7 +227,8 @@ struct icap_handle {
   DevBuf rflag;
   // persistent decode step (decstep.hip): per-layer weight pointers and per-step arguments in device memory, the
   // per-step counter blocks (zeroed by one memset per decode), and the key the argument array was built for
-  bool use_step = false;  // icap_set_decode_step / ICAP_DEC_STEP=1 (tools): the persistent decode step (opt-in)
+  bool use_step = false;  // icap_set_decode_step(1) / ICAP_DEC_STEP=1 (tools): the persistent task step (opt-in)
+  bool use_xdec = false;  // icap_set_decode_step(2) / ICAP_DEC_STEP=2 (tools): the group-persistent step (xdec.hip)
   DevBuf step_layers, step_args[2], step_state[2];
   DevBuf step_trace;  // tools build (ICAP_DEC_STEP_TRACE=1): per-task stamps of every step, + per-workgroup slots
   long step_key[2][8] = {};
@@ -974,6 +975,7 @@ void encode_grid(icap_handle* h, const float* img, int B, int IH, int IW, float*
 }
 
 constexpr int MAX_KSPLIT = 16;  // partial slabs: split-K GEMMs, 8 heads (dec_sa), 16 hidden slices (dec_ffn)
+constexpr int XDEC_SLABS = 33;  // the group-persistent step: 32 feed-forward slabs + the pre-LN sums
 
 struct DecodeBufs {
   float *x, *qkv, *kc, *vc, *part;
@@ -1019,7 +1021,7 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   w.o.ensure((size_t)rows * D * 2 * ns);
   w.h.ensure((size_t)rows * d.dim_ff * 2 * ns);
   w.kv.ensure((size_t)2 * d.n_dec_layers * kv_rows * H * Lmax * 64 * 4);
-  w.part.ensure((size_t)MAX_KSPLIT * rows * D * 4);
+  w.part.ensure((size_t)XDEC_SLABS * rows * D * 4);  // (the split-K slabs use MAX_KSPLIT of them)
   w.gs.ensure((size_t)rows * H * 4);
   const bool xsplit = cross_attn_splits(S) > 1 || (ns == 2 && cross_attn_f16_splits() > 1);
   if (xsplit) w.xpart.ensure(cross_attn_part_floats(rows) * 4);
@@ -1187,13 +1189,10 @@ bool step_path(const icap_handle* h, int max_len, const DropCfg* drop) {
          d.n_dec_layers >= 1 && d.n_dec_layers <= DEC_STEP_MAX_LAYERS && (!h->wlo || drop);
 }
 
-// The per-step argument structs of one decode configuration, built on the host and copied to device memory (the
-// kernel reads its arguments there).  Rebuilt when the configuration or the workspace changes; never during a
-// stream capture (decode_loop prepares them before it captures).
-const DecStepArgs* step_args(icap_handle* h, const DecodeBufs& b, int B, int S, int max_len, int wsi,
-                             const DropCfg* drop, hipStream_t s) {
+// The decoder layers' weight pointers in device memory (DecStepLayer[n_dec_layers]) for the persistent steps.
+const DecStepLayer* step_layers(icap_handle* h) {
   const icap_model_desc& d = h->d;
-  const int L = d.n_dec_layers, steps = max_len - 1;
+  const int L = d.n_dec_layers;
   if (!h->step_layers.p) {
     std::vector<DecStepLayer> v(L);
     for (int l = 0; l < L; ++l) {
@@ -1210,6 +1209,26 @@ const DecStepArgs* step_args(icap_handle* h, const DecodeBufs& b, int B, int S, 
     h->step_layers.ensure(sizeof(DecStepLayer) * L);
     HIPCHK(hipMemcpy(h->step_layers.p, v.data(), sizeof(DecStepLayer) * L, hipMemcpyHostToDevice));
   }
+  return h->step_layers.as<DecStepLayer>();
+}
+
+// Whether the decode loop runs as the group-persistent step (xdec.hip): its shapes (d 512, 8 heads, dim_ff 2048,
+// at most 256 rows, one row per memory image, S <= 256), two activation planes, bf16 decoder weights, eval mode.
+bool xdec_path(const icap_handle* h, int B, int S, int max_len, const DropCfg* drop) {
+  const icap_model_desc& d = h->d;
+  return h->use_xdec && h->ns == 2 && d.d_model == 512 && d.nhead == 8 && d.dim_ff == 2048 && max_len <= 65 &&
+         B <= 256 && S <= 256 && d.n_dec_layers >= 1 && d.n_dec_layers <= DEC_STEP_MAX_LAYERS && !h->wlo && !drop &&
+         xdec_supported();
+}
+
+// The per-step argument structs of one decode configuration, built on the host and copied to device memory (the
+// kernel reads its arguments there).  Rebuilt when the configuration or the workspace changes; never during a
+// stream capture (decode_loop prepares them before it captures).
+const DecStepArgs* step_args(icap_handle* h, const DecodeBufs& b, int B, int S, int max_len, int wsi,
+                             const DropCfg* drop, hipStream_t s) {
+  const icap_model_desc& d = h->d;
+  const int L = d.n_dec_layers, steps = max_len - 1;
+  step_layers(h);
   const size_t st_ints = dec_step_state_ints(L, B);
   const long key[8] = {B, S, max_len, (long)g_ws_generation, drop ? (long)drop->thr : -1,
                        drop ? (long)(intptr_t)drop->seed : 0, (long)(intptr_t)b.x, (long)st_ints};
@@ -1281,6 +1300,48 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   // Round 2 (fused decode blocks, tools/chains_r2.sh, B = 256): 2 chains 13.25 ms/step of decode, 3 chains of
   // 85 rows 12.73, 4 chains of 64 rows 13.37 - so 3 chains from 80 rows each (B = 128 keeps one chain)
   static const int min_rows = std::max(16, icap_knob("ICAP_DEC_MIN_ROWS", 80));
+  if (xdec_path(h, B, S, max_len, drop)) {  // one group-persistent launch per step (all layers) + the head
+    const size_t st = xdec_state_ints();
+    h->step_state[wsi].ensure(st * 4 * (size_t)(max_len - 1));
+    HIPCHK(hipMemsetAsync(h->step_state[wsi].p, 0, st * 4 * (size_t)(max_len - 1), s));
+    const DecStepLayer* layers = step_layers(h);
+    for (int t = 0; t + 1 < max_len; ++t) {
+      XdecArgs a{};
+      a.layers = layers; a.n_layers = d.n_dec_layers; a.rows = B; a.t0 = t; a.Lmax = max_len; a.S = S;
+      a.x = b.x; a.a = b.a; a.aL = b.aL;
+      a.kc = b.kc; a.vc = b.vc; a.kvl = (long)b.kvl;
+      a.qv = b.qkv; a.ctx = b.o; a.ctxL = b.aL;
+      a.slab = b.part; a.y = b.part + (size_t)32 * b.PS;
+      a.q2 = b.q; a.q2L = b.qL; a.qt = b.qt; a.cL = b.cL; a.c = b.c;
+      a.mem16 = b.memp;
+      a.ctr = h->step_state[wsi].as<int>() + (size_t)t * st;
+      a.err = h->range_word();
+#ifdef ICAP_TOOLS
+      static const int xtrace = icap_knob("ICAP_XDEC_TRACE", 0);
+      if (xtrace) {  // per-workgroup barrier stamps of every step (tools/xdec_trace.py)
+        const size_t per = (size_t)256 * XDEC_TRACE_BARRIERS * 2;
+        h->step_trace.ensure(per * 8 * (size_t)(max_len - 1));
+        a.trace = h->step_trace.as<unsigned long long>() + per * t;
+      }
+#endif
+      const double fl = 2.0 * B * d.n_dec_layers * (4.0 * D * D * 2 + 2.0 * D * d.dim_ff + 4.0 * d.nhead * S * D);
+      h->timed(PROF_DEC_FUSED, fl, 0.0, s, [&] { HIPCHK(launch_xdec(a, s)); });
+      HeadArgs ha{};  // the kernel leaves x = the last layer's LN3 output: no fold
+      ha.x = b.x; ha.rows = B; ha.Dm = D; ha.W = h->fc_w; ha.W4 = head_w4(h); ha.bias = h->fc_b; ha.V = d.vocab;
+      ha.logits = step_logits ? step_logits + (size_t)t * B * d.vocab : nullptr;
+      ha.ld_logits = d.vocab;
+      ha.ids = ids; ha.ld_ids = max_len; ha.id_col = t + 1;
+      ha.uniforms = uniforms ? uniforms + (size_t)t * B : nullptr;
+      ha.logp = logp ? logp + t : nullptr; ha.ld_logp = max_len - 1;
+      ha.finished = fin; ha.end_token = end;
+      if (t + 2 < max_len) {
+        ha.emb = h->emb; ha.pe = h->pe; ha.pe_pos = t + 1; ha.emb_scale = scale;
+        ha.x_next = b.x; ha.a_next = b.a; ha.lo = b.aL; ha.nsplit = h->ns;
+      }
+      HIPCHK(launch_head(ha, s));
+    }
+    return;
+  }
   const bool persist = step_path(h, max_len, drop);
   const int nb = persist ? 1 : std::max(1, std::min(h->dec_branches, B / min_rows));
   if (persist) {  // one persistent launch per step (all layers) + the head
@@ -1413,6 +1474,10 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     DecodeBufs pb = dec_bufs(h, B, B, max_len, S, 0, mode);  // make sure nothing allocates during capture
     if (mode) h->dws[mode].fin.ensure((size_t)B);
     if (step_path(h, max_len, dp)) step_args(h, pb, B, S, max_len, mode, dp, s);  // ... nor uploads
+    if (xdec_path(h, B, S, max_len, dp)) {
+      h->step_state[mode].ensure(xdec_state_ints() * 4 * (size_t)(max_len - 1));
+      step_layers(h);
+    }
     if (!h->cap_stream) HIPCHK(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(hipStreamSynchronize(s));
     const bool prof = h->prof_on;
@@ -1804,7 +1869,11 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
       h->t16 = desc->precision == ICAP_PREC_F16 && desc->kind == ICAP_KIND_GRID;
       REQUIRE(desc->dec_weight_planes >= 0 && desc->dec_weight_planes <= 2, "dec_weight_planes must be 0, 1 or 2");
       h->wlo = desc->dec_weight_planes == 2;
-      h->use_step = icap_knob("ICAP_DEC_STEP", 0) != 0;
+      {
+        const int mode = icap_knob("ICAP_DEC_STEP", 0);
+        h->use_step = mode == 1;
+        h->use_xdec = mode == 2;
+      }
       // measured and rejected as the default: MLP-2 fed by the block-scaled GELU output takes
       // 1211 us (two-step fold: 256 VGPRs, 30 spilled) / 646 us (per-step fold, 64-column blocks) against
       // 467 us for the bf16x2 form
@@ -2079,12 +2148,14 @@ int icap_set_decode_chains(icap_handle* h, int chains) {
   });
 }
 
-int icap_set_decode_step(icap_handle* h, int enable) {
+int icap_set_decode_step(icap_handle* h, int mode) {
   return guarded([&] {
     REQUIRE(h, "null handle");
-    if (h->use_step != (enable != 0))
+    REQUIRE(mode >= 0 && mode <= 2, "decode step mode must be 0, 1 or 2");
+    if (h->use_step != (mode == 1) || h->use_xdec != (mode == 2))
       for (DecodeGraph& g : h->dg) g.reset();  // the captured loops follow the mode
-    h->use_step = enable != 0;
+    h->use_step = mode == 1;
+    h->use_xdec = mode == 2;
   });
 }
 

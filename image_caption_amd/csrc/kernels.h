@@ -234,6 +234,34 @@ hipError_t launch_dec_step(const DecStepArgs& a, const DecStepArgs* dev_args, hi
 // ints of the per-launch state block (counters + queue head), zeroed before every launch
 size_t dec_step_state_ints(int n_layers, int rows);
 
+// Group-persistent decode step (xdec.hip): every decoder layer of one decode step in one launch of 8 row groups x 32
+// workgroups (one per CU); products split over a group's workgroups by output columns, row-local work one row per
+// workgroup, group barriers on write-through hand-offs.  rows <= 256, d 512 / 8 heads / dim_ff 2048, bf16 weights,
+// two activation planes, eval mode (no dropout), one row per memory image.
+struct XdecArgs {
+  const DecStepLayer* layers;             // device array [n_layers]
+  int n_layers, rows, t0, Lmax, S;
+  float* x; bf16_t* a; long aL;           // residual stream [rows][512] fp32 and its bf16 hi/lo planes
+  float* kc; float* vc; long kvl;         // KV cache [layer][rows][8][Lmax][64] fp32
+  float* qv;                              // [rows][1536] fp32: this step's q | k | v
+  bf16_t* ctx; long ctxL;                 // [rows][512] planes: self-attention context, then the value projection
+  float* y;                               // [rows][512] fp32: the sums a LayerNorm normalises
+  bf16_t* q2; long q2L;                   // [rows][512] planes: the cross-attention query
+  bf16_t* qt; long cL;                    // [rows][8][512] planes: q~
+  bf16_t* c;                              // [rows][8][512] planes (lo at + cL): cross-attention context
+  float* slab;                            // [32][rows][512] fp32: feed-forward partials, one per hidden slice
+  const bf16_t* mem16;                    // the memory as one fp16 plane [rows][S][512]
+  int* ctr;                               // 8 group counters, 16 ints apart, zeroed before the launch
+  unsigned* err;                          // the handle's status word (DEC_STEP_GAVE_UP on a give-up)
+  // tools build: per-workgroup stamps [256][XDEC_TRACE_BARRIERS][2] (s_memrealtime at each arrival, and when the
+  // barrier released the workgroup), or null
+  unsigned long long* trace;
+};
+constexpr int XDEC_TRACE_BARRIERS = 12 * DEC_STEP_MAX_LAYERS;
+size_t xdec_state_ints();
+int xdec_supported();  // the device has the 256 CUs the launch needs
+hipError_t launch_xdec(const XdecArgs& a, hipStream_t s);
+
 // LayerNorm over rows of D fp32 values; optional fp32 output (may alias input) and
 // bf16 hi(/lo) planes.  Input row r is read from (r / in_group) * in_stride + in_off + r % in_group.
 hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_group, long in_stride,

@@ -414,9 +414,10 @@ class Engine:
         """Independent decode chains per batch (1..4, default 2, used from 128 rows per chain)."""
         check(self.lib.icap_set_decode_chains(self.handle, int(chains)), "icap_set_decode_chains")
 
-    def set_decode_step(self, enable: bool) -> None:
-        """Decode loop form: one persistent launch per step (default) or one launch per fused block."""
-        check(self.lib.icap_set_decode_step(self.handle, int(bool(enable))), "icap_set_decode_step")
+    def set_decode_step(self, mode) -> None:
+        """Decode loop form (icap_set_decode_step): 0 / False = one launch per fused block, 1 / True = the persistent
+        task step (decstep.hip), 2 = the group-persistent step (xdec.hip)."""
+        check(self.lib.icap_set_decode_step(self.handle, int(mode)), "icap_set_decode_step")
 
     def set_graphs(self, enable: bool) -> None:
         """hipGraph replay of the decode loop (default on)."""

@@ -242,11 +242,13 @@ int icap_set_graphs(icap_handle* h, int enable);
  * since the last check is not trustworthy: re-encode with a 16-bit-significand precision (bf16x2). */
 int icap_range_check(icap_handle* h, void* stream, int* overflowed);
 
-/* Decode loop form: 1 (default) = one persistent launch per decode step running every decoder
- * layer as dependency-ordered tasks (decstep.hip), where the shapes allow it (d_model 512, 8 heads, dim_ff 2048,
- * max_len <= 65, two activation planes, bf16 decoder weights); 0 = one launch per fused block.  Same results to
- * rounding (the residual LayerNorm sums in another order). */
-int icap_set_decode_step(icap_handle* h, int enable);
+/* Decode loop form: 0 (default) = one launch per fused block; 1 = one persistent launch per decode
+ * step running every decoder layer as dependency-ordered tasks (decstep.hip); 2 = one group-persistent launch per
+ * step (xdec.hip: 8 row groups x 32 workgroups, products split by output columns, eval mode, <= 256 rows, a device
+ * with >= 256 CUs).  1 and 2 apply where the shapes allow (d_model 512, 8 heads, dim_ff 2048, max_len <= 65, two
+ * activation planes, bf16 decoder weights), else the loop falls back to 0.  Same results to rounding (sums in
+ * another order). */
+int icap_set_decode_step(icap_handle* h, int mode);
 
 /* Number of independent decode chains a batch is split into (1..4, default 2; used from 128 rows
  * per chain): the chains are parallel branches of the captured decode graph. */
