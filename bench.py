@@ -41,16 +41,28 @@ METRIC = "captions/sec (224×224, max_len=30, greedy) at 1/2/4/8 MI355X vs CPU r
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA, MI355X_MICROARCH.md chip table
 PEAK_I8_TOPS = 5000.0      # dense i8 MFMA (2x bf16 per clock: 16x16x64 i8 = cycles of 16x16x32 bf16), same table
 PEAK_HBM_GBS = 8000.0
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")  # collected on the default (f16) bench
+# HBM-side bytes per launch from rocprofv3 PMC passes over the default bench of each greedy workload
+# (tools/r3_profile.sh); the round-2 summary is the fallback for the ViT line
+TRAFFIC_JSON = {"vit": [os.path.join(ROOT, "profiles", "r03", "pmc_traffic_vit.json"),
+                        os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")],
+                "grid": [os.path.join(ROOT, "profiles", "r03", "pmc_traffic_grid.json")]}
 
 
-def pmc_traffic(kernel: str, headline: bool = True):
-    """Per-launch HBM-side bytes of `kernel` from the committed PMC summary (collected on the
-    headline workload: ViT greedy, tools/pmc_bench.sh), or None for any other workload."""
-    if not headline:
+def traffic_source(workload):
+    for path in TRAFFIC_JSON.get(workload, []):
+        if os.path.exists(path):
+            return os.path.relpath(path, ROOT)
+    return None
+
+
+def pmc_traffic(kernel: str, workload):
+    """Per-launch HBM-side bytes of `kernel` from the committed PMC summary of `workload` ("vit" / "grid" greedy,
+    collected on this bench's default command), or None when there is none (other modes)."""
+    src = traffic_source(workload)
+    if src is None:
         return None
     try:
-        with open(TRAFFIC_JSON) as f:
+        with open(os.path.join(ROOT, src)) as f:
             table = json.load(f)
     except (OSError, ValueError):
         return None
@@ -327,7 +339,7 @@ def main():
     if rank == 0:
         step_ms = el / args.steps * 1e3
         dom = max(prof, key=lambda p: p["ms"])
-        headline = args.model == "vit" and args.mode == "greedy"  # the PMC summary's workload
+        workload = args.model if args.mode == "greedy" else None  # the PMC summaries' workloads
         avg_ms = dom["ms"] / max(dom["launches"], 1)
         for p in prof:
             if not p["launches"]:
@@ -338,7 +350,7 @@ def main():
         if "attn" in dom["kernel"] and "cross" in dom["kernel"]:
             achieved = dom["bytes"] / dom["launches"] / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(dom["kernel"], headline)}
+                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(dom["kernel"], workload)}
         else:
             # achieved = algorithmic 2MNK per launch / launch time.  The MFMA work behind it: bf16x2 GEMMs
             # issue 2 bf16 products per algorithmic MAC (hi and lo activation planes), the i8x2 GEMM 3 i8
@@ -349,14 +361,14 @@ def main():
             achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
             roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak,
                     "unit": "TFLOP/s", "peak_dtype": "i8" if i8 else ("f16" if args.precision == "f16" else "bf16"), "frac": round(achieved / peak, 4),
-                    "traffic": pmc_traffic(dom["kernel"], headline),
+                    "traffic": pmc_traffic(dom["kernel"], workload),
                     "mfma_products_per_alg_mac": work, "mfma_issue_frac": round(achieved * work / peak, 4)}
         roof.update({"kernel": dom["kernel"], "launches_per_step": dom["launches"] // args.steps,
                      "avg_launch_us": round(avg_ms * 1e3, 2),
                      "share_of_step": round(dom["ms"] / args.steps / step_ms, 3)})
         cpu = None
         if roof["traffic"] is not None:
-            roof["traffic_unit"] = "bytes/launch (HBM-side, rocprofv3 PMC, profiles/r02/pmc_traffic.json)"
+            roof["traffic_unit"] = f"bytes/launch (HBM-side, rocprofv3 PMC, {traffic_source(workload)})"
         if ws == 1 and not args.no_cpu_baseline and args.model == "vit":
             cpu = cpu_baseline(args.cpu_seconds, args.cpu_batch, L)
         line = {

@@ -716,13 +716,14 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       // store-only epilogues with whole 256-row bands (the ViT QKV and MLP-1 GEMMs): the persistent counted-seam
       // form (QKV 305 -> 265 us, MLP-1 423 -> 342 us at B = 256, tools/f16_forms_r2.sh); the residual GEMMs on
       // 224-row tiles (678 tiles = 2.65 per CU at N = 768 instead of 591 = 2.3)
+      const int blocks = g.max_grid > 0 ? std::min(g.max_grid, cus) : cus;
       if (g.out == OUT_F32_RESID) {
         const int tiles224 = (g.N / 256) * ((g.M + 223) / 224);
-        hipLaunchKernelGGL((gemm_f16p_kernel<2, 0, 224>), dim3(std::min(tiles224, cus)), dim3(512),
+        hipLaunchKernelGGL((gemm_f16p_kernel<2, 0, 224>), dim3(std::min(tiles224, blocks)), dim3(512),
                            2 * (224 * 128 + 256 * 128) + 2048, s, g);
       } else {
         const int tiles = (g.N / 256) * ((g.M + 255) / 256);
-        hipLaunchKernelGGL(gemm_f16p_kernel<1>, dim3(std::min(tiles, cus)), dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        hipLaunchKernelGGL(gemm_f16p_kernel<1>, dim3(std::min(tiles, blocks)), dim3(512), 2 * 64 * 1024 + 2048, s, g);
       }
       return hipGetLastError();
     }

@@ -148,6 +148,7 @@ struct icap_handle {
   // fp16 plane, fp16 weights and MFMA (encode_grid); the tail and the decoder stay bf16x2, train-mode
   // BatchNorm stays on the bf16x2 trunk
   bool t16 = false;
+  int enc_cus = 0;  // icap_set_encoder_cus: persistent encoder GEMM grids sized for a CU-masked stream (0 = all CUs)
   // hi/lo decoder weights (icap_model_desc.dec_weight_planes = 2: fp32 checkpoints that are not bf16-exact): every
   // decoder GEMM weight is packed as hi = bf16(W) and lo = bf16(W - hi) and the decode runs the unfused launches,
   // whose GEMMs add W_lo . X_hi; the train-mode dropout sampler keeps the fused blocks (W_hi only)
@@ -386,6 +387,7 @@ struct icap_handle {
     g.M = M; g.N = W.N; g.K = W.K; g.nsplit = 1; g.c_planes = 1; g.f16 = 1;
     g.epi = epi; g.out = out;
     g.range_flag = range_word();
+    g.max_grid = enc_cus;
     run_gemm(g, s);
   }
   // residual-output GEMMs (N = 768 / 512: a partial last round of tiles) split their tail tiles in K when
@@ -2136,6 +2138,13 @@ int icap_range_check(icap_handle* h, void* stream, int* overflowed) {
     if (v) HIPCHK(hipMemsetAsync(w, 0, 16, s));
     *overflowed = (v & 1u) ? 1 : 0;
     REQUIRE(!(v & DEC_STEP_GAVE_UP), "internal error: a persistent decode step gave up waiting for a dependency");
+  });
+}
+
+int icap_set_encoder_cus(icap_handle* h, int cus) {
+  return guarded([&] {
+    REQUIRE(h && cus >= 0, "null handle / negative CU count");
+    h->enc_cus = cus;
   });
 }
 

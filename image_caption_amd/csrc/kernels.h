@@ -89,6 +89,9 @@ struct GemmArgs {
   // fp16 range guard (gemm_f16p_kernel store-only fp16 outputs): set to 1 when a stored value is not finite in
   // fp16 (|v| >= 65520 before rounding, or NaN); nullptr = unchecked
   unsigned* range_flag;
+  // persistent GEMMs: at most this many workgroups (0 = one per CU of the device) - the CUs a CU-masked encoder
+  // stream owns (batch pipelining, icap_set_encoder_cus)
+  int max_grid;
 };
 // bytes of split_ws for split_slots block slots per XCD
 inline size_t gemm_split_ws_bytes(int split_slots) { return (size_t)8 * split_slots * 2 * 128 * 256 * 4; }

@@ -419,6 +419,10 @@ class Engine:
         task step (decstep.hip), 2 = the group-persistent step (xdec.hip)."""
         check(self.lib.icap_set_decode_step(self.handle, int(mode)), "icap_set_decode_step")
 
+    def set_encoder_cus(self, cus: int) -> None:
+        """Persistent encoder GEMM grids for an encoder stream restricted to `cus` CUs (0 = every CU)."""
+        check(self.lib.icap_set_encoder_cus(self.handle, int(cus)), "icap_set_encoder_cus")
+
     def set_graphs(self, enable: bool) -> None:
         """hipGraph replay of the decode loop (default on)."""
         check(self.lib.icap_set_graphs(self.handle, int(bool(enable))), "icap_set_graphs")

@@ -43,6 +43,8 @@ class CaptionPipeline:
                            "icap_stream_create_cu_mask")
                 ptrs.append(p.value)
             self._owned = ptrs
+            # the persistent encoder GEMMs size their grids to the encoder stream's CUs
+            engine.set_encoder_cus(torch.cuda.get_device_properties(dev).multi_processor_count - int(decode_cus))
             self.dec_stream = torch.cuda.ExternalStream(ptrs[0], device=dev)
             self.enc_stream = torch.cuda.ExternalStream(ptrs[1], device=dev)
         else:
@@ -52,6 +54,11 @@ class CaptionPipeline:
             self.dec_stream = torch.cuda.Stream(device=dev, priority=prio)
 
     def __del__(self):
+        if getattr(self, "_owned", []):
+            try:
+                self.eng.set_encoder_cus(0)
+            except Exception:
+                pass
         for p in getattr(self, "_owned", []):
             try:
                 torch.cuda.synchronize(self.eng.device)

@@ -250,6 +250,11 @@ int icap_range_check(icap_handle* h, void* stream, int* overflowed);
  * another order). */
 int icap_set_decode_step(icap_handle* h, int mode);
 
+/* Encoder CU budget (batch pipelining, image_caption_amd/pipeline.py): the persistent encoder GEMMs launch at most
+ * `cus` workgroups - the CUs of the CU-masked stream the encoder runs on while the previous batch decodes on the
+ * others (0 = one per CU of the device, the default).  Results are unchanged. */
+int icap_set_encoder_cus(icap_handle* h, int cus);
+
 /* Number of independent decode chains a batch is split into (1..4, default 2; used from 128 rows
  * per chain): the chains are parallel branches of the captured decode graph. */
 int icap_set_decode_chains(icap_handle* h, int chains);
