@@ -633,17 +633,18 @@ hipError_t launch_gemm_256(const GemmArgs& g0, hipStream_t s) {
 namespace {
 
 // The bf16 / bf16x2 encoder and trunk GEMMs, and (F16) the ICAP_PREC_F16 Grid trunk's convolutions on fp16 planes.
-template <bool F16>
+// EPC: the convolution epilogue (GemmArgs::scale set), compiled into its own kernels.
+template <bool F16, bool EPC>
 hipError_t run_256(const GemmArgs& g, hipStream_t s) {
   static bool attr = false;
   constexpr int lds2 = 3 * 3 * 256 * 32 * 2, lds1 = 4 * 2 * 256 * 32 * 2;
   if (!attr) {
     hipError_t e = hipSuccess;
-    for (const void* f : {(const void*)gemm_256_kernel<2, 16, 0, 0, 256, 0, 32, 0, F16>,
-                          (const void*)gemm_256_kernel<2, 16, 0, 1, 256, 0, 32, 0, F16>})
+    for (const void* f : {(const void*)gemm_256_kernel<2, 16, 0, 0, 256, 0, 32, 0, F16, EPC>,
+                          (const void*)gemm_256_kernel<2, 16, 0, 1, 256, 0, 32, 0, F16, EPC>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds2);
-    for (const void* f : {(const void*)gemm_256_kernel<1, 16, 0, 0, 256, 0, 32, 0, F16>,
-                          (const void*)gemm_256_kernel<1, 16, 0, 1, 256, 0, 32, 0, F16>})
+    for (const void* f : {(const void*)gemm_256_kernel<1, 16, 0, 0, 256, 0, 32, 0, F16, EPC>,
+                          (const void*)gemm_256_kernel<1, 16, 0, 1, 256, 0, 32, 0, F16, EPC>})
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
     if (e != hipSuccess) return e;
     attr = true;
@@ -652,27 +653,29 @@ hipError_t run_256(const GemmArgs& g, hipStream_t s) {
   if (g.split_slots) return hipErrorNotSupported;  // the tail split is a tools-build form
   // 128 x 256 tiles, 2-stage ring, 2 blocks per CU for K >= 128: ViT 42.9 -> 41.8 ms/step (MLP-out's 591 tiles
   // become 1182: 4.6 instead of 2.3 rounds), trunk conv3 203 -> 177 us; at K = 64 the 3-stage 256 x 256 ring
-  // stays ahead (tools/halfk_sweep.sh)
-  if (g.K >= 128) {
+  // stays ahead (tools/halfk_sweep.sh; round 3, tools/r3_trunk_sweep.sh: still so for the fp16 trunk)
+  // ICAP_GEMM_TALL_MIN_K (tools): the smallest K of the two-block form
+  static const int tall_min_k = icap_knob("ICAP_GEMM_TALL_MIN_K", 128);
+  if (tall_min_k && g.K >= tall_min_k) {
     const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
     constexpr int ldsh = 2 * (2 * 128 * 32 * 2 + 256 * 32 * 2), ldsh1 = 2 * (128 * 32 * 2 + 256 * 32 * 2);
     if (g.nsplit == 2) {
-      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 1, 128, 2, 32, 0, F16>), dim3(nwgh), dim3(512), ldsh, s, g);
-      else hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 0, 128, 2, 32, 0, F16>), dim3(nwgh), dim3(512), ldsh, s, g);
+      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 1, 128, 2, 32, 0, F16, EPC>), dim3(nwgh), dim3(512), ldsh, s, g);
+      else hipLaunchKernelGGL((gemm_256_kernel<2, 8, 0, 0, 128, 2, 32, 0, F16, EPC>), dim3(nwgh), dim3(512), ldsh, s, g);
     } else {
-      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 1, 128, 2, 32, 0, F16>), dim3(nwgh), dim3(512), ldsh1, s, g);
-      else hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 0, F16>), dim3(nwgh), dim3(512), ldsh1, s, g);
+      if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 1, 128, 2, 32, 0, F16, EPC>), dim3(nwgh), dim3(512), ldsh1, s, g);
+      else hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 0, F16, EPC>), dim3(nwgh), dim3(512), ldsh1, s, g);
     }
     return hipGetLastError();
   }
   // K < 128: 256 x 256 tiles, 16 waves, 3-stage (two planes) / 4-stage ring
   const int nwg = (g.N / 256) * ((g.M + 255) / 256);
   if (g.nsplit == 2) {
-    if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 16, 0, 1, 256, 0, 32, 0, F16>), dim3(nwg), dim3(1024), lds2, s, g);
-    else hipLaunchKernelGGL((gemm_256_kernel<2, 16, 0, 0, 256, 0, 32, 0, F16>), dim3(nwg), dim3(1024), lds2, s, g);
+    if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<2, 16, 0, 1, 256, 0, 32, 0, F16, EPC>), dim3(nwg), dim3(1024), lds2, s, g);
+    else hipLaunchKernelGGL((gemm_256_kernel<2, 16, 0, 0, 256, 0, 32, 0, F16, EPC>), dim3(nwg), dim3(1024), lds2, s, g);
   } else {
-    if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 16, 0, 1, 256, 0, 32, 0, F16>), dim3(nwg), dim3(1024), lds1, s, g);
-    else hipLaunchKernelGGL((gemm_256_kernel<1, 16, 0, 0, 256, 0, 32, 0, F16>), dim3(nwg), dim3(1024), lds1, s, g);
+    if (g.cv) hipLaunchKernelGGL((gemm_256_kernel<1, 16, 0, 1, 256, 0, 32, 0, F16, EPC>), dim3(nwg), dim3(1024), lds1, s, g);
+    else hipLaunchKernelGGL((gemm_256_kernel<1, 16, 0, 0, 256, 0, 32, 0, F16, EPC>), dim3(nwg), dim3(1024), lds1, s, g);
   }
   return hipGetLastError();
 }
@@ -733,7 +736,10 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 0, true>), dim3(nwgh), dim3(512), ldsh1, s, g);
     return hipGetLastError();
   }
-  return g.f16 ? run_256<true>(g, s) : run_256<false>(g, s);
+  if (g.scale && !g.addend && !g.rm_group && !g.hm_n && g.out == OUT_SPLIT && g.bias &&
+      (g.epi == EPI_NONE || g.epi == EPI_RELU))  // the trunk convolutions' epilogue form
+    return g.f16 ? run_256<true, true>(g, s) : run_256<false, true>(g, s);
+  return g.f16 ? run_256<true, false>(g, s) : run_256<false, false>(g, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -87,14 +87,14 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
       for (int i = 0; i < TM; ++i) {
         const long ro = (long)min(mb + i * 16 + fr, M - 1) * p.res_ld + nb + j * 16 + 4 * fq;
         rh[i] = *(const u32x2*)(p.res + ro);
-        rl[i] = F16 && p.res_planes == 1 ? (u32x2){0u, 0u} : *(const u32x2*)(p.res + ro + p.res_lo);
+        rl[i] = *(const u32x2*)(p.res + ro + p.res_lo);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const uint32_t wh = rh[i][r >> 1] >> ((r & 1) * 16), wl = rl[i][r >> 1] >> ((r & 1) * 16);
-          if constexpr (F16)  // fp16 planes (the ICAP_PREC_F16 Grid trunk's residual stream)
+          if constexpr (F16)
             acc[i][j][r] += h2f((bf16_t)(wh & 0xffff)) + h2f((bf16_t)(wl & 0xffff));
           else
             acc[i][j][r] += bf2f((bf16_t)(wh & 0xffff)) + bf2f((bf16_t)(wl & 0xffff));
@@ -195,6 +195,88 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
   }
 }
 
+// Epilogue of the trunk convolutions (GemmArgs::scale set: eval BatchNorm folded into scale / shift): out =
+// relu?(acc * scale + shift (+ residual planes)) as split planes (bf16, or fp16 with F16), nothing else - no row
+// remaps, addends or other output forms, so the accumulators plus one column group's operands are all that is live
+// (the generic epilogue_256 spilled 34-38 VGPRs at the 128-register budget of two blocks per CU).
+template <int TM, int TN, bool F16>
+__device__ __forceinline__ void epilogue_conv(const GemmArgs& p, f32x4 (&acc)[TM][TN], int mb, int nb, int fr, int fq) {
+  const int M = p.M;
+  const bool res = p.res != nullptr, res2 = !(F16 && p.res_planes == 1), lo_out = p.c_planes == 2;
+  const bool relu = p.epi == EPI_RELU;
+  constexpr int JG = TN >= 2 ? 2 : 1;  // column groups per batch of loads (one memory latency per batch; all 4: 172 VGPRs spilled)
+  bf16_t* C = (bf16_t*)p.C;
+  bool bad = false;  // F16: a stored value that is not finite in fp16 (range guard)
+#pragma unroll
+  for (int j0 = 0; j0 < TN; j0 += JG) {
+    f32x4 sv[JG], bv[JG];
+    u32x2 rh[JG][TM], rl[JG][TM];
+#pragma unroll
+    for (int jj = 0; jj < JG; ++jj) {
+      const int col = nb + (j0 + jj) * 16 + 4 * fq;
+      sv[jj] = *(const f32x4*)(p.scale + col);
+      bv[jj] = *(const f32x4*)(p.bias + col);
+    }
+    if (res) {  // (plane count hoisted: a per-element "load or not" select would wait after each load)
+      if (res2) {
+#pragma unroll
+        for (int jj = 0; jj < JG; ++jj)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const long ro = (long)min(mb + i * 16 + fr, M - 1) * p.res_ld + nb + (j0 + jj) * 16 + 4 * fq;
+            rh[jj][i] = *(const u32x2*)(p.res + ro);
+            rl[jj][i] = *(const u32x2*)(p.res + ro + p.res_lo);
+          }
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < JG; ++jj)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const long ro = (long)min(mb + i * 16 + fr, M - 1) * p.res_ld + nb + (j0 + jj) * 16 + 4 * fq;
+            rh[jj][i] = *(const u32x2*)(p.res + ro);
+            rl[jj][i] = (u32x2){0u, 0u};
+          }
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < JG; ++jj) {
+      const int j = j0 + jj, col = nb + j * 16 + 4 * fq;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = mb + i * 16 + fr;
+        f32x4 v = acc[i][j] * sv[jj] + bv[jj];
+        if (res)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t wh = rh[jj][i][r >> 1] >> ((r & 1) * 16), wl = rl[jj][i][r >> 1] >> ((r & 1) * 16);
+            if constexpr (F16)
+              v[r] += h2f((bf16_t)(wh & 0xffff)) + h2f((bf16_t)(wl & 0xffff));
+            else
+              v[r] += bf2f((bf16_t)(wh & 0xffff)) + bf2f((bf16_t)(wl & 0xffff));
+          }
+        if (relu)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        if (m >= M) continue;
+        const long o = (long)m * p.ldc + col;
+        const u32x2 hv = pack16x4<F16>(v);
+        if (F16) bad |= f16_pair_nonfinite(hv[0]) || f16_pair_nonfinite(hv[1]);
+        *(u32x2*)(C + o) = hv;
+        if (lo_out) {
+          f32x4 lo;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bf16_t hb = (bf16_t)((hv[r >> 1] >> ((r & 1) * 16)) & 0xffff);
+            lo[r] = v[r] - (F16 ? h2f(hb) : bf2f(hb));
+          }
+          *(u32x2*)(C + o + p.c_lo) = pack16x4<F16>(lo);
+        }
+      }
+    }
+  }
+  if (F16 && p.range_flag && __any(bad) && (threadIdx.x & 63) == 0) range_flag_set(p.range_flag);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -220,8 +302,10 @@ namespace {
 // two blocks each, one per K half.  Both halves leave their fp32 partial tile with agent-scope stores,
 // wait for them to complete and take a ticket; the second adds the other's partial (a + b: the same
 // bits whichever finished first) and runs the epilogue.
+// EPC: the epilogue is epilogue_conv (the trunk convolutions: GemmArgs::scale set) instead of epilogue_256 - a
+// compile-time choice, so each kernel holds one epilogue's registers (both in one kernel spilled 27-36 VGPRs).
 template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0, int KSD = 32, int TS = 0,
-          bool F16 = false>
+          bool F16 = false, bool EPC = false>
 __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64 ? 3 : 1)) void gemm_256_kernel(
     GemmArgs p) {
   constexpr int WGM = NW / 4;                       // wave grid WGM x 4
@@ -411,7 +495,8 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
           acc[i][j][e] += __hip_atomic_load(other + ((i * TN + j) * 4 + e) * NT + tid, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
   }
-  epilogue_256<TM, TN, F16>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
+  if constexpr (EPC) epilogue_conv<TM, TN, F16>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);  // trunk convolutions
+  else epilogue_256<TM, TN, F16>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
 }
 
 // ---------------------------------------------------------------------------------------------
