@@ -165,6 +165,19 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs p) {
 template <int BM, int BN, int WM, int WN>
 hipError_t run(const GemmArgs& g, hipStream_t s) {
   constexpr int lds = 2 * (BM + BN) * BK * 2;
+  if constexpr (lds > 65536) {
+    static bool attr = false;
+    if (!attr) {
+      for (const void* f : {(const void*)gemm_bf16_kernel<BM, BN, WM, WN>, (const void*)gemm_bf16_kernel<BM, BN, WM, WN, 1>,
+                            (const void*)gemm_bf16_kernel<BM, BN, WM, WN, 2>, (const void*)gemm_bf16_kernel<BM, BN, WM, WN, 0, true>,
+                            (const void*)gemm_bf16_kernel<BM, BN, WM, WN, 1, true>,
+                            (const void*)gemm_bf16_kernel<BM, BN, WM, WN, 2, true>}) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+      }
+      attr = true;
+    }
+  }
   dim3 grid(g.N / BN, (g.M + BM - 1) / BM, g.batch);
   if (grid.y > 65535) return hipErrorInvalidValue;
   if (g.f16) {
@@ -217,6 +230,10 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {
   const int cls = gemm_tile_class(g);
   if (cls == PROF_GEMM_256 || cls == PROF_GEMM_F16P) return launch_gemm_256(g, s);
   if (cls == PROF_GEMM_128) return run<128, 128, 64, 64>(g, s);
+  // narrow outputs over many rows (the trunk's stem and layer1-2 convolutions: N 64 / 128, M up to 3.2 M): 256 x 64
+  // tiles of four 64 x 64 wave tiles (80 KiB of LDS, two blocks per CU) instead of 64 x 64 tiles of 32 x 32
+  static const int tall64 = icap_knob("ICAP_GEMM_TALL64", 1);
+  if (tall64 && g.N <= 128 && g.M >= 65536 && g.batch == 1) return run<256, 64, 64, 64>(g, s);
   return run<64, 64, 32, 32>(g, s);
 }
 

@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -1836,7 +1838,7 @@ const char* icap_knobs_set() {
       "ICAP_QKV_HEAD_MAJOR", "ICAP_DEC_MIN_ROWS", "ICAP_I8_MLP2", "ICAP_DEC_BRANCHES", "ICAP_F16_GEMM",
       "ICAP_F16_PRES", "ICAP_XATTN16_KS", "ICAP_XATTN16_CK", "ICAP_ENC_ATTN16_QPW", "ICAP_F16_PP",
       "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
-      "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE", "ICAP_XDEC_TRACE"};
+      "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE", "ICAP_XDEC_TRACE", "ICAP_GEMM_TALL64"};
   for (const char* n : names)
     if (getenv(n)) return n;
   return "";
@@ -2311,6 +2313,20 @@ size_t icap_decoder_train_workspace(const icap_model_desc* d, int B, int T, int 
   return TrainWS(*d, B, T, S, nullptr, drop_p).floats * sizeof(float);
 }
 
+// What each live training workspace holds: the forward records the call that filled `ws`; the backward must be
+// the backward of that call (same decoder, shapes, ids, memory and dropout), else it would differentiate
+// activations of another batch.  Host-side (no device read, no sync), keyed by the workspace pointer.
+struct TrainRecord {
+  const void* emb;  // the decoder's parameter storage (the descriptor struct itself is rebuilt per call)
+  const void* fc_w;
+  const void* ids;
+  const void* memory;
+  int B, T, S, end_token;
+  float drop_p;
+};
+static std::mutex g_train_mu;
+static std::map<const void*, TrainRecord> g_train_ws;
+
 int icap_decoder_train_forward(const icap_model_desc* d, const int32_t* ids, int B, int T, const float* memory, int S,
                                int end_token, float drop_p, uint32_t drop_seed, float* logp, void* ws, size_t ws_bytes,
                                void* stream) {
@@ -2322,6 +2338,8 @@ int icap_decoder_train_forward(const icap_model_desc* d, const int32_t* ids, int
     REQUIRE(ws_bytes >= w.floats * sizeof(float), "workspace too small (icap_decoder_train_workspace)");
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)w.seed, (int)drop_seed, 1, (hipStream_t)stream));
     train_forward(*d, w, ids, memory, end_token, logp, (hipStream_t)stream);
+    std::lock_guard<std::mutex> lk(g_train_mu);
+    g_train_ws[ws] = TrainRecord{d->emb, d->fc_w, ids, memory, B, T, S, end_token, drop_p};
   });
 }
 
@@ -2332,9 +2350,21 @@ int icap_decoder_train_backward(const icap_model_desc* d, const icap_model_desc*
     train_check(d, B, T, S);
     REQUIRE(grad && grad->dec_layers && grad->emb && grad->fc_w && grad->fc_b, "null gradient pointers");
     REQUIRE(ids && memory && dlogp && ws, "null argument");
+    {
+      std::lock_guard<std::mutex> lk(g_train_mu);
+      auto it = g_train_ws.find(ws);
+      REQUIRE(it != g_train_ws.end(), "workspace holds no forward (icap_decoder_train_forward first)");
+      const TrainRecord& r = it->second;
+      REQUIRE(r.B == B && r.T == T && r.S == S && r.end_token == end_token && r.drop_p == drop_p,
+              "backward arguments differ from the forward that filled ws (B, T, S, end_token, drop_p)");
+      REQUIRE(r.emb == d->emb && r.fc_w == d->fc_w && r.ids == ids && r.memory == memory,
+              "backward decoder / ids / memory differ from the forward that filled ws");
+    }
     TrainWS w(*d, B, T, S, (float*)ws, drop_p);  // the seed word the forward left in ws
     REQUIRE(ws_bytes >= w.floats * sizeof(float), "workspace too small (icap_decoder_train_workspace)");
     train_backward(*d, *grad, w, ids, memory, end_token, dlogp, dmemory, (hipStream_t)stream);
+    std::lock_guard<std::mutex> lk(g_train_mu);
+    g_train_ws.erase(ws);
   });
 }
 

@@ -305,16 +305,25 @@ __global__ void embed_fwd_kernel(const int32_t* ids, long ld, int B, int T, cons
   }
 }
 
-// dE[v][c] = scale * sum over rows m with tok[m] == v of dx[m][c] (row order: deterministic)
+// dE[v][c] = scale * sum over rows m with tok[m] == v of dx[m][c], in row order (deterministic).  One workgroup
+// per row m; the row that holds the FIRST occurrence of its token owns that token's dE row and sums the rows with
+// the same token from m on; the others exit.  O(M^2) id compares + one read of dx, against O(V M D) for a
+// workgroup per vocabulary row.  Rows of tokens that do not occur are zeroed by the launcher.
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const int32_t* ids, long ld, int B, int T, const float* dx,
-                                                        int D, float scale, float* dE) {
-  const int v = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= D) return;
-  float s = 0.f;
-  for (int b = 0; b < B; ++b)
-    for (int t = 0; t < T; ++t)
-      if (ids[(long)b * ld + t] == v) s += dx[((long)b * T + t) * D + c];
-  dE[(long)v * D + c] = s * scale;
+                                                        int D, int V, float scale, float* dE) {
+  const int m = blockIdx.x, M = B * T;
+  auto tok_of = [&](int r) { return ids[(long)(r / T) * ld + r % T]; };
+  const int v = tok_of(m);
+  if (v < 0 || v >= V) return;  // ids outside [0, V) break the call contract: never write outside dE
+  int seen = 0;
+  for (int r = threadIdx.x; r < m; r += 256) seen |= tok_of(r) == v;
+  if (__syncthreads_or(seen)) return;
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float s = 0.f;
+    for (int r = m; r < M; ++r)
+      if (tok_of(r) == v) s += dx[(long)r * D + c];
+    dE[(long)v * D + c] = s * scale;
+  }
 }
 
 // log p(ids[b][t+1] | prefix) from logits (B*T, V), zero after the row's first <end> among ids[b][1..t]
@@ -450,7 +459,9 @@ hipError_t launch_embed_fwd(const int32_t* ids, long ld, int B, int T, const flo
 
 hipError_t launch_embed_bwd(const int32_t* ids, long ld, int B, int T, const float* dx, int D, int V, float scale,
                             float* dE, hipStream_t s) {
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3((D + 255) / 256, V), dim3(256), 0, s, ids, ld, B, T, dx, D, scale, dE);
+  hipError_t e = hipMemsetAsync(dE, 0, (size_t)V * D * sizeof(float), s);
+  if (e != hipSuccess || B * T == 0) return e;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(B * T), dim3(256), 0, s, ids, ld, B, T, dx, D, V, scale, dE);
   return hipGetLastError();
 }
 

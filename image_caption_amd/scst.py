@@ -28,12 +28,26 @@ from .parallel import gather_rows
 
 class TeacherForcedLogProbs(nn.Module):
     """forward(images, ids) -> (B, L-1) log p(ids[:, t+1] | ids[:, :t+1], image), zeroed after a
-    row's first <end> (the masked_fill of the reference sampler, scst_loss.py:236-239)."""
+    row's first <end> (the masked_fill of the reference sampler, scst_loss.py:236-239).
 
-    def __init__(self, model: nn.Module, end_token: int):
+    Dropout: `dropout_seed` set and the model in train mode -> the HIP recompute applies the decoder's dropout with
+    the counter-based masks of (p, dropout_seed) - the masks `sample_and_greedy(..., dropout=(p, seed))` sampled
+    with, as SCSTLoss does on one GPU; `dropout_seed` None -> eval-mode semantics on the HIP path (no dropout,
+    matching a sampler without dropout)."""
+
+    def __init__(self, model: nn.Module, end_token: int, dropout_seed: Optional[int] = None):
         super().__init__()
         self.model = model
         self.end_token = end_token
+        self.dropout_seed = dropout_seed
+
+    def dropout(self) -> Tuple[float, int]:
+        """(p, seed) of the train-mode masks shared with the sampler, or (0, 0)."""
+        from .train import decoder_dropout
+
+        if self.dropout_seed is None or not self.model.training:
+            return (0.0, 0)
+        return (decoder_dropout(self.model.decoder), int(self.dropout_seed))
 
     def forward(self, images: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
         from utils.scst_loss import masked_token_logp
@@ -43,7 +57,7 @@ class TeacherForcedLogProbs(nn.Module):
             from .train import decoder_token_logp, hip_memory_with_grad
 
             return decoder_token_logp(self.model.decoder, hip_memory_with_grad(self.model, images), ids,
-                                      self.end_token)
+                                      self.end_token, dropout=self.dropout())
         memory = self.model.encoder(images)
         L = ids.shape[1]
         mask = self.model.decoder.generate_square_subsequent_mask(L - 1, images.device)
@@ -54,11 +68,13 @@ class TeacherForcedLogProbs(nn.Module):
 _STREAMS = {}
 
 
-def sample_and_greedy(eng, memory: torch.Tensor, uniforms: torch.Tensor, start: int, end: int, max_len: int):
-    """The SCST step's two decodes of one memory, the sampled one (icap_decode_sample) and the
-    greedy baseline (icap_decode_greedy), replayed CONCURRENTLY on two streams: each decode mode owns
-    its workspace and captured graph, and both are latency-bound chains of small kernels that leave
-    most CUs idle.  Returns (sample_ids, sample_logp, greedy_ids) ready on the current stream."""
+def sample_and_greedy(eng, memory: torch.Tensor, uniforms: torch.Tensor, start: int, end: int, max_len: int,
+                      dropout: Optional[Tuple[float, int]] = None):
+    """The SCST step's two decodes of one memory, the sampled one (icap_decode_sample, or with dropout = (p, seed)
+    icap_decode_sample_dropout: the train-mode masks TeacherForcedLogProbs(dropout_seed=seed) recomputes with) and the
+    greedy baseline (icap_decode_greedy, eval mode as the reference's generate), replayed CONCURRENTLY on two streams:
+    each decode mode owns its workspace and captured graph, and both are latency-bound chains of small kernels that
+    leave most CUs idle.  Returns (sample_ids, sample_logp, greedy_ids) ready on the current stream."""
     dev = memory.device
     cur = torch.cuda.current_stream(dev)
     if dev not in _STREAMS:
@@ -67,7 +83,7 @@ def sample_and_greedy(eng, memory: torch.Tensor, uniforms: torch.Tensor, start: 
     s1.wait_stream(cur)
     s2.wait_stream(cur)
     with torch.cuda.stream(s1):
-        sid, lp = eng.sample(memory, uniforms, start, end, max_len)
+        sid, lp = eng.sample(memory, uniforms, start, end, max_len, dropout=dropout)
     with torch.cuda.stream(s2):
         gid, _ = eng.greedy_raw(memory, start, end, max_len)
     for t, st in ((memory, s1), (memory, s2), (uniforms, s1)):
@@ -112,10 +128,15 @@ def rewards(sample_ids: torch.Tensor, greedy_ids: torch.Tensor, ref_rows: torch.
 
 def scst_step(lp_module: nn.Module, images: torch.Tensor, ref_rows: torch.Tensor,
               sampler: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]], start: int, end: int, pad: int,
-              global_batch: Optional[int] = None) -> Tuple[torch.Tensor, dict]:
+              global_batch: Optional[int] = None, dropout_seed: Optional[int] = None) -> Tuple[torch.Tensor, dict]:
     """One SCST loss on the local shard.  lp_module: TeacherForcedLogProbs, DDP-wrapped when R > 1;
     ref_rows (B_local, Lr) raw id rows; sampler(images) -> (sample_ids, greedy_ids) for the shard.
+    dropout_seed: the seed the sampler drew its train-mode dropout masks with (sample_and_greedy(...,
+    dropout=(p, seed))); the teacher-forced recompute then applies the same masks (scst_loss.py:114-184 on one
+    GPU).  None keeps the module's own setting.
     Returns (loss, info); the caller runs loss.backward() (DDP all-reduces) and the optimizer."""
+    if dropout_seed is not None:
+        getattr(lp_module, "module", lp_module).dropout_seed = int(dropout_seed)
     B = images.shape[0]
     total = global_batch or B
     with torch.no_grad():

@@ -330,7 +330,9 @@ int icap_op_gemm_i8_blocks(const int8_t* A, const float* a_scale, const float* a
  * the steps after a row's first end_token zeroed.  The forward keeps its activations in ws (bytes from
  * icap_decoder_train_workspace), which the backward of the same call reads: dlogp (B, T) -> gradients of
  * every decoder parameter written (not accumulated) to the pointers of `grad` (same layout as `d`) and
- * dmemory (B, S, d_model) (may be NULL).  fp32 products (fp32 MFMA). */
+ * dmemory (B, S, d_model) (may be NULL).  fp32 products (fp32 MFMA).  The forward records its call per
+ * ws; a backward whose parameter (emb, fc_w) / ids / memory pointers, B, T, S, end_token or drop_p
+ * differ from that record, or on a ws no forward filled, returns non-zero (icap_last_error says which). */
 size_t icap_decoder_train_workspace(const icap_model_desc* d, int B, int T, int S, float drop_p);
 int icap_decoder_train_forward(const icap_model_desc* d, const int32_t* ids, int B, int T, const float* memory, int S,
                                int end_token, float drop_p, uint32_t drop_seed, float* logp, void* ws, size_t ws_bytes,

@@ -137,3 +137,33 @@ def test_concurrent_sample_and_greedy_equal_sequential(cuda):
         sid, lp, gid = sample_and_greedy(eng, mem, uni, W.START_TOKEN, W.END_TOKEN, 12)
         torch.cuda.synchronize()
         assert torch.equal(sid, ref_s) and torch.equal(lp, ref_lp) and torch.equal(gid, ref_g)
+
+
+def test_teacher_forced_dropout_follows_sampler_seed():
+    """The DDP SCST recompute takes the sampler's dropout seed (scst_step(dropout_seed=...)) through a DDP-style
+    wrapper and applies (p, seed) only in train mode - the masks sample_and_greedy(dropout=(p, seed)) drew."""
+    from image_caption_amd.scst import TeacherForcedLogProbs, scst_step
+
+    model, imgs, refs, _ = _setup()
+    lp = TeacherForcedLogProbs(model, W.END_TOKEN)
+    assert lp.dropout() == (0.0, 0)
+
+    class Wrap(torch.nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.module = m
+
+        def forward(self, *a):
+            return self.module(*a)
+
+    def sampler(im):
+        ids = torch.full((im.shape[0], 3), W.END_TOKEN, dtype=torch.int64)
+        ids[:, 0] = W.START_TOKEN
+        return ids, ids
+
+    scst_step(Wrap(lp), imgs[:2], refs[:2], sampler, W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN, dropout_seed=77)
+    assert lp.dropout_seed == 77
+    assert lp.dropout() == (0.0, 0)  # eval mode: no masks
+    model.train()
+    p, seed = lp.dropout()
+    assert seed == 77 and p > 0.0
