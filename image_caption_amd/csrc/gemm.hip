@@ -221,6 +221,9 @@ int gemm_tile_class(const GemmArgs& g) {
   return (g.N % 128 == 0 && g.N >= 256 && big_tiles >= 512) ? PROF_GEMM_128 : PROF_GEMM_64;
 }
 
+bool gemm_narrow_ok(const GemmArgs& g);
+hipError_t launch_gemm_narrow(const GemmArgs& g, hipStream_t s, int form);
+
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
   if (g.hm_n && (g.out != OUT_SPLIT || g.N % 64 || g.batch != 1 || g.rm_group || g.M % g.hm_n)) return hipErrorInvalidValue;
@@ -230,10 +233,10 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {
   const int cls = gemm_tile_class(g);
   if (cls == PROF_GEMM_256 || cls == PROF_GEMM_F16P) return launch_gemm_256(g, s);
   if (cls == PROF_GEMM_128) return run<128, 128, 64, 64>(g, s);
-  // narrow outputs over many rows (the trunk's stem and layer1-2 convolutions: N 64 / 128, M up to 3.2 M): 256 x 64
-  // tiles of four 64 x 64 wave tiles (80 KiB of LDS, two blocks per CU) instead of 64 x 64 tiles of 32 x 32
-  static const int tall64 = icap_knob("ICAP_GEMM_TALL64", 1);
-  if (tall64 && g.N <= 128 && g.M >= 65536 && g.batch == 1) return run<256, 64, 64, 64>(g, s);
+  // the fp16 trunk's N = 64 / 128 convolutions on the 256-family k-loop (launch_gemm_narrow); ICAP_GEMM_NARROW (tools):
+  // 0 = the 64 x 64 kernel below, 2-4 = the other measured tile forms
+  static const int narrow = icap_knob("ICAP_GEMM_NARROW", 1);
+  if (narrow && gemm_narrow_ok(g)) return launch_gemm_narrow(g, s, narrow);
   return run<64, 64, 32, 32>(g, s);
 }
 
@@ -699,6 +702,76 @@ hipError_t run_256(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
+// Narrow trunk convolutions (N = 64 / 128: the Grid trunk's layer1-2 conv1 / conv2 on fp16 planes): the 256-family
+// k-loop with 64-deep stages on BM x BN block tiles of 64-column wave tiles, NST-stage ring.
+namespace {
+
+template <int BM, int BN, int NST, int CONV, bool EPC>
+hipError_t run_narrow_(const GemmArgs& g, hipStream_t s) {
+  constexpr int lds = NST * (BM * 64 * 2 + BN * 64 * 2);
+  static bool attr = false;
+  if (!attr && lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute((const void*)gemm_256_kernel<1, 8, 0, CONV, BM, NST, 64, 0, true, EPC, BN>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nwg = (g.N / BN) * ((g.M + BM - 1) / BM);
+  static const int pre = icap_knob("ICAP_CONV_PRE", 1);
+  GemmArgs ga = g;
+  ga.no_pre = !pre;
+  hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, CONV, BM, NST, 64, 0, true, EPC, BN>), dim3(nwg), dim3(512), lds, s, ga);
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int NST>
+hipError_t run_narrow(const GemmArgs& g, hipStream_t s) {
+  const bool epc = g.out == OUT_SPLIT && g.bias && (g.epi == EPI_NONE || g.epi == EPI_RELU);
+  if (g.cv == 2) return epc ? run_narrow_<BM, BN, NST, 2, true>(g, s) : run_narrow_<BM, BN, NST, 2, false>(g, s);
+  if (g.cv == 1) return epc ? run_narrow_<BM, BN, NST, 1, true>(g, s) : run_narrow_<BM, BN, NST, 1, false>(g, s);
+  return epc ? run_narrow_<BM, BN, NST, 0, true>(g, s) : run_narrow_<BM, BN, NST, 0, false>(g, s);
+}
+
+}  // namespace
+
+// The fp16 trunk's narrow convolutions: the stem (N = 64 on the bordered NHWC4 image) and layer1-2's conv1 / conv2.
+bool gemm_narrow_ok(const GemmArgs& g) {
+  return g.f16 && g.scale && (g.N == 64 || g.N == 128) && g.K % 64 == 0 && g.batch == 1 && g.nsplit == 1 &&
+         !g.addend && !g.rm_group && !g.hm_n && !g.split_slots;
+}
+
+// form 1 (default; round 3, tools/r3_narrow.sh, per launch at B = 256 against the 64 x 64 kernel): N = 64 on 256 x 64
+// tiles (l1c1 162 -> 114 us, l1c2 197 -> 114), N = 128 on 128 x 128 tiles (l2c1 177 -> 102, l2c2 168 -> 97), 2-stage
+// rings, two blocks per CU.  Tools forms: 2 = 128-row tiles for N = 64 too (3-stage; l1c2 137), 3 = 256 x 64 with a
+// 3-stage ring (l1c2 155), 4 = 256-row tiles for N = 128 (l2c1 108, l2c2 116).
+// The fp16 trunk's N % 256 == 0 convolutions on 64 x 256 tiles of the 64-deep k-loop (2-stage ring, 80 KiB: two blocks
+// per CU) instead of the 128 x 256 / 256 x 256 forms, where the epilogue's HBM traffic or the tile count rules: the
+// residual conv3 (l1c3 349 -> 288 us, l2c3 172 -> 161, l3c3 178 -> 154, l4c3 108 -> 93), two-plane outputs (l3ds 165 ->
+// 134), K < 128 (l1ds 201 -> 183) and launches of fewer 128-row tiles than CUs (l4c2 121 -> 87); the compute-heavy rest
+// stays (l3c2 82 -> 88, l2ds 141 -> 152 on 64-row tiles).  Round 3, tools/r3_c3.sh.  ICAP_GEMM_C3 (tools): 0 = off,
+// 1 = 64 x 256 for the residual convolutions only, 2 = 128 x 256 2-stage, 3 = 64 x 256 3-stage, +10 = every one.
+bool gemm_c3_form(const GemmArgs& g, int cus, int* form) {
+  static const int knob = icap_knob("ICAP_GEMM_C3", -1);
+  if (!knob || !g.f16 || !g.scale || g.N % 256 || g.K % 64 || g.batch != 1 || g.nsplit != 1 || g.cv == 2 ||
+      g.addend || g.rm_group || g.hm_n || g.split_slots)
+    return false;
+  const long tiles128 = (long)(g.N / 256) * ((g.M + 127) / 128);
+  const bool pick = knob < 0 ? (g.res || g.c_planes == 2 || g.K < 128 || tiles128 < cus) : (knob >= 10 || g.res);
+  *form = knob < 0 ? 1 : knob % 10;
+  return pick;
+}
+
+hipError_t launch_gemm_c3(const GemmArgs& g, hipStream_t s, int form) {
+  return form == 2 ? run_narrow<128, 256, 2>(g, s) : form == 3 ? run_narrow<64, 256, 3>(g, s) : run_narrow<64, 256, 2>(g, s);
+}
+
+hipError_t launch_gemm_narrow(const GemmArgs& g, hipStream_t s, int form) {
+  if (g.N == 128) return form == 4 ? run_narrow<256, 128, 2>(g, s) : run_narrow<128, 128, 2>(g, s);
+  if (form == 2) return run_narrow<128, 64, 3>(g, s);
+  if (form == 3) return run_narrow<256, 64, 3>(g, s);
+  return run_narrow<256, 64, 2>(g, s);
+}
+
 hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N % 256 || g.K % 32 || g.batch != 1 || (g.nsplit != 1 && g.nsplit != 2))
     return hipErrorInvalidValue;
@@ -753,6 +826,8 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 0, true>), dim3(nwgh), dim3(512), ldsh1, s, g);
     return hipGetLastError();
   }
+  int c3 = 0;
+  if (gemm_c3_form(g, cus, &c3)) return launch_gemm_c3(g, s, c3);
   if (g.scale && !g.addend && !g.rm_group && !g.hm_n && g.out == OUT_SPLIT && g.bias &&
       (g.epi == EPI_NONE || g.epi == EPI_RELU))  // the trunk convolutions' epilogue form
     return g.f16 ? run_256<true, true>(g, s) : run_256<false, true>(g, s);

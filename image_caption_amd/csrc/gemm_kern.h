@@ -199,8 +199,27 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
 // relu?(acc * scale + shift (+ residual planes)) as split planes (bf16, or fp16 with F16), nothing else - no row
 // remaps, addends or other output forms, so the accumulators plus one column group's operands are all that is live
 // (the generic epilogue_256 spilled 34-38 VGPRs at the 128-register budget of two blocks per CU).
+// The residual planes of a wave's conv tile, loaded whole (PRE: issued before the tile's first stage, so their latency
+// overlaps the stage DMA instead of adding one more memory round trip after the k-loop).  Rows >= M load row M - 1.
 template <int TM, int TN, bool F16>
-__device__ __forceinline__ void epilogue_conv(const GemmArgs& p, f32x4 (&acc)[TM][TN], int mb, int nb, int fr, int fq) {
+__device__ __forceinline__ void conv_res_load(const GemmArgs& p, int mb, int nb, int fr, int fq, u32x2 (&rh)[TN][TM],
+                                              u32x2 (&rl)[TN][TM]) {
+  if (!p.res) return;
+  const bool res2 = !(F16 && p.res_planes == 1);
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const long ro = (long)min(mb + i * 16 + fr, p.M - 1) * p.res_ld + nb + j * 16 + 4 * fq;
+      rh[j][i] = *(const u32x2*)(p.res + ro);
+      rl[j][i] = res2 ? *(const u32x2*)(p.res + ro + p.res_lo) : (u32x2){0u, 0u};
+    }
+}
+
+// PRE: the residual planes come in prh / prl (conv_res_load), else they are loaded here per column-group batch.
+template <int TM, int TN, bool F16, bool PRE = false>
+__device__ __forceinline__ void epilogue_conv(const GemmArgs& p, f32x4 (&acc)[TM][TN], int mb, int nb, int fr, int fq,
+                                              const u32x2 (*prh)[TM] = nullptr, const u32x2 (*prl)[TM] = nullptr) {
   const int M = p.M;
   const bool res = p.res != nullptr, res2 = !(F16 && p.res_planes == 1), lo_out = p.c_planes == 2;
   const bool relu = p.epi == EPI_RELU;
@@ -217,7 +236,15 @@ __device__ __forceinline__ void epilogue_conv(const GemmArgs& p, f32x4 (&acc)[TM
       sv[jj] = *(const f32x4*)(p.scale + col);
       bv[jj] = *(const f32x4*)(p.bias + col);
     }
-    if (res) {  // (plane count hoisted: a per-element "load or not" select would wait after each load)
+    if (PRE) {
+#pragma unroll
+      for (int jj = 0; jj < JG; ++jj)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          rh[jj][i] = prh[j0 + jj][i];
+          rl[jj][i] = prl[j0 + jj][i];
+        }
+    } else if (res) {  // (plane count hoisted: a per-element "load or not" select would wait after each load)
       if (res2) {
 #pragma unroll
         for (int jj = 0; jj < JG; ++jj)
@@ -304,12 +331,14 @@ namespace {
 // bits whichever finished first) and runs the epilogue.
 // EPC: the epilogue is epilogue_conv (the trunk convolutions: GemmArgs::scale set) instead of epilogue_256 - a
 // compile-time choice, so each kernel holds one epilogue's registers (both in one kernel spilled 27-36 VGPRs).
+// BNT: block tile columns, 256 or (narrow outputs: the trunk's layer1-2 convolutions, N = 64 / 128) 128 or 64 - the
+// wave grid becomes (NW / (BNT / 64)) x (BNT / 64) of 64-column wave tiles, two blocks per CU.
 template <int NS, int NW, int NOMFMA = 0, int CONV = 0, int BMT = 256, int NST = 0, int KSD = 32, int TS = 0,
-          bool F16 = false, bool EPC = false>
-__global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64 ? 3 : 1)) void gemm_256_kernel(
-    GemmArgs p) {
-  constexpr int WGM = NW / 4;                       // wave grid WGM x 4
-  constexpr int BM = BMT, BN = 256, WM = BM / WGM, WN = 64, TM = WM / 16, TN = WN / 16;
+          bool F16 = false, bool EPC = false, int BNT = 256>
+__global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BNT < 256 ? 2 : (BMT == 64 ? 3 : 1)))
+void gemm_256_kernel(GemmArgs p) {
+  constexpr int WGN = BNT / 64, WGM = NW / WGN;     // wave grid WGM x WGN
+  constexpr int BM = BMT, BN = BNT, WM = BM / WGM, WN = 64, TM = WM / 16, TN = WN / 16;
   constexpr int KS = KSD;                           // k per stage (one or two MFMA k-steps)
   constexpr int RPI = KS == 64 ? 8 : 16;            // rows per 1 KiB DMA instruction
   constexpr int OPB = BM * KS * 2;                  // A bytes per plane per stage (16 KiB at BM 256)
@@ -323,7 +352,7 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WGN, wn = wave % WGN;
   // XCD-aware bijective remap of the linear block id
   const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
   const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
@@ -415,6 +444,12 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
 
   const int fr = lane & 15, fq = lane >> 4;
   const int foff = fr * 64 + ((fq ^ (((fr >> 3) & 1) << 1)) << 4);
+  // PRE (the 64-deep conv forms): the residual planes load before the first stage - older than every stage DMA, so
+  // the counted waits below still count only stages (the first one also covers these loads)
+  constexpr bool PRE = EPC && KSD == 64;
+  u32x2 prh[PRE ? TN : 1][TM], prl[PRE ? TN : 1][TM];
+  if constexpr (PRE)
+    if (!p.no_pre) conv_res_load<TM, TN, F16>(p, m0 + wm * WM, n0 + wn * WN, fr, fq, prh, prl);
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
     if (kbeg + s < kend) stage(kbeg + s, s);
@@ -495,8 +530,13 @@ __global__ __launch_bounds__(NW * 64, (BMT == 128 && KSD == 32) ? 4 : (BMT == 64
           acc[i][j][e] += __hip_atomic_load(other + ((i * TN + j) * 4 + e) * NT + tid, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
   }
-  if constexpr (EPC) epilogue_conv<TM, TN, F16>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);  // trunk convolutions
-  else epilogue_256<TM, TN, F16>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
+  if constexpr (EPC) {  // trunk convolutions
+    if (PRE && !p.no_pre) epilogue_conv<TM, TN, F16, PRE>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq, prh, prl);
+    else epilogue_conv<TM, TN, F16>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
+  }
+  else {
+    epilogue_256<TM, TN, F16>(p, acc, m0 + wm * WM, n0 + wn * WN, fr, fq);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -92,6 +92,7 @@ struct GemmArgs {
   // persistent GEMMs: at most this many workgroups (0 = one per CU of the device) - the CUs a CU-masked encoder
   // stream owns (batch pipelining, icap_set_encoder_cus)
   int max_grid;
+  int no_pre;     // tools (ICAP_CONV_PRE=0): the 64-deep conv forms load the residual after the k-loop
 };
 // bytes of split_ws for split_slots block slots per XCD
 inline size_t gemm_split_ws_bytes(int split_slots) { return (size_t)8 * split_slots * 2 * 128 * 256 * 4; }
