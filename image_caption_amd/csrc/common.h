@@ -142,6 +142,35 @@ __device__ __forceinline__ f32x2 gelu_erf_fast2(f32x2 v) {
   const f32x2 r = {v.x >= 0.f ? 2.f - erfc_z.x : erfc_z.x, v.y >= 0.f ? 2.f - erfc_z.y : erfc_z.y};
   return 0.5f * v * r;
 }
+// gelu_erf_fast on eight values (two column groups of an MFMA tile): every step is four independent packed FMAs,
+// so the ten-term chain issues without the nop a dependent v_pk_fma_f32 needs behind its producer (the f32x2 form
+// ran each pair's chain alone: ~500 s_nop in the MLP-1 epilogue).  The same operations per value, so the same results.
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x8 gelu_erf_fast8(f32x8 v) {
+  const f32x8 z = __builtin_elementwise_abs(v) * 0.70710678118654752f;
+  const f32x8 den = __builtin_elementwise_fma(z, (f32x8)0.5f, (f32x8)1.f);
+  f32x8 t;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = __builtin_amdgcn_rcpf(den[e]);
+  f32x8 y = 0.17087277f;
+  y = __builtin_elementwise_fma(y, t, (f32x8)-0.82215223f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)1.48851587f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)-1.13520398f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)0.27886807f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)-0.18628806f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)0.09678418f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)0.37409196f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)1.00002368f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)-1.26551223f);
+  const f32x8 ex = __builtin_elementwise_fma(-z, z, y);
+  f32x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float erfc_z = t[e] * __expf(ex[e]);
+    r[e] = v[e] >= 0.f ? 2.f - erfc_z : erfc_z;
+  }
+  return 0.5f * v * r;
+}
 
 // int8 two-slice quantisation (the operand form of gemm_i8_kernel): 16-bit fixed point relative to
 // the row maximum, q = rint(v / s) in [-32639, 32639], v1 = (q + 128) >> 8 in [-127, 127],

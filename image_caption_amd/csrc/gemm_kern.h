@@ -567,7 +567,9 @@ void gemm_256_kernel(GemmArgs p) {
 // ABL (tools build only): 1 = no k-loop DMA, 2 = no MFMA - timing ablations (tools/f16_ablate.sh); 3 = the
 // compiler's own fragment-read order, 4 = the read pipeline per k-half, 5 = the stage DMA before the first reads,
 // 6 = reads 3 groups ahead instead of 2 (within box noise, tools/f16x3_check.sh), 7 = s_setprio(1) around each
-// MFMA group (no gain, tools/f16_pf.sh), 8 = 8-byte SO stores.
+// MFMA group (no gain, tools/f16_pf.sh), 8 = 8-byte SO stores, 9 = no LDS fragment reads (opaque registers), 10 = no
+// k-loop DMA and no k-step barrier, 11 = 10 without the SO stores, 12 = 10 without the SO epilogue (timing
+// ablations, round 3: tools/r3_ablate.sh).
 // BMT: tile rows, 256 or (RES) 224 - wave tiles 112 x 64, the A stage 224 rows (wave 7 DMAs W rows only): at
 // N = 768 the 256-row tiles are 591 = 2.3 per CU (3 rounds, the last 30 % full), 224-row tiles 678 = 2.65 per CU
 // (3 rounds of 7/8 the work).
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       else if (SO && seam && kt == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
       else if (RES && seam && kt == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if (ABL < 10) __builtin_amdgcn_s_barrier();
       int st_t = -1, st_kt = 0;  // the stage this k-step DMAs into the other buffer (-1: none)
       if ((SO || RES) && seam && kt == 0) {
         // stage 1 of this tile is already in flight
@@ -660,7 +662,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         if (SO || RES) load_bias(tn, (tcount + 1) & 1);
         st_t = tn;
       }
-      if (ABL == 1) st_t = -1;
+      if (ABL == 1 || ABL >= 10) st_t = -1;
       // XK (default): the k-step's first fragment reads go out before the stage's 8 DMA instructions, whose
       // issue then covers their latency (ABL 5: DMA first)
       if (!XK_LATE && st_t >= 0) stage(st_t, st_kt, (step + 1) & 1);
@@ -668,10 +670,19 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       if constexpr (XK) {
         const int fo0 = fr * 128 + ((fq ^ (fr & 7)) << 4), fo1 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
         bf16x8 b2[2][TN], a2[2 * TM];
+        auto rd = [&](const char* ptr) -> bf16x8 {  // ABL 9: an opaque register instead of the LDS read
+          if constexpr (ABL == 9) {
+            u32x4 v = {(uint32_t)lane, 1u, 2u, (uint32_t)tid};
+            asm volatile("" : "+v"(v));
+            return __builtin_bit_cast(bf16x8, v);
+          } else {
+            return *(const bf16x8*)ptr;
+          }
+        };
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b2[0][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo0);
+        for (int j = 0; j < TN; ++j) b2[0][j] = rd(s0 + OPA + (wn * WN + j * 16) * 128 + fo0);
 #pragma unroll
-        for (int g = 0; g < XD; ++g) a2[g] = *(const bf16x8*)(s0 + (wm * WM + g * 16) * 128 + fo0);
+        for (int g = 0; g < XD; ++g) a2[g] = rd(s0 + (wm * WM + g * 16) * 128 + fo0);
         if constexpr (XK_LATE) {
           __builtin_amdgcn_sched_barrier(0);
           if (st_t >= 0) stage(st_t, st_kt, (step + 1) & 1);
@@ -682,9 +693,9 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
           const int nx = g + XD;
           if (nx == TM) {
 #pragma unroll
-            for (int j = 0; j < TN; ++j) b2[1][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo1);
+            for (int j = 0; j < TN; ++j) b2[1][j] = rd(s0 + OPA + (wn * WN + j * 16) * 128 + fo1);
           }
-          if (nx < 2 * TM) a2[nx] = *(const bf16x8*)(s0 + (wm * WM + (nx % TM) * 16) * 128 + (nx < TM ? fo0 : fo1));
+          if (nx < 2 * TM) a2[nx] = rd(s0 + (wm * WM + (nx % TM) * 16) * 128 + (nx < TM ? fo0 : fo1));
           __builtin_amdgcn_sched_barrier(0);
           if (XPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -730,30 +741,69 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       if (tn >= 0) {  // every wave is done reading the last stage's buffer: stage 1 of the next tile into it
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (ABL != 1) stage(tn, 1, (step + 1) & 1);  // step = the next tile's k-step 0 here; its k-step 1 reads (step + 1) & 1
+        if (ABL != 1 && ABL < 10) stage(tn, 1, (step + 1) & 1);  // step = the next tile's k-step 0 here; its k-step 1 reads (step + 1) & 1
       }
       const bool tail = bm * BM + BM > M;  // the last row band of a ragged M: rows >= M are not stored
+      // straight-line per row tile (no per-element branches, so the scheduler interleaves the TN x 2 independent GELU
+      // chains instead of padding each dependent packed FMA with a nop): bias in registers, head-major row offsets
+      // stepped by 16 rows, the fp16 range test as an OR of exponent carries - (h & 0x7c00) + 0x400 reaches bit 15
+      // exactly when h is Inf / NaN - masked by the row's store predicate
+      f32x4 bj[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bj[j] = p.bias ? *(const f32x4*)(sbias + (tcount & 1) * 256 + wn * WN + j * 16 + 4 * fq) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      const bool gelu = p.epi == EPI_GELU, hm_step = p.hm_n >= 16;
+      int hq = 0, hr = 0;  // (row / hm_n, row % hm_n) of row tile i's row (hm_step)
+      if (hm_step) {
+        hq = (mb + fr) / p.hm_n;
+        hr = mb + fr - hq * p.hm_n;
+      }
+      uint32_t rbits = 0;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int m = min(mb + i * 16 + fr, M - 1);
-        const long orow = p.hm_n ? (((long)(m / p.hm_n) * (p.N / 64) + nb / 64) * p.hm_n + m % p.hm_n) * 64 - nb
-                                 : (long)m * p.ldc;
-        bf16_t* C = (bf16_t*)p.C + orow + 4 * fq;
-        const bool ok = !tail || mb + i * 16 + fr < M;
-        u32x2 pk[TN];
+        if constexpr (ABL == 12) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          f32x4 v = acc[i][j];
-          if (p.bias) v += *(const f32x4*)(sbias + (tcount & 1) * 256 + wn * WN + j * 16 + 4 * fq);
-          if (p.epi == EPI_GELU) {
-            const f32x2 lo = gelu_erf_fast2((f32x2){v[0], v[1]}), hi = gelu_erf_fast2((f32x2){v[2], v[3]});
-            v = (f32x4){lo[0], lo[1], hi[0], hi[1]};
-          }
-          pk[j] = pack16x4<true>(v);
-          if (ok && (f16_pair_nonfinite(pk[j][0]) || f16_pair_nonfinite(pk[j][1]))) range_bad = true;
-          if (!WIDE && ok) *(u32x2*)(C + nb + j * 16) = pk[j];
+          for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+          continue;
         }
-        if constexpr (WIDE) {
+        const int mr = mb + i * 16 + fr;
+        const bool ok = !tail || mr < M;
+        long orow;
+        if (hm_step) {
+          orow = (((long)hq * (p.N / 64) + nb / 64) * p.hm_n + hr) * 64 - nb;
+          hr += 16;
+          if (hr >= p.hm_n) hr -= p.hm_n, ++hq;
+        } else if (p.hm_n) {
+          const int m = min(mr, M - 1);
+          orow = (((long)(m / p.hm_n) * (p.N / 64) + nb / 64) * p.hm_n + m % p.hm_n) * 64 - nb;
+        } else {
+          orow = (long)min(mr, M - 1) * p.ldc;
+        }
+        bf16_t* C = (bf16_t*)p.C + orow + 4 * fq;
+        u32x2 pk[TN];
+        if (gelu) {
+          static_assert(TN % 2 == 0, "GELU in column-group pairs");
+#pragma unroll
+          for (int j = 0; j < TN; j += 2) {
+            const f32x4 v0 = acc[i][j] + bj[j], v1 = acc[i][j + 1] + bj[j + 1];
+            const f32x8 g = gelu_erf_fast8((f32x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
+            pk[j] = pack16x4<true>((f32x4){g[0], g[1], g[2], g[3]});
+            pk[j + 1] = pack16x4<true>((f32x4){g[4], g[5], g[6], g[7]});
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) pk[j] = pack16x4<true>(acc[i][j] + bj[j]);
+        }
+        uint32_t rb = 0;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          rb |= ((pk[j][0] & 0x7c007c00u) + 0x04000400u) | ((pk[j][1] & 0x7c007c00u) + 0x04000400u);
+        rbits |= ok ? rb : 0u;
+        if constexpr (!WIDE) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            if (ok) *(u32x2*)(C + nb + j * 16) = pk[j];
+        } else {
           // lanes fq (even) and fq + 1 hold columns 4 fq .. 4 fq + 7 of tiles j and j + 1: the even lane keeps
           // tile j's 8 columns, the odd lane tile j + 1's (the partner is 16 lanes away, same row)
           const bool odd = fq & 1;
@@ -763,10 +813,12 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
             const u32x2 rcv = {(uint32_t)__shfl_xor((int)snd[0], 16, 64), (uint32_t)__shfl_xor((int)snd[1], 16, 64)};
             const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], pk[j + 1][0], pk[j + 1][1]}
                                 : (u32x4){pk[j][0], pk[j][1], rcv[0], rcv[1]};
-            if (ok) *(u32x4*)(C + nb + (odd ? (j + 1) * 16 - 4 : j * 16)) = w;
+            if constexpr (ABL == 11) asm volatile("" ::"v"(w), "v"(C));
+            else if (ok) *(u32x4*)(C + nb + (odd ? (j + 1) * 16 - 4 : j * 16)) = w;
           }
         }
       }
+      if (rbits & 0x80008000u) range_bad = true;
       // the counted waits of the next tile assume all NSTORE stores per wave were issued: not after a ragged tile
       // (its next tile waits vmcnt(0) and re-issues its stage 1 - the same bytes into the same buffer)
       seam = !tail;
@@ -799,7 +851,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       if (tn >= 0) {  // stage 1 of the next tile into the last stage's buffer, after the stores
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (ABL != 1) stage(tn, 1, (step + 1) & 1);
+        if (ABL != 1 && ABL < 10) stage(tn, 1, (step + 1) & 1);
       }
       // k-step 0 of the next tile skips its vmcnt wait because the residual loads retired after its stage 0;
       // every lane loads (rows clamped), so that holds for ragged tiles too

@@ -428,7 +428,7 @@ bool launch_gemm_256_tools(const GemmArgs& g, hipStream_t s, int cus, hipError_t
     // timing only (tools/f16_ablate.sh); 3 / 4 / 5: the compiler's fragment-read order / the read pipeline per
     // k-half / the stage's DMA before the first fragment reads; 6: reads 3 groups ahead; 7: setprio; 8: 8-B stores
     static const int abl = icap_knob("ICAP_F16P_ABL", 0);
-    if (so && abl >= 1 && abl <= 8) {
+    if (so && abl >= 1 && abl <= 12) {
 #define F16P_ABL(A_)                                                                                  \
   if (abl == A_) {                                                                                    \
     if (!res) {                                                                                       \
@@ -445,6 +445,7 @@ bool launch_gemm_256_tools(const GemmArgs& g, hipStream_t s, int cus, hipError_t
     return done();                                                                                    \
   }
       F16P_ABL(1) F16P_ABL(2) F16P_ABL(3) F16P_ABL(4) F16P_ABL(5) F16P_ABL(6) F16P_ABL(7) F16P_ABL(8)
+      F16P_ABL(9) F16P_ABL(10) F16P_ABL(11) F16P_ABL(12)
 #undef F16P_ABL
     }
     // ICAP_F16_PP=1: the ping-pong k-loop (gemm_f16q_kernel; slower)
