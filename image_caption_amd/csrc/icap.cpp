@@ -955,8 +955,11 @@ void encode_grid(icap_handle* h, const float* img, int B, int IH, int IW, float*
           res = R;
           rpl = pout;
         }
+        // f16: conv1 reads only the hi plane of a hi/lo residual stream - the branch it starts is one fp16 plane anyway
+        // (CPU emulation, tools/numerics_trunk16_c1.py: features 3.2e-4 -> 3.7e-4 relative, memory 1.14e-3 -> 1.38e-3,
+        // logits 1.07e-4 -> 1.22e-4, ids equal), and layer3-4's conv1 GEMMs then run half the MFMA work
         trunk_conv(h, c1, X, c1.cin, aL, Min, T1, aL, true, nullptr, 0, s, ConvGeom(), bnp(i1), bt.momentum,
-                   t16(pin, 1));
+                   t16(f16 ? 1 : pin, 1));
         ConvGeom g3;  // 3x3 conv2 read straight from T1 (implicit GEMM)
         g3.cv = 1; g3.H = hh; g3.W = ww; g3.C = c1.cout; g3.OH = oh; g3.OW = ow;
         trunk_conv(h, c2, T1, 0, aL, Mout, T2, aL, true, nullptr, 0, s, g3, bnp(i1 + 1), bt.momentum, t16(1, 1));
