@@ -9,7 +9,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 LIB = HERE / "libicap.so"
-SOURCES = ["gemm.hip", "rows.hip", "attention.hip", "head.hip", "beam.hip", "decode.hip", "decstep.hip", "xdec.hip", "trunk.hip", "preprocess.hip", "cider.hip", "train.hip", "icap.cpp"]
+SOURCES = ["gemm.hip", "rows.hip", "attention.hip", "head.hip", "beam.hip", "decode.hip", "decstep.hip", "xdec.hip", "trunk.hip", "conv_rmw.hip", "preprocess.hip", "cider.hip", "train.hip", "icap.cpp"]
 # measured-and-rejected kernel forms: compiled into the tools build only
 TOOLS_SOURCES = ["gemm_tools.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

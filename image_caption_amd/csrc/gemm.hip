@@ -826,6 +826,12 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
     hipLaunchKernelGGL((gemm_256_kernel<1, 8, 0, 0, 128, 2, 32, 0, true>), dim3(nwgh), dim3(512), ldsh1, s, g);
     return hipGetLastError();
   }
+  // the fp16 trunk's 1x1 convolutions with K <= 256 and N >= 128 (the residual conv3, the layer1-2 downsamples):
+  // W-stationary persistent blocks (conv_rmw.hip; round 3, tools/r3_rmw.sh: l1c3 290 -> 168 us, l2c3 163 -> 100, l3c3
+  // 158 -> 99, l1ds 188 -> 162, l2ds 154 -> 128; Grid 9819-9935 -> 10829-10891 captions/s).  ICAP_CONV_RMW (tools):
+  // 0 = the 64 x 256 tiles below, 1 = the residual convolutions only
+  static const int rmw = icap_knob("ICAP_CONV_RMW", 2);
+  if (rmw && conv_rmw_ok(g) && (g.res || rmw == 2)) return launch_conv_rmw(g, s, cus);
   int c3 = 0;
   if (gemm_c3_form(g, cus, &c3)) return launch_gemm_c3(g, s, c3);
   if (g.scale && !g.addend && !g.rm_group && !g.hm_n && g.out == OUT_SPLIT && g.bias &&

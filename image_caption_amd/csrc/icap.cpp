@@ -1842,7 +1842,7 @@ const char* icap_knobs_set() {
       "ICAP_F16_PRES", "ICAP_XATTN16_KS", "ICAP_XATTN16_CK", "ICAP_ENC_ATTN16_QPW", "ICAP_F16_PP",
       "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
       "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE", "ICAP_XDEC_TRACE", "ICAP_GEMM_NARROW",
-      "ICAP_GEMM_C3", "ICAP_CONV_PRE"};
+      "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW"};
   for (const char* n : names)
     if (getenv(n)) return n;
   return "";

@@ -102,6 +102,9 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
 int gemm_tile_class(const GemmArgs& g);
 // 256 x 256-tile, 8-wave encoder GEMM (batch 1, N % 256 == 0).
 hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s);
+// conv_rmw.hip: W-stationary persistent form of the fp16 trunk's residual 1x1 convolutions (K 64 / 128 / 256)
+bool conv_rmw_ok(const GemmArgs& g);
+hipError_t launch_conv_rmw(const GemmArgs& g, hipStream_t s, int cus);
 #ifdef ICAP_TOOLS
 // gemm_tools.hip (tools build only): takes the launch when a measurement knob selects a rejected form
 bool launch_gemm_256_tools(const GemmArgs& g, hipStream_t s, int cus, hipError_t* err);

@@ -24,7 +24,7 @@ for r in rows[first[-1]:]:
     if "layernorm" in n or "enc_attention" in n:
         break
     d = (r[2] - r[1]) / 1e3
-    if "gemm" in n:
+    if "gemm" in n or "conv_rmw" in n:
         key = f"{names[gi] if gi < len(names) else 'tail'} {n[:26]}"
         gi += 1
     else:
