@@ -756,6 +756,7 @@ bool gemm_c3_form(const GemmArgs& g, int cus, int* form) {
       g.addend || g.rm_group || g.hm_n || g.split_slots)
     return false;
   const long tiles128 = (long)(g.N / 256) * ((g.M + 127) / 128);
+  // (layer3 conv1 - K = 1024, 392 tiles of 128 rows - measured slower on these tiles: 62 -> 68 us, tools/r3_c3b.sh)
   const bool pick = knob < 0 ? (g.res || g.c_planes == 2 || g.K < 128 || tiles128 < cus) : (knob >= 10 || g.res);
   *form = knob < 0 ? 1 : knob % 10;
   return pick;
