@@ -66,7 +66,9 @@ def pmc_traffic(kernel: str, workload):
             table = json.load(f)
     except (OSError, ValueError):
         return None
-    rows = [row for name, row in table.items() if name.split("<")[0] == kernel]  # every template variant
+    # every template variant; the 256-family class also covers the W-stationary conv form it launches (conv_rmw.hip)
+    fam = {kernel, "conv_rmw_kernel"} if kernel == "gemm_256_kernel" else {kernel}
+    rows = [row for name, row in table.items() if name.split("<")[0] in fam]
     n = sum(r["launches"] for r in rows)
     return int(sum(r["traffic_bytes"] * r["launches"] for r in rows) / n) if n else None
 

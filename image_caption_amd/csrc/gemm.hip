@@ -224,6 +224,13 @@ int gemm_tile_class(const GemmArgs& g) {
 bool gemm_narrow_ok(const GemmArgs& g);
 hipError_t launch_gemm_narrow(const GemmArgs& g, hipStream_t s, int form);
 
+// Profile class of a launch = the kernel family that runs it: the fp16 trunk's narrow convolutions run on the
+// 256-family k-loop (launch_gemm_narrow) although their tile class is the 64 x 64 one
+int gemm_prof_class(const GemmArgs& g) {
+  const int cls = gemm_tile_class(g);
+  return cls == PROF_GEMM_64 && gemm_narrow_ok(g) && icap_knob("ICAP_GEMM_NARROW", 1) ? PROF_GEMM_256 : cls;
+}
+
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
   if (g.hm_n && (g.out != OUT_SPLIT || g.N % 64 || g.batch != 1 || g.rm_group || g.M % g.hm_n)) return hipErrorInvalidValue;

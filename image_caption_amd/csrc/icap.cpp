@@ -209,7 +209,7 @@ struct icap_handle {
   void run_gemm(const GemmArgs& g, hipStream_t s) {
     const double flops = 2.0 * g.M * g.N * g.K * g.batch;  // algorithmic (one plane)
     const double bytes = 2.0 * g.batch * ((double)g.M * g.K * g.nsplit + (double)g.N * g.K);
-    timed(gemm_tile_class(g), flops, bytes, s, [&] { HIPCHK(launch_gemm(g, s)); });
+    timed(gemm_prof_class(g), flops, bytes, s, [&] { HIPCHK(launch_gemm(g, s)); });
   }
 
   // workspaces

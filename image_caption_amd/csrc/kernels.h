@@ -100,6 +100,8 @@ inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_plane
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t s);
 // Which kernel launch_gemm picks (PROF_GEMM_256 / PROF_GEMM_128 / PROF_GEMM_64).
 int gemm_tile_class(const GemmArgs& g);
+// The profile class icap_profile_* records a GEMM launch under (the kernel family that runs it).
+int gemm_prof_class(const GemmArgs& g);
 // 256 x 256-tile, 8-wave encoder GEMM (batch 1, N % 256 == 0).
 hipError_t launch_gemm_256(const GemmArgs& g, hipStream_t s);
 // conv_rmw.hip: W-stationary persistent form of the fp16 trunk's residual 1x1 convolutions (K 64 / 128 / 256)
