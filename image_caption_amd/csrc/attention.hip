@@ -395,32 +395,66 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
         }
         s[u] = acc;
       }
-      float cm = -INFINITY;
+      if constexpr (F16) {
+        // the f16 encoder's softmax in the exp2 domain with packed fp32 math: scores scaled by scale * log2(e) once
+        // (v_pk_mul), the key mask only in a ragged last chunk, max through 3-input maxima, exponents
+        // v_exp_f32(s - m) with the running max and sum in log2 units (the same softmax, ~half the VALU
+        // instructions per score of the exp / compare / mask per element form)
+        const float sc2 = scale * 1.44269504088896341f;
+        s[0] *= sc2;
+        s[1] *= sc2;
+        if (c * CK + CK > N) {  // (wave-uniform) ragged last chunk
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+          for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = c * CK + u * 16 + g * 4 + r;
-          const float v = key < N ? s[u][r] * scale : -INFINITY;
-          s[u][r] = v;
-          cm = fmaxf(cm, v);
+            for (int r = 0; r < 4; ++r)
+              if (c * CK + u * 16 + g * 4 + r >= N) s[u][r] = -INFINITY;
         }
-      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-      const float m_new = fmaxf(m[t], cm);  // finite: every chunk holds at least one real key
-      const float alpha = __expf(m[t] - m_new);
-      m[t] = m_new;
-      l[t] *= alpha;
+        float cm = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]);
+        cm = fmaxf(fmaxf(cm, s[0][3]), s[1][0]);
+        cm = fmaxf(fmaxf(cm, s[1][1]), s[1][2]);
+        cm = rows4_max(fmaxf(cm, s[1][3]));
+        const float m_new = fmaxf(m[t], cm);  // finite: every chunk holds at least one real key
+        const float alpha = __builtin_amdgcn_exp2f(m[t] - m_new);
+        m[t] = m_new;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[t][dt] *= alpha;
+        for (int dt = 0; dt < 4; ++dt) o[t][dt] *= alpha;
+        s[0] -= m_new;
+        s[1] -= m_new;
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = __expf(s[u][r] - m_new);
-          s[u][r] = e;
-          l[t] += e;
-        }
+          for (int r = 0; r < 4; ++r) s[u][r] = __builtin_amdgcn_exp2f(s[u][r]);
+        const f32x4 e4 = s[0] + s[1];
+        l[t] = l[t] * alpha + ((e4[0] + e4[1]) + (e4[2] + e4[3]));
+      } else {
+        float cm = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = c * CK + u * 16 + g * 4 + r;
+            const float v = key < N ? s[u][r] * scale : -INFINITY;
+            s[u][r] = v;
+            cm = fmaxf(cm, v);
+          }
+        cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        const float m_new = fmaxf(m[t], cm);  // finite: every chunk holds at least one real key
+        const float alpha = __expf(m[t] - m_new);
+        m[t] = m_new;
+        l[t] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[t][dt] *= alpha;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = __expf(s[u][r] - m_new);
+            s[u][r] = e;
+            l[t] += e;
+          }
+      }
       bf16x8 ph, pl;
       if constexpr (F16) {  // probabilities as one fp16 plane
         const u32x2 p0 = pack16x4<true>(s[0]), p1 = pack16x4<true>(s[1]);
@@ -456,8 +490,12 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
     const int qt = wave + t * NW;
     if (qt >= nqt) break;
     float lt = l[t];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    if constexpr (F16) {
+      lt = rows4_sum(lt);
+    } else {
+      lt += __shfl_xor(lt, 16, 64);
+      lt += __shfl_xor(lt, 32, 64);
+    }
     const float inv = 1.f / lt;
     const int qq = qt * 16 + fr;
     if constexpr (F16) {
@@ -469,7 +507,7 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
       for (int dt = 0; dt < 4; dt += 2) {
         const u32x2 p0 = pack16x4<true>(o[t][dt] * inv), p1 = pack16x4<true>(o[t][dt + 1] * inv);
         const u32x2 snd = odd ? p0 : p1;
-        const u32x2 rcv = {(uint32_t)__shfl_xor((int)snd[0], 16, 64), (uint32_t)__shfl_xor((int)snd[1], 16, 64)};
+        const u32x2 rcv = {xor16_partner(snd[0]), xor16_partner(snd[1])};
         const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], p1[0], p1[1]} : (u32x4){p0[0], p0[1], rcv[0], rcv[1]};
         if (qq < N) *(u32x4*)(dst + (odd ? (dt + 1) * 16 - 4 : dt * 16)) = w;
       }

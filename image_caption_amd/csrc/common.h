@@ -142,6 +142,27 @@ __device__ __forceinline__ f32x2 gelu_erf_fast2(f32x2 v) {
   const f32x2 r = {v.x >= 0.f ? 2.f - erfc_z.x : erfc_z.x, v.y >= 0.f ? 2.f - erfc_z.y : erfc_z.y};
   return 0.5f * v * r;
 }
+// Cross-row lane exchange without the LDS crossbar (gfx950 v_permlane16_swap / v_permlane32_swap, VALU): with both
+// operands the same value, the swap leaves lane l holding {v of its row pair's even row, v of the odd row} (16-swap)
+// or {v of rows 0-1, v of rows 2-3} (32-swap), whichever row l is in - so max / sum over the pair is the xor-16 / xor-32
+// reduction and the other element is the partner.  (__shfl_xor compiles to ds_bpermute: an LDS round trip each.)
+__device__ __forceinline__ uint32_t xor16_partner(uint32_t v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return (threadIdx.x & 16) ? p[0] : p[1];
+}
+__device__ __forceinline__ float rows4_max(float v) {  // max over lanes l, l ^ 16, l ^ 32, l ^ 48
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float rows4_sum(float v) {  // sum over lanes l, l ^ 16, l ^ 32, l ^ 48 (same order in all four)
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
 // gelu_erf_fast on eight values (two column groups of an MFMA tile): every step is four independent packed FMAs,
 // so the ten-term chain issues without the nop a dependent v_pk_fma_f32 needs behind its producer (the f32x2 form
 // ran each pair's chain alone: ~500 s_nop in the MLP-1 epilogue).  The same operations per value, so the same results.

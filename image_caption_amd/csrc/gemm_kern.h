@@ -810,7 +810,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
           for (int j = 0; j < TN; j += 2) {
             const u32x2 snd = odd ? pk[j] : pk[j + 1];
-            const u32x2 rcv = {(uint32_t)__shfl_xor((int)snd[0], 16, 64), (uint32_t)__shfl_xor((int)snd[1], 16, 64)};
+            const u32x2 rcv = {xor16_partner(snd[0]), xor16_partner(snd[1])};
             const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], pk[j + 1][0], pk[j + 1][1]}
                                 : (u32x4){pk[j][0], pk[j][1], rcv[0], rcv[1]};
             if constexpr (ABL == 11) asm volatile("" ::"v"(w), "v"(C));
