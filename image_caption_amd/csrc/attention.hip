@@ -145,8 +145,7 @@ __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __
           cm = fmaxf(cm, v);
         }
       }
-      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      cm = rows4_max(cm);
       const float m_new = fmaxf(m, cm);
       if (m_new == -INFINITY) continue;  // every key of this chunk is padding (uniform per query)
       const float alpha = __expf(m - m_new);
@@ -193,8 +192,7 @@ __global__ __launch_bounds__(NW * 64) void enc_attention_kernel(const bf16_t* __
         }
       }
     }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    l = rows4_sum(l);
     const float inv = 1.f / l;
     const int qq = qt * 16 + fr;
     if (qq < N) {
@@ -438,8 +436,7 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
             s[u][r] = v;
             cm = fmaxf(cm, v);
           }
-        cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        cm = rows4_max(cm);
         const float m_new = fmaxf(m[t], cm);  // finite: every chunk holds at least one real key
         const float alpha = __expf(m[t] - m_new);
         m[t] = m_new;
@@ -493,8 +490,7 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
     if constexpr (F16) {
       lt = rows4_sum(lt);
     } else {
-      lt += __shfl_xor(lt, 16, 64);
-      lt += __shfl_xor(lt, 32, 64);
+      lt = rows4_sum(lt);
     }
     const float inv = 1.f / lt;
     const int qq = qt * 16 + fr;
@@ -745,8 +741,7 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
         s[kt][j] = v;
         cmax = fmaxf(cmax, v);
       }
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    cmax = rows4_max(cmax);
     const float m_new = fmaxf(m_run, cmax);
     const float alpha = __expf(m_run - m_new);
     float psum = 0.f;
@@ -758,8 +753,7 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
         s[kt][j] = e;
         psum += e;
       }
-    psum += __shfl_xor(psum, 16, 64);
-    psum += __shfl_xor(psum, 32, 64);
+    psum = rows4_sum(psum);
     l_run = l_run * alpha + psum;
     m_run = m_new;
     // P^T as the B operand (k = key, permuted): element j < 4 -> key 4fq + j, j >= 4 -> 16 + 4fq + j - 4
@@ -991,8 +985,7 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
         sc[kt][j] = v;
         cmax = fmaxf(cmax, v);
       }
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    cmax = rows4_max(cmax);
     const float m_new = fmaxf(m_run, cmax);
     const float alpha = __expf(m_run - m_new);
     float psum = 0.f;
@@ -1004,8 +997,7 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
         sc[kt][j] = e;
         psum += e;
       }
-    psum += __shfl_xor(psum, 16, 64);
-    psum += __shfl_xor(psum, 32, 64);
+    psum = rows4_sum(psum);
     l_run = l_run * alpha + psum;
     m_run = m_new;
 #pragma unroll
@@ -1020,8 +1012,7 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
           if (valid && key < S) sc[kt][j] *= drop_mul(drop, 3, (int)r, drop.pos, hd * 256 + key);
           dsum += sc[kt][j];
         }
-      dsum += __shfl_xor(dsum, 16, 64);
-      dsum += __shfl_xor(dsum, 32, 64);
+      dsum = rows4_sum(dsum);
       d_run = d_run * alpha + dsum;
     }
 #pragma unroll

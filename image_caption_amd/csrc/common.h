@@ -42,15 +42,76 @@ __device__ __forceinline__ void split_bf2(f32x2 v, uint32_t& hi, uint32_t& lo) {
   lo = pack_bf2(v - hf);
 }
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+// Cross-row lane exchange without the LDS crossbar (gfx950 v_permlane16_swap / v_permlane32_swap, VALU): with both
+// operands the same value, the swap leaves lane l holding {v of its row pair's even row, v of the odd row} (16-swap)
+// or {v of rows 0-1, v of rows 2-3} (32-swap), whichever row l is in - so max / sum over the pair is the xor-16 / xor-32
+// reduction and the other element is the partner.  (__shfl_xor compiles to ds_bpermute: an LDS round trip each.)
+__device__ __forceinline__ uint32_t xor16_partner(uint32_t v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return (threadIdx.x & 16) ? p[0] : p[1];
 }
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+__device__ __forceinline__ float rows4_max(float v) {  // max over lanes l, l ^ 16, l ^ 32, l ^ 48
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float rows4_sum(float v) {  // sum over lanes l, l ^ 16, l ^ 32, l ^ 48 (same order in all four)
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
+// Lane exchanges inside a 16-lane row through DPP (a VALU operand modifier, no LDS round trip): CTRL 0xB1 / 0x4E =
+// quad_perm [1,0,3,2] / [2,3,0,1] (xor 1 / xor 2), 0x141 = half-row mirror (the other quad of the lane's 8), 0x140 =
+// row mirror (the other 8 of the row).  Applied in that order to a symmetric operation (+, max), every lane of the
+// row ends with the same bits.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+// whole-wave reductions: the row reduction, then the rows (every lane the same bits)
+__device__ __forceinline__ float wave_max(float v) { return rows4_max(row16_max(v)); }
+__device__ __forceinline__ float wave_sum(float v) { return rows4_sum(row16_sum(v)); }
+// (value, index) argmax over the wave, ties to the lower index: the same total order in every pairing, so every lane
+// ends with the exact winner (DPP inside rows, permlane swaps across them)
+__device__ __forceinline__ void argmax_take(float& bv, int& bi, float ov, int oi) {
+  if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+}
+__device__ __forceinline__ void wave_argmax(float& bv, int& bi) {
+  argmax_take(bv, bi, dpp_f<0xB1>(bv), dpp_i<0xB1>(bi));
+  argmax_take(bv, bi, dpp_f<0x4E>(bv), dpp_i<0x4E>(bi));
+  argmax_take(bv, bi, dpp_f<0x141>(bv), dpp_i<0x141>(bi));
+  argmax_take(bv, bi, dpp_f<0x140>(bv), dpp_i<0x140>(bi));
+  const auto pv = __builtin_amdgcn_permlane16_swap(__float_as_uint(bv), __float_as_uint(bv), false, false);
+  const auto pi = __builtin_amdgcn_permlane16_swap((uint32_t)bi, (uint32_t)bi, false, false);
+  argmax_take(bv, bi, __uint_as_float(pv[0]), (int)pi[0]);
+  argmax_take(bv, bi, __uint_as_float(pv[1]), (int)pi[1]);
+  const auto qv = __builtin_amdgcn_permlane32_swap(__float_as_uint(bv), __float_as_uint(bv), false, false);
+  const auto qi = __builtin_amdgcn_permlane32_swap((uint32_t)bi, (uint32_t)bi, false, false);
+  argmax_take(bv, bi, __uint_as_float(qv[0]), (int)qi[0]);
+  argmax_take(bv, bi, __uint_as_float(qv[1]), (int)qi[1]);
+}
+// value of `v` in lane `src` (a wave-uniform lane index) for every lane
+__device__ __forceinline__ float lane_bcast(float v, int src) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
 }
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -142,27 +203,6 @@ __device__ __forceinline__ f32x2 gelu_erf_fast2(f32x2 v) {
   const f32x2 r = {v.x >= 0.f ? 2.f - erfc_z.x : erfc_z.x, v.y >= 0.f ? 2.f - erfc_z.y : erfc_z.y};
   return 0.5f * v * r;
 }
-// Cross-row lane exchange without the LDS crossbar (gfx950 v_permlane16_swap / v_permlane32_swap, VALU): with both
-// operands the same value, the swap leaves lane l holding {v of its row pair's even row, v of the odd row} (16-swap)
-// or {v of rows 0-1, v of rows 2-3} (32-swap), whichever row l is in - so max / sum over the pair is the xor-16 / xor-32
-// reduction and the other element is the partner.  (__shfl_xor compiles to ds_bpermute: an LDS round trip each.)
-__device__ __forceinline__ uint32_t xor16_partner(uint32_t v) {
-  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-  return (threadIdx.x & 16) ? p[0] : p[1];
-}
-__device__ __forceinline__ float rows4_max(float v) {  // max over lanes l, l ^ 16, l ^ 32, l ^ 48
-  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
-}
-__device__ __forceinline__ float rows4_sum(float v) {  // sum over lanes l, l ^ 16, l ^ 32, l ^ 48 (same order in all four)
-  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
-  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
-}
-
 // gelu_erf_fast on eight values (two column groups of an MFMA tile): every step is four independent packed FMAs,
 // so the ten-term chain issues without the nop a dependent v_pk_fma_f32 needs behind its producer (the f32x2 form
 // ran each pair's chain alone: ~500 s_nop in the MLP-1 epilogue).  The same operations per value, so the same results.

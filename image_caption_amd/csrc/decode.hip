@@ -182,10 +182,11 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
         part = fmaf(q4[1], k4[1], part);
         part = fmaf(q4[2], k4[2], part);
         part = fmaf(q4[3], k4[3], part);
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);  // sum over the key's 16 lanes
-        // scores of keys 4i..4i+3 sit in lanes 0, 16, 32, 48: lane j takes key j's
-        const float sc = __shfl(part, ((lane - 4 * i) & 3) * 16, 64);
+        part = row16_sum(part);  // sum over the key's 16 lanes (DPP: no LDS round trip)
+        // scores of keys 4i..4i+3 sit in rows 0..3: lane j takes key j's (lane broadcasts of the row leaders)
+        const float p0 = lane_bcast(part, 0), p1 = lane_bcast(part, 16), p2 = lane_bcast(part, 32), p3 = lane_bcast(part, 48);
+        const int kr = (lane - 4 * i) & 3;
+        const float sc = kr == 0 ? p0 : kr == 1 ? p1 : kr == 2 ? p2 : p3;
         if (lane >= 4 * i && lane < 4 * i + 4) s_mine = lane < nkeys ? sc * p.scale : -INFINITY;
       };
       auto pick = [&](int j, f32x4 cur, f32x4 pre) -> f32x4 {
@@ -204,23 +205,26 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
       l = wave_sum(e);
       // train mode: dropout on the attention probabilities (key = lane), the normaliser stays undropped
       const float ed = p.drop.thr && lane < nkeys ? e * drop_mul(p.drop, 1, b, t0, h * 128 + lane) : e;
-      // context: lane accumulates dims dq..dq+3 over keys j = 4 i + jg, then the 4 key groups are summed
+      // context: lane accumulates dims dq..dq+3 over keys j = 4 i + jg, then the 4 key groups are summed.  The
+      // probability of key j (held by lane j) reaches row jg through four lane broadcasts (no LDS round trip)
+      auto prob = [&](int i) {
+        const float e0 = lane_bcast(ed, min(4 * i, 63)), e1 = lane_bcast(ed, min(4 * i + 1, 63));
+        const float e2 = lane_bcast(ed, min(4 * i + 2, 63)), e3 = lane_bcast(ed, min(4 * i + 3, 63));
+        return jg == 0 ? e0 : jg == 1 ? e1 : jg == 2 ? e2 : e3;
+      };
 #pragma unroll
       for (int i = 0; i < PRE; ++i)
         if (4 * i < nkeys) {
           const int j = 4 * i + jg;
-          ctx += __shfl(ed, min(j, 63), 64) * pick(j, vcur, vpre[i]);
+          ctx += prob(i) * pick(j, vcur, vpre[i]);
         }
       for (int i = PRE; 4 * i < nkeys; ++i) {
         const int j = 4 * i + jg;
         const f32x4 v4 = j < t0 ? hist(p.vc, j) : vcur;
-        ctx += __shfl(ed, min(j, 63), 64) * pick(j, vcur, v4);
+        ctx += prob(i) * pick(j, vcur, v4);
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        ctx[k] += __shfl_xor(ctx[k], 16, 64);
-        ctx[k] += __shfl_xor(ctx[k], 32, 64);
-      }
+      for (int k = 0; k < 4; ++k) ctx[k] = rows4_sum(ctx[k]);
       ctx /= l;
     }
     if (lane < 16) put_planes(sc, ns, r, dq, ctx);

@@ -99,12 +99,7 @@ __global__ __launch_bounds__(128) void head_kernel(HeadArgs a) {
   // argmax (value, lowest index on ties) within each wave, then across the two waves
   float bv = logit;
   int bi = tid < a.V ? tid : 0x7fffffff;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(bv, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-  }
+  wave_argmax(bv, bi);
   if (lane == 0) { s_red[w] = bv; s_idx[w] = bi; }
   __syncthreads();
   const float mx = fmaxf(s_red[0], s_red[1]);
@@ -189,12 +184,7 @@ __global__ __launch_bounds__(256) void head_wide_kernel(HeadArgs a) {
     lg[v] = logit;
     if (logit > bv) { bv = logit; bi = v; }  // v increases: the first maximum of this thread's subset
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(bv, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-  }
+  wave_argmax(bv, bi);
   if (lane == 0) { s_red[w] = bv; s_idx[w] = bi; }
   __syncthreads();
   if (tid == 0) {
