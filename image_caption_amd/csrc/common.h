@@ -233,6 +233,45 @@ __device__ __forceinline__ f32x8 gelu_erf_fast8(f32x8 v) {
   return 0.5f * v * r;
 }
 
+// GELU for fp16 outputs (the f16 encoder's MLP-1 epilogue): erfc(z) from Abramowitz & Stegun 7.1.26 (five coefficients,
+// |error| <= 1.5e-7 absolute in erf) - one rcp, one exp2, five FMA per value instead of ten: the result differs from
+// the exact GELU by at most 4.2e-7 (fp32 evaluation over [-12, 12]), i.e. at most one fp16 ulp after the store's
+// rounding (2.8 % of values), against the fp16 plane's own 2^-11 relative rounding.  (The bf16x2 paths keep the
+// 1.2e-7-relative form above: their planes carry 16 significand bits.)
+__device__ __forceinline__ float gelu_erf_as(float v) {  // the same operations on one value (bitwise equal)
+  const float z = fabsf(v) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(z, 0.3275911f, 1.f));
+  float y = 1.061405429f;
+  y = fmaf(y, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  y *= t;
+  const float erfc_z = y * __builtin_amdgcn_exp2f((z * z) * -1.44269504088896341f);
+  return 0.5f * v * (v >= 0.f ? 2.f - erfc_z : erfc_z);
+}
+__device__ __forceinline__ f32x8 gelu_erf_as8(f32x8 v) {
+  const f32x8 z = __builtin_elementwise_abs(v) * 0.70710678118654752f;
+  const f32x8 den = __builtin_elementwise_fma(z, (f32x8)0.3275911f, (f32x8)1.f);
+  f32x8 t;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = __builtin_amdgcn_rcpf(den[e]);
+  f32x8 y = 1.061405429f;
+  y = __builtin_elementwise_fma(y, t, (f32x8)-1.453152027f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)1.421413741f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)-0.284496736f);
+  y = __builtin_elementwise_fma(y, t, (f32x8)0.254829592f);
+  y *= t;
+  const f32x8 ex = (z * z) * -1.44269504088896341f;  // -z^2 in log2 units
+  f32x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float erfc_z = y[e] * __builtin_amdgcn_exp2f(ex[e]);
+    r[e] = v[e] >= 0.f ? 2.f - erfc_z : erfc_z;
+  }
+  return 0.5f * v * r;
+}
+
 // int8 two-slice quantisation (the operand form of gemm_i8_kernel): 16-bit fixed point relative to
 // the row maximum, q = rint(v / s) in [-32639, 32639], v1 = (q + 128) >> 8 in [-127, 127],
 // v2 = q - 256 v1 in [-128, 127]; four consecutive values -> one 32-bit word per slice.  Row image

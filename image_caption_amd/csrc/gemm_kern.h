@@ -107,7 +107,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[TM]
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = gelu_erf_fast(acc[i][j][r]);
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = F16 ? gelu_erf_as(acc[i][j][r]) : gelu_erf_fast(acc[i][j][r]);
   } else if (p.epi == EPI_RELU) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -786,7 +786,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
           for (int j = 0; j < TN; j += 2) {
             const f32x4 v0 = acc[i][j] + bj[j], v1 = acc[i][j + 1] + bj[j + 1];
-            const f32x8 g = gelu_erf_fast8((f32x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
+            const f32x8 g = gelu_erf_as8((f32x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
             pk[j] = pack16x4<true>((f32x4){g[0], g[1], g[2], g[3]});
             pk[j + 1] = pack16x4<true>((f32x4){g[4], g[5], g[6], g[7]});
           }
