@@ -683,6 +683,17 @@ hipError_t run_256(const GemmArgs& g, hipStream_t s) {
   // stays ahead (tools/halfk_sweep.sh; round 3, tools/r3_trunk_sweep.sh: still so for the fp16 trunk)
   // ICAP_GEMM_TALL_MIN_K (tools): the smallest K of the two-block form
   static const int tall_min_k = icap_knob("ICAP_GEMM_TALL_MIN_K", 128);
+  // the Grid encoder tail (M = B x 49 = 12544 at B = 256, bf16x2): 64 x 256 tiles of 4 waves, three blocks per CU - its
+  // 196-tile GEMMs (out-proj, FFN-2, projection) otherwise leave a quarter of the CUs idle (round 3, tools/r3_ab.sh +
+  // tools/r3_tail_trace.sh: projection 87.5 -> 76 us, QKV 72 -> 64, out-proj 33 -> 29, FFN-1 87 -> 84, FFN-2 82 -> 71;
+  // at the ViT's M = 50432 the 128-row form stays ahead, round 1)
+  if (tall_min_k && g.K >= tall_min_k && !F16 && !g.cv && g.M <= 16384) {
+    const int nwgq = (g.N / 256) * ((g.M + 63) / 64);
+    constexpr int ldsq = 2 * (2 * 64 * 32 * 2 + 256 * 32 * 2), ldsq1 = 2 * (64 * 32 * 2 + 256 * 32 * 2);
+    if (g.nsplit == 2) hipLaunchKernelGGL((gemm_256_kernel<2, 4, 0, 0, 64, 2, 32, 0, false, EPC>), dim3(nwgq), dim3(256), ldsq, s, g);
+    else hipLaunchKernelGGL((gemm_256_kernel<1, 4, 0, 0, 64, 2, 32, 0, false, EPC>), dim3(nwgq), dim3(256), ldsq1, s, g);
+    return hipGetLastError();
+  }
   if (tall_min_k && g.K >= tall_min_k) {
     const int nwgh = (g.N / 256) * ((g.M + 127) / 128);
     constexpr int ldsh = 2 * (2 * 128 * 32 * 2 + 256 * 32 * 2), ldsh1 = 2 * (128 * 32 * 2 + 256 * 32 * 2);
