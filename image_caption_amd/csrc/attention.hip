@@ -326,8 +326,7 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
         const bool isK = !(mat & 1);
         const int ch = lch ^ (isK ? kswz(row) : vswz(row));
         const bf16_t* src = (isK ? kb : vb) + (mat >= 2 ? lo : 0) + (long)min(key, N - 1) * rs + ch * 8;
-        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
-                                         (LDS_AS void*)(smem + buf * CHUNK + mat * MAT + part * 1024), 16, 0, 0);
+        lds_dma16(src, (LDS_AS void*)(smem + buf * CHUNK + mat * MAT + part * 1024));
       }
     }
   };
@@ -684,8 +683,7 @@ __global__ __launch_bounds__(1024) void cross_attn_mfma_kernel(const bf16_t* __r
         const int g = min(c * CK + key, S - 1);
         const int cs = lane ^ (key & 15);
         const bf16_t* src = mb + (pl ? mem_lo : 0) + (long)g * DM + cs * 8;
-        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
-                                         (LDS_AS void*)(smem + buf * BUF + pl * PLANE + key * 1024), 16, 0, 0);
+        lds_dma16(src, (LDS_AS void*)(smem + buf * BUF + pl * PLANE + key * 1024));
       }
     }
   };
@@ -921,8 +919,7 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
       const int key = wave * 4 + i;
       const int g = min(c * CK + key, S - 1);
       const bf16_t* src = mb + (long)g * DM + (lane ^ (key & 15)) * 8;
-      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)(smem + buf * BUF + key * 1024), 16,
-                                       0, 0);
+      lds_dma16(src, (LDS_AS void*)(smem + buf * BUF + key * 1024));
     }
   };
   auto mma16h = [](f16x8 a, f16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); };

@@ -17,6 +17,21 @@ typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 #define GLOBAL_AS __attribute__((address_space(1)))
 #define LDS_AS __attribute__((address_space(3)))
 
+// LDS DMA of 16 B per lane (global_load_lds_dwordx4: lane l's 16 bytes land at M0 + 16 l) issued from inline asm.
+// hipcc's waitcnt pass books the builtin's LDS write on the LGKM counter too, so behind an in-flight builtin DMA every
+// use of an LDS read waits lgkmcnt(0) - the whole fragment-read pipeline drained before each MFMA group (the
+// persistent fp16 GEMM's k-loop had twelve per k-step).  Issued here the DMA is invisible to that pass: the reads keep
+// counted waits.  Only for kernels whose own inline-asm `s_waitcnt vmcnt` waits order the DMA before its data is read
+// (a compiler-generated fence would not wait for it); extra VMEM operations the compiler does not count only make its
+// own vmcnt waits conservative (in-order retirement).  M0 is saved and restored inside the statement.
+__device__ __forceinline__ void lds_dma16(const void* gsrc, __attribute__((address_space(3))) void* ldst) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+  uint32_t save;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(save)
+               : "v"(gsrc), "s"(l));
+}
+
 __device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 
 __device__ __forceinline__ bf16_t f2bf(float f) {

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(512, 1) void conv_rmw_kernel(GemmArgs p) {
   for (int i = 0; i < IPW_W; ++i) {
     const int ins = wave * IPW_W + i, kb = ins >> 4, r = (ins & 15) * 8 + (lane >> 3);
     const bf16_t* src = p.W + (long)(n0 + r) * p.ldw + kb * 64 + (((lane & 7) ^ (r & 7)) << 3);
-    __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)(wimg + ins * 1024), 16, 0, 0);
+    lds_dma16(src, (LDS_AS void*)(wimg + ins * 1024));
   }
   // row tile rt's A rows (8 rows x 128 B per instruction) and residual rows (4 rows x 256 B) into buffer buf
   auto stage = [&](int rt, int buf) {
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(512, 1) void conv_rmw_kernel(GemmArgs p) {
       const int ins = wave * IPW_A + i, kb = ins / (BM / 8), r = (ins % (BM / 8)) * 8 + (lane >> 3);
       const int row = min(rt * BM + r, M - 1);
       const bf16_t* src = p.A + (long)row * p.lda + kb * 64 + (((lane & 7) ^ (r & 7)) << 3);
-      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)(b0 + ins * 1024), 16, 0, 0);
+      lds_dma16(src, (LDS_AS void*)(b0 + ins * 1024));
     }
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl) {
@@ -69,8 +69,7 @@ __global__ __launch_bounds__(512, 1) void conv_rmw_kernel(GemmArgs p) {
         const int ins = wave * IPW_R + i, r = ins * 4 + (lane >> 4);
         const int row = min(rt * BM + r, M - 1);
         const bf16_t* src = p.res + pl * p.res_lo + (long)row * p.res_ld + n0 + (((lane & 15) ^ (r & 15)) << 3);
-        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src, (LDS_AS void*)(b0 + AIMG + pl * RPL + ins * 1024),
-                                         16, 0, 0);
+        lds_dma16(src, (LDS_AS void*)(b0 + AIMG + pl * RPL + ins * 1024));
       }
     }
   };

@@ -40,7 +40,7 @@ __device__ __forceinline__ void dma_8rows(const char* src, long ld, int i, char*
   const int lane = threadIdx.x & 63;
   const int r = i * 8 + (lane >> 3), pos = lane & 7;
   const char* s = src + (long)r * ld + ((pos ^ ((r >> 1) & 7)) << 4);
-  __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)s, (LDS_AS void*)(dst + i * 1024), 16, 0, 0);
+  lds_dma16(s, (LDS_AS void*)(dst + i * 1024));
 }
 // nrows x 128 B, instructions spread over the 16 waves starting at wave `first` (balance across calls)
 __device__ __forceinline__ void dma_rows(const char* src, long ld, int nrows, char* dst, int first = 0) {
@@ -63,7 +63,7 @@ __device__ __forceinline__ void dma_x(const bf16_t* A, long aL, int ns, int row0
     const int kp = i >> 1, half = i & 1, k64 = kp / ns, pl = kp - k64 * ns;
     const int r = half * 8 + lr, gr = min(row0 + r, rows - 1);
     const char* s = (const char*)(A + pl * aL + (long)gr * ld + k64 * 64) + ((pos ^ ((r >> 1) & 7)) << 4);
-    __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)s, (LDS_AS void*)(sx + kp * 2048 + half * 1024), 16, 0, 0);
+    lds_dma16(s, (LDS_AS void*)(sx + kp * 2048 + half * 1024));
   }
 }
 

@@ -426,14 +426,12 @@ void gemm_256_kernel(GemmArgs p) {
         const bf16_t* src = Ab + i * a_step;
         if (CONV) src = conv_src<CONV>(p, p.A + pl * p.a_lo, cr[CONV ? i : 0], kin + schunk * 8);
         else if (a_tail && m0 + srow + i * RPI >= M) src = Ab + (long)(M - 1 - m0 - srow) * p.lda;
-        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)src,
-                                         (LDS_AS void*)(s0 + pl * OPB + (wave * IPW + i) * 1024), 16, 0, 0);
+        lds_dma16(src, (LDS_AS void*)(s0 + pl * OPB + (wave * IPW + i) * 1024));
       }
     }
 #pragma unroll
     for (int i = 0; i < IPWW; ++i)
-      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(b_base + kin + i * b_step),
-                                       (LDS_AS void*)(s0 + NS * OPB + (wave * IPWW + i) * 1024), 16, 0, 0);
+      lds_dma16(b_base + kin + i * b_step, (LDS_AS void*)(s0 + NS * OPB + (wave * IPWW + i) * 1024));
   };
 
   f32x4 acc[TM][TN];
@@ -614,13 +612,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
     for (int i = 0; i < IPW; ++i) {
       if (BM < 256 && (wave * IPW + i) * 8 >= BM) break;  // (wave-uniform) rows past the tile's A image
       const int row = min(m0 + srow + i * 8, M - 1);
-      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(Ab + (long)row * p.lda),
-                                       (LDS_AS void*)(s0 + (wave * IPW + i) * 1024), 16, 0, 0);
+      lds_dma16(Ab + (long)row * p.lda, (LDS_AS void*)(s0 + (wave * IPW + i) * 1024));
     }
 #pragma unroll
-    for (int i = 0; i < IPW; ++i)
-      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(Wb + (long)i * 8 * p.ldw),
-                                       (LDS_AS void*)(s0 + OPA + (wave * IPW + i) * 1024), 16, 0, 0);
+    for (int i = 0; i < IPW; ++i) lds_dma16(Wb + (long)i * 8 * p.ldw, (LDS_AS void*)(s0 + OPA + (wave * IPW + i) * 1024));
   };
   // SO: the tile's 256 bias values go to LDS slot (tile count & 1) by one DMA instruction of wave 0, issued
   // before the tile's first stage (so the counted waits below never count it) - no registers held across
@@ -629,8 +624,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   auto load_bias = [&](int t, int slot) {
     if (wave == 0 && p.bias) {
       const int n0 = (t - (t / nbn) * nbn) * BN;
-      __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(p.bias + n0 + lane * 4),
-                                       (LDS_AS void*)(sbias + slot * 256), 16, 0, 0);
+      lds_dma16(p.bias + n0 + lane * 4, (LDS_AS void*)(sbias + slot * 256));
     }
   };
 

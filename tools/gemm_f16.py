@@ -12,7 +12,7 @@ import torch
 from image_caption_amd import _lib
 
 TOOLS_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libicap_tools.so")  # tools build (ICAP_* knobs read)
-lib = _lib.load(TOOLS_LIB if os.path.exists(TOOLS_LIB) else None)
+lib = _lib.load(os.environ.get("GEMM_LIB") or (TOOLS_LIB if os.path.exists(TOOLS_LIB) else None))  # GEMM_LIB: A/B of two builds
 dev = torch.device("cuda", 0)
 SHAPES = {"qkv": (2304, 768, 0, 2), "out": (768, 768, 0, 3), "mlp0": (3072, 768, 1, 2), "mlp3": (768, 3072, 0, 3)}
 if os.environ.get("SHAPE_NK"):  # SHAPE_NK=2304,768: one plain GEMM of M = GEMM_M rows (fp16 out, bias, no epilogue op)
