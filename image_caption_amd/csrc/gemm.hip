@@ -193,10 +193,10 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 bool gemm_f16_persistent(const GemmArgs& g) {
-  // tools: ICAP_F16_GEMM 6 = persistent for every fp16 GEMM; ICAP_F16_PRES 0 = the residual GEMMs in the
+  // tools: ICAP_F16_GEMM 6 = persistent for every fp16 GEMM, 7 = gemm_f16r_kernel; ICAP_F16_PRES 0 = the residual GEMMs in the
   // two-block form (out-proj 131 / MLP-2 340 us against 124 / 314 persistent, encoder 15.7 -> 15.0 ms/step)
   static const int form = icap_knob("ICAP_F16_GEMM", 0), pres = icap_knob("ICAP_F16_PRES", 1);
-  const bool common = g.f16 && (form == 0 || form == 6) && !g.addend && !g.rm_group && !g.res && !g.scale && !g.cv &&
+  const bool common = g.f16 && (form == 0 || form == 6 || form == 7) && !g.addend && !g.rm_group && !g.res && !g.scale && !g.cv &&
                       g.batch == 1 && g.nsplit == 1 && g.N % 256 == 0 && g.M >= 256 && g.K >= 128 && g.K % 64 == 0;
   if (!common) return false;
   if (g.out == OUT_SPLIT) return g.c_planes == 1 && (g.epi == EPI_NONE || g.epi == EPI_GELU);

@@ -865,4 +865,212 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   if (SO && p.range_flag && __any(range_bad) && lane == 0) range_flag_set(p.range_flag);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent fp16 encoder GEMM with the A operand two k-steps ahead (round 3; tools build only, ICAP_F16_GEMM=7:
+// correct - 104 GPU tests with it as the product form - but per ViT layer 973-991 us against 979-981 for
+// gemm_f16p_kernel on the same box, tools/r3_lib_ab.sh: the k-loop is not held by the stage's DMA latency).  gemm_f16p_kernel's 2-stage ring keeps
+// ONE 64 KiB stage in flight per CU, so every k-step waits out that stage's whole DMA latency (its timing ablations:
+// the DMA path alone runs as long as the MFMA path alone and the two overlap poorly).  Here the 160 KiB hold three A
+// slots and two W slots: the block's (tile, k-step) sequence is one stream of steps s, and step s issues W(s + 1) and
+// A(s + 2) - up to 96 KiB in flight, and the A rows (row bands from HBM / MALL; W is L2-resident) get two k-steps to
+// land.  Tiles, raster, fragment-read pipeline and epilogues as gemm_f16p_kernel; the bias is read from global
+// memory in the epilogue (no LDS left at 256-row tiles; 1 KiB per tile, L2-resident).
+// Waits at step s: W(s) and A(s) landed; younger in issue order are A(s + 1) (this wave's IPW instructions, if it
+// stages A rows and A(s + 1) exists) and the previous tile's epilogue stores (NSTORE per wave) - a ragged tile (rows
+// >= M not stored) leaves an uncounted number, and the next step waits for everything.  The epilogue's own loads
+// (bias, RES residual) are waited for by the compiler, which retires every older DMA with them (in-order counter).
+constexpr int F16R_LDS_256 = 3 * 256 * 128 + 2 * 256 * 128, F16R_LDS_224 = 3 * 224 * 128 + 2 * 256 * 128;
+template <int MODE, int BMT>
+__global__ __launch_bounds__(512, 1) void gemm_f16r_kernel(GemmArgs p) {
+  constexpr bool SO = MODE == 1, RES = MODE == 2;
+  static_assert(SO || RES, "store-only or residual epilogue");
+  static_assert(BMT == 256 || BMT == 224, "tile rows");
+  constexpr int BM = BMT, BN = 256, KS = 64, NW = 8, WM = BM / 2, WN = 64, TM = WM / 16, TN = 4, XD = 2;
+  constexpr int OPA = BM * KS * 2, OPB = BN * KS * 2;  // bytes per A / W slot
+  constexpr int IPW = OPB / 1024 / NW;                 // 4 DMA instructions per wave per W stage (A: 4 or none)
+  constexpr int NSTORE = SO ? TM * TN / 2 : TM * TN;   // epilogue stores per wave (SO: 16 B per lane)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const sa = smem;            // A slots [3][BM rows][128 B]
+  char* const sw = smem + 3 * OPA;  // W slots [2][256 rows][128 B]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
+  const int xcd = blockIdx.x & 7, q = nwg >> 3, r = nwg & 7;
+  const int xbase = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, xcnt = q + (xcd < r);
+  const int nbx = ((int)gridDim.x - xcd + 7) >> 3, lb = blockIdx.x >> 3;
+  if (lb >= xcnt) return;
+  const int M = p.M, nk = p.K / KS, tend = xbase + xcnt;
+  const int srow = wave * IPW * 8 + (lane >> 3), schunk = (lane & 7) ^ (srow & 7);
+  const bool a_rows = BM == 256 || wave * IPW * 8 < BM;  // (wave-uniform) BM 224: wave 7 stages W rows only
+  const int fr = lane & 15, fq = lane >> 4;
+
+  auto stage_a = [&](int t, int kt, int slot) {
+    if (!a_rows) return;
+    const int m0 = (t / nbn) * BM;
+    const bf16_t* Ab = p.A + kt * KS + schunk * 8;
+    char* d = sa + slot * OPA + wave * IPW * 1024;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) lds_dma16(Ab + (long)min(m0 + srow + i * 8, M - 1) * p.lda, (LDS_AS void*)(d + i * 1024));
+  };
+  auto stage_w = [&](int t, int kt, int slot) {
+    const int n0 = (t - (t / nbn) * nbn) * BN;
+    const bf16_t* Wb = p.W + (long)(n0 + srow) * p.ldw + kt * KS + schunk * 8;
+    char* d = sw + slot * OPB + wave * IPW * 1024;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) lds_dma16(Wb + (long)i * 8 * p.ldw, (LDS_AS void*)(d + i * 1024));
+  };
+  auto adv = [&](int& tt, int& kk) {  // next position of the block's step stream
+    if (++kk == nk) kk = 0, tt += nbx;
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  int t = xbase + lb;
+  int t1 = t, k1 = 0, t2, k2;  // positions of steps s + 1 and s + 2
+  adv(t1, k1);
+  t2 = t1, k2 = k1;
+  adv(t2, k2);
+  stage_a(t, 0, 0);
+  stage_w(t, 0, 0);
+  if (t1 < tend) stage_a(t1, k1, 1);
+  int sA = 0, sW = 0;                    // slots of step s
+  bool st_prev = false, rag_prev = false;  // the previous step ended a tile (counted stores / ragged)
+  bool range_bad = false;
+  for (;;) {
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool a_pend = a_rows && t1 < tend;  // A(s + 1) in flight behind W(s)
+      if (rag_prev) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else if (a_pend && st_prev) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(IPW + NSTORE) : "memory");
+      else if (a_pend) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(IPW) : "memory");
+      else if (st_prev) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      st_prev = rag_prev = false;
+      const char* A0 = sa + sA * OPA;
+      const char* W0 = sw + sW * OPB;
+      const int fo0 = fr * 128 + ((fq ^ (fr & 7)) << 4), fo1 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
+      bf16x8 b2[2][TN], a2[2 * TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b2[0][j] = *(const bf16x8*)(W0 + (wn * WN + j * 16) * 128 + fo0);
+#pragma unroll
+      for (int g = 0; g < XD; ++g) a2[g] = *(const bf16x8*)(A0 + (wm * WM + g * 16) * 128 + fo0);
+      __builtin_amdgcn_sched_barrier(0);
+      // every wave is past step s - 1: its W slot takes W(s + 1), its A slot A(s + 2)
+      if (t1 < tend) stage_w(t1, k1, sW ^ 1);
+      if (t2 < tend) stage_a(t2, k2, sA == 0 ? 2 : sA - 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < 2 * TM; ++g) {
+        const int nx = g + XD;
+        if (nx == TM) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) b2[1][j] = *(const bf16x8*)(W0 + (wn * WN + j * 16) * 128 + fo1);
+        }
+        if (nx < 2 * TM) a2[nx] = *(const bf16x8*)(A0 + (wm * WM + (nx % TM) * 16) * 128 + (nx < TM ? fo0 : fo1));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[g % TM][j] = mma<true>(b2[g / TM][j], a2[g], acc[g % TM][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      sA = sA == 2 ? 0 : sA + 1;
+      sW ^= 1;
+      t1 = t2, k1 = k2;
+      adv(t2, k2);
+    }
+    const int bm = t / nbn, bn = t - bm * nbn, mb = bm * BM + wm * WM, nb = bn * BN + wn * WN;
+    const bool tail = bm * BM + BM > M;  // ragged last row band: rows >= M neither read (RES) nor stored
+    f32x4 bj[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bj[j] = p.bias ? *(const f32x4*)(p.bias + nb + j * 16 + 4 * fq) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    if constexpr (SO) {
+      // as gemm_f16p_kernel's store-only epilogue (straight-line, head-major rows stepped, fp16 range OR)
+      const bool gelu = p.epi == EPI_GELU, hm_step = p.hm_n >= 16;
+      int hq = 0, hr = 0;
+      if (hm_step) {
+        hq = (mb + fr) / p.hm_n;
+        hr = mb + fr - hq * p.hm_n;
+      }
+      uint32_t rbits = 0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int mr = mb + i * 16 + fr;
+        const bool ok = !tail || mr < M;
+        long orow;
+        if (hm_step) {
+          orow = (((long)hq * (p.N / 64) + nb / 64) * p.hm_n + hr) * 64 - nb;
+          hr += 16;
+          if (hr >= p.hm_n) hr -= p.hm_n, ++hq;
+        } else if (p.hm_n) {
+          const int m = min(mr, M - 1);
+          orow = (((long)(m / p.hm_n) * (p.N / 64) + nb / 64) * p.hm_n + m % p.hm_n) * 64 - nb;
+        } else {
+          orow = (long)min(mr, M - 1) * p.ldc;
+        }
+        bf16_t* C = (bf16_t*)p.C + orow + 4 * fq;
+        u32x2 pk[TN];
+        if (gelu) {
+#pragma unroll
+          for (int j = 0; j < TN; j += 2) {
+            const f32x4 v0 = acc[i][j] + bj[j], v1 = acc[i][j + 1] + bj[j + 1];
+            const f32x8 g = gelu_erf_as8((f32x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
+            pk[j] = pack16x4<true>((f32x4){g[0], g[1], g[2], g[3]});
+            pk[j + 1] = pack16x4<true>((f32x4){g[4], g[5], g[6], g[7]});
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) pk[j] = pack16x4<true>(acc[i][j] + bj[j]);
+        }
+        uint32_t rb = 0;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          rb |= ((pk[j][0] & 0x7c007c00u) + 0x04000400u) | ((pk[j][1] & 0x7c007c00u) + 0x04000400u);
+        rbits |= ok ? rb : 0u;
+        const bool odd = fq & 1;
+#pragma unroll
+        for (int j = 0; j < TN; j += 2) {
+          const u32x2 snd = odd ? pk[j] : pk[j + 1];
+          const u32x2 rcv = {xor16_partner(snd[0]), xor16_partner(snd[1])};
+          const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], pk[j + 1][0], pk[j + 1][1]}
+                              : (u32x4){pk[j][0], pk[j][1], rcv[0], rcv[1]};
+          if (ok) *(u32x4*)(C + nb + (odd ? (j + 1) * 16 - 4 : j * 16)) = w;
+        }
+      }
+      if (rbits & 0x80008000u) range_bad = true;
+    } else {
+      float* Cb = (float*)p.C + nb + 4 * fq;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {  // row tiles [4 h2, min(TM, 4 h2 + 4))
+        f32x4 rv[4][TN];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            if (h2 * 4 + i < TM)
+              rv[i][j] = *(const f32x4*)(Cb + (long)min(mb + (h2 * 4 + i) * 16 + fr, M - 1) * p.ldc + j * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (h2 * 4 + i >= TM) break;
+          const int m = mb + (h2 * 4 + i) * 16 + fr;
+          if (tail && m >= M) continue;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) *(f32x4*)(Cb + (long)m * p.ldc + j * 16) = rv[i][j] + (acc[h2 * 4 + i][j] + bj[j]);
+        }
+      }
+    }
+    st_prev = true;
+    rag_prev = tail;
+    t += nbx;
+    if (t >= tend) break;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  if (SO && p.range_flag && __any(range_bad) && lane == 0) range_flag_set(p.range_flag);
+}
+
 }  // namespace

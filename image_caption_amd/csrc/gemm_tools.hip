@@ -423,6 +423,17 @@ bool launch_gemm_256_tools(const GemmArgs& g, hipStream_t s, int cus, hipError_t
     }
     const bool so = gemm_f16_persistent(g), res = g.out == OUT_F32_RESID;
     const dim3 grid(std::min((g.N / 256) * ((g.M + 255) / 256), cus));
+    if (form == 7 && so) {  // the A operand two k-steps ahead (gemm_kern.h; measured equal)
+      if (res) {
+        if (!attr((const void*)gemm_f16r_kernel<2, 224>, F16R_LDS_224)) return true;
+        hipLaunchKernelGGL((gemm_f16r_kernel<2, 224>), dim3(std::min((g.N / 256) * ((g.M + 223) / 224), cus)), dim3(512),
+                           F16R_LDS_224, s, g);
+      } else {
+        if (!attr((const void*)gemm_f16r_kernel<1, 256>, F16R_LDS_256)) return true;
+        hipLaunchKernelGGL((gemm_f16r_kernel<1, 256>), grid, dim3(512), F16R_LDS_256, s, g);
+      }
+      return done();
+    }
     const dim3 grid224(std::min((g.N / 256) * ((g.M + 223) / 224), cus));
     // ICAP_F16P_ABL: gemm_f16p_kernel without its k-loop DMA (1) or without its MFMAs (2) - wrong results,
     // timing only (tools/f16_ablate.sh); 3 / 4 / 5: the compiler's fragment-read order / the read pipeline per
