@@ -1,7 +1,8 @@
 // Device templates of the encoder GEMMs, shared by the product translation unit (gemm.hip) and the tools
 // build's measurement unit (gemm_tools.hip, compiled only with -DICAP_TOOLS): the implicit-conv row helpers,
 // the 256-wide epilogue, gemm_256_kernel and the persistent fp16 gemm_f16p_kernel.  Template parameters that
-// select measured-and-rejected variants (NOMFMA, TS, KSD = 64, ABL) are instantiated only by gemm_tools.hip.
+// select measured-and-rejected variants (NOMFMA, TS, KSD = 64, ABL) and the rejected gemm_f16r_kernel (three A
+// slots) are instantiated only by gemm_tools.hip.
 #pragma once
 #include "common.h"
 #include "kernels.h"
