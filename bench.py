@@ -160,10 +160,12 @@ def main():
                          "of the default, profiles/r01/v16_pipeline_sweep.txt)")
     args = ap.parse_args()
 
-    rank, ws, local = parallel.init()
+    # BENCH_DIST_BACKEND / BENCH_ONE_DEVICE: rehearsal of the N > 1 flow on a one-GPU box (every rank on cuda:0,
+    # gloo collectives; tools/r3_dist_rehearsal.sh) - never set for a measured line
+    rank, ws, local = parallel.init(backend=os.environ.get("BENCH_DIST_BACKEND") or None)
     if ws != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using WORLD_SIZE")
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", 0 if os.environ.get("BENCH_ONE_DEVICE") == "1" else local)
     torch.cuda.set_device(dev)
 
     sd = W.to_torch(W.vit_state_dict(0) if args.model == "vit" else W.grid_state_dict(0))
