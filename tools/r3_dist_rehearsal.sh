@@ -6,6 +6,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r3
 BENCH_DIST_BACKEND=gloo BENCH_ONE_DEVICE=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${N:-2} \
-  --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus ${N:-2} --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline \
-  > gpurun_out/r3/dist${N:-2}.json 2> gpurun_out/r3/dist${N:-2}.err || { tail -30 gpurun_out/r3/dist${N:-2}.err; exit 1; }
-tail -1 gpurun_out/r3/dist${N:-2}.json
+  --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus ${N:-2} --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline ${EXTRA} \
+  > gpurun_out/r3/dist${N:-2}${TAG}.json 2> gpurun_out/r3/dist${N:-2}${TAG}.err || { tail -30 gpurun_out/r3/dist${N:-2}${TAG}.err; exit 1; }
+tail -1 gpurun_out/r3/dist${N:-2}${TAG}.json
