@@ -9,9 +9,9 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 LIB = HERE / "libicap.so"
-SOURCES = ["gemm.hip", "rows.hip", "attention.hip", "head.hip", "beam.hip", "decode.hip", "decstep.hip", "xdec.hip", "trunk.hip", "conv_rmw.hip", "preprocess.hip", "cider.hip", "train.hip", "icap.cpp"]
+SOURCES = ["gemm.hip", "rows.hip", "attention.hip", "head.hip", "beam.hip", "decode.hip", "trunk.hip", "conv_rmw.hip", "preprocess.hip", "cider.hip", "train.hip", "icap.cpp"]
 # measured-and-rejected kernel forms: compiled into the tools build only
-TOOLS_SOURCES = ["gemm_tools.hip"]
+TOOLS_SOURCES = ["gemm_tools.hip", "decstep.hip", "xdec.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-munsafe-fp-atomics"]

@@ -1186,7 +1186,9 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
   }
 }
 
-// ---- persistent decode step (decstep.hip) ----
+// ---- persistent decode steps (decstep.hip, xdec.hip): measured slower than the launch loop, compiled
+// into the tools build only; a product build has neither kernel and icap_set_decode_step refuses modes 1 / 2.
+#ifdef ICAP_TOOLS
 // Whether the decode loop runs as one persistent launch per step: the fused blocks' shapes (d 512, 8 heads,
 // dim_ff 2048), two activation planes, decode positions below 64, the bf16 weights (hi/lo weights keep the unfused
 // launches, except for the dropout sampler as in decoder_layers).
@@ -1279,6 +1281,11 @@ const DecStepArgs* step_args(icap_handle* h, const DecodeBufs& b, int B, int S, 
   return h->step_args[wsi].as<DecStepArgs>();
 }
 
+#else
+bool step_path(const icap_handle*, int, const DropCfg*) { return false; }
+bool xdec_path(const icap_handle*, int, int, int, const DropCfg*) { return false; }
+#endif
+
 void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
                        float* step_logits, const float* uniforms, float* logp, hipStream_t s,
                        const DropCfg* drop = nullptr) {
@@ -1307,6 +1314,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   // Round 2 (fused decode blocks, tools/chains_r2.sh, B = 256): 2 chains 13.25 ms/step of decode, 3 chains of
   // 85 rows 12.73, 4 chains of 64 rows 13.37 - so 3 chains from 80 rows each (B = 128 keeps one chain)
   static const int min_rows = std::max(16, icap_knob("ICAP_DEC_MIN_ROWS", 80));
+#ifdef ICAP_TOOLS
   if (xdec_path(h, B, S, max_len, drop)) {  // one group-persistent launch per step (all layers) + the head
     const size_t st = xdec_state_ints();
     h->step_state[wsi].ensure(st * 4 * (size_t)(max_len - 1));
@@ -1349,8 +1357,6 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
     }
     return;
   }
-  const bool persist = step_path(h, max_len, drop);
-  const int nb = persist ? 1 : std::max(1, std::min(h->dec_branches, B / min_rows));
   if (persist) {  // one persistent launch per step (all layers) + the head
     const DecStepArgs* dargs = step_args(h, b, B, S, max_len, wsi, drop, s);
     const size_t st_ints = dec_step_state_ints(d.n_dec_layers, B);
@@ -1391,6 +1397,9 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
     }
     return;
   }
+#endif
+  const bool persist = step_path(h, max_len, drop);
+  const int nb = persist ? 1 : std::max(1, std::min(h->dec_branches, B / min_rows));
   if (nb > 1) {
     if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventRecord(h->ev_fork, s));
@@ -1480,11 +1489,15 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     }
     DecodeBufs pb = dec_bufs(h, B, B, max_len, S, 0, mode);  // make sure nothing allocates during capture
     if (mode) h->dws[mode].fin.ensure((size_t)B);
+#ifdef ICAP_TOOLS
     if (step_path(h, max_len, dp)) step_args(h, pb, B, S, max_len, mode, dp, s);  // ... nor uploads
     if (xdec_path(h, B, S, max_len, dp)) {
       h->step_state[mode].ensure(xdec_state_ints() * 4 * (size_t)(max_len - 1));
       step_layers(h);
     }
+#else
+    (void)pb;
+#endif
     if (!h->cap_stream) HIPCHK(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(hipStreamSynchronize(s));
     const bool prof = h->prof_on;
@@ -1877,11 +1890,13 @@ int icap_create(const icap_model_desc* desc, void* stream, icap_handle** out) {
       h->t16 = desc->precision == ICAP_PREC_F16 && desc->kind == ICAP_KIND_GRID;
       REQUIRE(desc->dec_weight_planes >= 0 && desc->dec_weight_planes <= 2, "dec_weight_planes must be 0, 1 or 2");
       h->wlo = desc->dec_weight_planes == 2;
+#ifdef ICAP_TOOLS
       {
         const int mode = icap_knob("ICAP_DEC_STEP", 0);
         h->use_step = mode == 1;
         h->use_xdec = mode == 2;
       }
+#endif
       // measured and rejected as the default: MLP-2 fed by the block-scaled GELU output takes
       // 1211 us (two-step fold: 256 VGPRs, 30 spilled) / 646 us (per-step fold, 64-column blocks) against
       // 467 us for the bf16x2 form
@@ -2167,6 +2182,9 @@ int icap_set_decode_step(icap_handle* h, int mode) {
   return guarded([&] {
     REQUIRE(h, "null handle");
     REQUIRE(mode >= 0 && mode <= 2, "decode step mode must be 0, 1 or 2");
+#ifndef ICAP_TOOLS
+    REQUIRE(mode == 0, "decode step modes 1 / 2 (the persistent steps, measured slower) exist in the tools build only");
+#endif
     if (h->use_step != (mode == 1) || h->use_xdec != (mode == 2))
       for (DecodeGraph& g : h->dg) g.reset();  // the captured loops follow the mode
     h->use_step = mode == 1;

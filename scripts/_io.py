@@ -72,10 +72,30 @@ def preprocess_to_device(image_paths, mode: str, device, image_size: int = 224) 
     return torch.stack([preprocess(p, mode, image_size) for p in image_paths])
 
 
+def _numpy_safe_globals() -> list:
+    """The numpy names a reference checkpoint pickles besides tensors: its `scores` / `loss` / `cider` values and the
+    LR scheduler's `best` are numpy scalars (pycocoevalcap returns numpy floats; train_vit_transformer.py:413-423,
+    train_*_scst_optimized.py:509-520).  Scalars reduce to multiarray.scalar(dtype, bytes) and dtypes to
+    numpy.dtype(str, ...): plain data constructors, nothing that runs code from the file.  Checkpoints written under
+    numpy 1.x name the module numpy.core (the reference's own loader shims numpy._core for the other direction,
+    scripts/inference_vit_transformer.py:37-42), so both spellings are allowlisted."""
+    import numpy as np
+
+    core = np._core if hasattr(np, "_core") else np.core
+    objs = [core.multiarray.scalar, np.dtype, np.ndarray, core.multiarray._reconstruct]
+    out = list(objs)
+    for mod in ("numpy.core.multiarray", "numpy._core.multiarray"):
+        out += [(core.multiarray.scalar, f"{mod}.scalar"), (core.multiarray._reconstruct, f"{mod}._reconstruct")]
+    out += [type(np.dtype(t)) for t in ("f2", "f4", "f8", "i1", "i2", "i4", "i8", "u1", "b1")]
+    return out
+
+
 def load_checkpoint(path: str, device):
-    """torch.load with weights_only=True (no unpickling of arbitrary objects)."""
+    """torch.load with weights_only=True (no unpickling of arbitrary objects), with numpy scalars / dtypes / arrays
+    allowlisted so the reference's training checkpoints (numpy-float scores and losses) load as they are."""
     try:
-        return torch.load(path, map_location=device, weights_only=True)
+        with torch.serialization.safe_globals(_numpy_safe_globals()):
+            return torch.load(path, map_location=device, weights_only=True)
     except Exception as e:
         raise RuntimeError(f"{path}: cannot be loaded with weights_only=True ({e}); re-save it as a plain "
                            "{'model_state_dict': ..., 'config': {...}} dict of tensors and primitives") from e

@@ -256,6 +256,132 @@ def make_nomask(ref, out):
     out["nomask_b1"] = len(ids)
 
 
+SCRIPT_END_BIAS = {"vit": 1.6, "grid": 1.9}  # <end> logit offsets of the entry-script fixtures (varied lengths)
+
+
+def make_scripts(ref, out):
+    # The drop-in entry scripts, run through the reference's OWN script functions on PNG files:
+    #  * scripts/inference_vit_transformer.py: generate_caption (:88-129, greedy and beam_search, max_len 50)
+    #    and batch_generate_captions (:158-180, one generate_caption per image);
+    #  * scripts/inference_grid_transformer.py: generate_caption (:52-76, greedy and beam_search, beam 5);
+    #  * scripts/inference.py: generate_caption (:60-101, the no-mask loop) with the real vocabulary;
+    #  * utils/scst_loss.py: SCSTLoss._decode_captions (:256-269) and get_reference_captions (:328-354) on a
+    #    crafted id matrix (<end> mid-row, <pad> / <start> inside, unknown-free).
+    # The scripts' preprocess_image is torchvision (absent): for the call it is replaced by the oracle's
+    # Pillow-pinned restatement (oracle/preprocess.py) of the same transforms, applied to the decoded PNG.
+    # Images: tests/golden/inputs.script_images (seeded uint8 arrays of several sizes, PNG is lossless).
+    # Vocabulary: data/vocab.json (identical to the reference's data/vocab.json).  Weights: the seed-0
+    # state dicts with the <end> logit raised by SCRIPT_END_BIAS.
+    import json
+    import tempfile
+
+    from oracle import captioner as O
+    from oracle import preprocess as OP
+    from tests.golden.inputs import script_images, write_pngs
+
+    vocab = json.load(open(os.path.join(ROOT, "data", "vocab.json"), encoding="utf-8"))
+    arrays = script_images()
+    tmp = tempfile.mkdtemp()
+    paths = write_pngs(arrays, tmp)
+
+    def patched(mod, mode):
+        def preprocess_image(image_path, image_size=224):
+            i = paths.index(image_path)
+            return torch.from_numpy(OP.preprocess(arrays[i], mode, image_size))[None]
+        mod.preprocess_image = preprocess_image
+        return mod
+
+    def biased(sd, kind):
+        sd = dict(sd)
+        b = sd["decoder.fc_out.bias"].clone()
+        b[W.END_TOKEN] += SCRIPT_END_BIAS[kind]
+        sd["decoder.fc_out.bias"] = b
+        return sd
+
+    evalm = _module("utils.eval_metrics", COCOScoreEvaluator=object)
+    vsd = biased(W.to_torch(W.vit_state_dict(0)), "vit")
+    vmodel = ref_vit_model(ref, vsd)
+    vit_s = patched(load_ref("scripts/inference_vit_transformer.py", "ref_inference_vit",
+                             {"models.vit_transformer_model": ref, "utils.eval_metrics": evalm}), "crop")
+    res = {}
+    with torch.no_grad():
+        greedy = [vit_s.generate_caption(vmodel, p, vocab, "cpu", "greedy") for p in paths]
+        res["vit_batch"] = vit_s.batch_generate_captions(vmodel, paths, vocab, "cpu", "greedy")
+        beam = vit_s.generate_caption(vmodel, paths[0], vocab, "cpu", "beam_search")
+    res["vit_greedy_caps"] = [c for c, _ in greedy]
+    res["vit_greedy_ids"] = [i for _, i in greedy]
+    res["vit_beam_cap"], res["vit_beam_ids"] = beam
+    # the oracle's top-2 margin along each greedy caption (teacher-forced on the reference's ids)
+    imgs = torch.stack([torch.from_numpy(OP.preprocess(a, "crop")) for a in arrays])
+    with torch.no_grad():
+        vmem = O.vit_encode(vsd, imgs)
+    res["vit_greedy_margin"] = [float(O.top2_margin(O.teacher_forced_logits(vsd, vmem[i:i + 1],
+                                      torch.tensor([ids]))).min()) for i, ids in enumerate(res["vit_greedy_ids"])]
+    res["vit_beam_margin"] = O.beam_from_memory(vsd, vmem[:1], W.START_TOKEN, W.END_TOKEN, 50, 5, False,
+                                                return_margins=True)[1]
+
+    gmod = load_ref("models/grid_transformer_model.py", "ref_grid_transformer_model")
+    gsd = biased(W.to_torch(W.grid_state_dict(0)), "grid")
+    gmodel = gmod.GridTransformerCaptioning(W.VOCAB_SIZE, pretrained_cnn=False)
+    gmodel.load_state_dict(gsd, strict=True)
+    gmodel.eval()
+    grid_s = patched(load_ref("scripts/inference_grid_transformer.py", "ref_inference_grid",
+                              {"models.grid_transformer_model": gmod, "utils.eval_metrics": evalm}), "square")
+    with torch.no_grad():
+        gg = [grid_s.generate_caption(gmodel, p, vocab, "cpu", "greedy") for p in paths]
+        gb = grid_s.generate_caption(gmodel, paths[1], vocab, "cpu", "beam_search", beam_size=5)
+    res["grid_greedy_caps"] = [c for c, _ in gg]
+    res["grid_greedy_ids"] = [i for _, i in gg]
+    res["grid_beam_cap"], res["grid_beam_ids"] = gb
+    gimgs = torch.stack([torch.from_numpy(OP.preprocess(a, "square")) for a in arrays])
+    with torch.no_grad():
+        gmem = O.grid_encode(gsd, gimgs)
+    res["grid_greedy_margin"] = [float(O.top2_margin(O.teacher_forced_logits(gsd, gmem[i:i + 1],
+                                       torch.tensor([ids]))).min()) for i, ids in enumerate(res["grid_greedy_ids"])]
+    res["grid_beam_margin"] = O.beam_from_memory(gsd, gmem[1:2], W.START_TOKEN, W.END_TOKEN, 50, 5, True,
+                                                 return_margins=True)[1]
+
+    inf = load_ref("scripts/inference.py", "ref_inference", {"models.vit_transformer_model": ref})
+    sq = torch.stack([torch.from_numpy(OP.preprocess(a, "square")) for a in arrays])
+    with torch.no_grad():
+        res["nomask_caps"] = [inf.generate_caption(vmodel, sq[i], vocab, torch.device("cpu")) for i in range(len(arrays))]
+        # the oracle's top-2 margin at every step of the no-mask loop, along the reference's words
+        smem = O.vit_encode(vsd, sq)
+        res["nomask_margin"] = []
+        for i, cap in enumerate(res["nomask_caps"]):
+            ids, m = [W.START_TOKEN], float("inf")
+            for w in cap.split() + [None]:
+                lg = O.decoder_forward(vsd, torch.tensor([ids]), smem[i:i + 1], causal=False)[:, -1, :]
+                m = min(m, float(O.top2_margin(lg)))
+                if w is not None:
+                    ids.append(vocab[w])
+            res["nomask_margin"].append(m)
+
+    # detokenize on a crafted id matrix: rows with <end> mid-row, <pad> and <start> inside, no <end> at all
+    rng = np.random.Generator(np.random.PCG64(5))
+    crafted = rng.integers(1, 106, size=(6, 12)).astype(np.int64)
+    crafted[0, 5] = W.END_TOKEN
+    crafted[1, 0], crafted[1, 3], crafted[1, 7] = W.START_TOKEN, W.PAD_TOKEN, W.END_TOKEN
+    crafted[2, 0] = W.END_TOKEN
+    crafted[3, :] = W.PAD_TOKEN
+    crafted[4, 2], crafted[4, 4] = W.START_TOKEN, W.PAD_TOKEN  # row 4: no <end>
+    crafted[5, 11] = W.END_TOKEN
+    scst = load_ref("utils/scst_loss.py", "ref_scst_loss")
+    idx2word = {i: w for w, i in vocab.items()}
+    res["detok_ids"] = crafted.tolist()
+    res["detok_scst"] = scst.SCSTLoss()._decode_captions(torch.from_numpy(crafted), idx2word, W.END_TOKEN,
+                                                         W.PAD_TOKEN, W.START_TOKEN)
+    res["detok_refs"] = scst.get_reference_captions(torch.from_numpy(crafted), vocab)
+    res["end_bias"] = SCRIPT_END_BIAS
+    with open(os.path.join(HERE, "scripts.json"), "w", encoding="utf-8") as f:
+        json.dump(res, f, ensure_ascii=False, indent=1)
+    for p in paths:
+        os.remove(p)
+    os.rmdir(tmp)
+    out["scripts"] = (len(paths), [len(i) for i in res["vit_greedy_ids"]], [len(i) for i in res["grid_greedy_ids"]],
+                      [round(m, 5) for m in res["vit_greedy_margin"] + res["grid_greedy_margin"]])
+
+
 def make_grid(out):
     # (iv) Grid: the reference's OWN GridTransformerCaptioning (trunk = the torchvision-named restatement)
     # generate(greedy) at B = 4, its trunk features (B, 2048, 7, 7) and memory, teacher-forced logits of
@@ -318,6 +444,8 @@ def main():
         make_sample(ref, out)
     elif only == "nomask":
         make_nomask(ref, out)
+    elif only == "scripts":
+        make_scripts(ref, out)
     elif only is not None:
         raise SystemExit(f"unknown fixture {only!r}")
     if only is not None:
@@ -355,6 +483,7 @@ def main():
     make_grid(out)
     make_beam(ref, sd, imgs, out)
     make_forward(ref, out)
+    make_scripts(ref, out)
     for k, v in out.items():
         print(k, tuple(v) if hasattr(v, "__len__") else v)
 

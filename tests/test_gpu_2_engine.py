@@ -91,6 +91,13 @@ def test_pipeline_matches_sequential(cuda, vit_sd, B):
         assert torch.equal(a.cpu(), apply_stop_rule(b.long(), 108))
 
 
+def _tools_only():
+    from image_caption_amd import _lib
+
+    if not _lib.load().icap_tools_build():
+        pytest.skip("measured-and-rejected decode steps (decstep.hip / xdec.hip): tools build only (-DICAP_TOOLS)")
+
+
 @pytest.mark.parametrize("kind,B,S", [("vit", 256, 196), ("vit", 37, 196), ("grid", 64, 49)])
 def test_persistent_decode_step_matches_launch_loop(cuda, vit_sd, kind, B, S):
     """The persistent decode step (one launch per step running every layer as dependency-ordered tasks,
@@ -98,6 +105,7 @@ def test_persistent_decode_step_matches_launch_loop(cuda, vit_sd, kind, B, S):
     within 1e-4, sampled ids / log-probs with train-mode dropout
     likewise (measured 2.4e-5: 64- instead of 32-key cross-attention chunks and the LayerNorm sums' order; the
     oracle bar is 1e-3); graph capture and replay included (three calls each), a partial last 16-row tile (B = 37)."""
+    _tools_only()
     from image_caption_amd.engine import Engine
 
     sd = vit_sd if kind == "vit" else W.to_torch(W.grid_state_dict(0))
@@ -128,6 +136,7 @@ def test_group_decode_step_matches_launch_loop(cuda, vit_sd, kind, B, S):
     memory: greedy ids identical and step logits within 1e-4 (the residual sums run in another order), sampled ids
     identical and log-probs within 1e-4; graph capture and replay included (three calls each), partial groups
     (B = 37: 5 rows per group, the last group 2), the Grid memory length, the SCST per-rank batch (B = 128)."""
+    _tools_only()
     from image_caption_amd.engine import Engine
 
     sd = vit_sd if kind == "vit" else W.to_torch(W.grid_state_dict(0))

@@ -76,6 +76,22 @@ def test_product_build_refuses_measurement_knobs(monkeypatch):
     assert b"ICAP_I8_NOMFMA" in lib.icap_last_error() and b"tools build" in lib.icap_last_error()
 
 
+def test_product_build_ships_only_shipped_forms():
+    """The measured-and-rejected kernel forms (gemm_tools.hip, the persistent decode steps decstep.hip / xdec.hip) are
+    compiled into the tools build only: the product source list does not hold them and the product library's code
+    object has none of their kernels."""
+    from image_caption_amd import _lib, build
+
+    for src in ("gemm_tools.hip", "decstep.hip", "xdec.hip"):
+        assert src not in build.SOURCES and src in build.TOOLS_SOURCES
+    lib = _lib.load()
+    if lib.icap_tools_build():
+        pytest.skip("tools build")
+    blob = build.LIB.read_bytes()
+    for kernel in (b"dec_step_kernel", b"xdec_kernel", b"gemm_f16q_kernel", b"gemm_8ph_kernel"):
+        assert kernel not in blob, kernel
+
+
 def test_dropin_vit_model_state_dict_and_greedy():
     from models.vit_transformer_model import build_model
 
