@@ -154,6 +154,9 @@ def main():
     ap.add_argument("--torch-trunk", action="store_true", help="grid: ResNet trunk via PyTorch/MIOpen fp32")
     ap.add_argument("--mode", default="greedy", choices=["greedy", "scst", "beam"])
     ap.add_argument("--beam", type=int, default=5, help="beam width of --mode beam")
+    ap.add_argument("--fp32-weights", action="store_true",
+                    help="weights NOT rounded to bf16 (a real fp32 checkpoint): the engine packs the decoder's GEMM weights "
+                         "as hi/lo bf16 pairs and decodes with the unfused launches (config.dec_weight_planes = 2)")
     ap.add_argument("--pipeline", action="store_true",
                     help="greedy: overlap the encode of step i+1 with the decode of step i on two streams "
                          "(image_caption_amd/pipeline.py; measured +2-4 %% with ICAP_DEC_BRANCHES=1, within noise "
@@ -168,7 +171,8 @@ def main():
     dev = torch.device("cuda", 0 if os.environ.get("BENCH_ONE_DEVICE") == "1" else local)
     torch.cuda.set_device(dev)
 
-    sd = W.to_torch(W.vit_state_dict(0) if args.model == "vit" else W.grid_state_dict(0))
+    exact = not args.fp32_weights
+    sd = W.to_torch(W.vit_state_dict(0, bf16_exact=exact) if args.model == "vit" else W.grid_state_dict(0, bf16_exact=exact))
     eng = Engine(sd, args.model, {}, precision=args.precision, device=dev)
     trunk = None
     if args.model == "grid" and args.torch_trunk:
@@ -390,13 +394,23 @@ def main():
                        "per_gpu_batch": B, "global_batch": total, "max_len": L, "precision": args.precision,
                        "decode_steps": L - 1, "output_len": int(out.shape[1]) if args.mode == "greedy" else None,
                        "parallelism": f"dp{ws}",
-                       "pipelined": pipe is not None},
+                       "pipelined": pipe is not None,
+                       # 1: bf16-exact decoder weights (the seeded synthetic weights), fused decode blocks; 2: hi/lo pairs
+                       # (--fp32-weights, a real fp32 checkpoint), unfused decode launches
+                       "dec_weight_planes": eng.dec_weight_planes},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if phases is not None:
             line["roofline"]["phases"] = phases
         if stop_check is not None:
             line["config"]["multi_gpu_check"] = stop_check
+        if os.environ.get("BENCH_DIST_BACKEND") or os.environ.get("BENCH_ONE_DEVICE") == "1":
+            # a rehearsal of the N > 1 flow with every rank on one GPU: not a measurement of N GPUs
+            line["rehearsal"] = True
+            line["physical_devices"] = 1 if os.environ.get("BENCH_ONE_DEVICE") == "1" else None
+            line["rehearsal_value"] = line["value"]
+            line["value"] = None
+            line["metric"] = "REHEARSAL (ranks share one GPU, not a measurement): " + line["metric"]
         print(json.dumps(line), flush=True)
     if ws > 1:
         dist.barrier()

@@ -32,6 +32,24 @@ __device__ __forceinline__ void lds_dma16(const void* gsrc, __attribute__((addre
                : "v"(gsrc), "s"(l));
 }
 
+// The same DMA as a buffer load: source = the resource's base + voff (per lane) + soff (wave-uniform SGPR).  The
+// per-lane address is one 32-bit VGPR, so a stage's pieces share it and differ by soff (hipBLASLt's form), and a lane
+// whose voff is at or past the resource's byte count (num_records; soff is not part of the range check) reads zeros.
+typedef int32_t i32x4r __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4r buf_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return (i32x4r){(int32_t)(uint32_t)a, (int32_t)(uint32_t)(a >> 32), (int32_t)bytes, 0x00020000};  // gfx9 raw buffer
+}
+__device__ __forceinline__ void lds_dma_buf16(i32x4r rsrc, uint32_t voff, uint32_t soff,
+                                              __attribute__((address_space(3))) void* ldst) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+  const uint32_t so = __builtin_amdgcn_readfirstlane(soff);  // (uniform by contract; the asm needs an SGPR)
+  uint32_t save;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(save)
+               : "v"(voff), "s"(rsrc), "s"(l), "s"(so));
+}
+
 __device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 
 __device__ __forceinline__ bf16_t f2bf(float f) {

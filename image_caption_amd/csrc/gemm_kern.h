@@ -867,6 +867,285 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Persistent fp16 encoder GEMM, one wave per SIMD (round 4): the 256 x 256 tile as 4 waves (2 x 2), each a 128 x 128
+// wave tile = 8 x 8 MFMA 16x16 tiles, 256 fp32 accumulators per lane in AGPRs (1 wave per SIMD owns the whole
+// 512-register file).  This is the shape of hipBLASLt's own gfx950 kernel for these GEMMs
+// (Custom_Cijk_Alik_Bljk_HHS_BH_MT256x256x64_MI16x16x1: 256 threads; per wave and 64-deep k-step 128 MFMA,
+// 32 ds_read_b128, 16 LDS-DMA pieces and one barrier - read from its disassembly).  Against gemm_f16p_kernel (8 waves
+// of 128 x 64) the CU reads 128 KiB of fragments from LDS per k-step instead of 192 KiB for the same 512 MFMAs (every
+// fragment feeds 8 MFMAs), and each SIMD's matrix pipe is fed by ONE wave's stream.
+// Kept from gemm_f16p_kernel: the XCD raster, 64-deep full-line stages (chunk c of row r at c ^ (r & 7)) in a 2-stage
+// ring, the bias slot, the counted tile seams.  A stage is 16 DMA pieces per wave (8 A + 8 W); DI = 1 issues them one
+// per 8-MFMA group, DI = 0 in one burst behind the k-step's first fragment reads.
+// Register discipline (all 256 AGPRs hold accumulators, so the compiler has no room to re-assign them): the MFMAs
+// update their accumulator in place from inline asm ("+a"), the k-loop is one do-while body (no peeled copies, no
+// zero-trip path), the epilogue reads each accumulator through an opaque copy where it is used, and every epilogue
+// load / store is a buffer operation on a 32-bit offset (rows >= M: loads return zeros, stores are dropped by the
+// resource's range check), so the epilogue has no per-element branches and issues exactly NSTORE stores per tile.
+// EP (store-only modes, MODE 1): 0 = + bias, 1 = + bias then GELU, 2 = + bias into head-major planes (the ViT QKV:
+// [image][q|k|v x head][token][64], hm_n tokens per image; a wave tile spans two heads).  MODE 2 = residual (C += acc
+// + bias, fp32).  BMT = 224 (MODE 2 only): wave tiles 112 x 128, wave 3 stages 4 A pieces.
+// acc += W-fragment x A-fragment (v_mfma_f32_16x16x32_f16), the accumulator tied in place to an AGPR tuple.  A chain of
+// MFMAs on one accumulator needs no wait states; the epilogue's first accumulator read is behind explicit s_nops.
+__device__ __forceinline__ void mfma16_f16_acc(f32x4& acc, bf16x8 a, bf16x8 b) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// An accumulator's value in VGPRs at this point of the epilogue.  The empty "+a" statement re-defines the accumulator in
+// its AGPR here, so the AGPR -> VGPR copy cannot be hoisted above it: without it the compiler copies every accumulator
+// to VGPRs right at the k-loop exit (~250 v_accvgpr_read at once, then the epilogue spills).
+__device__ __forceinline__ f32x4 acc_v(f32x4& a) {
+  asm volatile("" : "+a"(a));
+  f32x4 v = a;
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+template <int MODE, int EP = 0, int DI = 1, int BMT = 256>
+__global__ __launch_bounds__(256, 1) void gemm_f16w_kernel(GemmArgs p) {
+  constexpr bool SO = MODE == 1, RES = MODE == 2;
+  static_assert(SO || RES, "store-only or residual epilogue");
+  static_assert(BMT == 256 || (RES && BMT == 224), "224-row tiles only for the residual form (no counted waits)");
+  constexpr int BM = BMT, BN = 256, KS = 64, NW = 4, WM = BM / 2, WN = 128, TM = WM / 16, TN = WN / 16, XD = 2;
+  constexpr int OPA = BM * KS * 2, OPB = BN * KS * 2, STAGE = OPA + OPB;
+  constexpr int IPW = OPB / 1024 / NW;  // 8 DMA pieces per wave per operand
+  constexpr int PER_STAGE = 2 * IPW;    // 16 per wave per stage (BM 256)
+  constexpr int NSTORE = TM * TN / 2;   // SO: 16-byte stores per wave per tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // wave-uniform values in SGPRs (the divergence analysis cannot see that threadIdx.x >> 6 is uniform)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
+  const int xcd = blockIdx.x & 7, q = nwg >> 3, r = nwg & 7;
+  const int xbase = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, xcnt = q + (xcd < r);
+  const int nbx = ((int)gridDim.x - xcd + 7) >> 3, lb = blockIdx.x >> 3;
+  if (lb >= xcnt) return;
+  const int M = p.M, nk = p.K / KS;
+  const int srow = wave * IPW * 8 + (lane >> 3), schunk = (lane & 7) ^ (srow & 7);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // stage pieces: one per-lane 32-bit offset per operand (A: this lane's row of the staged tile; W: fixed), the piece's
+  // row step and the k-step in the wave-uniform soffset; A rows >= M read zeros (past the resource's byte count)
+  const i32x4r ra = buf_rsrc(p.A, (uint32_t)((long)M * p.lda * 2)), rw = buf_rsrc(p.W, (uint32_t)((long)p.N * p.ldw * 2));
+  const uint32_t vw = (uint32_t)((srow * p.ldw + schunk * 8) * 2);
+  struct Src {
+    uint32_t va;  // this lane's A offset (piece 0) in the staged tile
+    uint32_t sw;  // W: the staged tile's first row + k-step byte offset
+    uint32_t sk;  // A: k-step byte offset
+  };
+  auto src = [&](int t, int kt) -> Src {
+    const int bm = t / nbn, bn = t - bm * nbn;
+    return {(uint32_t)(((bm * BM + srow) * p.lda + schunk * 8) * 2), (uint32_t)((bn * BN) * p.ldw * 2 + kt * KS * 2),
+            (uint32_t)(kt * KS * 2)};
+  };
+  auto piece = [&](const Src& sc, int buf, int i) {
+    char* s0 = smem + buf * STAGE;
+    if (i < IPW) {
+      if (BM < 256 && (wave * IPW + i) * 8 >= BM) return;  // (wave-uniform) rows past the tile's A image
+      lds_dma_buf16(ra, sc.va + (uint32_t)(i * 16 * p.lda), sc.sk, (LDS_AS void*)(s0 + (wave * IPW + i) * 1024));
+    } else {
+      const int j = i - IPW;
+      lds_dma_buf16(rw, vw, sc.sw + (uint32_t)(j * 16 * p.ldw), (LDS_AS void*)(s0 + OPA + (wave * IPW + j) * 1024));
+    }
+  };
+  auto stage = [&](int t, int kt, int buf) {
+    const Src sc = src(t, kt);
+#pragma unroll
+    for (int i = 0; i < PER_STAGE; ++i) piece(sc, buf, i);
+  };
+  float* sbias = (float*)(smem + 2 * STAGE);
+  auto load_bias = [&](int t, int slot) {
+    if (wave == 0 && p.bias) {
+      const int n0 = (t - (t / nbn) * nbn) * BN;
+      lds_dma16(p.bias + n0 + lane * 4, (LDS_AS void*)(sbias + slot * 256));
+    }
+  };
+  // epilogue buffer resources: rows >= M (ragged last band) fall past the byte count
+  const long cbytes = EP == 2 ? (long)M * p.N * 2 : (long)M * p.ldc * (RES ? 4 : 2);  // (the launcher keeps it < 2^31)
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, (int)cbytes, 0x00020000);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  int t = xbase + lb, step = 0, tcount = 0;
+  load_bias(t, 0);
+  stage(t, 0, 0);
+  bool seam = false;       // this tile's stages 0 and 1 were issued before the previous tile's epilogue stores
+  bool range_bad = false;  // SO: some stored fp16 value is not finite
+  for (;;) {
+    const int tn = t + nbx < xbase + xcnt ? t + nbx : -1;
+    int kt = 0;
+#pragma clang loop unroll(disable)
+    do {
+      if (SO && seam && kt == 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE + NSTORE) : "memory");
+      else if (SO && seam && kt == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+      else if (RES && seam && kt == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      int st_t = -1, st_kt = 0;
+      if (seam && kt == 0) {
+        // stage 1 of this tile is already in flight
+      } else if (kt + 1 < nk) {
+        st_t = t, st_kt = kt + 1;
+      } else if (tn >= 0) {
+        load_bias(tn, (tcount + 1) & 1);
+        st_t = tn;
+      }
+      st_t = __builtin_amdgcn_readfirstlane(st_t);
+      const Src sc = src(st_t >= 0 ? st_t : t, st_kt);
+      const int sbuf = (step + 1) & 1;
+      const char* s0 = smem + (step & 1) * STAGE;
+      const int fo0 = fr * 128 + ((fq ^ (fr & 7)) << 4), fo1 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
+      bf16x8 b2[2][TN], a2[2 * TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b2[0][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo0);
+#pragma unroll
+      for (int g = 0; g < XD; ++g) a2[g] = *(const bf16x8*)(s0 + (wm * WM + g * 16) * 128 + fo0);
+      if (!DI && st_t >= 0) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < PER_STAGE; ++i) piece(sc, sbuf, i);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < 2 * TM; ++g) {
+        const int nx = g + XD;
+        if (nx == TM) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) b2[1][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo1);
+        }
+        if (nx < 2 * TM) a2[nx] = *(const bf16x8*)(s0 + (wm * WM + (nx % TM) * 16) * 128 + (nx < TM ? fo0 : fo1));
+        if (DI && st_t >= 0) {  // 16 pieces over 2 TM groups (TM 7: the last two groups take two)
+          constexpr int EXTRA = PER_STAGE - 2 * TM;
+          piece(sc, sbuf, g);
+          if (EXTRA > 0 && g >= 2 * TM - EXTRA) piece(sc, sbuf, g + EXTRA);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma16_f16_acc(acc[g % TM][j], b2[g / TM][j], a2[g]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      ++step;
+    } while (++kt < nk);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");  // XDL MFMA write -> v_accvgpr_read (<= 18 states)
+    const int bm = t / nbn, bn = t - bm * nbn, mb = bm * BM + wm * WM, nb = bn * BN + wn * WN;
+    const float* bl = sbias + (tcount & 1) * 256 + wn * WN + 4 * fq;  // re-read from LDS where used
+    if constexpr (SO) {
+      // every wave is done reading the last stage's buffer: stage 1 of the next tile into it.  Unconditional (after the
+      // last tile: a re-read of this tile's stage 1 that nothing reads), so no branch separates the k-loop from the
+      // epilogue - the accumulator reads then stay in the epilogue's row-tile blocks instead of all being hoisted to
+      // the loop exit
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      stage(tn >= 0 ? tn : t, 1, (step + 1) & 1);
+      // byte offset of (row tile i, column tile j = 0) for this lane; head-major: columns 64..127 of the wave tile are
+      // the next head, hm_n * 64 elements further
+      int hq = 0, hr = 0;
+      if (EP == 2) {
+        hq = (mb + fr) / p.hm_n;
+        hr = mb + fr - hq * p.hm_n;
+      }
+      const uint32_t head2 = EP == 2 ? (uint32_t)(p.hm_n * 64 - 64) * 2 : 0;
+      const bool odd = fq & 1;
+      uint32_t rbits = 0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t orow;  // element offset of column nb in this lane's row
+        if (EP == 2) {
+          orow = (uint32_t)(((hq * (p.N / 64) + nb / 64) * p.hm_n + hr) * 64);
+          hr += 16;
+          if (hr >= p.hm_n) hr -= p.hm_n, ++hq;
+        } else {
+          orow = (uint32_t)((mb + i * 16 + fr) * p.ldc + nb);
+        }
+        const uint32_t ob = (orow + 4 * fq) * 2;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {  // the row tile in two halves of 4 column tiles (one 64-column head each)
+          u32x2 pk[4];
+          f32x4 av[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[j] = acc_v(acc[i][hh * 4 + j]) + *(const f32x4*)(bl + (hh * 4 + j) * 16);
+          if (EP == 1) {
+#pragma unroll
+            for (int j = 0; j < 4; j += 2) {
+              const f32x8 gv = gelu_erf_as8((f32x8){av[j][0], av[j][1], av[j][2], av[j][3], av[j + 1][0], av[j + 1][1],
+                                                     av[j + 1][2], av[j + 1][3]});
+              pk[j] = pack16x4<true>((f32x4){gv[0], gv[1], gv[2], gv[3]});
+              pk[j + 1] = pack16x4<true>((f32x4){gv[4], gv[5], gv[6], gv[7]});
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pk[j] = pack16x4<true>(av[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            rbits |= ((pk[j][0] & 0x7c007c00u) + 0x04000400u) | ((pk[j][1] & 0x7c007c00u) + 0x04000400u);
+#pragma unroll
+          for (int j = 0; j < 4; j += 2) {
+            // lanes fq (even) and fq + 1 hold columns 4 fq .. 4 fq + 7 of tiles j and j + 1: the even lane stores tile j's
+            // 8 columns, the odd lane tile j + 1's (the partner is 16 lanes away, same row)
+            const u32x2 snd = odd ? pk[j] : pk[j + 1];
+            const u32x2 rcv = {xor16_partner(snd[0]), xor16_partner(snd[1])};
+            const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], pk[j + 1][0], pk[j + 1][1]}
+                                : (u32x4){pk[j][0], pk[j][1], rcv[0], rcv[1]};
+            const uint32_t off = ob + (uint32_t)((odd ? (hh * 4 + j + 1) * 16 - 4 : (hh * 4 + j) * 16) * 2) + (hh ? head2 : 0);
+            __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 0);
+          }
+        }
+      }
+      // rows >= M (zeros + bias) are finite whenever the real rows' bias is: the OR over all rows is the guard
+      if (rbits & 0x80008000u) range_bad = true;
+      seam = true;
+    } else {
+      constexpr int RB = 4;  // row tiles per residual batch (RB x TN 16-byte loads in flight per lane)
+#pragma unroll
+      for (int h2 = 0; h2 < (TM + RB - 1) / RB; ++h2) {
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 rv[RB][TN];
+#pragma unroll
+        for (int i = 0; i < RB; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            if (h2 * RB + i < TM)
+              rv[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rc, (uint32_t)(((mb + (h2 * RB + i) * 16 + fr) * p.ldc + nb + j * 16 + 4 * fq) * 4),
+                                                       0, 0));
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          if (h2 * RB + i >= TM) break;
+          __builtin_amdgcn_sched_barrier(0);
+          const uint32_t orow = (uint32_t)(((mb + (h2 * RB + i) * 16 + fr) * p.ldc + nb + 4 * fq) * 4);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            f32x4 a = acc_v(acc[h2 * RB + i][j]);
+            if (p.bias) a += *(const f32x4*)(bl + j * 16);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv[i][j] + a), rc, orow + j * 64, 0, 0);
+          }
+        }
+      }
+      if (tn >= 0) {  // stage 1 of the next tile into the last stage's buffer, after the stores
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        stage(tn, 1, (step + 1) & 1);
+      }
+      seam = true;
+    }
+    if (tn < 0) break;
+    t = tn;
+    ++tcount;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup has ended
+  if (SO && p.range_flag && __any(range_bad) && lane == 0) range_flag_set(p.range_flag);
+}
+constexpr int f16w_lds(int bm) { return 2 * (bm * 128 + 256 * 128) + 2048; }
+
+// ---------------------------------------------------------------------------------------------
 // Persistent fp16 encoder GEMM with the A operand two k-steps ahead (round 3; tools build only, ICAP_F16_GEMM=7:
 // correct - 104 GPU tests with it as the product form - but per ViT layer 973-991 us against 979-981 for
 // gemm_f16p_kernel on the same box, tools/r3_lib_ab.sh: the k-loop is not held by the stage's DMA latency).  gemm_f16p_kernel's 2-stage ring keeps

@@ -435,6 +435,31 @@ bool launch_gemm_256_tools(const GemmArgs& g, hipStream_t s, int cus, hipError_t
       return done();
     }
     const dim3 grid224(std::min((g.N / 256) * ((g.M + 223) / 224), cus));
+    // ICAP_F16_GEMM 8 / 9 / 10: the one-wave-per-SIMD form (gemm_f16w_kernel) with the stage pieces spread over the
+    // MFMA groups (8), in one burst (9), or spread with 256-row residual tiles (10)
+    if ((form == 8 || form == 9 || form == 10) && so) {
+#define F16W(MODE_, EP_, DI_, BM_, GRID_)                                                                 \
+  {                                                                                                       \
+    if (!attr((const void*)gemm_f16w_kernel<MODE_, EP_, DI_, BM_>, f16w_lds(BM_))) return true;           \
+    hipLaunchKernelGGL((gemm_f16w_kernel<MODE_, EP_, DI_, BM_>), GRID_, dim3(256), f16w_lds(BM_), s, g);  \
+  }
+      if (!res) {
+        const int ep = g.hm_n ? 2 : g.epi == EPI_GELU ? 1 : 0;
+        if (form == 9) {
+          if (ep == 2) F16W(1, 2, 0, 256, grid) else if (ep == 1) F16W(1, 1, 0, 256, grid) else F16W(1, 0, 0, 256, grid)
+        } else {
+          if (ep == 2) F16W(1, 2, 1, 256, grid) else if (ep == 1) F16W(1, 1, 1, 256, grid) else F16W(1, 0, 1, 256, grid)
+        }
+      } else if (form == 10) {
+        F16W(2, 0, 1, 256, grid)
+      } else if (form == 9) {
+        F16W(2, 0, 0, 224, grid224)
+      } else {
+        F16W(2, 0, 1, 224, grid224)
+      }
+#undef F16W
+      return done();
+    }
     // ICAP_F16P_ABL: gemm_f16p_kernel without its k-loop DMA (1) or without its MFMAs (2) - wrong results,
     // timing only (tools/f16_ablate.sh); 3 / 4 / 5: the compiler's fragment-read order / the read pipeline per
     // k-half / the stage's DMA before the first fragment reads; 6: reads 3 groups ahead; 7: setprio; 8: 8-B stores

@@ -1357,7 +1357,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
     }
     return;
   }
-  if (persist) {  // one persistent launch per step (all layers) + the head
+  if (step_path(h, max_len, drop)) {  // one persistent launch per step (all layers) + the head
     const DecStepArgs* dargs = step_args(h, b, B, S, max_len, wsi, drop, s);
     const size_t st_ints = dec_step_state_ints(d.n_dec_layers, B);
     HIPCHK(hipMemsetAsync(h->step_state[wsi].p, 0, st_ints * 4 * (size_t)(max_len - 1), s));

@@ -353,7 +353,8 @@ class Engine:
         return ids, logits
 
     def greedy(self, memory: torch.Tensor, start: int, end: int, max_len: int) -> torch.Tensor:
-        """Reference-identical greedy output (int64, stop rule applied)."""
+        """Reference-identical greedy output (int64, stop rule applied).  With the f16 encoder, a direct Engine user
+        checks range_overflowed() after encode (the drop-in models do; CaptionPipeline(check_range=True) does)."""
         ids, _ = self.greedy_raw(memory, start, end, max_len)
         return apply_stop_rule(ids.long(), end)
 
@@ -420,8 +421,14 @@ class Engine:
         check(self.lib.icap_set_decode_step(self.handle, int(mode)), "icap_set_decode_step")
 
     def set_encoder_cus(self, cus: int) -> None:
-        """Persistent encoder GEMM grids for an encoder stream restricted to `cus` CUs (0 = every CU)."""
+        """Persistent encoder GEMM grids for an encoder stream restricted to `cus` CUs (0 = every CU).  The value
+        belongs to the handle: a user that changes it restores the previous one (encoder_cus) when done."""
         check(self.lib.icap_set_encoder_cus(self.handle, int(cus)), "icap_set_encoder_cus")
+        self._encoder_cus = int(cus)
+
+    @property
+    def encoder_cus(self) -> int:
+        return getattr(self, "_encoder_cus", 0)
 
     def set_graphs(self, enable: bool) -> None:
         """hipGraph replay of the decode loop (default on)."""

@@ -27,10 +27,15 @@ class CaptionPipeline:
     so neither phase waits for the other's workgroups to retire before it gets a CU."""
 
     def __init__(self, engine: Engine, start: int, end: int, max_len: int, decode_priority: int = -1,
-                 decode_cus: Optional[int] = None):
+                 decode_cus: Optional[int] = None, check_range: bool = False):
+        """check_range: after each run(), raise if the f16 encoder's fp16 range guard fired for any batch
+        (Engine.range_overflowed, DESIGN.md §3: those memories must be re-encoded in bf16x2, which the drop-in
+        models do by themselves; a direct Engine / pipeline user opts in here).  Costs one stream sync per run."""
         import ctypes
 
         self.eng = engine
+        self.check_range = bool(check_range)
+        self._prev_cus = engine.encoder_cus
         self.start, self.end, self.max_len = int(start), int(end), int(max_len)
         dev = engine.device
         self._owned = []
@@ -55,8 +60,8 @@ class CaptionPipeline:
 
     def __del__(self):
         if getattr(self, "_owned", []):
-            try:
-                self.eng.set_encoder_cus(0)
+            try:  # the budget this pipeline found, not 0: another pipeline on the engine may still use its own
+                self.eng.set_encoder_cus(self._prev_cus)
             except Exception:
                 pass
         for p in getattr(self, "_owned", []):
@@ -100,4 +105,7 @@ class CaptionPipeline:
                 outs.append(post(ids) if post is not None else ids)
         cur.wait_stream(D)
         cur.wait_stream(E)
+        if self.check_range and eng.range_overflowed():
+            raise RuntimeError("fp16 range guard: an f16 encoder activation overflowed in this run; re-encode the "
+                               "batches with a bf16x2 engine (Engine(..., precision='bf16x2'))")
         return outs

@@ -133,10 +133,20 @@ def scst_step(lp_module: nn.Module, images: torch.Tensor, ref_rows: torch.Tensor
     ref_rows (B_local, Lr) raw id rows; sampler(images) -> (sample_ids, greedy_ids) for the shard.
     dropout_seed: the seed the sampler drew its train-mode dropout masks with (sample_and_greedy(...,
     dropout=(p, seed))); the teacher-forced recompute then applies the same masks (scst_loss.py:114-184 on one
-    GPU).  None keeps the module's own setting.
+    GPU).  The seed applies to THIS call only (the module's own setting is restored on return); None keeps the
+    module's own setting for the call.
     Returns (loss, info); the caller runs loss.backward() (DDP all-reduces) and the optimizer."""
+    inner = getattr(lp_module, "module", lp_module)
+    saved = getattr(inner, "dropout_seed", None)
     if dropout_seed is not None:
-        getattr(lp_module, "module", lp_module).dropout_seed = int(dropout_seed)
+        inner.dropout_seed = int(dropout_seed)
+    try:
+        return _scst_step(lp_module, images, ref_rows, sampler, start, end, pad, global_batch)
+    finally:
+        inner.dropout_seed = saved
+
+
+def _scst_step(lp_module, images, ref_rows, sampler, start, end, pad, global_batch):
     B = images.shape[0]
     total = global_batch or B
     with torch.no_grad():

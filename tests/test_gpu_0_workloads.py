@@ -59,21 +59,43 @@ def _oracle_memory(fn, sd_dev, imgs, chunk=64):
         return torch.cat([fn(sd_dev, imgs[i:i + chunk]) for i in range(0, imgs.shape[0], chunk)])
 
 
-def _check_greedy(ids, step_logits, sd_dev, mem_o, end):
-    """ids (B, L) int32 HIP greedy output; step_logits (L-1, B, V) its per-step logits."""
+GATED_ROWS_MAX = 3  # rows allowed a near-tie step (verdict r3 item 5): every other row is id-identical to the oracle
+
+
+def _check_greedy(ids, step_logits, sd_dev, mem_o, end, tag=""):
+    """ids (B, L) int32 HIP greedy output; step_logits (L-1, B, V) its per-step logits.
+
+    1. The oracle's teacher-forced logits on the HIP ids: within 1e-3 of the HIP step logits on every row and step.
+    2. The oracle's OWN greedy decode (O.greedy_from_memory, the reference's _greedy_search loop, vit:296-325) on the
+       oracle memory: the HIP ids equal it on every row up to that row's first near-tie step - a step whose oracle
+       top-2 margin is within twice that row-step's measured HIP-vs-oracle logit error, where either token is a
+       correct reading of the reference - and on the whole row when it has none.  The number of rows with a near-tie
+       is printed and pinned to GATED_ROWS_MAX."""
     ids = ids.long()
     tf = O.teacher_forced_logits(sd_dev, mem_o, ids)                      # (B, L-1, V)
     hip = step_logits.permute(1, 0, 2)
-    err = (hip - tf).abs().max().item()
+    err_rs = (hip - tf).abs().amax(-1)                                    # (B, L-1) per row-step
+    err = err_rs.max().item()
     assert err < 1e-3, f"step logits vs oracle {err}"
     top = tf.topk(2, dim=-1)
     margin = top.values[..., 0] - top.values[..., 1]
-    sure = margin > 2 * max(err, 1e-6)
+    sure = margin > 2 * err_rs + 1e-6
     agree = ids[:, 1:] == top.indices[..., 0]
     assert bool(agree[sure].all()), f"{int((~agree & sure).sum())} confident steps disagree"
-    gated = int((~sure).sum())
-    assert gated <= max(2, ids.numel() // 500), f"{gated} near-tie steps"
-    return err, gated
+    with torch.no_grad():
+        o_ids = O.greedy_from_memory(sd_dev, mem_o, W.START_TOKEN, end, ids.shape[1])
+    assert o_ids.shape == ids.shape  # random-init weights: no batch-global stop before max_len
+    gated_rows = 0
+    for r in range(ids.shape[0]):
+        near = torch.nonzero(~sure[r]).flatten()
+        upto = int(near[0]) + 1 if len(near) else ids.shape[1]           # positions 0..k0 come from sure steps
+        gated_rows += bool(len(near))
+        assert torch.equal(ids[r, :upto], o_ids[r, :upto]), (r, upto)
+    print(f"\n[{tag}] greedy vs oracle greedy: {ids.shape[0]} rows, max logit err {err:.2e}, "
+          f"near-tie steps {int((~sure).sum())}, rows id-identical to the oracle {ids.shape[0] - gated_rows}, "
+          f"rows gated at a near-tie {gated_rows}")
+    assert gated_rows <= GATED_ROWS_MAX, f"{gated_rows} rows with a near-tie step"
+    return err, gated_rows
 
 
 def test_config2_vit_b256_every_row(cuda, vit_sd):
@@ -92,7 +114,7 @@ def test_config2_vit_b256_every_row(cuda, vit_sd):
             rows = [0, 255]
             cpu = O.vit_encode(vit_sd, imgs[rows].cpu())
             assert (cpu - mem_o[rows].cpu()).abs().max().item() < 1e-4
-        _check_greedy(ids, lg, sdd, mem_o, W.END_TOKEN)
+        _check_greedy(ids, lg, sdd, mem_o, W.END_TOKEN, f"config2 seed {seed}")
         # the teacher-forced HIP decoder (icap_decoder_forward) on the same ids
         tf = eng.decoder_forward(ids[:, :-1], mem, causal=True)
         assert (tf - O.teacher_forced_logits(sdd, mem_o, ids.long())).abs().max().item() < 1e-3
@@ -122,7 +144,7 @@ def test_config3_grid_b256_trunk_and_every_row(cuda, grid_sd):
         cpu = O.grid_encode(grid_sd, imgs[rows].cpu())
     assert (cpu - mem_o[rows].cpu()).abs().max().item() < 1e-4
     ids, lg = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L, want_logits=True)
-    _check_greedy(ids, lg, sdd, mem_o, W.END_TOKEN)
+    _check_greedy(ids, lg, sdd, mem_o, W.END_TOKEN, "config3")
     distinct = len({tuple(r) for r in ids.cpu().tolist()})
     assert distinct >= 4, distinct  # the rows really differ (the decoder, not the memory, limits variety)
 
@@ -172,7 +194,7 @@ def test_config5_scst_reward_step_128_rows(cuda, vit_sd):
     # greedy rows (no step logits from the concurrent pair: teacher-forced HIP decoder logits instead)
     g = gid.long()
     hip_tf = eng.decoder_forward(gid[:, :-1], mem, causal=True)
-    _check_greedy(gid, hip_tf.permute(1, 0, 2), sdd, mem_o, W.END_TOKEN)
+    _check_greedy(gid, hip_tf.permute(1, 0, 2), sdd, mem_o, W.END_TOKEN, "config5 greedy")
     # CIDEr-D of both sets (one reference caption per image), GPU pass vs the host restatement
     refs = [[torch.randint(1, 100, (int(torch.randint(5, 13, (1,), generator=gen)),), generator=gen).tolist()]
             for _ in range(B)]

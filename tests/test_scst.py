@@ -141,7 +141,8 @@ def test_concurrent_sample_and_greedy_equal_sequential(cuda):
 
 def test_teacher_forced_dropout_follows_sampler_seed():
     """The DDP SCST recompute takes the sampler's dropout seed (scst_step(dropout_seed=...)) through a DDP-style
-    wrapper and applies (p, seed) only in train mode - the masks sample_and_greedy(dropout=(p, seed)) drew."""
+    wrapper and applies (p, seed) only in train mode - the masks sample_and_greedy(dropout=(p, seed)) drew - for THAT
+    call only: the module's own setting is back afterwards (a later call without a seed never reuses a stale one)."""
     from image_caption_amd.scst import TeacherForcedLogProbs, scst_step
 
     model, imgs, refs, _ = _setup()
@@ -154,6 +155,7 @@ def test_teacher_forced_dropout_follows_sampler_seed():
             self.module = m
 
         def forward(self, *a):
+            seen.append(self.module.dropout())
             return self.module(*a)
 
     def sampler(im):
@@ -161,9 +163,17 @@ def test_teacher_forced_dropout_follows_sampler_seed():
         ids[:, 0] = W.START_TOKEN
         return ids, ids
 
+    seen = []
     scst_step(Wrap(lp), imgs[:2], refs[:2], sampler, W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN, dropout_seed=77)
-    assert lp.dropout_seed == 77
-    assert lp.dropout() == (0.0, 0)  # eval mode: no masks
+    assert seen[-1] == (0.0, 0)  # eval mode: no masks
+    assert lp.dropout_seed is None  # restored
     model.train()
-    p, seed = lp.dropout()
-    assert seed == 77 and p > 0.0
+    try:
+        scst_step(Wrap(lp), imgs[:2], refs[:2], sampler, W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN, dropout_seed=77)
+        p, seed = seen[-1]
+        assert seed == 77 and p > 0.0
+        assert lp.dropout_seed is None and lp.dropout() == (0.0, 0)
+        scst_step(Wrap(lp), imgs[:2], refs[:2], sampler, W.START_TOKEN, W.END_TOKEN, W.PAD_TOKEN)
+        assert seen[-1] == (0.0, 0)  # no seed given: no stale masks
+    finally:
+        model.eval()
