@@ -128,6 +128,7 @@ SIGNATURES = {
     "icap_op_layernorm": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_long,
                                   c_int, c_void_p]),
     "icap_op_enc_attention": (c_int, [c_void_p, c_long, c_int, c_int, c_int, c_void_p, c_long, c_int, c_void_p]),
+    "icap_op_enc_attention_hm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "icap_op_cross_attn": (c_int, [c_void_p, c_long, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p]),
     "icap_decoder_train_workspace": (ctypes.c_size_t, [c_void_p, c_int, c_int, c_int, c_float]),
     "icap_decoder_train_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float,

@@ -525,6 +525,133 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
   }
 }
 
+// Whole-sequence form of the f16 encoder attention (round 4; head-major fp16 qkv, N <= 256): one workgroup of 4 waves
+// per (image, head) stages ALL of its K and V (N x 64 fp16 each: 50 KiB at N = 197) in one DMA burst, and each wave
+// takes query tiles w, w + 4, ...: S^T = K Q^T over every key tile at once (13 tiles x 2 MFMA at N = 197, 52 score
+// registers), one exact softmax (no running max / rescale), P as fp16, O = P V over key-tile pairs with transposed V
+// reads.  Against enc_attention_pipe_kernel (7 chunks of 32 keys, a counted wait + barrier and an online-softmax
+// rescale per chunk, 2 blocks per CU at 98.5 us per ViT layer): no chunk loop, one barrier, and 3 workgroups per CU
+// (50 KiB each) keep 12 waves resident.  Swizzles as the pipelined form (kswz / vswz over the whole image).
+constexpr int EAF_MAXKT = 16;
+// abl (tools knob ICAP_EAF_ABL, timing ablations; 0 in a product build): 1 = loads only, 2 = no K / V / Q loads,
+// 3 = no output stores
+__global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t* __restrict__ qkv, int N, int H,
+                                                                     float scale, bf16_t* out, long out_ld, int abl) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  const int nkt = (N + 15) >> 4;             // key tiles
+  const bf16_t* qb = qkv + ((long)b * 3 * H + h) * N * 64;  // [q|k|v x head][token][64]
+  const bf16_t* kb = qb + (long)H * N * 64;
+  const bf16_t* vb = qb + 2L * H * N * 64;
+  char* const Ks = smem;                    // [nkt * 16 rows][128 B]
+  char* const Vs = smem + nkt * 16 * 128;   // [nkt * 16 rows][128 B]
+  // stage: instruction i = 8 rows x 128 B of K (i < nkt * 2) or V; rows >= N read row N - 1 (finite; masked / P = 0)
+  {
+    const int lrow = lane >> 3, lch = lane & 7, ni = nkt * 2;
+    for (int i = wave; i < (abl == 2 ? 0 : 2 * ni); i += 4) {
+      const bool isK = i < ni;
+      const int row = (isK ? i : i - ni) * 8 + lrow;
+      const int ch = lch ^ (isK ? kswz(row) : vswz(row));
+      const bf16_t* src = (isK ? kb : vb) + (long)min(row, N - 1) * 64 + ch * 8;
+      lds_dma16(src, (LDS_AS void*)((isK ? Ks : Vs) + (isK ? i : i - ni) * 1024));
+    }
+  }
+  const int nqt = nkt;
+  // every query tile of this wave (w, w + 4, ... : at most EAF_MAXKT / 4) loaded into registers in the same burst as
+  // the K / V DMA, so no tile pays its own global-load latency after the barrier
+  bf16x8 qreg[EAF_MAXKT / 4][2];
+#pragma unroll
+  for (int qi = 0; qi < EAF_MAXKT / 4; ++qi) {
+    const int q = min((wave + 4 * qi) * 16 + fr, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      qreg[qi][ks] = abl == 2 ? (bf16x8){} : *(const bf16x8*)(qb + (long)q * 64 + ks * 32 + g * 8);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (abl == 1) {
+    if (__builtin_bit_cast(u32x4, qreg[0][0])[0] == 0x12345678u) out[threadIdx.x] = 0;  // keep the loads
+    return;
+  }
+  const float sc2 = scale * 1.44269504088896341f;  // exp2 domain
+  const int q4 = fr >> 2, p4 = fr & 3;
+#pragma unroll
+  for (int qi = 0; qi < EAF_MAXKT / 4; ++qi) {
+    const int qt = wave + 4 * qi;
+    if (qt >= nqt) continue;  // (uniform per wave)
+    const bf16x8* const qh = qreg[qi];
+    // scores: lane holds query fr, keys 16 kt + 4 g + r
+    f32x4 s[EAF_MAXKT];
+#pragma unroll
+    for (int kt = 0; kt < EAF_MAXKT; ++kt) {
+      s[kt] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      if (kt >= nkt) continue;  // (uniform; every index stays a compile-time one: no private array)
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int row = kt * 16 + fr;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 kh = *(const bf16x8*)(Ks + row * 128 + (((ks * 4 + g) ^ kswz(row)) << 4));
+        acc = mma<true>(kh, qh[ks], acc);
+      }
+      s[kt] = acc * sc2;
+      if (kt * 16 + 16 > N) {  // (uniform) the ragged last tile; kt is a compile-time index (no private array)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kt * 16 + g * 4 + r >= N) s[kt][r] = -INFINITY;
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < EAF_MAXKT; ++kt)
+      if (kt < nkt) mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
+    mx = rows4_max(mx);
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < EAF_MAXKT; ++kt) {
+      if (kt >= nkt) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[kt][r] = __builtin_amdgcn_exp2f(s[kt][r] - mx);
+      l += (s[kt][0] + s[kt][1]) + (s[kt][2] + s[kt][3]);
+    }
+    l = rows4_sum(l);
+    // O = P V: key-tile pairs (2 c, 2 c + 1) as one 32-deep k-step; P (fp16) element j < 4 -> key 4 g + j of the
+    // first tile, j >= 4 -> of the second (a tile past nkt contributes zeros)
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < EAF_MAXKT / 2; ++c) {
+      if (2 * c >= nkt) continue;
+      const f32x4 s1 = 2 * c + 1 < nkt ? s[2 * c + 1] : (f32x4){0.f, 0.f, 0.f, 0.f};
+      const u32x2 p0 = pack16x4<true>(s[2 * c]), p1 = pack16x4<true>(s1);
+      const bf16x8 ph = __builtin_bit_cast(bf16x8, (u32x4){p0[0], p0[1], p1[0], p1[1]});
+      const int key0 = c * 32 + 4 * g + q4;  // and key0 + 16 (vswz has period 8)
+      const int second = 2 * c + 1 < nkt ? 16 * 128 : 0;  // past the last tile: re-read tile 2 c (finite, P = 0)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int off0 = key0 * 128 + (((dt * 2 + (p4 >> 1)) ^ vswz(key0)) << 4) + (p4 & 1) * 8;
+        const bf16x8 vh = tr_pair(Vs + off0, Vs + off0 + second);
+        o[dt] = mma<true>(vh, ph, o[dt]);
+      }
+    }
+    // 16-byte stores: lanes g (even) and g + 1 hold d = 16 dt + 4 g .. + 7 of d-tiles dt and dt + 1
+    const float inv = 1.f / l;
+    const int qq = qt * 16 + fr;
+    const bool odd = g & 1;
+    bf16_t* dst = out + ((long)b * N + qq) * out_ld + h * 64 + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; dt += 2) {
+      const u32x2 a0 = pack16x4<true>(o[dt] * inv), a1 = pack16x4<true>(o[dt + 1] * inv);
+      const u32x2 snd = odd ? a0 : a1;
+      const u32x2 rcv = {xor16_partner(snd[0]), xor16_partner(snd[1])};
+      const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], a1[0], a1[1]} : (u32x4){a0[0], a0[1], rcv[0], rcv[1]};
+      if (qq < N && (abl != 3 || w[0] == 0x12345678u)) *(u32x4*)(dst + (odd ? (dt + 1) * 16 - 4 : dt * 16)) = w;
+    }
+  }
+}
+
 template <int NKT, bool SPLIT>
 hipError_t run_enc(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale, bf16_t* out,
                    long out_ld, long out_lo, hipStream_t s) {
@@ -560,6 +687,23 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
     // two query tiles per wave (8 waves, 119 VGPRs, two blocks per CU): every K/V fragment read from LDS serves
     // 32 queries - 1.57 -> 1.28 ms/step at B = 256 (tools/knob_ab.sh); ICAP_ENC_ATTN16_QPW=1 (tools): 16 waves
     static const int qpw16 = icap_knob("ICAP_ENC_ATTN16_QPW", 2);
+    // round 4: the whole-sequence form (enc_attention_full_kernel; tools knob ICAP_ENC_ATTN16_FULL=0: the pipelined
+    // form)
+    static const int full = icap_knob("ICAP_ENC_ATTN16_FULL", 1);
+    if (head_major && full) {
+      const int lds_full = 2 * ((N + 15) / 16) * 16 * 128;
+      static bool fattr = false;
+      if (!fattr) {
+        const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_full_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16 * 16 * 128);
+        if (e != hipSuccess) return e;
+        fattr = true;
+      }
+      static const int abl = icap_knob("ICAP_EAF_ABL", 0);
+      hipLaunchKernelGGL(enc_attention_full_kernel, dim3(H, B), dim3(256), lds_full, s, qkv, N, H, scale, out, out_ld,
+                         abl);
+      return hipGetLastError();
+    }
     if (head_major && qpw16 == 2)
       hipLaunchKernelGGL((enc_attention_pipe_kernel<false, true, 2, true>), dim3(H, B), dim3(512), lds, s, qkv, ld, lo,
                          N, H, scale, out, out_ld, out_lo);
@@ -1101,6 +1245,195 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
 constexpr int xa16_lds(int ck, int nb = 2) { return nb * ck * 512 * 2 + (ck / 16) * (1024 + 256) * 4 + 16; }
 constexpr int XA16_LDS = xa16_lds(64);
 
+// ------------------------------------------------------------------------------------------------
+// Cross-attention over the fp16 memory plane, key-split single-burst form (round 4; one decoder row per memory
+// image and no dropout: the greedy / sampled decode).  cross_attn_f16_kernel spends its 15.5 us per launch at B = 256
+// in its 7-chunk loop (a DMA round trip and three barriers per 32-key chunk, ~2.2 us each) - a row's 196 KiB of
+// memory arrive at ~13 GB/s per workgroup.  Here the keys of a row split over two workgroups (part 0: keys [0, SH),
+// part 1: [SH, S), SH = ceil(S / 2) rounded up to 16) and each stages its <= 128 keys in ONE DMA burst, then
+//   scores   wave w < KT: key tile w (16 keys) x all 512 dims, 16 MFMA 16x16x32 f16 with q~ as the B operand's 16
+//            columns = 8 heads x {fp16 hi, fp16 lo} of q~ (one MFMA per k-step covers both planes; column n + 8 is added
+//            to column n by a DPP row rotate)
+//   softmax  per head over the part's keys: wave maxima / sums through LDS (two barriers), P (fp32) -> LDS
+//   context  wave w: dims [64 w, 64 w + 64) = 4 d-tiles x KT / 2 key steps, A = memory^T by transposed LDS reads,
+//            B = P as {fp16 hi, fp16 lo} columns (summed as the scores)
+// and leaves (unnormalised context, max, sum) with agent-scope stores; the second of the pair to take the row's ticket
+// merges part 0 then part 1 (the same operations whatever the arrival order), normalises and writes c as bf16 hi / lo
+// planes - the layout cross_attn_f16_kernel writes.  The pair shares an XCD under round-robin dispatch (blocks b and
+// b + 8; speed only).  LDS: KTE x 16 keys x 1 KiB (KTE = KT rounded up to even; keys past S read row S - 1, P = 0)
+// + 9 KiB.
+constexpr int XAS_THREADS = 512;
+constexpr int xas_lds(int S) {
+  const int sh = ((S + 1) / 2 + 15) & ~15, kte = ((sh / 16) + 1) & ~1;
+  return kte * 16 * 1024 + 8 * 64 * 4 * 4 + 2 * 8 * 16 * 4 + 16;
+}
+
+__global__ __launch_bounds__(XAS_THREADS) void cross_attn_f16s_kernel(const bf16_t* __restrict__ qt, long qt_lo,
+                                                                     const bf16_t* __restrict__ mem, int rows, int S,
+                                                                     float scale, bf16_t* out, long out_lo, float* xpart,
+                                                                     int* xcnt) {
+  constexpr int DM = 512, H = 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int gq = blockIdx.x >> 3, part = gq & 1, r = (gq >> 1) * 8 + (blockIdx.x & 7);
+  if (r >= rows) return;  // (the whole workgroup: grid padded to 8 rows)
+  const int SH = ((S + 1) / 2 + 15) & ~15;
+  const int k0 = part * SH, nk = min(S - k0, SH);              // this part's keys [k0, k0 + nk); nk <= 0: none
+  const int KT = nk > 0 ? (nk + 15) >> 4 : 0, KTE = (KT + 1) & ~1;
+  char* const cb = smem;                                        // keys [KTE * 16][1024 B], chunk c at c ^ (key & 15)
+  float* const pimg = (float*)(smem + KTE * 16 * 1024);         // P [tile][lane][4]
+  float* const wmax = pimg + 8 * 64 * 4;                        // [wave][16 columns]
+  float* const wsum = wmax + 8 * 16;
+  int* const flag = (int*)(wsum + 8 * 16);
+  const bf16_t* mb = mem + (long)r * S * DM;
+
+  // stage every key row of the part at once: wave w loads rows w, w + 8, ... (1 KiB per instruction)
+  for (int key = wave; key < KTE * 16; key += 8) {
+    const int g = min(k0 + key, S - 1);
+    lds_dma16(mb + (long)g * DM + (lane ^ (key & 15)) * 8, (LDS_AS void*)(cb + key * 1024));
+  }
+  // q~ as the B operand: column n = fr -> head n & 7, plane n >> 3 of the fp16 hi / lo split of (bf16 hi + bf16 lo)
+  const int hd = fr & 7;
+  f16x8 qb[16];
+  if (wave < KT) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const long off = (long)r * H * DM + hd * DM + s * 32 + fq * 8;
+      const bf16x8 a = *(const bf16x8*)(qt + off), b = *(const bf16x8*)(qt + qt_lo + off);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = (float)a[j] + (float)b[j];
+        const _Float16 h = (_Float16)v;
+        qb[s][j] = fr < 8 ? h : (_Float16)(v - (float)h);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  auto mma16h = [](f16x8 a, f16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); };
+  auto ror8 = [](float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, true)); };
+  // ---- scores of key tile `wave`: lane holds column fr (head hd), keys 16 wave + 4 fq + i
+  f32x4 sc = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  if (wave < KT) {
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    const int key = wave * 16 + fr;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const f16x8 mh = *(const f16x8*)(cb + key * 1024 + (((s * 4 + fq) ^ (key & 15)) << 4));
+      a = mma16h(mh, qb[s], a);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v = (a[i] + ror8(a[i])) * scale;  // hi + lo columns (fr < 8 and fr >= 8 both hold the sum)
+      sc[i] = wave * 16 + fq * 4 + i < nk ? v : -INFINITY;
+    }
+  }
+  float mx = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
+  mx = rows4_max(mx);
+  if (lane < 16) wmax[wave * 16 + lane] = mx;
+  __syncthreads();
+  float m = wmax[fr];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) m = fmaxf(m, wmax[w * 16 + fr]);
+  f32x4 e = {0.f, 0.f, 0.f, 0.f};
+  float es = 0.f;
+  if (wave < KT) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      e[i] = sc[i] == -INFINITY ? 0.f : __expf(sc[i] - m);
+      es += e[i];
+    }
+  }
+  es = rows4_sum(es);
+  if (lane < 16) wsum[wave * 16 + lane] = es;
+  if (wave < KTE) *(f32x4*)(pimg + (wave * 64 + lane) * 4) = e;  // (tile KT of an odd KT: zeros)
+  __syncthreads();
+  float l = 0.f;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) l += wsum[w * 16 + fr];
+
+  // ---- context: wave w, d-tiles 4 w .. 4 w + 3 (dims 64 w + 16 dt + 4 (fr & 3) + ...), keys in pairs of tiles
+  const int q4 = fr >> 2, p4 = fr & 3;
+  f32x4 acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int s2 = 0; s2 < KTE / 2; ++s2) {
+    // B = P^T: element j < 4 -> key 4 fq + j of tile 2 s2, j >= 4 -> key 4 fq + j - 4 of tile 2 s2 + 1; column fr:
+    // fp16 hi of P (fr < 8) or the fp16 lo remainder (fr >= 8)
+    const f32x4 p0 = *(const f32x4*)(pimg + ((2 * s2) * 64 + lane) * 4);
+    const f32x4 p1 = *(const f32x4*)(pimg + ((2 * s2 + 1) * 64 + lane) * 4);
+    f16x8 pb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const _Float16 h0 = (_Float16)p0[j], h1 = (_Float16)p1[j];
+      pb[j] = fr < 8 ? h0 : (_Float16)(p0[j] - (float)h0);
+      pb[4 + j] = fr < 8 ? h1 : (_Float16)(p1[j] - (float)h1);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int d = wave * 64 + dt * 16 + 4 * p4;
+      const int kk0 = 32 * s2 + 4 * fq + q4, kk1 = kk0 + 16;
+      const int o0 = kk0 * 1024 + ((((d >> 3) ^ (kk0 & 15))) << 4) + (d & 7) * 2;
+      const int o1 = kk1 * 1024 + ((((d >> 3) ^ (kk1 & 15))) << 4) + (d & 7) * 2;
+      const f16x8 vh = __builtin_bit_cast(f16x8, tr_pair(cb + o0, cb + o1));
+      acc[dt] = mma16h(vh, pb, acc[dt]);
+    }
+  }
+  // lane (fr < 8): head fr's unnormalised context at dims 64 wave + 16 dt + 4 fq + i
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[dt][i] += ror8(acc[dt][i]);
+
+  // ---- the pair's merge: both parts publish (context, max, sum); the second to take the ticket merges
+  constexpr int CF = H * DM;  // context floats per part
+  float* mine = xpart + ((long)r * 2 + part) * XA_PART_FLOATS;
+  const float* other = xpart + ((long)r * 2 + (part ^ 1)) * XA_PART_FLOATS;
+  if (fr < 8) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __hip_atomic_store(mine + hd * DM + wave * 64 + dt * 16 + fq * 4 + i, acc[dt][i], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x < 8) {
+    __hip_atomic_store(mine + CF + threadIdx.x, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mine + CF + 8 + threadIdx.x, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores are complete
+  __syncthreads();                                   // ... and every thread's
+  if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(xcnt + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (*flag == 0) return;  // the partner merges
+  if (threadIdx.x == 0) __hip_atomic_store(xcnt + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (fr >= 8) return;
+  const float om = __hip_atomic_load(other + CF + hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float ol = __hip_atomic_load(other + CF + 8 + hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float m0 = part ? om : m, m1 = part ? m : om, l0 = part ? ol : l, l1 = part ? l : ol;
+  const float mn = fmaxf(m0, m1);
+  const float f0 = m0 == -INFINITY ? 0.f : __expf(m0 - mn), f1 = m1 == -INFINITY ? 0.f : __expf(m1 - mn);
+  const float inv = 1.f / __fadd_rn(__fmul_rn(l0, f0), __fmul_rn(l1, f1));
+  bf16_t* dst = out + (long)r * H * DM + hd * DM + wave * 64;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    bf16_t hv[4], lv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float o = __hip_atomic_load(other + hd * DM + wave * 64 + dt * 16 + fq * 4 + i, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+      const float x0 = part ? o : acc[dt][i], x1 = part ? acc[dt][i] : o;
+      split_bf(__fadd_rn(__fmul_rn(x0, f0), __fmul_rn(x1, f1)) * inv, hv[i], lv[i]);
+    }
+    const int d = dt * 16 + 4 * fq;
+    *(u32x2*)(dst + d) = (u32x2){(uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16)};
+    *(u32x2*)(dst + out_lo + d) =
+        (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
+  }
+}
+
 }  // namespace
 
 int cross_attn_splits(int S) {
@@ -1121,6 +1454,14 @@ int cross_attn_f16_splits() {
   // key split of the fp16 cross-attention (tools knob ICAP_XATTN16_KS, default 1)
   static const int ks = icap_knob("ICAP_XATTN16_KS", 1);
   return ks == 2 ? 2 : 1;
+}
+
+bool cross_attn_f16s_on() {
+  // the key-split single-burst form (cross_attn_f16s_kernel) for one row per image without dropout: tools knob
+  // ICAP_XATTN16_S=1.  Off by default: inside the three-chain decode graph it measured 18.2 us per launch against
+  // 15.5 for the chunk-loop form (decode 14.5 vs 12.2 ms/step, same box, profiles/r04/xattn_split_ab.txt)
+  static const int on = icap_knob("ICAP_XATTN16_S", 0);
+  return on != 0;
 }
 
 hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem16, int rows, int rows_per_image,
@@ -1153,6 +1494,18 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
   // 32-key chunks, 8 waves, 74 KiB of LDS: two blocks (rows) share a CU, so the three decode chains' cross-
   // attentions hold half the CUs (decode 12.70 -> 12.47 ms/step, tools/knob_ab.sh); ICAP_XATTN16_CK=64 (tools):
   // 64-key chunks, 16 waves, 148 KiB (one block per CU)
+  if (rows_per_image == 1 && !drop.thr && xpart && xcnt && S <= 256 && cross_attn_f16s_on()) {
+    static bool sattr = false;
+    if (!sattr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)cross_attn_f16s_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, xas_lds(256));
+      if (e != hipSuccess) return e;
+      sattr = true;
+    }
+    hipLaunchKernelGGL(cross_attn_f16s_kernel, dim3((rows + 7) / 8 * 16), dim3(XAS_THREADS), xas_lds(S), s, qt, qt_lo,
+                       mem16, rows, S, scale, out, out_lo, xpart, xcnt);
+    return hipGetLastError();
+  }
   static const int ck = icap_knob("ICAP_XATTN16_CK", 32) == 64 ? 64 : 32;
   const int pairs = rows / rows_per_image * ((rows_per_image + 1) / 2);
   const bool ks2 = xpart && xcnt && !drop.thr && S > ck && cross_attn_f16_splits() == 2;

@@ -95,15 +95,60 @@ __device__ __forceinline__ f32x4 mma_rows(f32x4 acc, const char* wimg, int wrows
   return acc;
 }
 
+// acc += register-held W fragments (frag_pack image, fragment 2 k + hf of k64-step k) x X-image (16 rows) over NK
+// k64-steps of ximg; the same MFMA order as mma_rows (bit-identical sums)
+template <int NK>
+__device__ __forceinline__ f32x4 mma_frag(f32x4 acc, const bf16x8* wf, const char* ximg, int ns) {
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const bf16x8 b = wf[2 * k + hf];
+      acc = mfma16(b, frag(ximg + k * ns * 2048, 0, hf), acc);
+      if (ns == 2) acc = mfma16(b, frag(ximg + k * ns * 2048 + 2048, 0, hf), acc);
+    }
+  }
+  return acc;
+}
+// this wave's n fragments first .. first + n - 1 of a frag_pack image: each one 1 KiB contiguous (full lines)
+template <int N>
+__device__ __forceinline__ void load_frags(bf16x8* w, const bf16_t* img, long first) {
+  const bf16x8* src = (const bf16x8*)(img + first * 512) + (threadIdx.x & 63);
+#pragma unroll
+  for (int i = 0; i < N; ++i) w[i] = src[i * 64];
+}
+
+// Fragment images of the decode weights (launch_frag_pack, kernels.h): one thread per 16-byte lane piece.
+__global__ void frag_pack_kernel(const bf16_t* __restrict__ W, long ldw, int ntiles, int nk, int mode, int tps,
+                                 int ksl, bf16_t* __restrict__ out) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)ntiles * nk * 64) return;
+  const int l = (int)(idx & 63), s = (int)((idx >> 6) % nk), t = (int)((idx >> 6) / nk);
+  int row0 = 16 * t, k0 = 0;
+  if (mode == 1) {
+    const int hh = t / 12, i = t - hh * 12;
+    row0 = (i >> 2) * DEC_D + hh * DEC_HD + (i & 3) * 16;
+  } else if (mode == 2) {
+    const int j = t / tps, n = t - j * tps;
+    row0 = 16 * n;
+    k0 = ksl * j;
+  }
+  *(bf16x8*)(out + idx * 8) = *(const bf16x8*)(W + (long)(row0 + (l & 15)) * ldw + k0 + 32 * s + 8 * (l >> 4));
+}
+
 // ------------------------------------------------------------------------------------------------
 // Self-attention block of one decode step.
 //   round 1: X image (32 KiB, region B) + Wq_h, Wk_h images [8 k64][128 rows][128 B] (region A)
 //   round 2: Wv_h [8 k64][64 rows][128 B] + Wo[:, 64h:64h+64] [512 rows][128 B] (region A)
 //   then q|k|v rows fp32 [16][192] + ctx image in region B
+// FR (DecSaArgs::Wqkv_f / Wo_f, round 4): no weight region - waves 0-11 load their q|k|v tile's 16 KiB of fragments
+// straight into registers in the same burst as the X image, and every wave its 4 KiB of Wo fragments after its QKV
+// MFMAs (behind the attention): one memory round instead of two, 32 KiB of LDS instead of 160.
+template <bool FR>
 __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ra = smem;                        // 128 KiB weight region
-  char* sx = smem + 128 * 1024;           // 32 KiB row region
+  char* ra = smem;                        // 128 KiB weight region (FR: none)
+  char* sx = smem + (FR ? 0 : 128 * 1024);  // 32 KiB row region
   float* qkv = (float*)sx;                // after the v projection: [16][192]
   char* sc = sx + 16 * 192 * 4;           // ctx image [1 k64][ns][16][128 B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -115,14 +160,19 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   const char* wv = (const char*)(p.Wqkv + (long)(2 * DEC_D + h * DEC_HD) * DEC_D);
 
   dma_x(p.A, p.aL, ns, row0, p.rows, sx);
-  for (int k = 0; k < DEC_K64; ++k) {  // Wq_h, Wk_h: image [k64][128 rows] (q rows 0..63, k rows 64..127)
-    dma_rows(wq + k * 128, DEC_D * 2, 64, ra + k * 128 * 128, 8 * (2 * k) + 2);
-    dma_rows(wk + k * 128, DEC_D * 2, 64, ra + k * 128 * 128 + 64 * 128, 8 * (2 * k + 1) + 2);
+  bf16x8 wf[FR ? 2 * DEC_K64 : 1];  // FR: this wave's q|k|v tile (waves 0-11), all 16 k32-steps
+  if (FR) {
+    if (wave < 12) load_frags<2 * DEC_K64>(wf, p.Wqkv_f, (long)(h * 12 + wave) * 2 * DEC_K64);
+  } else {
+    for (int k = 0; k < DEC_K64; ++k) {  // Wq_h, Wk_h: image [k64][128 rows] (q rows 0..63, k rows 64..127)
+      dma_rows(wq + k * 128, DEC_D * 2, 64, ra + k * 128 * 128, 8 * (2 * k) + 2);
+      dma_rows(wk + k * 128, DEC_D * 2, 64, ra + k * 128 * 128 + 64 * 128, 8 * (2 * k + 1) + 2);
+    }
   }
   // the cached keys / values of positions < t0 of this wave's row (it attends for row row0 + wave below) do
   // not depend on this step: fetch the first 32 positions now, while the projections are staged.  Lane l
   // holds key / value j = 4 i + (l >> 4), dims 4 (l & 15) ..; 16 lanes read one 256-B row.
-  constexpr int PRE = 8;
+  constexpr int PRE = FR ? 6 : 8;  // FR: 24 cached positions in registers (8 fewer VGPRs: no spill next to the W fragments)
   const int dq = (lane & 15) * 4, jg = lane >> 4;
   const int brow = row0 + wave, t0 = p.t0;
   f32x4 kpre[PRE], vpre[PRE];
@@ -139,14 +189,20 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (wave < 8) acc = mma_rows(acc, ra, 128, wave * 16, sx, ns, 0, DEC_K64);  // q tiles 0..3, k tiles 4..7
-  __syncthreads();  // Wq / Wk no longer read
-  for (int k = 0; k < DEC_K64; ++k) dma_rows(wv + k * 128, DEC_D * 2, 64, ra + k * 64 * 128, 8 * k);
-  dma_rows((const char*)(p.Wo + h * DEC_HD), DEC_D * 2, DEC_D, ra + DEC_K64 * 64 * 128);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (wave >= 8 && wave < 12) acc = mma_rows(acc, ra, 64, (wave - 8) * 16, sx, ns, 0, DEC_K64);  // v tiles
+  bf16x8 wo[FR ? 4 : 1];  // FR: Wo fragments of output column tiles 2 wave, 2 wave + 1 (2 k32-steps each)
+  if (FR) {
+    if (wave < 12) acc = mma_frag<DEC_K64>(acc, wf, sx, ns);  // q tiles 0..3, k tiles 4..7, v tiles 8..11
+  } else {
+    if (wave < 8) acc = mma_rows(acc, ra, 128, wave * 16, sx, ns, 0, DEC_K64);  // q tiles 0..3, k tiles 4..7
+    __syncthreads();  // Wq / Wk no longer read
+    for (int k = 0; k < DEC_K64; ++k) dma_rows(wv + k * 128, DEC_D * 2, 64, ra + k * 64 * 128, 8 * k);
+    dma_rows((const char*)(p.Wo + h * DEC_HD), DEC_D * 2, DEC_D, ra + DEC_K64 * 64 * 128);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave >= 8 && wave < 12) acc = mma_rows(acc, ra, 64, (wave - 8) * 16, sx, ns, 0, DEC_K64);  // v tiles
+  }
   __syncthreads();  // X image no longer read: it becomes the q|k|v rows
+  if (FR) load_frags<4>(wo, p.Wo_f, (long)(h * 32 + 2 * wave) * 2);  // needed after the attention
   if (wave < 12) {
     const int c = wave * 16 + 4 * fq;  // column in [q | k | v] of this head
     acc += *(const f32x4*)(p.bqkv + (c >> 6) * DEC_D + h * DEC_HD + (c & 63));
@@ -232,11 +288,12 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   __syncthreads();
 
   // ---- out-projection slab of head h: 16 rows x 512 columns, K = 64 (one k64 step)
-  const char* wo = ra + DEC_K64 * 64 * 128;
+  const char* woi = ra + DEC_K64 * 64 * 128;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
-    o = mma_rows(o, wo, DEC_D, wave * 32 + i * 16, sc, ns, 0, 1);
+    if (FR) o = mma_frag<1>(o, wo + 2 * i, sc, ns);
+    else o = mma_rows(o, woi, DEC_D, wave * 32 + i * 16, sc, ns, 0, 1);
     const int row = row0 + fr;
     if (row < p.rows)
       *(f32x4*)(p.part + (long)h * p.part_stride + (long)row * DEC_D + wave * 32 + i * 16 + 4 * fq) = o;
@@ -247,10 +304,13 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
 // Feed-forward block of one decode step.
 //   round 1: X image (region B) + W1 slice [8 k64][128 rows][128 B] (region A)
 //   round 2: W2 slice [2 k64][512 rows][128 B] (region A); h image + k-half reduction in region B
+// FR (DecFfnArgs::W1f / W2f, round 4): each wave loads its W1 fragments (tile t, k-half kh: 8 KiB) and its W2
+// fragments (column tiles 2 wave, 2 wave + 1 of the slice: 8 KiB) into registers with the X image - one memory round.
+template <bool FR>
 __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ra = smem;
-  char* sx = smem + 128 * 1024;
+  char* sx = smem + (FR ? 0 : 128 * 1024);
   f32x4* red = (f32x4*)sx;                 // after FFN-1: [8 tiles][64 lanes]
   char* sh = sx + 8 * 64 * 16;             // h image [2 k64][ns][16][128 B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -259,17 +319,26 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   const int j = blockIdx.x % nslice, row0 = (blockIdx.x / nslice) * DEC_ROWS;
   const int ns = p.nsplit;
 
+  const int t = wave & 7, kh = wave >> 3;  // FFN-1 tile, k half (4 of the 8 k64 steps)
   dma_x(p.A, p.aL, ns, row0, p.rows, sx);
-  const char* w1 = (const char*)(p.W1 + (long)j * 128 * DEC_D);
-  for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 128, ra + k * 128 * 128);
+  bf16x8 w1f[FR ? DEC_K64 : 1], w2f[FR ? 8 : 1];
+  if (FR) {
+    load_frags<DEC_K64>(w1f, p.W1f, (long)(j * 8 + t) * 2 * DEC_K64 + kh * DEC_K64);
+    load_frags<8>(w2f, p.W2f, (long)(j * 32 + 2 * wave) * 4);
+  } else {
+    const char* w1 = (const char*)(p.W1 + (long)j * 128 * DEC_D);
+    for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 128, ra + k * 128 * 128);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int t = wave & 7, kh = wave >> 3;  // FFN-1 tile, k half (4 of the 8 k64 steps)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  acc = mma_rows(acc, ra, 128, t * 16, sx, ns, kh * 4, kh * 4 + 4);
+  if (FR) acc = mma_frag<4>(acc, w1f, sx + kh * 4 * ns * 2048, ns);
+  else acc = mma_rows(acc, ra, 128, t * 16, sx, ns, kh * 4, kh * 4 + 4);
   __syncthreads();  // W1 and X no longer read
-  const char* w2 = (const char*)(p.W2 + (long)j * 128);
-  for (int k = 0; k < 2; ++k) dma_rows(w2 + k * 128, DEC_F * 2, DEC_D, ra + k * DEC_D * 128);
+  if (!FR) {
+    const char* w2 = (const char*)(p.W2 + (long)j * 128);
+    for (int k = 0; k < 2; ++k) dma_rows(w2 + k * 128, DEC_F * 2, DEC_D, ra + k * DEC_D * 128);
+  }
   if (kh) red[t * 64 + lane] = acc;
   __syncthreads();
   if (!kh) {
@@ -283,12 +352,13 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
       for (int r = 0; r < 4; ++r) acc[r] *= drop_mul(p.drop, 5, row0 + fr, p.drop.pos, j * 128 + n + r);
     put_planes(sh, ns, fr, n, acc);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!FR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
-    o = mma_rows(o, ra, DEC_D, wave * 32 + i * 16, sh, ns, 0, 2);
+    if (FR) o = mma_frag<2>(o, w2f + 4 * i, sh, ns);
+    else o = mma_rows(o, ra, DEC_D, wave * 32 + i * 16, sh, ns, 0, 2);
     const int row = row0 + fr;
     if (row < p.rows)
       *(f32x4*)(p.part + (long)j * p.part_stride + (long)row * DEC_D + wave * 32 + i * 16 + 4 * fq) = o;
@@ -300,26 +370,36 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
 //   Y_h = X_h W1_h^T + b1_h (16 x 64, K = 512), O_h = Y_h W2_h^T (16 x 512, K = 64)
 // block = (16 rows, head h), one DMA round: X image 32 KiB + W1_h [8 k64][64][128 B] 64 KiB +
 // W2_h [512 rows][128 B] 64 KiB.  out = OUT_SPLIT (q~ planes of head h) or OUT_PARTIAL (slab h).
+// FR (ChainArgs::W1f / W2f, round 4): W1 (tile t, k-quarter kq: 4 KiB) and W2 (column tiles 2 wave, 2 wave + 1: 4 KiB)
+// fragments per wave in registers, 32 KiB of LDS (the X image) instead of 160.
+template <bool FR>
 __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* w1i = smem;                       // 64 KiB
-  char* w2i = smem + 64 * 1024;           // 64 KiB
-  char* sx = smem + 128 * 1024;           // 32 KiB: X image, then the k-quarter reduction + Y image
+  char* w1i = smem;                       // 64 KiB (FR: none)
+  char* w2i = smem + 64 * 1024;           // 64 KiB (FR: none)
+  char* sx = smem + (FR ? 0 : 128 * 1024);  // 32 KiB: X image, then the k-quarter reduction + Y image
   f32x4* red = (f32x4*)sx;                // [3 quarters][4 tiles][64 lanes]
   char* sy = sx + 12 * 64 * 16;           // Y image [1 k64][ns][16][128 B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int h = blockIdx.x % p.H, row0 = (blockIdx.x / p.H) * DEC_ROWS;
   const int ns = p.nsplit;
+  const int t = wave & 3, kq = wave >> 2;  // Y tile, k quarter (2 of the 8 k64 steps)
   dma_x(p.X + (long)h * p.x_hstride, p.x_lo, ns, row0, p.M, sx, p.ldx);
-  const char* w1 = (const char*)(p.W1 + (long)h * 64 * DEC_D);
-  for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 64, w1i + k * 64 * 128, 8 * k + 2);
-  dma_rows((const char*)(p.W2 + (long)h * p.w2_hstride), p.ldw2 * 2, DEC_D, w2i, 2);
+  bf16x8 w1f[FR ? 4 : 1], w2f[FR ? 4 : 1];
+  if (FR) {
+    load_frags<4>(w1f, p.W1f, (long)(h * 4 + t) * 2 * DEC_K64 + kq * 4);
+    load_frags<4>(w2f, p.W2f, (long)(h * 32 + 2 * wave) * 2);
+  } else {
+    const char* w1 = (const char*)(p.W1 + (long)h * 64 * DEC_D);
+    for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 64, w1i + k * 64 * 128, 8 * k + 2);
+    dma_rows((const char*)(p.W2 + (long)h * p.w2_hstride), p.ldw2 * 2, DEC_D, w2i, 2);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int t = wave & 3, kq = wave >> 2;  // Y tile, k quarter (2 of the 8 k64 steps)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  acc = mma_rows(acc, w1i, 64, t * 16, sx, ns, kq * 2, kq * 2 + 2);
+  if (FR) acc = mma_frag<2>(acc, w1f, sx + kq * 2 * ns * 2048, ns);
+  else acc = mma_rows(acc, w1i, 64, t * 16, sx, ns, kq * 2, kq * 2 + 2);
   __syncthreads();  // X no longer read
   if (kq) red[((kq - 1) * 4 + t) * 64 + lane] = acc;
   __syncthreads();
@@ -337,7 +417,8 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
-    o = mma_rows(o, w2i, DEC_D, wave * 32 + i * 16, sy, ns, 0, 1);
+    if (FR) o = mma_frag<1>(o, w2f + 2 * i, sy, ns);
+    else o = mma_rows(o, w2i, DEC_D, wave * 32 + i * 16, sy, ns, 0, 1);
     const int col = wave * 32 + i * 16 + 4 * fq;
     if (row >= p.M) continue;
     if (p.out == OUT_PARTIAL) {
@@ -357,47 +438,62 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
 
 }  // namespace
 
+namespace {
+constexpr int DEC_LDS_FR = 32 * 1024;  // the FR forms: the X image region only
+hipError_t dec_lds_attr() {
+  static bool attr = false;
+  if (attr) return hipSuccess;
+  for (const void* f : {(const void*)dec_sa_kernel<false>, (const void*)dec_ffn_kernel<false>,
+                        (const void*)dec_chain_kernel<false>}) {
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, DEC_LDS);
+    if (e != hipSuccess) return e;
+  }
+  attr = true;
+  return hipSuccess;
+}
+}  // namespace
+
 hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N2 != DEC_D || a.H <= 0 || (a.nsplit != 1 && a.nsplit != 2)) return hipErrorInvalidValue;
   if (a.out != OUT_PARTIAL && a.out != OUT_SPLIT) return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)dec_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             DEC_LDS);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  if (!a.W1f != !a.W2f || (a.W1f && a.H != DEC_H)) return hipErrorInvalidValue;
+  const hipError_t e = dec_lds_attr();
+  if (e != hipSuccess) return e;
   const int blocks = (a.M + DEC_ROWS - 1) / DEC_ROWS * a.H;
-  hipLaunchKernelGGL(dec_chain_kernel, dim3(blocks), dim3(1024), DEC_LDS, s, a);
+  if (a.W1f) hipLaunchKernelGGL(dec_chain_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  else hipLaunchKernelGGL(dec_chain_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s) {
   if (a.rows <= 0 || a.t0 < 0 || a.t0 >= a.Lmax || a.t0 >= 64 || (a.nsplit != 1 && a.nsplit != 2))
     return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    for (const void* f : {(const void*)dec_sa_kernel, (const void*)dec_ffn_kernel}) {
-      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, DEC_LDS);
-      if (e != hipSuccess) return e;
-    }
-    attr = true;
-  }
+  if (!a.Wqkv_f != !a.Wo_f) return hipErrorInvalidValue;
+  const hipError_t e = dec_lds_attr();
+  if (e != hipSuccess) return e;
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * DEC_H;
-  hipLaunchKernelGGL(dec_sa_kernel, dim3(blocks), dim3(1024), DEC_LDS, s, a);
+  if (a.Wqkv_f) hipLaunchKernelGGL(dec_sa_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  else hipLaunchKernelGGL(dec_sa_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s) {
   if (a.rows <= 0 || (a.nsplit != 1 && a.nsplit != 2)) return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)dec_ffn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             DEC_LDS);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  if (!a.W1f != !a.W2f) return hipErrorInvalidValue;
+  const hipError_t e = dec_lds_attr();
+  if (e != hipSuccess) return e;
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * (DEC_F / 128);
-  hipLaunchKernelGGL(dec_ffn_kernel, dim3(blocks), dim3(1024), DEC_LDS, s, a);
+  if (a.W1f) hipLaunchKernelGGL(dec_ffn_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  else hipLaunchKernelGGL(dec_ffn_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_frag_pack(const bf16_t* W, long ldw, int ntiles, int nk, int mode, int tps, int ksl, bf16_t* out,
+                            hipStream_t s) {
+  if (!W || !out || ntiles <= 0 || nk <= 0 || mode < 0 || mode > 2 || (mode == 2 && (tps <= 0 || ksl <= 0)))
+    return hipErrorInvalidValue;
+  const long n = (long)ntiles * nk * 64;
+  hipLaunchKernelGGL(frag_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, ldw, ntiles, nk, mode,
+                     tps, ksl, out);
   return hipGetLastError();
 }

@@ -109,6 +109,10 @@ struct DecLayer {
   bf16_t* ca_v = nullptr;   // [d_model][d_model] = rows [2d, 3d) of in_proj (per-head slices of 64 rows)
   float* ca_vb = nullptr;   // bias rows [2d, 3d)
   LN n1, n2, n3;
+  // MFMA fragment images of the fused decode blocks' weights (launch_frag_pack; d 512 / 8 heads / dim_ff 2048 only):
+  // the blocks load them straight into registers instead of staging weight slices through LDS
+  bf16_t *f_qkv = nullptr, *f_sao = nullptr, *f_caq = nullptr, *f_kT = nullptr, *f_cav = nullptr, *f_cao = nullptr,
+         *f_l1 = nullptr, *f_l2 = nullptr;
 };
 
 }  // namespace
@@ -504,6 +508,24 @@ void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PA
     o.n1 = h->ln(L.norm1, D, s);
     o.n2 = h->ln(L.norm2, D, s);
     o.n3 = h->ln(L.norm3, D, s);
+    // round 4: register-direct weight fragments for the fused decode blocks (tools knob ICAP_DEC_FRAG=0: the LDS-staged
+    // forms, for A/B)
+    static const int frag_on = icap_knob("ICAP_DEC_FRAG", 1);
+    if (frag_on && D == 512 && d.nhead == 8 && F == 2048) {
+      auto fp = [&](const bf16_t* w, long ldw, int ntiles, int nk, int mode, int tps, int ksl) {
+        bf16_t* out = (bf16_t*)h->alloc((size_t)ntiles * nk * 512 * 2);
+        HIPCHK(launch_frag_pack(w, ldw, ntiles, nk, mode, tps, ksl, out, s));
+        return out;
+      };
+      o.f_qkv = fp(o.sa_qkv.w, D, 96, 16, 1, 0, 0);
+      o.f_sao = fp(o.sa_out.w, D, 256, 2, 2, 32, 64);
+      o.f_caq = fp(o.ca_q.w, D, 32, 16, 0, 0, 0);
+      o.f_kT = fp(o.ca_kT, 64, 256, 2, 0, 0, 0);
+      o.f_cav = fp(o.ca_v, D, 32, 16, 0, 0, 0);
+      o.f_cao = fp(o.ca_out.w, D, 256, 2, 2, 32, 64);
+      o.f_l1 = fp(o.lin1.w, D, 128, 16, 0, 0, 0);
+      o.f_l2 = fp(o.lin2.w, F, 512, 4, 2, 32, 128);
+    }
     h->dec.push_back(o);
   }
   if (!h->repack) h->dec_allocs = h->owned.size();
@@ -1030,7 +1052,7 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   w.kv.ensure((size_t)2 * d.n_dec_layers * kv_rows * H * Lmax * 64 * 4);
   w.part.ensure((size_t)XDEC_SLABS * rows * D * 4);  // (the split-K slabs use MAX_KSPLIT of them)
   w.gs.ensure((size_t)rows * H * 4);
-  const bool xsplit = cross_attn_splits(S) > 1 || (ns == 2 && cross_attn_f16_splits() > 1);
+  const bool xsplit = cross_attn_splits(S) > 1 || (ns == 2 && (cross_attn_f16_splits() > 1 || cross_attn_f16s_on()));
   if (xsplit) w.xpart.ensure(cross_attn_part_floats(rows) * 4);
   if (xsplit && w.xcnt.n < (size_t)rows * 4) {  // tickets: zero at rest (each launch resets its own)
     w.xcnt.ensure((size_t)rows * 4);
@@ -1099,6 +1121,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       DecSaArgs sa{};
       sa.A = b.a; sa.aL = b.aL; sa.nsplit = ns; sa.rows = rows;
       sa.Wqkv = L.sa_qkv.w; sa.bqkv = L.sa_qkv.b; sa.Wo = L.sa_out.w;
+      sa.Wqkv_f = L.f_qkv; sa.Wo_f = L.f_sao;
       sa.kc = b.kc + l * kv_layer; sa.vc = b.vc + l * kv_layer; sa.Lmax = Lmax; sa.t0 = t0; sa.scale = 0.125f;
       sa.anc = anc;
       sa.part = b.part; sa.part_stride = PS;
@@ -1131,6 +1154,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.W2 = L.ca_kT; c.ldw2 = 64; c.w2_hstride = (long)D * 64;
       c.C = b.qt; c.ldc = (long)H * D; c.c_lo = b.cL; c.c_hstride = D;
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_SPLIT;
+      if (fused) c.W1f = L.f_caq, c.W2f = L.f_kT;
       h->chain(c, s, fused);
     }
     h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * (double)(rows / mem_rpi) * S * D, s, [&] {
@@ -1156,6 +1180,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.C = b.part; c.ldc = D; c.part_stride = PS;
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_PARTIAL;
       if (drop) c.b1_scale = b.gs;  // the value bias weighs sum_s P_s m_s under probability dropout
+      if (fused) c.W1f = L.f_cav, c.W2f = L.f_cao;
       h->chain(c, s, fused);
     }
     HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, wl ? KS_D : H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a,
@@ -1165,6 +1190,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       DecFfnArgs ff{};
       ff.A = b.a; ff.aL = b.aL; ff.nsplit = ns; ff.rows = rows;
       ff.W1 = L.lin1.w; ff.b1 = L.lin1.b; ff.W2 = L.lin2.w;
+      ff.W1f = L.f_l1; ff.W2f = L.f_l2;
       ff.part = b.part; ff.part_stride = PS;
       ff.drop = dl;
       h->timed(PROF_DEC_FUSED, 4.0 * rows * (double)D * F, 2.0 * (2.0 * D * F + (double)rows * D * ns), s,
@@ -1852,7 +1878,8 @@ const char* icap_knobs_set() {
       "ICAP_GEMM_TALL_KS", "ICAP_I8_NOMFMA", "ICAP_I8_GROUP", "ICAP_I8_NT_STORE", "ICAP_I8_TILE",
       "ICAP_ENC_ATTN_PIPE", "ICAP_ENC_ATTN_QPW", "ICAP_XATTN_KS", "ICAP_POISON", "ICAP_GEMM_TAIL",
       "ICAP_QKV_HEAD_MAJOR", "ICAP_DEC_MIN_ROWS", "ICAP_I8_MLP2", "ICAP_DEC_BRANCHES", "ICAP_F16_GEMM",
-      "ICAP_F16_PRES", "ICAP_XATTN16_KS", "ICAP_XATTN16_CK", "ICAP_ENC_ATTN16_QPW", "ICAP_F16_PP",
+      "ICAP_F16_PRES", "ICAP_XATTN16_KS", "ICAP_XATTN16_CK", "ICAP_ENC_ATTN16_QPW", "ICAP_F16_PP", "ICAP_DEC_FRAG",
+      "ICAP_ENC_ATTN16_FULL", "ICAP_XATTN16_S", "ICAP_EAF_ABL",
       "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
       "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE", "ICAP_XDEC_TRACE", "ICAP_GEMM_NARROW",
       "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW"};
@@ -2330,6 +2357,12 @@ int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uin
   });
 }
 
+int icap_op_enc_attention_hm(const uint16_t* qkv, int B, int N, int H, uint16_t* out, void* stream) {
+  return guarded([&] {
+    HIPCHK(launch_enc_attention(qkv, 0, 0, B, N, H, 0.125f, out, (long)H * 64, 0, NS_F16, (hipStream_t)stream, 1));
+  });
+}
+
 size_t icap_decoder_train_workspace(const icap_model_desc* d, int B, int T, int S, float drop_p) {
   if (!d) return 0;
   return TrainWS(*d, B, T, S, nullptr, drop_p).floats * sizeof(float);
@@ -2414,8 +2447,15 @@ uint32_t icap_drop_hash_host(uint32_t seed, uint32_t site, uint32_t layer, uint3
 int icap_op_cross_attn(const uint16_t* qt, long qt_lo, const uint16_t* mem16, int rows, int rows_per_image, int S,
                        uint16_t* out, long out_lo, void* stream) {
   return guarded([&] {
+    // the key-split form's partial states and tickets (op entry: a process-wide workspace, tickets zero at rest)
+    static DevBuf xp, xc;
+    if (rows > 0 && xc.n < (size_t)rows * 4) {
+      xp.ensure(cross_attn_part_floats(rows) * 4);
+      xc.ensure((size_t)rows * 4);
+      HIPCHK(hipMemset(xc.p, 0, xc.n));
+    }
     HIPCHK(launch_cross_attn_f16(qt, qt_lo, mem16, rows, rows_per_image, S, 0.125f, out, out_lo,
-                                 (hipStream_t)stream));
+                                 (hipStream_t)stream, DropCfg{}, nullptr, xp.as<float>(), xc.as<int>()));
   });
 }
 

@@ -176,6 +176,9 @@ struct ChainArgs {
   // dec_chain only: b1 scaled per (row, head) by b1_scale[row * H + h] - the value projection of the
   // key-absorbed cross-attention under probability dropout, whose bias enters as sum_s P_s m_s (not 1)
   const float* b1_scale;
+  // dec_chain only (frag_pack images, both or neither): W1 of head h as tiles h * 4 + t x 16 k32-steps, W2 as tiles
+  // h * 32 + n x 2 k32-steps - each wave loads its own fragments straight into registers (no LDS weight staging)
+  const bf16_t* W1f; const bf16_t* W2f;
 };
 hipError_t launch_chain_dec(const ChainArgs& a, hipStream_t s);
 
@@ -189,6 +192,9 @@ struct DecSaArgs {
   float *kc, *vc; int Lmax, t0; float scale; const int32_t* anc;
   float* part; long part_stride;
   DropCfg drop;  // thr 0: no dropout (site 1: the attention probabilities)
+  // frag_pack images (both or neither): Wqkv as tiles h * 12 + i (q 0-3, k 4-7, v 8-11) x 16 k32-steps (mode 1), Wo
+  // as tiles h * 32 + n x 2 k32-steps (mode 2, ksl 64)
+  const bf16_t* Wqkv_f; const bf16_t* Wo_f;
 };
 hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s);
 // dec_ffn: slab j of 16 = relu(a W1[128j:128j+128]^T + b1) W2[:, 128j:128j+128]^T -> part[j][rows][512]
@@ -197,11 +203,20 @@ struct DecFfnArgs {
   const bf16_t* W1; const float* b1; const bf16_t* W2;
   float* part; long part_stride;
   DropCfg drop;  // site 5: the hidden activations (pos = the decode position)
+  // frag_pack images (both or neither): W1 as tiles 0..127 x 16 k32-steps, W2 as tiles j * 32 + n x 4 k32-steps
+  const bf16_t* W1f; const bf16_t* W2f;
 };
 hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s);
 // The chained per-head cross-attention products (ChainArgs as launch_chain_dec, N2 = 512) with 16-row
 // blocks and one full-line DMA round (decode.hip); used by the decode loops.
 hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s);
+// MFMA fragment image of a bf16 matrix W [rows][ldw] for the decode blocks' register-direct weight loads: tile t,
+// 32-deep k-step s -> 64 lanes x 16 B at out + (t * nk + s) * 512 elements, lane l = W[row0(t) + (l & 15)][k0(t) + 32 s
+// + 8 (l >> 4) ..+7] (the A-operand fragment of v_mfma_f32_16x16x32 as frag() reads it from an LDS row image).
+// mode 0: row0 = 16 t, k0 = 0; mode 1 (self-attention in_proj, d 512, 8 heads): t = 12 h + i, row0 = 512 (i >> 2) +
+// 64 h + 16 (i & 3); mode 2 (column slices): t = tps j + n, row0 = 16 n, k0 = ksl j.
+hipError_t launch_frag_pack(const bf16_t* W, long ldw, int ntiles, int nk, int mode, int tps, int ksl, bf16_t* out,
+                            hipStream_t s);
 
 // Persistent decode step (decstep.hip): all decoder layers of one decode step (one new token per row) in ONE
 // launch of one 1024-thread workgroup per CU.  Work items are tasks of 16-row tiles - self-attention per head,
@@ -363,6 +378,9 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
 int cross_attn_splits(int S);
 // blocks per row pair of launch_cross_attn_f16 (2: key split, needs xpart / xcnt as launch_cross_attn_mfma)
 int cross_attn_f16_splits();
+// the key-split single-burst fp16 cross-attention (cross_attn_f16s_kernel: one row per image, no dropout, S <= 256;
+// needs xpart / xcnt) is on
+bool cross_attn_f16s_on();
 size_t cross_attn_part_floats(int rows);
 // Batched beam search (beam.hip): state init, per-step selection, final pick.
 hipError_t launch_beam_init(int B, int K, int start, int Lmax, int32_t* seq_a, int32_t* seq_b, int32_t* anc_a,

@@ -344,6 +344,10 @@ int icap_decoder_train_backward(const icap_model_desc* d, const icap_model_desc*
 /* qkv planes (B*N, 3*H*64) -> out planes (B*N, H*64), non-causal softmax(QK^T/8)V. */
 int icap_op_enc_attention(const uint16_t* qkv, long lo, int B, int N, int H, uint16_t* out, long out_lo,
                           int nsplit, void* stream);
+/* The f16 ViT encoder's attention on the head-major fp16 qkv the QKV GEMM writes ([B][q|k|v][H][N][64], GemmArgs::hm_n)
+ * -> out fp16 (B*N, H*64); N in (64, 256] (replaces the self-attention of torchvision's EncoderBlock,
+ * models/vit_transformer_model.py:71-100 through VisionTransformer.encoder). */
+int icap_op_enc_attention_hm(const uint16_t* qkv, int B, int N, int H, uint16_t* out, void* stream);
 /* Decoder cross-attention, key-absorbed (the decode loops' form): q~ (rows, 8, 512) as bf16 hi/lo planes
  * (plane stride qt_lo), memory (rows / rows_per_image, S, 512) as one fp16 plane; row r attends to image
  * r / rows_per_image: out[r][h] = softmax_s(q~[r][h] . mem[s] / 8) . mem -> (rows, 8, 512) bf16 hi/lo

@@ -16,8 +16,8 @@ Checks and tolerances (north star: logits within 1e-3, token ids identical):
     cannot pass);
   * greedy: the oracle's teacher-forced logits on the HIP ids (every row, every step) within 1e-3 of
     the HIP step logits; each HIP token = the oracle argmax wherever the oracle's top-2 margin exceeds
-    2x the measured logit error (then by induction the HIP ids ARE the oracle's greedy ids up to the
-    first near-tie; the number of such gated steps is asserted tiny);
+    2x the measured logit error; and the oracle's own greedy decode on all rows: every row id-identical
+    to it, except at most 3 rows whose first differing token comes from a near-tie step (counts printed);
   * sampled: each HIP token = the oracle's inverse-CDF draw on the same uniform wherever the draw is
     further than 2x the measured probability error from a CDF boundary; log-probs within 1e-3 (zero
     after <end>, the reference's masked_fill);
@@ -59,7 +59,7 @@ def _oracle_memory(fn, sd_dev, imgs, chunk=64):
         return torch.cat([fn(sd_dev, imgs[i:i + chunk]) for i in range(0, imgs.shape[0], chunk)])
 
 
-GATED_ROWS_MAX = 3  # rows allowed a near-tie step (verdict r3 item 5): every other row is id-identical to the oracle
+DIVERGED_ROWS_MAX = 3  # rows whose ids may leave the oracle's greedy ids (at a near-tie step only; verdict r3 item 5)
 
 
 def _check_greedy(ids, step_logits, sd_dev, mem_o, end, tag=""):
@@ -67,10 +67,11 @@ def _check_greedy(ids, step_logits, sd_dev, mem_o, end, tag=""):
 
     1. The oracle's teacher-forced logits on the HIP ids: within 1e-3 of the HIP step logits on every row and step.
     2. The oracle's OWN greedy decode (O.greedy_from_memory, the reference's _greedy_search loop, vit:296-325) on the
-       oracle memory: the HIP ids equal it on every row up to that row's first near-tie step - a step whose oracle
-       top-2 margin is within twice that row-step's measured HIP-vs-oracle logit error, where either token is a
-       correct reading of the reference - and on the whole row when it has none.  The number of rows with a near-tie
-       is printed and pinned to GATED_ROWS_MAX."""
+       oracle memory, compared on every row: the rows are id-identical to it, except rows whose FIRST differing token
+       comes from a near-tie step - a step whose oracle top-2 margin is within twice that row-step's measured
+       HIP-vs-oracle logit error, where either token is a correct reading of the reference (after it the two decodes
+       feed different tokens).  Those rows are counted, printed with the near-tie step count, and pinned to
+       DIVERGED_ROWS_MAX; a difference at a confident step fails."""
     ids = ids.long()
     tf = O.teacher_forced_logits(sd_dev, mem_o, ids)                      # (B, L-1, V)
     hip = step_logits.permute(1, 0, 2)
@@ -85,17 +86,20 @@ def _check_greedy(ids, step_logits, sd_dev, mem_o, end, tag=""):
     with torch.no_grad():
         o_ids = O.greedy_from_memory(sd_dev, mem_o, W.START_TOKEN, end, ids.shape[1])
     assert o_ids.shape == ids.shape  # random-init weights: no batch-global stop before max_len
-    gated_rows = 0
+    diverged = 0
     for r in range(ids.shape[0]):
-        near = torch.nonzero(~sure[r]).flatten()
-        upto = int(near[0]) + 1 if len(near) else ids.shape[1]           # positions 0..k0 come from sure steps
-        gated_rows += bool(len(near))
-        assert torch.equal(ids[r, :upto], o_ids[r, :upto]), (r, upto)
+        diff = torch.nonzero(ids[r] != o_ids[r]).flatten()
+        if len(diff) == 0:
+            continue
+        c = int(diff[0])                    # >= 1 (both start with START); token c comes from step c - 1
+        assert not bool(sure[r, c - 1]), (r, c, "first difference at a confident step")
+        diverged += 1
+    near_rows = int((~sure).any(-1).sum())
     print(f"\n[{tag}] greedy vs oracle greedy: {ids.shape[0]} rows, max logit err {err:.2e}, "
-          f"near-tie steps {int((~sure).sum())}, rows id-identical to the oracle {ids.shape[0] - gated_rows}, "
-          f"rows gated at a near-tie {gated_rows}")
-    assert gated_rows <= GATED_ROWS_MAX, f"{gated_rows} rows with a near-tie step"
-    return err, gated_rows
+          f"near-tie steps {int((~sure).sum())} (in {near_rows} rows), rows id-identical to the oracle "
+          f"{ids.shape[0] - diverged}, rows diverging at a near-tie {diverged}")
+    assert diverged <= DIVERGED_ROWS_MAX, f"{diverged} rows diverge from the oracle greedy at a near-tie"
+    return err, diverged
 
 
 def test_config2_vit_b256_every_row(cuda, vit_sd):

@@ -117,11 +117,14 @@ def test_enc_attention(cuda, B, N, H, nsplit):
     assert (got - ref).abs().max().item() < tol
 
 
-@pytest.mark.parametrize("rows,rpi,S", [(256, 1, 196), (40, 5, 196), (24, 3, 49), (6, 2, 1), (8, 1, 70)])
+@pytest.mark.parametrize("rows,rpi,S", [(256, 1, 196), (40, 5, 196), (24, 3, 49), (6, 2, 1), (8, 1, 70),
+                                        (37, 1, 49), (5, 1, 1), (16, 1, 17), (9, 1, 256), (3, 1, 33), (85, 1, 196)])
 def test_cross_attn_f16(cuda, rows, rpi, S):
     """Key-absorbed decoder cross-attention over one fp16 memory plane (decode loops, beam slots and
     teacher-forced rows of an image share a block): against fp64 softmax(q~ mem^T / 8) mem on the same
-    rounded operands, ragged last chunks (S = 196, 70, 49, 1) and odd rows per image."""
+    rounded operands, ragged last chunks (S = 196, 70, 49, 1) and odd rows per image.  One row per image runs the
+    key-split form (cross_attn_f16s_kernel: two workgroups per row merged by the second to finish): S = 1 and 17
+    leave part 1 with no / one key, S = 256 fills 8 key tiles, rows not a multiple of 8 pad the grid."""
     L, lib = _lib()
     g = torch.Generator(device="cpu").manual_seed(rows * 7 + S)
     B = rows // rpi
@@ -138,6 +141,13 @@ def test_cross_attn_f16(cuda, rows, rpi, S):
     torch.cuda.synchronize()
     got = value(out, 2).double().cpu()
     assert (got - ref).abs().max().item() < 2e-4
+    if rpi == 1:  # the merge of the two halves is order-independent: repeated launches are bitwise equal
+        for _ in range(3):
+            again = torch.zeros_like(out)
+            L.check(lib.icap_op_cross_attn(Q.data_ptr(), rows * 8 * 512, mem.to(cuda).data_ptr(), rows, rpi, S,
+                                           again.data_ptr(), rows * 8 * 512, L.stream_ptr()), "cross_attn")
+            torch.cuda.synchronize()
+            assert torch.equal(again, out)
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1, 0.5])
@@ -542,3 +552,26 @@ def test_enc_attention_f16(cuda, B, N, H):
     L.check(lib.icap_op_enc_attention(qkv.data_ptr(), 0, B, N, H, out.data_ptr(), 0, -1, L.stream_ptr()), "attn f16")
     torch.cuda.synchronize()
     assert (out.double() - ref).abs().max().item() < 4e-3
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (3, 100, 8), (1, 65, 2), (2, 256, 4), (5, 208, 3)])
+def test_enc_attention_f16_head_major(cuda, B, N, H):
+    """The f16 ViT encoder's attention on the head-major qkv its QKV GEMM writes ([B][q|k|v][H][N][64]): the
+    whole-sequence form (enc_attention_full_kernel: every key of an (image, head) in LDS, one exact softmax) against
+    fp64, ragged last key tiles (N = 197, 100, 65) and full ones (256, 208); repeated launches bitwise equal."""
+    L, lib = _lib()
+    D = H * 64
+    g = torch.Generator(device="cpu").manual_seed(B * N + H + 7)
+    hm = (torch.randn(B, 3, H, N, 64, generator=g) * 1.5).to(torch.float16)
+    v = hm.double()
+    ref = torch.softmax(v[:, 0] @ v[:, 1].transpose(-1, -2) / 8.0, -1) @ v[:, 2]  # (B, H, N, 64)
+    ref = ref.transpose(1, 2).reshape(B * N, D)
+    qkv = hm.to(cuda).contiguous()
+    out = torch.zeros(B * N, D, device=cuda, dtype=torch.float16)
+    L.check(lib.icap_op_enc_attention_hm(qkv.data_ptr(), B, N, H, out.data_ptr(), L.stream_ptr()), "attn f16 hm")
+    torch.cuda.synchronize()
+    assert (out.double().cpu() - ref).abs().max().item() < 4e-3
+    again = torch.zeros_like(out)
+    L.check(lib.icap_op_enc_attention_hm(qkv.data_ptr(), B, N, H, again.data_ptr(), L.stream_ptr()), "attn f16 hm")
+    torch.cuda.synchronize()
+    assert torch.equal(again, out)

@@ -22,3 +22,8 @@ sys.exit(pytest.main(['tests/test_gpu_6_ops.py','tests/test_gpu_1_parity.py','te
 " > $O/${T}_ops$f.log 2>&1 || { tail -30 $O/${T}_ops$f.log; exit 1; }
   tail -3 $O/${T}_ops$f.log
 done
+# the key-split cross-attention (product build): op tests, then the decode parity tests
+timeout -k 10 300 python -u -m pytest tests/test_gpu_6_ops.py -m gpu -x -q -k cross_attn --timeout 120 --timeout-method thread > $O/${T}_xattn.log 2>&1 || { tail -30 $O/${T}_xattn.log; exit 1; }
+tail -2 $O/${T}_xattn.log
+timeout -k 10 200 python bench.py --no-cpu-baseline --steps 10 --warmup 2 > $O/${T}_bench.json 2> $O/${T}_bench.err || { tail -20 $O/${T}_bench.err; exit 1; }
+python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); p=d["roofline"]["phases"]; print("bench", d["value"], d["ms_per_step"], p["encoder"]["ms_per_step"], p["decode"]["ms_per_step"])' $O/${T}_bench.json
