@@ -532,24 +532,30 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
 // reads.  Against enc_attention_pipe_kernel (7 chunks of 32 keys, a counted wait + barrier and an online-softmax
 // rescale per chunk, 2 blocks per CU at 98.5 us per ViT layer): no chunk loop, one barrier, and 3 workgroups per CU
 // (50 KiB each) keep 12 waves resident.  Swizzles as the pipelined form (kswz / vswz over the whole image).
-constexpr int EAF_MAXKT = 16;
+// NKT = ceil(N / 16) is a template parameter: every score register, key tile and guard is compile-time, so the
+// softmax is straight-line (a runtime key count made hipcc guard each of 16 possible tiles: 2.4x the VALU
+// instructions per query tile, and VALU is what bounds this kernel - timing ablations, tools/r4_eaf.sh: 110 us per
+// ViT launch, 33 us of it loads only, 74 us without any loads).  The 1/8 scale is folded into the exponent's FMA
+// (the maximum is taken over the raw scores).
 // abl (tools knob ICAP_EAF_ABL, timing ablations; 0 in a product build): 1 = loads only, 2 = no K / V / Q loads,
 // 3 = no output stores
+template <int NKT>
 __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t* __restrict__ qkv, int N, int H,
                                                                      float scale, bf16_t* out, long out_ld, int abl) {
+  constexpr int NQW = (NKT + 3) / 4;  // query tiles per wave (tiles w, w + 4, ...)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int h = blockIdx.x, b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, g = lane >> 4;
-  const int nkt = (N + 15) >> 4;             // key tiles
   const bf16_t* qb = qkv + ((long)b * 3 * H + h) * N * 64;  // [q|k|v x head][token][64]
   const bf16_t* kb = qb + (long)H * N * 64;
   const bf16_t* vb = qb + 2L * H * N * 64;
-  char* const Ks = smem;                    // [nkt * 16 rows][128 B]
-  char* const Vs = smem + nkt * 16 * 128;   // [nkt * 16 rows][128 B]
-  // stage: instruction i = 8 rows x 128 B of K (i < nkt * 2) or V; rows >= N read row N - 1 (finite; masked / P = 0)
+  char* const Ks = smem;                    // [NKT * 16 rows][128 B]
+  char* const Vs = smem + NKT * 16 * 128;   // [NKT * 16 rows][128 B]
+  // stage: instruction i = 8 rows x 128 B of K (i < NKT * 2) or V; rows >= N read row N - 1 (finite; masked / P = 0)
   {
-    const int lrow = lane >> 3, lch = lane & 7, ni = nkt * 2;
+    const int lrow = lane >> 3, lch = lane & 7;
+    constexpr int ni = NKT * 2;
     for (int i = wave; i < (abl == 2 ? 0 : 2 * ni); i += 4) {
       const bool isK = i < ni;
       const int row = (isK ? i : i - ni) * 8 + lrow;
@@ -558,12 +564,11 @@ __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t
       lds_dma16(src, (LDS_AS void*)((isK ? Ks : Vs) + (isK ? i : i - ni) * 1024));
     }
   }
-  const int nqt = nkt;
-  // every query tile of this wave (w, w + 4, ... : at most EAF_MAXKT / 4) loaded into registers in the same burst as
-  // the K / V DMA, so no tile pays its own global-load latency after the barrier
-  bf16x8 qreg[EAF_MAXKT / 4][2];
+  // every query tile of this wave loaded into registers in the same burst as the K / V DMA, so no tile pays its own
+  // global-load latency after the barrier
+  bf16x8 qreg[NQW][2];
 #pragma unroll
-  for (int qi = 0; qi < EAF_MAXKT / 4; ++qi) {
+  for (int qi = 0; qi < NQW; ++qi) {
     const int q = min((wave + 4 * qi) * 16 + fr, N - 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -578,16 +583,14 @@ __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t
   const float sc2 = scale * 1.44269504088896341f;  // exp2 domain
   const int q4 = fr >> 2, p4 = fr & 3;
 #pragma unroll
-  for (int qi = 0; qi < EAF_MAXKT / 4; ++qi) {
+  for (int qi = 0; qi < NQW; ++qi) {
     const int qt = wave + 4 * qi;
-    if (qt >= nqt) continue;  // (uniform per wave)
+    if (qt >= NKT) continue;  // (uniform per wave)
     const bf16x8* const qh = qreg[qi];
-    // scores: lane holds query fr, keys 16 kt + 4 g + r
-    f32x4 s[EAF_MAXKT];
+    // raw scores: lane holds query fr, keys 16 kt + 4 g + r
+    f32x4 s[NKT];
 #pragma unroll
-    for (int kt = 0; kt < EAF_MAXKT; ++kt) {
-      s[kt] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-      if (kt >= nkt) continue;  // (uniform; every index stays a compile-time one: no private array)
+    for (int kt = 0; kt < NKT; ++kt) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       const int row = kt * 16 + fr;
 #pragma unroll
@@ -595,40 +598,51 @@ __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t
         const bf16x8 kh = *(const bf16x8*)(Ks + row * 128 + (((ks * 4 + g) ^ kswz(row)) << 4));
         acc = mma<true>(kh, qh[ks], acc);
       }
-      s[kt] = acc * sc2;
-      if (kt * 16 + 16 > N) {  // (uniform) the ragged last tile; kt is a compile-time index (no private array)
+      s[kt] = acc;
+    }
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (kt * 16 + g * 4 + r >= N) s[kt][r] = -INFINITY;
+    for (int r = 0; r < 4; ++r)  // the last tile's keys >= N
+      if ((NKT - 1) * 16 + g * 4 + r >= N) s[NKT - 1][r] = -INFINITY;
+    // maximum: v_max3 from asm (fmaxf would canonicalise every MFMA result first: one extra v_max per score)
+    float mx = s[0][0];
+    auto max3 = [](float a, float b, float c) {
+      float r;
+      asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+      return r;
+    };
+    mx = max3(mx, s[0][1], s[0][2]);
+    mx = max3(mx, s[0][3], s[1 < NKT ? 1 : 0][0]);
+#pragma unroll
+    for (int i = 5; i < 4 * NKT; i += 2)
+      mx = i + 1 < 4 * NKT ? max3(mx, s[i / 4][i % 4], s[(i + 1) / 4][(i + 1) % 4]) : max3(mx, s[i / 4][i % 4], mx);
+    const float mxs = rows4_max(mx) * sc2;
+    // exponent and row sum on packed fp32 pairs (v_pk_fma_f32 / v_pk_add_f32)
+    const f32x2 sc2v = {sc2, sc2}, nmx = {-mxs, -mxs};
+    f32x2 l2 = {0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const f32x2 t = __builtin_elementwise_fma((f32x2){s[kt][r], s[kt][r + 1]}, sc2v, nmx);
+        s[kt][r] = __builtin_amdgcn_exp2f(t[0]);
+        s[kt][r + 1] = __builtin_amdgcn_exp2f(t[1]);
+        l2 += (f32x2){s[kt][r], s[kt][r + 1]};
       }
     }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < EAF_MAXKT; ++kt)
-      if (kt < nkt) mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
-    mx = rows4_max(mx);
-    float l = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < EAF_MAXKT; ++kt) {
-      if (kt >= nkt) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s[kt][r] = __builtin_amdgcn_exp2f(s[kt][r] - mx);
-      l += (s[kt][0] + s[kt][1]) + (s[kt][2] + s[kt][3]);
-    }
-    l = rows4_sum(l);
+    const float l = rows4_sum(l2[0] + l2[1]);
     // O = P V: key-tile pairs (2 c, 2 c + 1) as one 32-deep k-step; P (fp16) element j < 4 -> key 4 g + j of the
-    // first tile, j >= 4 -> of the second (a tile past nkt contributes zeros)
+    // first tile, j >= 4 -> of the second (odd NKT: the last pair's second tile contributes zeros)
     f32x4 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < EAF_MAXKT / 2; ++c) {
-      if (2 * c >= nkt) continue;
-      const f32x4 s1 = 2 * c + 1 < nkt ? s[2 * c + 1] : (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < (NKT + 1) / 2; ++c) {
+      constexpr f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 s1 = 2 * c + 1 < NKT ? s[2 * c + 1 < NKT ? 2 * c + 1 : 0] : z;
       const u32x2 p0 = pack16x4<true>(s[2 * c]), p1 = pack16x4<true>(s1);
       const bf16x8 ph = __builtin_bit_cast(bf16x8, (u32x4){p0[0], p0[1], p1[0], p1[1]});
       const int key0 = c * 32 + 4 * g + q4;  // and key0 + 16 (vswz has period 8)
-      const int second = 2 * c + 1 < nkt ? 16 * 128 : 0;  // past the last tile: re-read tile 2 c (finite, P = 0)
+      const int second = 2 * c + 1 < NKT ? 16 * 128 : 0;  // past the last tile: re-read tile 2 c (finite, P = 0)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const int off0 = key0 * 128 + (((dt * 2 + (p4 >> 1)) ^ vswz(key0)) << 4) + (p4 & 1) * 8;
@@ -650,6 +664,21 @@ __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t
       if (qq < N && (abl != 3 || w[0] == 0x12345678u)) *(u32x4*)(dst + (odd ? (dt + 1) * 16 - 4 : dt * 16)) = w;
     }
   }
+}
+
+template <int NKT>
+hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf16_t* out, long out_ld, int abl,
+                        hipStream_t s) {
+  constexpr int lds = 2 * NKT * 16 * 128;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_full_kernel<NKT>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(enc_attention_full_kernel<NKT>, dim3(H, B), dim3(256), lds, s, qkv, N, H, scale, out, out_ld, abl);
+  return hipGetLastError();
 }
 
 template <int NKT, bool SPLIT>
@@ -691,18 +720,21 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
     // form)
     static const int full = icap_knob("ICAP_ENC_ATTN16_FULL", 1);
     if (head_major && full) {
-      const int lds_full = 2 * ((N + 15) / 16) * 16 * 128;
-      static bool fattr = false;
-      if (!fattr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_full_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 16 * 16 * 128);
-        if (e != hipSuccess) return e;
-        fattr = true;
-      }
       static const int abl = icap_knob("ICAP_EAF_ABL", 0);
-      hipLaunchKernelGGL(enc_attention_full_kernel, dim3(H, B), dim3(256), lds_full, s, qkv, N, H, scale, out, out_ld,
-                         abl);
-      return hipGetLastError();
+      switch ((N + 15) / 16) {  // N in (64, 256]
+        case 5: return run_enc_full<5>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 6: return run_enc_full<6>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 7: return run_enc_full<7>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 8: return run_enc_full<8>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 9: return run_enc_full<9>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 10: return run_enc_full<10>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 11: return run_enc_full<11>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 12: return run_enc_full<12>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 13: return run_enc_full<13>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 14: return run_enc_full<14>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 15: return run_enc_full<15>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        default: return run_enc_full<16>(qkv, B, N, H, scale, out, out_ld, abl, s);
+      }
     }
     if (head_major && qpw16 == 2)
       hipLaunchKernelGGL((enc_attention_pipe_kernel<false, true, 2, true>), dim3(H, B), dim3(512), lds, s, qkv, ld, lo,
@@ -1262,6 +1294,165 @@ constexpr int XA16_LDS = xa16_lds(64);
 // planes - the layout cross_attn_f16_kernel writes.  The pair shares an XCD under round-robin dispatch (blocks b and
 // b + 8; speed only).  LDS: KTE x 16 keys x 1 KiB (KTE = KT rounded up to even; keys past S read row S - 1, P = 0)
 // + 9 KiB.
+#ifdef ICAP_TOOLS
+// ------------------------------------------------------------------------------------------------
+// Cross-attention, wave-owned key tiles (round 4; one decoder row per memory image, no dropout, S <= 256: the greedy /
+// sampled decode).  One 8-wave workgroup per row; wave w owns key tiles w, w + 8 (16 keys each) and runs its own
+// online softmax over them - no block barrier until the final merge:
+//   stage    the tile's 16 key rows (16 KiB) by LDS-DMA into the wave's own region, one counted wait
+//   scores   16 MFMA 16x16x32 f16, A = the key rows, B = q~ as 16 columns = 8 heads x {fp16 hi, fp16 lo} (column
+//            n + 8 added to n by a DPP row rotate, both then hold the head's score)
+//   context  32 MFMA 16x16x16 f16 (one per 16-dim tile), A = memory^T by ds_read_b64_tr_b16, B = the probabilities
+//            straight from the score registers (the MFMA output layout IS the 16x16x16 B layout), columns fp16 hi /
+//            fp16 lo of P (summed at the end)
+//   merge    every wave's (max, sum, context) through LDS, combined in wave order (deterministic), normalised, bf16 hi /
+//            lo planes out - the layout cross_attn_f16_kernel writes.
+// Against cross_attn_f16_kernel (7 chunks of 32 keys, three block barriers and an LDS score reduction per chunk: 17 us
+// per launch at 256 rows) the per-row critical path is two tile rounds of one wave.  LDS: 128 KiB of key rows (then
+// the merge buffer) + 16 KiB of q~ fragments + 512 B.
+constexpr int XWK_LDS = 8 * 16 * 1024 + 16 * 1024 + 2 * 64 * 4;
+__global__ __launch_bounds__(512) void cross_attn_wk_kernel(const bf16_t* __restrict__ qt, long qt_lo,
+                                                            const bf16_t* __restrict__ mem, int S, float scale,
+                                                            bf16_t* out, long out_lo) {
+  constexpr int DM = 512, H = 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4, q4 = fr >> 2, p4 = fr & 3;
+  const int r = blockIdx.x;
+  const int KT = (S + 15) >> 4;
+  char* const cb = smem + wave * 16 * 1024;  // this wave's key rows [16][1024 B], chunk c at c ^ key
+  const bf16_t* mb = mem + (long)r * S * DM;
+  auto stage = [&](int t) {
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const int g = min(t * 16 + kk, S - 1);
+      lds_dma16(mb + (long)g * DM + (lane ^ kk) * 8, (LDS_AS void*)(cb + kk * 1024));
+    }
+  };
+  if (wave < KT) stage(wave);
+  // q~ as the B operand, fragment s (k-step) of lane l at qfrag[s][l]: column n = l & 15 -> head n & 7, plane n >> 3
+  // of the fp16 hi / lo split of (bf16 hi + bf16 lo); each thread converts fragments (s, l) = its own two
+  f16x8* const qfrag = (f16x8*)(smem + 8 * 16 * 1024);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int s = wave * 2 + u, n = fr, hd = n & 7;
+    const long off = (long)r * H * DM + hd * DM + s * 32 + fq * 8;
+    const bf16x8 a = *(const bf16x8*)(qt + off), b = *(const bf16x8*)(qt + qt_lo + off);
+    f16x8 q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = (float)a[j] + (float)b[j];
+      const _Float16 h = (_Float16)v;
+      q[j] = n < 8 ? h : (_Float16)(v - (float)h);
+    }
+    qfrag[s * 64 + lane] = q;
+  }
+  __syncthreads();  // q~ fragments written (the key DMA stays in flight: counted per wave below)
+  auto ror8 = [](float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, true)); };
+  f32x4 acc[32];
+#pragma unroll
+  for (int dt = 0; dt < 32; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  for (int t = wave; t < KT; t += 8) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's rows (and the q~ loads) landed
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const f16x8 mh = *(const f16x8*)(cb + fr * 1024 + (((s * 4 + fq) ^ fr) << 4));
+      a = __builtin_amdgcn_mfma_f32_16x16x32_f16(mh, qfrag[s * 64 + lane], a, 0, 0, 0);
+      if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // four k-steps of reads in flight at a time
+    }
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = (a[i] + ror8(a[i])) * scale;  // hi + lo columns (fr < 8 and fr >= 8 both hold the sum)
+      v[i] = t * 16 + fq * 4 + i < S ? x : -INFINITY;
+    }
+    const float mt = rows4_max(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = __expf(m_run - m_new);
+    float ps = 0.f;
+    f16x4 pb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float e = __expf(v[i] - m_new);
+      ps += e;
+      const _Float16 h = (_Float16)e;
+      pb[i] = fr < 8 ? h : (_Float16)(e - (float)h);
+    }
+    l_run = l_run * alpha + rows4_sum(ps);
+    m_run = m_new;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // 8 d-tiles per group: the transposed reads of one group in flight at a time
+      s16x4 ta[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int d = (g * 8 + u) * 16 + 4 * p4, k0 = 4 * fq + q4;
+        ta[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (LDS_AS s16x4*)(cb + k0 * 1024 + (((d >> 3) ^ k0) << 4) + (d & 7) * 2));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        f32x4& c = acc[g * 8 + u];
+        c *= alpha;
+        c = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(f16x4, ta[u]), pb, c, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t + 8 < KT) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the region are done
+      stage(t + 8);
+    }
+  }
+  // ---- merge: context [wave][head][512] (hi + lo columns summed), then (max, sum) per (wave, head)
+  __syncthreads();  // every wave is done with its key region
+  float* const mbuf = (float*)smem;
+  float* const mst = (float*)(smem + 8 * 16 * 1024 + 16 * 1024);  // [wave][8] maxima, then [wave][8] sums
+#pragma unroll
+  for (int dt = 0; dt < 32; ++dt) {
+    f32x4 c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = acc[dt][i] + ror8(acc[dt][i]);
+    if (fr < 8) *(f32x4*)(mbuf + (wave * H + fr) * DM + dt * 16 + 4 * fq) = c;
+  }
+  if (lane < 8) {
+    mst[wave * 8 + lane] = m_run;
+    mst[64 + wave * 8 + lane] = l_run;
+  }
+  __syncthreads();
+  {
+    const int h = threadIdx.x >> 6, d0 = (threadIdx.x & 63) * 8;
+    float M = mst[h];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) M = fmaxf(M, mst[w * 8 + h]);
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, L = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const float mw = mst[w * 8 + h];
+      const float f = mw == -INFINITY ? 0.f : __expf(mw - M);
+      L += f * mst[64 + w * 8 + h];
+      const f32x4 c0 = *(const f32x4*)(mbuf + (w * H + h) * DM + d0), c1 = *(const f32x4*)(mbuf + (w * H + h) * DM + d0 + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] += f * c0[i], o[4 + i] += f * c1[i];
+    }
+    const float inv = 1.f / L;
+    bf16_t hv[8], lv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) split_bf(o[i] * inv, hv[i], lv[i]);
+    u32x4 hw, lw;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hw[k] = (uint32_t)hv[2 * k] | ((uint32_t)hv[2 * k + 1] << 16);
+      lw[k] = (uint32_t)lv[2 * k] | ((uint32_t)lv[2 * k + 1] << 16);
+    }
+    bf16_t* dst = out + (long)r * H * DM + h * DM + d0;
+    *(u32x4*)dst = hw;
+    *(u32x4*)(dst + out_lo) = lw;
+  }
+}
+
+#endif  // ICAP_TOOLS
+
 constexpr int XAS_THREADS = 512;
 constexpr int xas_lds(int S) {
   const int sh = ((S + 1) / 2 + 15) & ~15, kte = ((sh / 16) + 1) & ~1;
@@ -1494,6 +1685,24 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
   // 32-key chunks, 8 waves, 74 KiB of LDS: two blocks (rows) share a CU, so the three decode chains' cross-
   // attentions hold half the CUs (decode 12.70 -> 12.47 ms/step, tools/knob_ab.sh); ICAP_XATTN16_CK=64 (tools):
   // 64-key chunks, 16 waves, 148 KiB (one block per CU)
+#ifdef ICAP_TOOLS
+  // round 4, measured slower and tools-only: the wave-owned key-tile form for one row per image without dropout
+  // (knob ICAP_XATTN16_WK=1; 19.9 against 16.2 us at 256 rows x 196 keys, 10.2 against 7.1 at one key:
+  // profiles/r04/xattn_wk.txt)
+  static const int wk = icap_knob("ICAP_XATTN16_WK", 0);
+  if (rows_per_image == 1 && !drop.thr && S <= 256 && wk && !cross_attn_f16s_on()) {
+    static bool wattr = false;
+    if (!wattr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)cross_attn_wk_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, XWK_LDS);
+      if (e != hipSuccess) return e;
+      wattr = true;
+    }
+    hipLaunchKernelGGL(cross_attn_wk_kernel, dim3(rows), dim3(512), XWK_LDS, s, qt, qt_lo, mem16, S, scale, out,
+                       out_lo);
+    return hipGetLastError();
+  }
+#endif
   if (rows_per_image == 1 && !drop.thr && xpart && xcnt && S <= 256 && cross_attn_f16s_on()) {
     static bool sattr = false;
     if (!sattr) {

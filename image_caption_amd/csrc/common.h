@@ -154,6 +154,7 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // fp16 single-plane operands (ICAP_PREC_F16 encoder): the same 16-bit storage type carries fp16 bits;
 // mma<F16> picks the MFMA, cvt16<F16> / pack16x4<F16> the conversion (both round to nearest even).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 template <bool F16>
 __device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {

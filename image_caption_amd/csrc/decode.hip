@@ -118,6 +118,97 @@ __device__ __forceinline__ void load_frags(bf16x8* w, const bf16_t* img, long fi
   for (int i = 0; i < N; ++i) w[i] = src[i * 64];
 }
 
+// A slab tile store: 16 bytes at byte offset off of a wave-uniform base; write-through (the sc1 bit of agent-scope
+// relaxed atomics, as one vector store) when the block's SlabMerge follows.  (Per-dword agent atomics instead:
+// dec_sa 12 -> 45 us, profiles/r04/merge_ab.txt.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void slab_store(float* base, uint32_t off, f32x4 v, bool wt) {
+#ifdef ICAP_TOOLS
+  if (wt) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), slab_rsrc(base), off, 0, 16);
+    return;
+  }
+#endif
+  *(f32x4*)((char*)base + off) = v;
+}
+
+// SlabMerge (kernels.h) after this block's slab stores: the last of the NP blocks of the 16-row tile row0 merges the
+// tile - wave w normalises row row0 + w, lane l columns 8 l .. 8 l + 7 (slabs read agent-scope, in index order, eight
+// at a time).  flag: an LDS word nothing reads any more.
+template <int NP>
+__device__ void slab_merge(const SlabMerge& m, const float* part, long ps, int row0, int rows, int ns, int* flag) {
+  const DropCfg& drop = m.drop;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are complete
+  __syncthreads();                                   // ... and every thread's
+  const int tile = row0 >> 4;
+  if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(m.tick + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (*flag != NP - 1) return;
+  if (threadIdx.x == 0) __hip_atomic_store(m.tick + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = row0 + wave;
+  if (wave >= 16 || row >= rows) return;
+  const int c = lane * 8;
+  float v[8], o[8];
+  {
+    const f32x4 x0 = *(const f32x4*)(m.x + (long)row * DEC_D + c), x1 = *(const f32x4*)(m.x + (long)row * DEC_D + c + 4);
+    const f32x4 b0 = *(const f32x4*)(m.bias + c), b1 = *(const f32x4*)(m.bias + c + 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = x0[k], v[4 + k] = x1[k], o[k] = b0[k], o[4 + k] = b1[k];
+  }
+  // v = x + bias + sum_p slab_p in residual_layernorm_kernel's order; under dropout x + drop(bias + sum_p slab_p)
+  float* const acc = drop.thr ? o : v;
+  if (!drop.thr)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += o[k];
+  const uint32_t off = (uint32_t)(row * DEC_D + c) * 4;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const __amdgpu_buffer_rsrc_t r = slab_rsrc(part + (long)p * ps);  // sc1 loads (agent-coherent)
+    const f32x4 a0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+    const f32x4 a1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 16));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += a0[k], acc[4 + k] += a1[k];
+  }
+  if (drop.thr)  // x + dropout(sublayer output)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += o[k] * drop_mul(drop, m.site, row, drop.pos, c + k);
+  float sm = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sm += v[k];
+  const float mean = wave_sum(sm) / (float)DEC_D;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[k] -= mean;
+    q += v[k] * v[k];
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)DEC_D + m.eps);
+  const f32x4 w0 = *(const f32x4*)(m.w + c), w1 = *(const f32x4*)(m.w + c + 4);
+  const f32x4 c0 = *(const f32x4*)(m.b + c), c1 = *(const f32x4*)(m.b + c + 4);
+  f32x4 y0, y1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    y0[k] = v[k] * rstd * w0[k] + c0[k];
+    y1[k] = v[4 + k] * rstd * w1[k] + c1[k];
+  }
+  *(f32x4*)(m.x + (long)row * DEC_D + c) = y0;
+  *(f32x4*)(m.x + (long)row * DEC_D + c + 4) = y1;
+  bf16_t hv[8], lv[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) split_bf(y0[k], hv[k], lv[k]), split_bf(y1[k], hv[4 + k], lv[4 + k]);
+  u32x4 hw, lw;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hw[k] = (uint32_t)hv[2 * k] | ((uint32_t)hv[2 * k + 1] << 16);
+    lw[k] = (uint32_t)lv[2 * k] | ((uint32_t)lv[2 * k + 1] << 16);
+  }
+  *(u32x4*)(m.a + (long)row * DEC_D + c) = hw;
+  if (ns == 2) *(u32x4*)(m.a + m.aL + (long)row * DEC_D + c) = lw;
+}
+
 // Fragment images of the decode weights (launch_frag_pack, kernels.h): one thread per 16-byte lane piece.
 __global__ void frag_pack_kernel(const bf16_t* __restrict__ W, long ldw, int ntiles, int nk, int mode, int tps,
                                  int ksl, bf16_t* __restrict__ out) {
@@ -296,8 +387,12 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
     else o = mma_rows(o, woi, DEC_D, wave * 32 + i * 16, sc, ns, 0, 1);
     const int row = row0 + fr;
     if (row < p.rows)
-      *(f32x4*)(p.part + (long)h * p.part_stride + (long)row * DEC_D + wave * 32 + i * 16 + 4 * fq) = o;
+      slab_store(p.part + (long)h * p.part_stride, (uint32_t)(row * DEC_D + wave * 32 + i * 16 + 4 * fq) * 4, o,
+                 p.mg.tick);
   }
+#ifdef ICAP_TOOLS  // (measured slower: tools build only, icap.cpp decoder_layers)
+  if (p.mg.tick) slab_merge<DEC_H>(p.mg, p.part, p.part_stride, row0, p.rows, ns, (int*)smem);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -361,8 +456,12 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
     else o = mma_rows(o, ra, DEC_D, wave * 32 + i * 16, sh, ns, 0, 2);
     const int row = row0 + fr;
     if (row < p.rows)
-      *(f32x4*)(p.part + (long)j * p.part_stride + (long)row * DEC_D + wave * 32 + i * 16 + 4 * fq) = o;
+      slab_store(p.part + (long)j * p.part_stride, (uint32_t)(row * DEC_D + wave * 32 + i * 16 + 4 * fq) * 4, o,
+                 p.mg.tick);
   }
+#ifdef ICAP_TOOLS  // (measured slower: tools build only, icap.cpp decoder_layers)
+  if (p.mg.tick) slab_merge<DEC_F / 128>(p.mg, p.part, p.part_stride, row0, p.rows, ns, (int*)smem);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -422,7 +521,7 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
     const int col = wave * 32 + i * 16 + 4 * fq;
     if (row >= p.M) continue;
     if (p.out == OUT_PARTIAL) {
-      *(f32x4*)((float*)p.C + (long)h * p.part_stride + (long)row * p.ldc + col) = o;
+      slab_store((float*)p.C + (long)h * p.part_stride, (uint32_t)(row * p.ldc + col) * 4, o, p.mg.tick);
     } else {
       bf16_t hv[4], lv[4];
 #pragma unroll
@@ -434,6 +533,10 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
             (u32x2){(uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16)};
     }
   }
+#ifdef ICAP_TOOLS  // (measured slower: tools build only, icap.cpp decoder_layers)
+  if (p.out == OUT_PARTIAL && p.mg.tick)
+    slab_merge<DEC_H>(p.mg, (const float*)p.C, p.part_stride, row0, p.M, ns, (int*)smem);
+#endif
 }
 
 }  // namespace
@@ -457,6 +560,7 @@ hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N2 != DEC_D || a.H <= 0 || (a.nsplit != 1 && a.nsplit != 2)) return hipErrorInvalidValue;
   if (a.out != OUT_PARTIAL && a.out != OUT_SPLIT) return hipErrorInvalidValue;
   if (!a.W1f != !a.W2f || (a.W1f && a.H != DEC_H)) return hipErrorInvalidValue;
+  if (a.mg.tick && (a.out != OUT_PARTIAL || a.H != DEC_H || a.ldc != DEC_D)) return hipErrorInvalidValue;
   const hipError_t e = dec_lds_attr();
   if (e != hipSuccess) return e;
   const int blocks = (a.M + DEC_ROWS - 1) / DEC_ROWS * a.H;

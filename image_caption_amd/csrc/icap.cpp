@@ -139,7 +139,11 @@ struct icap_handle {
   icap_model_desc d{};
   bool use_graphs = true;
   hipStream_t cap_stream = nullptr;
-  int dec_branches = 3;                 // ICAP_DEC_BRANCHES: independent decode chains per batch
+  // ICAP_DEC_BRANCHES: independent decode chains per batch.  One since round 4: with the register-fragment decode
+  // blocks three chains of 85 rows are bound by the dispatch of their 3 x 8 graph nodes per layer-step (≈2.9 us each,
+  // 4201 per decode), one chain of 256 rows by its own kernels: decode 12.12 -> 11.47 ms/step at B = 256
+  // (profiles/r04/chains_sweep.txt)
+  int dec_branches = 1;
   DevBuf drop_seed;                     // the sampler's dropout seed (device word read by the kernels)
   static constexpr int MAX_BRANCHES = 4;
   hipStream_t aux_stream[MAX_BRANCHES] = {};  // streams of chains 1.. (chain 0 runs on the caller's)
@@ -226,6 +230,7 @@ struct icap_handle {
   // the greedy and sampled graphs of an SCST step can replay concurrently on two streams
   struct DecWS {
     DevBuf x, a, qkv, q, qt, c, o, h, kv, fin, part, memp, xpart, xcnt;  // xpart / xcnt: split cross-attention
+    DevBuf tick;  // SlabMerge tickets of the decode blocks (one int per row; zero at rest)
     DevBuf gs;  // train-mode cross-attention value-bias weights
   } dws[2];
   DevBuf d_beam;
@@ -1015,6 +1020,7 @@ struct DecodeBufs {
   float* xpart;  // split cross-attention partial states / tickets
   int* xcnt;
   float* gs;     // train-mode cross-attention: per (row, head) weight of the value bias [rows][8]
+  int* tick;     // SlabMerge tickets (16-row tile t of a chain starting at row r0: tick[r0 + t])
 };
 
 // Rows [r0, r0 + n) of a decode buffer set (every plane / slab / layer stride stays the whole
@@ -1027,6 +1033,7 @@ DecodeBufs sub_bufs(const DecodeBufs& b, const icap_model_desc& d, int r0, int L
   v.kc += (size_t)r0 * H * Lmax * 64; v.vc += (size_t)r0 * H * Lmax * 64;
   v.part += (size_t)r0 * D; v.memp += (size_t)r0 * S * D;
   v.gs += (size_t)r0 * H;
+  v.tick += r0;
   if (v.xpart) {
     v.xpart += cross_attn_part_floats(r0);
     v.xcnt += r0;
@@ -1058,7 +1065,12 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
     w.xcnt.ensure((size_t)rows * 4);
     HIPCHK(hipMemset(w.xcnt.p, 0, w.xcnt.n));
   }
+  if (w.tick.n < (size_t)(rows + 16) * 4) {  // zero at rest: every merging block resets its tile's ticket
+    w.tick.ensure((size_t)(rows + 16) * 4);
+    HIPCHK(hipMemset(w.tick.p, 0, w.tick.n));
+  }
   DecodeBufs b;
+  b.tick = w.tick.as<int>();
   b.x = w.x.as<float>(); b.a = w.a.as<bf16_t>(); b.qkv = w.qkv.as<float>();
   b.q = w.q.as<bf16_t>(); b.qt = w.qt.as<bf16_t>(); b.c = w.c.as<bf16_t>();
   b.o = w.o.as<bf16_t>(); b.hb = w.h.as<bf16_t>();
@@ -1108,8 +1120,19 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
                      (!h->wlo || drop);
   const bool wl = h->wlo && !fused;  // GEMMs add W_lo . X_hi
   REQUIRE(!drop || (fused && ns == 2 && !anc), "dropout needs the one-token decode blocks in a parity precision");
+  // round 4, measured slower and tools-only: the residual LayerNorms merged into the producing decode blocks
+  // (SlabMerge; knob ICAP_DEC_MERGE, a mask: 1 = LN1 in dec_sa, 2 = LN2 in dec_chain, 4 = LN3 in dec_ffn) - the
+  // merging block's tail cost 8-15 us per producer against 5 us per residual_layernorm launch
+  // (profiles/r04/merge_ab.txt); a product build compiles no merge and launches the LayerNorms
+#ifdef ICAP_TOOLS
+  static const int merge_knob = icap_knob("ICAP_DEC_MERGE", 0);
+#else
+  constexpr int merge_knob = 0;
+#endif
+  const int merge = fused ? merge_knob : 0;
   for (int l = 0; l < d.n_dec_layers; ++l) {
     const DecLayer& L = h->dec[l];
+    bool merged2 = false;
     DropCfg dl{};
     if (drop) {
       dl = *drop;
@@ -1122,14 +1145,16 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       sa.A = b.a; sa.aL = b.aL; sa.nsplit = ns; sa.rows = rows;
       sa.Wqkv = L.sa_qkv.w; sa.bqkv = L.sa_qkv.b; sa.Wo = L.sa_out.w;
       sa.Wqkv_f = L.f_qkv; sa.Wo_f = L.f_sao;
+      if (merge & 1) sa.mg = SlabMerge{b.tick, b.x, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL, 2, dl};
       sa.kc = b.kc + l * kv_layer; sa.vc = b.vc + l * kv_layer; sa.Lmax = Lmax; sa.t0 = t0; sa.scale = 0.125f;
       sa.anc = anc;
       sa.part = b.part; sa.part_stride = PS;
       sa.drop = dl;
       h->timed(PROF_DEC_FUSED, 2.0 * rows * (3.0 * D * D + (double)D * D), 2.0 * (4.0 * D * D + (double)rows * D * ns),
                s, [&] { HIPCHK(launch_dec_sa(sa, s)); });
-      HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
-                                       ns, s, dl, 2));
+      if (!sa.mg.tick)
+        HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
+                                         ns, s, dl, 2));
     } else {
       h->wgemm(b.a, D, b.aL, L.sa_qkv.w, D, L.sa_qkv.b, rows, 3 * D, D, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, WAVE_2x2,
                1, 0, s, 1, 0, 0, 0, 0, wl ? L.sa_qkv.wl : nullptr);
@@ -1181,16 +1206,22 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_PARTIAL;
       if (drop) c.b1_scale = b.gs;  // the value bias weighs sum_s P_s m_s under probability dropout
       if (fused) c.W1f = L.f_cav, c.W2f = L.f_cao;
+      if (fused && (merge & 2)) c.mg = SlabMerge{b.tick, b.x, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL, 4, dl};
       h->chain(c, s, fused);
+      merged2 = c.mg.tick != nullptr;
     }
-    HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, wl ? KS_D : H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a,
-                                     b.aL, ns, s, dl, 4));
+    if (!merged2)
+      HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, wl ? KS_D : H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a,
+                                       b.aL, ns, s, dl, 4));
     // feed-forward block
     if (fused) {
       DecFfnArgs ff{};
       ff.A = b.a; ff.aL = b.aL; ff.nsplit = ns; ff.rows = rows;
       ff.W1 = L.lin1.w; ff.b1 = L.lin1.b; ff.W2 = L.lin2.w;
       ff.W1f = L.f_l1; ff.W2f = L.f_l2;
+      const bool head_folds = tail_ln && l + 1 == d.n_dec_layers;  // the caller's head normalises instead
+      if ((merge & 4) && !head_folds)
+        ff.mg = SlabMerge{b.tick, b.x, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a, b.aL, 6, dl};
       ff.part = b.part; ff.part_stride = PS;
       ff.drop = dl;
       h->timed(PROF_DEC_FUSED, 4.0 * rows * (double)D * F, 2.0 * (2.0 * D * F + (double)rows * D * ns), s,
@@ -1198,7 +1229,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       const RlnArgs ln3{b.x, nullptr, b.part, F / 128, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, dl, 6};
       if (tail_ln && l + 1 == d.n_dec_layers)
         *tail_ln = ln3;  // the caller's head normalises
-      else
+      else if (!ff.mg.tick)
         HIPCHK(launch_residual_layernorm(b.x, rows, D, ln3.parts, ln3.nparts, PS, ln3.bias, ln3.w, ln3.b, ln3.eps, b.a,
                                          b.aL, ns, s, dl, 6));
     } else {
@@ -1338,7 +1369,8 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   // (two chains pay from 128 rows each: B = 256 +3.4 %, B = 128 -6 %, tools/ab_env.sh)
   // ICAP_DEC_MIN_ROWS: smallest chain (64-row chains measured slower)
   // Round 2 (fused decode blocks, tools/chains_r2.sh, B = 256): 2 chains 13.25 ms/step of decode, 3 chains of
-  // 85 rows 12.73, 4 chains of 64 rows 13.37 - so 3 chains from 80 rows each (B = 128 keeps one chain)
+  // 85 rows 12.73, 4 chains of 64 rows 13.37 - so 3 chains from 80 rows each (B = 128 keeps one chain).  Round 4:
+  // one chain (icap_handle::dec_branches); icap_set_decode_chains still splits
   static const int min_rows = std::max(16, icap_knob("ICAP_DEC_MIN_ROWS", 80));
 #ifdef ICAP_TOOLS
   if (xdec_path(h, B, S, max_len, drop)) {  // one group-persistent launch per step (all layers) + the head
@@ -1879,7 +1911,7 @@ const char* icap_knobs_set() {
       "ICAP_ENC_ATTN_PIPE", "ICAP_ENC_ATTN_QPW", "ICAP_XATTN_KS", "ICAP_POISON", "ICAP_GEMM_TAIL",
       "ICAP_QKV_HEAD_MAJOR", "ICAP_DEC_MIN_ROWS", "ICAP_I8_MLP2", "ICAP_DEC_BRANCHES", "ICAP_F16_GEMM",
       "ICAP_F16_PRES", "ICAP_XATTN16_KS", "ICAP_XATTN16_CK", "ICAP_ENC_ATTN16_QPW", "ICAP_F16_PP", "ICAP_DEC_FRAG",
-      "ICAP_ENC_ATTN16_FULL", "ICAP_XATTN16_S", "ICAP_EAF_ABL",
+      "ICAP_ENC_ATTN16_FULL", "ICAP_XATTN16_S", "ICAP_EAF_ABL", "ICAP_DEC_MERGE", "ICAP_XATTN16_WK",
       "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
       "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE", "ICAP_XDEC_TRACE", "ICAP_GEMM_NARROW",
       "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW"};

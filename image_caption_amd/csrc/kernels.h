@@ -162,6 +162,16 @@ struct RlnArgs {
   DropCfg drop; int site;
 };
 
+// Residual-LayerNorm merge in the producing decode block (round 4): the slabs go out as agent-scope (write-through)
+// stores, and the LAST of the tile's nparts blocks to take the 16-row tile's ticket tick[row0 / 16] computes
+// x = LN(x + bias + sum_p slab_p) for those rows (residual_layernorm_kernel's arithmetic, the dropout site `site`
+// of `drop`) and writes x and the activation planes a (ns planes, plane stride aL), then resets the
+// ticket.  tick == nullptr: no merge (the caller launches residual_layernorm_kernel).
+struct SlabMerge {
+  int* tick; float* x; const float* bias; const float* w; const float* b; float eps; bf16_t* a; long aL; int site;
+  DropCfg drop;
+};
+
 // Two chained per-head GEMMs in one launch (decoder cross-attention block), for each head h:
 //   Y_h = X_h W1_h^T + b1_h      X_h: rows x 512 (bf16 planes), W1_h: rows [64h, 64h + 64) of W1 [.][512]
 //   O_h = Y_h W2_h^T             W2_h: N2 x 64 at W2 + h * w2_hstride, row stride ldw2
@@ -179,6 +189,7 @@ struct ChainArgs {
   // dec_chain only (frag_pack images, both or neither): W1 of head h as tiles h * 4 + t x 16 k32-steps, W2 as tiles
   // h * 32 + n x 2 k32-steps - each wave loads its own fragments straight into registers (no LDS weight staging)
   const bf16_t* W1f; const bf16_t* W2f;
+  SlabMerge mg;  // dec_chain, OUT_PARTIAL only
 };
 hipError_t launch_chain_dec(const ChainArgs& a, hipStream_t s);
 
@@ -195,6 +206,7 @@ struct DecSaArgs {
   // frag_pack images (both or neither): Wqkv as tiles h * 12 + i (q 0-3, k 4-7, v 8-11) x 16 k32-steps (mode 1), Wo
   // as tiles h * 32 + n x 2 k32-steps (mode 2, ksl 64)
   const bf16_t* Wqkv_f; const bf16_t* Wo_f;
+  SlabMerge mg;
 };
 hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s);
 // dec_ffn: slab j of 16 = relu(a W1[128j:128j+128]^T + b1) W2[:, 128j:128j+128]^T -> part[j][rows][512]
@@ -205,6 +217,7 @@ struct DecFfnArgs {
   DropCfg drop;  // site 5: the hidden activations (pos = the decode position)
   // frag_pack images (both or neither): W1 as tiles 0..127 x 16 k32-steps, W2 as tiles j * 32 + n x 4 k32-steps
   const bf16_t* W1f; const bf16_t* W2f;
+  SlabMerge mg;
 };
 hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s);
 // The chained per-head cross-attention products (ChainArgs as launch_chain_dec, N2 = 512) with 16-row

@@ -41,8 +41,8 @@ def test_vit_encode_and_greedy(cuda, vit_sd, precision):
 
 
 def test_two_chain_decode_matches_one_chain(cuda, vit_sd):
-    """The batch decoded as two or three independent graph branches (icap_set_decode_chains; 3 is the
-    default from B = 240) gives the same greedy ids, step logits and sampled ids / log-probs as one chain,
+    """The batch decoded as two or three independent graph branches (icap_set_decode_chains; one chain is the
+    default since round 4) gives the same greedy ids, step logits and sampled ids / log-probs as one chain,
     for an odd batch (uneven parts 128 + 129, 85 + 86 + 86), eagerly and on graph replay."""
     from image_caption_amd.engine import Engine
 

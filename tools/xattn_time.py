@@ -8,7 +8,7 @@ import torch
 
 from image_caption_amd import _lib as L
 
-lib = L.load()
+lib = L.load(os.environ.get("XATTN_LIB") or None)  # XATTN_LIB=tools/libicap_tools.so: with the tools knobs
 dev = torch.device("cuda", 0)
 for rows, S in ((128, 196), (256, 196), (128, 64), (128, 32), (128, 1)):
     mem = torch.randn(rows, S, 512, device=dev).to(torch.float16)
