@@ -142,7 +142,8 @@ def main():
     ap.add_argument("--max-len", type=int, default=30)
     ap.add_argument("--precision", default="f16", choices=sorted(_lib.PRECISIONS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--cpu-batch", type=int, default=16,
+                    help="images per oracle call of the CPU baseline sample (a slice of the B = 256 workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graphs", action="store_true", help="launch the decode loop eagerly (no hipGraph)")
     ap.add_argument("--decode-chains", type=int, default=0,
