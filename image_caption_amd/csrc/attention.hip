@@ -539,13 +539,10 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
 // (the maximum is taken over the raw scores).
 // abl (tools knob ICAP_EAF_ABL, timing ablations; 0 in a product build): 1 = loads only, 2 = no K / V / Q loads,
 // 3 = no output stores
-// VAR (tools knob ICAP_EAF_VAR, NKT 13 only): 1 = the row maximum and sum as trees (depth ~5 instead of chains of 26)
-// and scalar exponent FMAs (the guide prices packed fp32 VALU next to MFMAs as an anti-lever); 2 = VAR 1 with 8-wave
-// workgroups (query tiles w, w + 8: two workgroups of 8 waves per CU = 4 waves per SIMD instead of 3 by the LDS)
-template <int NKT, int VAR = 0, int NW = (VAR == 2 ? 8 : 4)>
-__global__ __launch_bounds__(NW * 64, NW == 4 ? 3 : 2) void enc_attention_full_kernel(const bf16_t* __restrict__ qkv, int N, int H,
+template <int NKT>
+__global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t* __restrict__ qkv, int N, int H,
                                                                      float scale, bf16_t* out, long out_ld, int abl) {
-  constexpr int NQW = (NKT + NW - 1) / NW;  // query tiles per wave (tiles w, w + NW, ...)
+  constexpr int NQW = (NKT + 3) / 4;  // query tiles per wave (tiles w, w + 4, ...)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int h = blockIdx.x, b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -559,7 +556,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 3 : 2) void enc_attention_full_k
   {
     const int lrow = lane >> 3, lch = lane & 7;
     constexpr int ni = NKT * 2;
-    for (int i = wave; i < (abl == 2 ? 0 : 2 * ni); i += NW) {
+    for (int i = wave; i < (abl == 2 ? 0 : 2 * ni); i += 4) {
       const bool isK = i < ni;
       const int row = (isK ? i : i - ni) * 8 + lrow;
       const int ch = lch ^ (isK ? kswz(row) : vswz(row));
@@ -572,7 +569,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 3 : 2) void enc_attention_full_k
   bf16x8 qreg[NQW][2];
 #pragma unroll
   for (int qi = 0; qi < NQW; ++qi) {
-    const int q = min((wave + NW * qi) * 16 + fr, N - 1);
+    const int q = min((wave + 4 * qi) * 16 + fr, N - 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       qreg[qi][ks] = abl == 2 ? (bf16x8){} : *(const bf16x8*)(qb + (long)q * 64 + ks * 32 + g * 8);
@@ -587,7 +584,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 3 : 2) void enc_attention_full_k
   const int q4 = fr >> 2, p4 = fr & 3;
 #pragma unroll
   for (int qi = 0; qi < NQW; ++qi) {
-    const int qt = wave + NW * qi;
+    const int qt = wave + 4 * qi;
     if (qt >= NKT) continue;  // (uniform per wave)
     const bf16x8* const qh = qreg[qi];
     // raw scores: lane holds query fr, keys 16 kt + 4 g + r
@@ -606,64 +603,27 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 3 : 2) void enc_attention_full_k
 #pragma unroll
     for (int r = 0; r < 4; ++r)  // the last tile's keys >= N
       if ((NKT - 1) * 16 + g * 4 + r >= N) s[NKT - 1][r] = -INFINITY;
-    // maximum: v_max3 from asm (fmaxf would canonicalise every MFMA result first: one extra v_max per score)
-    float mx = s[0][0];
-    auto max3 = [](float a, float b, float c) {
-      float r;
-      asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-      return r;
-    };
-    float l;
-    if constexpr (VAR >= 1) {
-      float tm[NKT];  // per-tile maxima, then a max3 tree over the tiles
+    // scale first: the product of a VALU multiply is known canonical, so fmaxf needs no canonicalising v_max per MFMA
+    // result and the chains below become v_max3.  (A v_max3 from inline asm read the MFMA results directly: the
+    // hazard recognizer does not see an inline-asm VALU read of an XDL result, and an 8-wave form of this kernel then
+    // read stale maxima - bitwise-nondeterministic outputs, tools/attn_repeat.py.)
 #pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) tm[kt] = max3(max3(s[kt][0], s[kt][1], s[kt][2]), s[kt][3], s[kt][3]);
-      int n = NKT;
+    for (int kt = 0; kt < NKT; ++kt) s[kt] *= sc2;
+    float mx = fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3]));
 #pragma unroll
-      for (int lvl = 0; lvl < 4; ++lvl) {
+    for (int kt = 1; kt < NKT; ++kt) mx = fmaxf(fmaxf(mx, fmaxf(s[kt][0], s[kt][1])), fmaxf(s[kt][2], s[kt][3]));
+    mx = rows4_max(mx);
+    f32x2 l2 = {0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < (NKT + 2) / 3; ++i) {
-          if (3 * i >= n) continue;
-          const float a = tm[3 * i], b = 3 * i + 1 < n ? tm[3 * i + 1] : a, c = 3 * i + 2 < n ? tm[3 * i + 2] : a;
-          tm[i] = max3(a, b, c);
-        }
-        n = (n + 2) / 3;
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        s[kt][r] = __builtin_amdgcn_exp2f(s[kt][r] - mx);
+        s[kt][r + 1] = __builtin_amdgcn_exp2f(s[kt][r + 1] - mx);
+        l2 += (f32x2){s[kt][r], s[kt][r + 1]};
       }
-      const float mxs = rows4_max(tm[0]) * sc2;
-      float ts[NKT];
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s[kt][r] = __builtin_amdgcn_exp2f(fmaf(s[kt][r], sc2, -mxs));
-        ts[kt] = (s[kt][0] + s[kt][1]) + (s[kt][2] + s[kt][3]);
-      }
-#pragma unroll
-      for (int w = 1; w < NKT; w *= 2)
-#pragma unroll
-        for (int i = 0; i + w < NKT; i += 2 * w) ts[i] += ts[i + w];
-      l = rows4_sum(ts[0]);
-    } else {
-      mx = max3(mx, s[0][1], s[0][2]);
-      mx = max3(mx, s[0][3], s[1 < NKT ? 1 : 0][0]);
-#pragma unroll
-      for (int i = 5; i < 4 * NKT; i += 2)
-        mx = i + 1 < 4 * NKT ? max3(mx, s[i / 4][i % 4], s[(i + 1) / 4][(i + 1) % 4]) : max3(mx, s[i / 4][i % 4], mx);
-      const float mxs = rows4_max(mx) * sc2;
-      // exponent and row sum on packed fp32 pairs (v_pk_fma_f32 / v_pk_add_f32)
-      const f32x2 sc2v = {sc2, sc2}, nmx = {-mxs, -mxs};
-      f32x2 l2 = {0.f, 0.f};
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          const f32x2 t = __builtin_elementwise_fma((f32x2){s[kt][r], s[kt][r + 1]}, sc2v, nmx);
-          s[kt][r] = __builtin_amdgcn_exp2f(t[0]);
-          s[kt][r + 1] = __builtin_amdgcn_exp2f(t[1]);
-          l2 += (f32x2){s[kt][r], s[kt][r + 1]};
-        }
-      }
-      l = rows4_sum(l2[0] + l2[1]);
     }
+    const float l = rows4_sum(l2[0] + l2[1]);
     // O = P V: key-tile pairs (2 c, 2 c + 1) as one 32-deep k-step; P (fp16) element j < 4 -> key 4 g + j of the
     // first tile, j >= 4 -> of the second (odd NKT: the last pair's second tile contributes zeros)
     f32x4 o[4];
@@ -700,20 +660,18 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 3 : 2) void enc_attention_full_k
   }
 }
 
-template <int NKT, int VAR = 0>
+template <int NKT>
 hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf16_t* out, long out_ld, int abl,
                         hipStream_t s) {
   constexpr int lds = 2 * NKT * 16 * 128;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_full_kernel<NKT, VAR>,
+    const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_full_kernel<NKT>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((enc_attention_full_kernel<NKT, VAR>), dim3(H, B), dim3(VAR == 2 ? 512 : 256), lds, s, qkv, N, H,
-                     scale, out,
-                     out_ld, abl);
+  hipLaunchKernelGGL(enc_attention_full_kernel<NKT>, dim3(H, B), dim3(256), lds, s, qkv, N, H, scale, out, out_ld, abl);
   return hipGetLastError();
 }
 
@@ -766,14 +724,7 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
         case 10: return run_enc_full<10>(qkv, B, N, H, scale, out, out_ld, abl, s);
         case 11: return run_enc_full<11>(qkv, B, N, H, scale, out, out_ld, abl, s);
         case 12: return run_enc_full<12>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 13: {
-#ifdef ICAP_TOOLS
-          static const int var = icap_knob("ICAP_EAF_VAR", 0);
-          if (var == 1) return run_enc_full<13, 1>(qkv, B, N, H, scale, out, out_ld, abl, s);
-          if (var == 2) return run_enc_full<13, 2>(qkv, B, N, H, scale, out, out_ld, abl, s);
-#endif
-          return run_enc_full<13>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        }
+        case 13: return run_enc_full<13>(qkv, B, N, H, scale, out, out_ld, abl, s);
         case 14: return run_enc_full<14>(qkv, B, N, H, scale, out, out_ld, abl, s);
         case 15: return run_enc_full<15>(qkv, B, N, H, scale, out, out_ld, abl, s);
         default: return run_enc_full<16>(qkv, B, N, H, scale, out, out_ld, abl, s);

@@ -1911,7 +1911,7 @@ const char* icap_knobs_set() {
       "ICAP_ENC_ATTN_PIPE", "ICAP_ENC_ATTN_QPW", "ICAP_XATTN_KS", "ICAP_POISON", "ICAP_GEMM_TAIL",
       "ICAP_QKV_HEAD_MAJOR", "ICAP_DEC_MIN_ROWS", "ICAP_I8_MLP2", "ICAP_DEC_BRANCHES", "ICAP_F16_GEMM",
       "ICAP_F16_PRES", "ICAP_XATTN16_KS", "ICAP_XATTN16_CK", "ICAP_ENC_ATTN16_QPW", "ICAP_F16_PP", "ICAP_DEC_FRAG",
-      "ICAP_ENC_ATTN16_FULL", "ICAP_XATTN16_S", "ICAP_EAF_ABL", "ICAP_DEC_MERGE", "ICAP_XATTN16_WK", "ICAP_EAF_VAR",
+      "ICAP_ENC_ATTN16_FULL", "ICAP_XATTN16_S", "ICAP_EAF_ABL", "ICAP_DEC_MERGE", "ICAP_XATTN16_WK",
       "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
       "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE", "ICAP_XDEC_TRACE", "ICAP_GEMM_NARROW",
       "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW"};

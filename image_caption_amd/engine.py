@@ -412,7 +412,7 @@ class Engine:
         return logits
 
     def set_decode_chains(self, chains: int) -> None:
-        """Independent decode chains per batch (1..4, default 2, used from 128 rows per chain)."""
+        """Independent decode chains per batch (1..4, default 1 since round 4, used from 80 rows per chain)."""
         check(self.lib.icap_set_decode_chains(self.handle, int(chains)), "icap_set_decode_chains")
 
     def set_decode_step(self, mode) -> None:

@@ -255,8 +255,8 @@ int icap_set_decode_step(icap_handle* h, int mode);
  * others (0 = one per CU of the device, the default).  Results are unchanged. */
 int icap_set_encoder_cus(icap_handle* h, int cus);
 
-/* Number of independent decode chains a batch is split into (1..4, default 2; used from 128 rows
- * per chain): the chains are parallel branches of the captured decode graph. */
+/* Number of independent decode chains a batch is split into (1..4, default 1 since round 4; used from 80 rows per
+ * chain): the chains are parallel branches of the captured decode graph (DESIGN.md §4 "Decode, round 4"). */
 int icap_set_decode_chains(icap_handle* h, int chains);
 
 /* ---- live kernel timing (bench.py roofline) ----
