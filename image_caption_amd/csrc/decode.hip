@@ -97,16 +97,23 @@ __device__ __forceinline__ f32x4 mma_rows(f32x4 acc, const char* wimg, int wrows
 
 // acc += register-held W fragments (frag_pack image, fragment 2 k + hf of k64-step k) x X-image (16 rows) over NK
 // k64-steps of ximg; the same MFMA order as mma_rows (bit-identical sums)
+// The X fragments of half-step j + 1 are read before the MFMAs of half-step j (with ns a compile-time constant in the
+// kernels' NSC forms), so each MFMA pair waits for reads issued one pair earlier instead of its own.
 template <int NK>
 __device__ __forceinline__ f32x4 mma_frag(f32x4 acc, const bf16x8* wf, const char* ximg, int ns) {
+  auto xf = [&](int j, int pl) { return frag(ximg + (j >> 1) * ns * 2048 + pl * 2048, 0, j & 1); };
+  bf16x8 xh = xf(0, 0), xl = ns == 2 ? xf(0, 1) : xh;
 #pragma unroll
-  for (int k = 0; k < NK; ++k) {
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const bf16x8 b = wf[2 * k + hf];
-      acc = mfma16(b, frag(ximg + k * ns * 2048, 0, hf), acc);
-      if (ns == 2) acc = mfma16(b, frag(ximg + k * ns * 2048 + 2048, 0, hf), acc);
+  for (int j = 0; j < 2 * NK; ++j) {
+    bf16x8 nh = xh, nl = xl;
+    if (j + 1 < 2 * NK) {
+      nh = xf(j + 1, 0);
+      if (ns == 2) nl = xf(j + 1, 1);
     }
+    __builtin_amdgcn_sched_barrier(0);  // keep the next pair's reads issued ahead of this pair's MFMAs
+    acc = mfma16(wf[j], xh, acc);
+    if (ns == 2) acc = mfma16(wf[j], xl, acc);
+    xh = nh, xl = nl;
   }
   return acc;
 }
@@ -235,7 +242,7 @@ __global__ void frag_pack_kernel(const bf16_t* __restrict__ W, long ldw, int nti
 // FR (DecSaArgs::Wqkv_f / Wo_f, round 4): no weight region - waves 0-11 load their q|k|v tile's 16 KiB of fragments
 // straight into registers in the same burst as the X image, and every wave its 4 KiB of Wo fragments after its QKV
 // MFMAs (behind the attention): one memory round instead of two, 32 KiB of LDS instead of 160.
-template <bool FR>
+template <bool FR, int NSC = 0>
 __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ra = smem;                        // 128 KiB weight region (FR: none)
@@ -245,7 +252,7 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int h = blockIdx.x & (DEC_H - 1), row0 = (blockIdx.x >> 3) * DEC_ROWS;
-  const int ns = p.nsplit;
+  const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
   const char* wq = (const char*)(p.Wqkv + (long)(h * DEC_HD) * DEC_D);
   const char* wk = (const char*)(p.Wqkv + (long)(DEC_D + h * DEC_HD) * DEC_D);
   const char* wv = (const char*)(p.Wqkv + (long)(2 * DEC_D + h * DEC_HD) * DEC_D);
@@ -263,7 +270,7 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   // the cached keys / values of positions < t0 of this wave's row (it attends for row row0 + wave below) do
   // not depend on this step: fetch the first 32 positions now, while the projections are staged.  Lane l
   // holds key / value j = 4 i + (l >> 4), dims 4 (l & 15) ..; 16 lanes read one 256-B row.
-  constexpr int PRE = FR ? 6 : 8;  // FR: 24 cached positions in registers (8 fewer VGPRs: no spill next to the W fragments)
+  constexpr int PRE = FR ? 5 : 8;  // FR: 20 cached positions in registers (no spill next to the W fragments and the prefetched X fragments)
   const int dq = (lane & 15) * 4, jg = lane >> 4;
   const int brow = row0 + wave, t0 = p.t0;
   f32x4 kpre[PRE], vpre[PRE];
@@ -319,6 +326,15 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
         const int j = 4 * i + jg;
         vpre[i] = j < t0 ? hist(p.vc, j) : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
+      // keys 4 PRE .. 31 in one batch beside the values (their values behind the scores), so no score or context step
+      // waits for its own cache load; positions >= 32 (max_len > 33) load in their loop
+      constexpr int LATE = 8 - PRE;
+      f32x4 klate[LATE > 0 ? LATE : 1], vlate[LATE > 0 ? LATE : 1];
+#pragma unroll
+      for (int i = 0; i < LATE; ++i) {
+        const int j = 4 * (PRE + i) + jg;
+        klate[i] = j < t0 ? hist(p.kc, j) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
       const f32x4 q4 = *(const f32x4*)(qr + dq);
       const f32x4 kcur = *(const f32x4*)(qr + 64 + dq), vcur = *(const f32x4*)(qr + 128 + dq);
       // scores: lane j of the wave ends up holding score j.  Keys j = 4 i + jg: the first PRE x 4 from the
@@ -342,10 +358,18 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
 #pragma unroll
       for (int i = 0; i < PRE; ++i)
         if (4 * i < nkeys) score(i, pick(4 * i + jg, kcur, kpre[i]));
-      for (int i = PRE; 4 * i < nkeys; ++i) {
+#pragma unroll
+      for (int i = 0; i < LATE; ++i)
+        if (4 * (PRE + i) < nkeys) score(PRE + i, pick(4 * (PRE + i) + jg, kcur, klate[i]));
+      for (int i = 8; 4 * i < nkeys; ++i) {
         const int j = 4 * i + jg;
         const f32x4 k4 = j < t0 ? hist(p.kc, j) : kcur;
         score(i, pick(j, kcur, k4));
+      }
+#pragma unroll
+      for (int i = 0; i < LATE; ++i) {  // the late values, in flight behind the softmax
+        const int j = 4 * (PRE + i) + jg;
+        vlate[i] = j < t0 ? hist(p.vc, j) : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
       const float m = wave_max(s_mine);
       const float e = lane < nkeys ? __expf(s_mine - m) : 0.f;
@@ -365,7 +389,10 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
           const int j = 4 * i + jg;
           ctx += prob(i) * pick(j, vcur, vpre[i]);
         }
-      for (int i = PRE; 4 * i < nkeys; ++i) {
+#pragma unroll
+      for (int i = 0; i < LATE; ++i)
+        if (4 * (PRE + i) < nkeys) ctx += prob(PRE + i) * pick(4 * (PRE + i) + jg, vcur, vlate[i]);
+      for (int i = 8; 4 * i < nkeys; ++i) {
         const int j = 4 * i + jg;
         const f32x4 v4 = j < t0 ? hist(p.vc, j) : vcur;
         ctx += prob(i) * pick(j, vcur, v4);
@@ -401,7 +428,7 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
 //   round 2: W2 slice [2 k64][512 rows][128 B] (region A); h image + k-half reduction in region B
 // FR (DecFfnArgs::W1f / W2f, round 4): each wave loads its W1 fragments (tile t, k-half kh: 8 KiB) and its W2
 // fragments (column tiles 2 wave, 2 wave + 1 of the slice: 8 KiB) into registers with the X image - one memory round.
-template <bool FR>
+template <bool FR, int NSC = 0>
 __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ra = smem;
@@ -412,7 +439,7 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   const int fr = lane & 15, fq = lane >> 4;
   const int nslice = DEC_F / 128;
   const int j = blockIdx.x % nslice, row0 = (blockIdx.x / nslice) * DEC_ROWS;
-  const int ns = p.nsplit;
+  const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
 
   const int t = wave & 7, kh = wave >> 3;  // FFN-1 tile, k half (4 of the 8 k64 steps)
   dma_x(p.A, p.aL, ns, row0, p.rows, sx);
@@ -471,7 +498,7 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
 // W2_h [512 rows][128 B] 64 KiB.  out = OUT_SPLIT (q~ planes of head h) or OUT_PARTIAL (slab h).
 // FR (ChainArgs::W1f / W2f, round 4): W1 (tile t, k-quarter kq: 4 KiB) and W2 (column tiles 2 wave, 2 wave + 1: 4 KiB)
 // fragments per wave in registers, 32 KiB of LDS (the X image) instead of 160.
-template <bool FR>
+template <bool FR, int NSC = 0>
 __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* w1i = smem;                       // 64 KiB (FR: none)
@@ -482,7 +509,7 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int h = blockIdx.x % p.H, row0 = (blockIdx.x / p.H) * DEC_ROWS;
-  const int ns = p.nsplit;
+  const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
   const int t = wave & 3, kq = wave >> 2;  // Y tile, k quarter (2 of the 8 k64 steps)
   dma_x(p.X + (long)h * p.x_hstride, p.x_lo, ns, row0, p.M, sx, p.ldx);
   bf16x8 w1f[FR ? 4 : 1], w2f[FR ? 4 : 1];
@@ -564,7 +591,8 @@ hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
   const hipError_t e = dec_lds_attr();
   if (e != hipSuccess) return e;
   const int blocks = (a.M + DEC_ROWS - 1) / DEC_ROWS * a.H;
-  if (a.W1f) hipLaunchKernelGGL(dec_chain_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_chain_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  else if (a.W1f) hipLaunchKernelGGL(dec_chain_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else hipLaunchKernelGGL(dec_chain_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
   return hipGetLastError();
 }
@@ -576,7 +604,8 @@ hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s) {
   const hipError_t e = dec_lds_attr();
   if (e != hipSuccess) return e;
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * DEC_H;
-  if (a.Wqkv_f) hipLaunchKernelGGL(dec_sa_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  if (a.Wqkv_f && a.nsplit == 2) hipLaunchKernelGGL((dec_sa_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  else if (a.Wqkv_f) hipLaunchKernelGGL(dec_sa_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else hipLaunchKernelGGL(dec_sa_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
   return hipGetLastError();
 }
@@ -587,7 +616,8 @@ hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s) {
   const hipError_t e = dec_lds_attr();
   if (e != hipSuccess) return e;
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * (DEC_F / 128);
-  if (a.W1f) hipLaunchKernelGGL(dec_ffn_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_ffn_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  else if (a.W1f) hipLaunchKernelGGL(dec_ffn_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else hipLaunchKernelGGL(dec_ffn_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
   return hipGetLastError();
 }
