@@ -603,23 +603,23 @@ __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t
 #pragma unroll
     for (int r = 0; r < 4; ++r)  // the last tile's keys >= N
       if ((NKT - 1) * 16 + g * 4 + r >= N) s[NKT - 1][r] = -INFINITY;
-    // scale first: the product of a VALU multiply is known canonical, so fmaxf needs no canonicalising v_max per MFMA
-    // result and the chains below become v_max3.  (A v_max3 from inline asm read the MFMA results directly: the
-    // hazard recognizer does not see an inline-asm VALU read of an XDL result, and an 8-wave form of this kernel then
-    // read stale maxima - bitwise-nondeterministic outputs, tools/attn_repeat.py.)
+    // maximum over the raw scores with llvm.maximum (gfx950 v_maximum3_f32: no canonicalising v_max per MFMA result,
+    // unlike fmaxf, and a compiler-visible VALU read of the XDL results - a v_max3 from inline asm was not spaced from
+    // them by the hazard recognizer: 8-wave forms of this kernel read stale maxima, tools/attn_repeat.py); the 1/8
+    // scale is folded into the exponent's FMA
+    float mx = s[0][0];
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) s[kt] *= sc2;
-    float mx = fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3]));
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-    for (int kt = 1; kt < NKT; ++kt) mx = fmaxf(fmaxf(mx, fmaxf(s[kt][0], s[kt][1])), fmaxf(s[kt][2], s[kt][3]));
-    mx = rows4_max(mx);
+      for (int r = (kt == 0 ? 1 : 0); r < 4; ++r) mx = __builtin_elementwise_maximum(mx, s[kt][r]);
+    const float mxs = rows4_max(mx) * sc2;
     f32x2 l2 = {0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
       for (int r = 0; r < 4; r += 2) {
-        s[kt][r] = __builtin_amdgcn_exp2f(s[kt][r] - mx);
-        s[kt][r + 1] = __builtin_amdgcn_exp2f(s[kt][r + 1] - mx);
+        s[kt][r] = __builtin_amdgcn_exp2f(fmaf(s[kt][r], sc2, -mxs));
+        s[kt][r + 1] = __builtin_amdgcn_exp2f(fmaf(s[kt][r + 1], sc2, -mxs));
         l2 += (f32x2){s[kt][r], s[kt][r + 1]};
       }
     }
@@ -1119,15 +1119,21 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
     // every wave is past chunk c - 1: its buffer takes chunk c + NB - 1
     if (NB > 2 && c + NB - 1 < c1) stage(c + NB - 1, (c - c0 + NB - 1) % NB);
     const char* cb = smem + ((c - c0) % NB) * BUF;
-    {  // partial scores: key tile skt, d-group sdg
+    {  // partial scores: key tile skt, d-group sdg (the four memory fragments read before the MFMAs: one LDS wait,
+       // not one per fragment)
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
       const int key = skt * 16 + fr;
+      f16x8 mh[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int ch = (sdg * 128 + ks * 32 + fq * 8) >> 3;
-        const f16x8 mh = *(const f16x8*)(cb + key * 1024 + ((ch ^ (key & 15)) << 4));
-        a = mma16h(mh, qh[ks], a);
-        a = mma16h(mh, ql[ks], a);
+        mh[ks] = *(const f16x8*)(cb + key * 1024 + ((ch ^ (key & 15)) << 4));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        a = mma16h(mh[ks], qh[ks], a);
+        a = mma16h(mh[ks], ql[ks], a);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) red[((sdg * NKT + skt) * 4 + j) * 64 + lane] = a[j];
@@ -1195,15 +1201,20 @@ __global__ __launch_bounds__(CK * 16) void cross_attn_f16_kernel(const bf16_t* _
         pl[j] = (_Float16)(sc[2 * s2][j] - (float)h0);
         pl[4 + j] = (_Float16)(sc[2 * s2 + 1][j] - (float)h1);
       }
+      f16x8 vh[NDT];  // every d-tile's transposed memory fragment read before the MFMAs
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         const int d = wave * (16 * NDT) + dt * 16 + 4 * p4;
         const int k0 = 32 * s2 + 4 * fq + q4, k1 = k0 + 16;
         const int o0 = k0 * 1024 + ((((d >> 3) ^ (k0 & 15))) << 4) + (d & 7) * 2;
         const int o1 = k1 * 1024 + ((((d >> 3) ^ (k1 & 15))) << 4) + (d & 7) * 2;
-        const f16x8 vh = __builtin_bit_cast(f16x8, tr_pair(cb + o0, cb + o1));
-        acc[dt] = mma16h(vh, ph, acc[dt]);
-        acc[dt] = mma16h(vh, pl, acc[dt]);
+        vh[dt] = __builtin_bit_cast(f16x8, tr_pair(cb + o0, cb + o1));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        acc[dt] = mma16h(vh[dt], ph, acc[dt]);
+        acc[dt] = mma16h(vh[dt], pl, acc[dt]);
       }
     }
     if (NB == 2 && c + 2 < c1) {
