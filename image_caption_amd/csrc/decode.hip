@@ -117,6 +117,25 @@ __device__ __forceinline__ f32x4 mma_frag(f32x4 acc, const bf16x8* wf, const cha
   }
   return acc;
 }
+// Opening of an FR block: the X image DMA is this wave's OLDEST VMEM work and its weight fragments (`younger`
+// loads, always issued) follow, so waiting for vmcnt(younger) lands the X image while the fragments stay in flight -
+// the MFMAs then wait for each fragment through the compiler's own counted waits instead of for all of them here.
+// (VMEM operations retire in issue order; a plain s_barrier: the X image is DMA'd, no store needs a fence.)
+template <int YOUNGER>
+__device__ __forceinline__ void x_landed() {
+  if constexpr (YOUNGER == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (YOUNGER == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void open_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+template <int YOUNGER>
+__device__ __forceinline__ void open_x() {
+  x_landed<YOUNGER>();
+  open_barrier();
+}
 // this wave's n fragments first .. first + n - 1 of a frag_pack image: each one 1 KiB contiguous (full lines)
 template <int N>
 __device__ __forceinline__ void load_frags(bf16x8* w, const bf16_t* img, long first) {
@@ -284,8 +303,14 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
     const int j = 4 * i + jg;
     kpre[i] = brow < p.rows && j < t0 ? hist(p.kc, j) : (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (FR && NSC == 2) {  // X landed, the 16 q|k|v fragments of waves 0-11 may still fly (the cached keys behind them)
+    if (wave < 12) x_landed<2 * DEC_K64>();
+    else x_landed<0>();
+    open_barrier();  // one barrier on every wave's path
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   bf16x8 wo[FR ? 4 : 1];  // FR: Wo fragments of output column tiles 2 wave, 2 wave + 1 (2 k32-steps each)
   if (FR) {
@@ -451,8 +476,12 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
     const char* w1 = (const char*)(p.W1 + (long)j * 128 * DEC_D);
     for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 128, ra + k * 128 * 128);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (FR && NSC == 2) {
+    open_x<DEC_K64 + 8>();  // X landed; W1 / W2 fragments may still fly
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (FR) acc = mma_frag<4>(acc, w1f, sx + kh * 4 * ns * 2048, ns);
   else acc = mma_rows(acc, ra, 128, t * 16, sx, ns, kh * 4, kh * 4 + 4);
@@ -521,8 +550,12 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
     for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 64, w1i + k * 64 * 128, 8 * k + 2);
     dma_rows((const char*)(p.W2 + (long)h * p.w2_hstride), p.ldw2 * 2, DEC_D, w2i, 2);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (FR && NSC == 2) {
+    open_x<8>();  // X landed; W1 / W2 fragments may still fly
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (FR) acc = mma_frag<2>(acc, w1f, sx + kq * 2 * ns * 2048, ns);
   else acc = mma_rows(acc, w1i, 64, t * 16, sx, ns, kq * 2, kq * 2 + 2);
