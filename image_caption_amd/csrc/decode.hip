@@ -276,6 +276,11 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   const char* wk = (const char*)(p.Wqkv + (long)(DEC_D + h * DEC_HD) * DEC_D);
   const char* wv = (const char*)(p.Wqkv + (long)(2 * DEC_D + h * DEC_HD) * DEC_D);
 
+  // this wave's bias columns first (the oldest load: the opening waits cover it, so the epilogue after the MFMAs
+  // waits for no load - a late bias load's vmcnt(0) also drained the Wo fragments issued behind the attention)
+  // (waves 12-15 load wave 0's columns and never use them: an unconditional load, see dec_chain_kernel)
+  const int bc = (wave < 12 ? wave : 0) * 16 + 4 * fq;
+  const f32x4 bias = *(const f32x4*)(p.bqkv + (bc >> 6) * DEC_D + h * DEC_HD + (bc & 63));
   dma_x(p.A, p.aL, ns, row0, p.rows, sx);
   bf16x8 wf[FR ? 2 * DEC_K64 : 1];  // FR: this wave's q|k|v tile (waves 0-11), all 16 k32-steps
   if (FR) {
@@ -289,7 +294,7 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   // the cached keys / values of positions < t0 of this wave's row (it attends for row row0 + wave below) do
   // not depend on this step: fetch the first 32 positions now, while the projections are staged.  Lane l
   // holds key / value j = 4 i + (l >> 4), dims 4 (l & 15) ..; 16 lanes read one 256-B row.
-  constexpr int PRE = FR ? 5 : 8;  // FR: 20 cached positions in registers (no spill next to the W fragments and the prefetched X fragments)
+  constexpr int PRE = FR ? 3 : 8;  // FR: 12 cached positions in registers (no spill next to the W fragments, the prefetched X fragments and the bias)
   const int dq = (lane & 15) * 4, jg = lane >> 4;
   const int brow = row0 + wave, t0 = p.t0;
   f32x4 kpre[PRE], vpre[PRE];
@@ -328,7 +333,7 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   if (FR) load_frags<4>(wo, p.Wo_f, (long)(h * 32 + 2 * wave) * 2);  // needed after the attention
   if (wave < 12) {
     const int c = wave * 16 + 4 * fq;  // column in [q | k | v] of this head
-    acc += *(const f32x4*)(p.bqkv + (c >> 6) * DEC_D + h * DEC_HD + (c & 63));
+    acc += bias;
     *(f32x4*)(qkv + fr * 192 + c) = acc;
   }
   __syncthreads();
@@ -467,6 +472,7 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
 
   const int t = wave & 7, kh = wave >> 3;  // FFN-1 tile, k half (4 of the 8 k64 steps)
+  const f32x4 bias = *(const f32x4*)(p.b1 + j * 128 + t * 16 + 4 * fq);  // oldest load (as dec_sa_kernel)
   dma_x(p.A, p.aL, ns, row0, p.rows, sx);
   bf16x8 w1f[FR ? DEC_K64 : 1], w2f[FR ? 8 : 1];
   if (FR) {
@@ -495,7 +501,7 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   if (!kh) {
     acc += red[t * 64 + lane];
     const int n = t * 16 + 4 * fq;
-    acc += *(const f32x4*)(p.b1 + j * 128 + n);
+    acc += bias;
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r], 0.f);
     if (p.drop.thr)  // train mode: dropout on the hidden activations
@@ -540,6 +546,9 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   const int h = blockIdx.x % p.H, row0 = (blockIdx.x / p.H) * DEC_ROWS;
   const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
   const int t = wave & 3, kq = wave >> 2;  // Y tile, k quarter (2 of the 8 k64 steps)
+  const f32x4 bv = *(const f32x4*)(p.b1 + h * 64 + t * 16 + 4 * fq);  // oldest loads (as dec_sa_kernel)
+  // (unconditional, from b1 when there is no scale: a load under a branch made hipcc wait for it at the join)
+  const float bsc = *(p.b1_scale ? p.b1_scale + (long)min(row0 + fr, p.M - 1) * p.H + h : p.b1);
   dma_x(p.X + (long)h * p.x_hstride, p.x_lo, ns, row0, p.M, sx, p.ldx);
   bf16x8 w1f[FR ? 4 : 1], w2f[FR ? 4 : 1];
   if (FR) {
@@ -566,8 +575,7 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) acc += red[(q * 4 + t) * 64 + lane];
     const int n = t * 16 + 4 * fq;
-    const f32x4 bv = *(const f32x4*)(p.b1 + h * 64 + n);
-    if (p.b1_scale) acc += bv * p.b1_scale[(long)min(row0 + fr, p.M - 1) * p.H + h];
+    if (p.b1_scale) acc += bv * bsc;
     else acc += bv;
     put_planes(sy, ns, fr, n, acc);
   }
