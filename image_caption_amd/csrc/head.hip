@@ -25,8 +25,9 @@ __device__ __forceinline__ void head_row_in(const HeadArgs& a, int r, float* xs,
   }
   const RlnArgs& ln = a.ln;
   const int col = 4 * tid;
-  f32x4 v = {0.f, 0.f, 0.f, 0.f}, dv = v;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f}, dv = v, wv = v, bv = v;
   if (tid < 128) {
+    wv = *(const f32x4*)(ln.w + col), bv = *(const f32x4*)(ln.b + col);  // with the slabs: no load after the sums
     f32x4 pp[HEAD_LN_PARTS];
 #pragma unroll
     for (int s = 0; s < HEAD_LN_PARTS; ++s)
@@ -58,7 +59,6 @@ __device__ __forceinline__ void head_row_in(const HeadArgs& a, int r, float* xs,
   __syncthreads();
   if (tid < 128) {
     const float rstd = 1.0f / sqrtf((red[2] + red[3]) / 512.f + ln.eps);
-    const f32x4 wv = *(const f32x4*)(ln.w + col), bv = *(const f32x4*)(ln.b + col);
     f32x4 y;
 #pragma unroll
     for (int k = 0; k < 4; ++k) y[k] = dv[k] * rstd * wv[k] + bv[k];

@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round 4 A/B on one box: the product build (new forms on) against the tools build with one form switched back by its
 # knob; then a kernel trace of the product bench's decode.  usage: bash tools/r4_ab.sh TAG "KNOB=0 ..." [TESTS]
+# OLD_LIB: the old arm's library (default the tools build; a product build of an earlier tree compares like with like -
+# the tools build carries the tools-only paths inside the decode kernels)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r4; mkdir -p $O
@@ -10,14 +12,15 @@ if [ -n "$3" ]; then
   tail -1 $O/${T}_tests.log
 fi
 bline() { python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); p=d["roofline"]["phases"]; print(sys.argv[2], d["value"], d["ms_per_step"], "enc", p["encoder"]["ms_per_step"], "dec", p["decode"]["ms_per_step"])' $1 $2; }
-for v in new old new old; do
+for v in ${ARMS:-new old new old}; do
   if [ $v = new ]; then
     timeout -k 10 200 python bench.py --no-cpu-baseline --steps 10 --warmup 2 $BENCH_ARGS > $O/${T}_b.json 2> $O/${T}_b.err || { tail -20 $O/${T}_b.err; exit 1; }
   else
-    env $2 BENCH_LIB=tools/libicap_tools.so timeout -k 10 200 python -c "
+    OL=${OLD_LIB:-tools/libicap_tools.so}
+    env $2 BENCH_LIB=$OL timeout -k 10 200 python -c "
 import sys, runpy
 from image_caption_amd import _lib
-_lib.load('tools/libicap_tools.so')
+_lib.load('$OL')
 sys.argv = ['bench.py', '--no-cpu-baseline', '--steps', '10', '--warmup', '2'] + '$BENCH_ARGS'.split()
 runpy.run_path('bench.py', run_name='__main__')
 " > $O/${T}_b.json 2> $O/${T}_b.err || { tail -20 $O/${T}_b.err; exit 1; }
