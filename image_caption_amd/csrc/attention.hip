@@ -1456,8 +1456,6 @@ __global__ __launch_bounds__(512) void cross_attn_wk_kernel(const bf16_t* __rest
   }
 }
 
-#endif  // ICAP_TOOLS
-
 constexpr int XAS_THREADS = 512;
 constexpr int xas_lds(int S) {
   const int sh = ((S + 1) / 2 + 15) & ~15, kte = ((sh / 16) + 1) & ~1;
@@ -1630,6 +1628,8 @@ __global__ __launch_bounds__(XAS_THREADS) void cross_attn_f16s_kernel(const bf16
   }
 }
 
+#endif  // ICAP_TOOLS
+
 }  // namespace
 
 int cross_attn_splits(int S) {
@@ -1646,18 +1646,28 @@ int cross_attn_splits(int S) {
 
 size_t cross_attn_part_floats(int rows) { return (size_t)rows * 2 * XA_PART_FLOATS; }
 
+// Both key-split forms of the fp16 cross-attention were measured slower and compile into the tools build only
+// (a product build has neither kernel and launches the chunk loop):
 int cross_attn_f16_splits() {
-  // key split of the fp16 cross-attention (tools knob ICAP_XATTN16_KS, default 1)
+  // key split of the chunk loop (tools knob ICAP_XATTN16_KS=2; decode 12.8 -> 13.4 ms/step)
+#ifdef ICAP_TOOLS
   static const int ks = icap_knob("ICAP_XATTN16_KS", 1);
   return ks == 2 ? 2 : 1;
+#else
+  return 1;
+#endif
 }
 
 bool cross_attn_f16s_on() {
   // the key-split single-burst form (cross_attn_f16s_kernel) for one row per image without dropout: tools knob
-  // ICAP_XATTN16_S=1.  Off by default: inside the three-chain decode graph it measured 18.2 us per launch against
-  // 15.5 for the chunk-loop form (decode 14.5 vs 12.2 ms/step, same box, profiles/r04/xattn_split_ab.txt)
+  // ICAP_XATTN16_S=1.  Inside the three-chain decode graph it measured 18.2 us per launch against 15.5 for the
+  // chunk-loop form (decode 14.5 vs 12.2 ms/step, same box, profiles/r04/xattn_split_ab.txt)
+#ifdef ICAP_TOOLS
   static const int on = icap_knob("ICAP_XATTN16_S", 0);
   return on != 0;
+#else
+  return false;
+#endif
 }
 
 hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem16, int rows, int rows_per_image,
@@ -1667,15 +1677,21 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
   if (drop.thr && (rows_per_image != 1 || S > 256 || !gsum)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
+    {
+      const hipError_t e = hipFuncSetAttribute((const void*)cross_attn_f16_kernel<1, 32>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, xa16_lds(32));
+      if (e != hipSuccess) return e;
+    }
+#ifdef ICAP_TOOLS
     for (const void* f : {(const void*)cross_attn_f16_kernel<1, 64>, (const void*)cross_attn_f16_kernel<2, 64>}) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, XA16_LDS);
       if (e != hipSuccess) return e;
     }
-    for (const void* f : {(const void*)cross_attn_f16_kernel<1, 32>, (const void*)cross_attn_f16_kernel<2, 32>}) {
-      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, xa16_lds(32));
+    {
+      const hipError_t e = hipFuncSetAttribute((const void*)cross_attn_f16_kernel<2, 32>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, xa16_lds(32));
       if (e != hipSuccess) return e;
     }
-#ifdef ICAP_TOOLS
     {
       hipError_t e = hipFuncSetAttribute((const void*)cross_attn_f16_kernel<1, 32, 3>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, xa16_lds(32, 3));
@@ -1708,6 +1724,7 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
     return hipGetLastError();
   }
 #endif
+#ifdef ICAP_TOOLS
   if (rows_per_image == 1 && !drop.thr && xpart && xcnt && S <= 256 && cross_attn_f16s_on()) {
     static bool sattr = false;
     if (!sattr) {
@@ -1720,6 +1737,7 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
                        mem16, rows, S, scale, out, out_lo, xpart, xcnt);
     return hipGetLastError();
   }
+#endif
   static const int ck = icap_knob("ICAP_XATTN16_CK", 32) == 64 ? 64 : 32;
   const int pairs = rows / rows_per_image * ((rows_per_image + 1) / 2);
   const bool ks2 = xpart && xcnt && !drop.thr && S > ck && cross_attn_f16_splits() == 2;
@@ -1739,11 +1757,16 @@ hipError_t launch_cross_attn_f16(const bf16_t* qt, long qt_lo, const bf16_t* mem
     return hipGetLastError();
   }
 #endif
+#ifdef ICAP_TOOLS
   if (ck == 32) {
     if (ks2) XA16(2, 32); else XA16(1, 32);
   } else {
     if (ks2) XA16(2, 64); else XA16(1, 64);
   }
+#else
+  (void)ck, (void)ks2;
+  XA16(1, 32);
+#endif
 #undef XA16
   return hipGetLastError();
 }

@@ -121,8 +121,11 @@ __device__ __forceinline__ f32x4 mma_frag(f32x4 acc, const bf16x8* wf, const cha
 // loads, always issued) follow, so waiting for vmcnt(younger) lands the X image while the fragments stay in flight -
 // the MFMAs then wait for each fragment through the compiler's own counted waits instead of for all of them here.
 // (VMEM operations retire in issue order; a plain s_barrier: the X image is DMA'd, no store needs a fence.)
+// YOUNGER = the fragment loads the caller issued after its X DMA (load_frags<N>: N one-instruction 16-byte loads),
+// written as the sum of the load_frags template arguments at each call
 template <int YOUNGER>
 __device__ __forceinline__ void x_landed() {
+  static_assert(YOUNGER == 16 || YOUNGER == 8 || YOUNGER == 0, "x_landed: add the s_waitcnt form for this count");
   if constexpr (YOUNGER == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if constexpr (YOUNGER == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -136,12 +139,110 @@ __device__ __forceinline__ void open_x() {
   x_landed<YOUNGER>();
   open_barrier();
 }
+// this wave's LDS stores done, then the barrier (no vmcnt wait: weight fragments stay in flight)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  open_barrier();
+}
 // this wave's n fragments first .. first + n - 1 of a frag_pack image: each one 1 KiB contiguous (full lines)
 template <int N>
 __device__ __forceinline__ void load_frags(bf16x8* w, const bf16_t* img, long first) {
   const bf16x8* src = (const bf16x8*)(img + first * 512) + (threadIdx.x & 63);
 #pragma unroll
   for (int i = 0; i < N; ++i) w[i] = src[i * 64];
+}
+
+// ---- residual LayerNorm folded into the consuming block (round 5; RlnArgs fold, kernels.h) ----
+// The block's X image is y = LN(x + drop(bias + sum_p slab_p)) of its 16 rows instead of the DMA of the a planes the
+// separate residual_layernorm launch used to write: wave w normalises row row0 + w, lane l columns 8 l .. 8 l + 7.
+// Step 1 (fold_issue) is the block's oldest VMEM work: waves 0-5 DMA one 1-KiB piece each of the LN parameters
+// (bias | weight | bias of the norm, 2 KiB each) into LDS at prm, every wave loads its row's x and NP slab columns into
+// registers; the caller then issues its weight fragments, so the compiler's counted wait for the slab data (step 2)
+// leaves them in flight - and, VMEM retiring in issue order, covers the older parameter DMA, which one barrier then
+// publishes to every wave.  Step 2 (fold_finish) sums, normalises, writes the bf16 hi / lo planes into the X image in
+// dma_x's layout, and the tile's writer block stores y to x_out (x_out != x: the tile's other blocks still read x).
+constexpr int FOLD_PRM = 32 * 1024;                    // LN parameters after the 32 KiB X image
+constexpr int DEC_LDS_FOLD = FOLD_PRM + 6 * 1024;
+
+template <int NP>
+struct FoldIn {
+  f32x4 x[2], s[NP][2];
+};
+
+template <int NP>
+__device__ __forceinline__ void fold_issue(const RlnArgs& f, int row0, int rows, char* prm, FoldIn<NP>& in) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave < 6) {  // (a wave-uniform select of the three pointers: no indexed kernel-argument load)
+    const float* src = wave < 2 ? f.bias : wave < 4 ? f.w : f.b;
+    lds_dma16(src + (wave & 1) * 256 + lane * 4, (LDS_AS void*)(prm + wave * 1024));
+  }
+  const long off = (long)min(row0 + wave, rows - 1) * DEC_D + lane * 8;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    in.s[p][0] = *(const f32x4*)(f.parts + p * f.part_stride + off);
+    in.s[p][1] = *(const f32x4*)(f.parts + p * f.part_stride + off + 4);
+  }
+  in.x[0] = *(const f32x4*)(f.x + off);
+  in.x[1] = *(const f32x4*)(f.x + off + 4);
+}
+
+template <int NP, int NSC>
+__device__ __forceinline__ void fold_finish(const RlnArgs& f, const FoldIn<NP>& in, int row0, int rows, const char* prm,
+                                            char* sx, bool writer) {
+  const int lane = threadIdx.x & 63, r = threadIdx.x >> 6, c = lane * 8;
+  f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) o0 += in.s[p][0], o1 += in.s[p][1];
+  asm volatile("" ::"v"(o0), "v"(o1));  // the slab sums (so the wait for their loads) stay before the barrier
+  open_barrier();  // every wave's parameter piece landed (its wait for the slabs above retired it)
+  const f32x4* pr = (const f32x4*)prm;
+  o0 += pr[2 * lane], o1 += pr[2 * lane + 1];  // + bias
+  if (f.drop.thr) {  // train mode: x + dropout(sublayer output)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o0[k] *= drop_mul(f.drop, f.site, row0 + r, f.drop.pos, c + k);
+      o1[k] *= drop_mul(f.drop, f.site, row0 + r, f.drop.pos, c + 4 + k);
+    }
+  }
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = in.x[0][k] + o0[k], v[4 + k] = in.x[1][k] + o1[k];
+  float sm = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sm += v[k];
+  const float mean = wave_sum(sm) / (float)DEC_D;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[k] -= mean;
+    q += v[k] * v[k];
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)DEC_D + f.eps);
+  const f32x4 w0 = pr[128 + 2 * lane], w1 = pr[128 + 2 * lane + 1];
+  const f32x4 b0 = pr[256 + 2 * lane], b1 = pr[256 + 2 * lane + 1];
+  f32x4 y0, y1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    y0[k] = v[k] * rstd * w0[k] + b0[k];
+    y1[k] = v[4 + k] * rstd * w1[k] + b1[k];
+  }
+  bf16_t hv[8], lv[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) split_bf(y0[k], hv[k], lv[k]), split_bf(y1[k], hv[4 + k], lv[4 + k]);
+  u32x4 hw, lw;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hw[k] = (uint32_t)hv[2 * k] | ((uint32_t)hv[2 * k + 1] << 16);
+    lw[k] = (uint32_t)lv[2 * k] | ((uint32_t)lv[2 * k + 1] << 16);
+  }
+  // X image [k64][NSC][16 rows][128 B]: columns 8 l .. 8 l + 7 are 16-byte chunk l & 7 of k64-step l >> 3
+  char* dst = sx + (lane >> 3) * NSC * 2048 + r * 128 + (((lane & 7) ^ ((r >> 1) & 7)) << 4);
+  *(u32x4*)dst = hw;
+  if (NSC == 2) *(u32x4*)(dst + 2048) = lw;
+  if (writer && row0 + r < rows) {
+    *(f32x4*)(f.x_out + (long)(row0 + r) * DEC_D + c) = y0;
+    *(f32x4*)(f.x_out + (long)(row0 + r) * DEC_D + c + 4) = y1;
+  }
 }
 
 // A slab tile store: 16 bytes at byte offset off of a wave-uniform base; write-through (the sc1 bit of agent-scope
@@ -282,9 +383,10 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   const int bc = (wave < 12 ? wave : 0) * 16 + 4 * fq;
   const f32x4 bias = *(const f32x4*)(p.bqkv + (bc >> 6) * DEC_D + h * DEC_HD + (bc & 63));
   dma_x(p.A, p.aL, ns, row0, p.rows, sx);
-  bf16x8 wf[FR ? 2 * DEC_K64 : 1];  // FR: this wave's q|k|v tile (waves 0-11), all 16 k32-steps
+  constexpr int NWQ = 2 * DEC_K64;  // fragments per wave (the opening's vmcnt counts them)
+  bf16x8 wf[FR ? NWQ : 1];  // FR: this wave's q|k|v tile (waves 0-11), all 16 k32-steps
   if (FR) {
-    if (wave < 12) load_frags<2 * DEC_K64>(wf, p.Wqkv_f, (long)(h * 12 + wave) * 2 * DEC_K64);
+    if (wave < 12) load_frags<NWQ>(wf, p.Wqkv_f, (long)(h * 12 + wave) * 2 * DEC_K64);
   } else {
     for (int k = 0; k < DEC_K64; ++k) {  // Wq_h, Wk_h: image [k64][128 rows] (q rows 0..63, k rows 64..127)
       dma_rows(wq + k * 128, DEC_D * 2, 64, ra + k * 128 * 128, 8 * (2 * k) + 2);
@@ -309,7 +411,7 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
     kpre[i] = brow < p.rows && j < t0 ? hist(p.kc, j) : (f32x4){0.f, 0.f, 0.f, 0.f};
   }
   if (FR && NSC == 2) {  // X landed, the 16 q|k|v fragments of waves 0-11 may still fly (the cached keys behind them)
-    if (wave < 12) x_landed<2 * DEC_K64>();
+    if (wave < 12) x_landed<NWQ>();
     else x_landed<0>();
     open_barrier();  // one barrier on every wave's path
   } else {
@@ -458,7 +560,9 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
 //   round 2: W2 slice [2 k64][512 rows][128 B] (region A); h image + k-half reduction in region B
 // FR (DecFfnArgs::W1f / W2f, round 4): each wave loads its W1 fragments (tile t, k-half kh: 8 KiB) and its W2
 // fragments (column tiles 2 wave, 2 wave + 1 of the slice: 8 KiB) into registers with the X image - one memory round.
-template <bool FR, int NSC = 0>
+// FOLD (round 5, FR with two planes): X = the residual LN2 of the cross-attention chain's FOLD slabs, written by the
+// block of slice 0; the W2 fragments are then issued after the fold (register budget) and fly behind FFN-1.
+template <bool FR, int NSC = 0, int FOLD = 0>
 __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ra = smem;
@@ -468,22 +572,33 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int nslice = DEC_F / 128;
-  const int j = blockIdx.x % nslice, row0 = (blockIdx.x / nslice) * DEC_ROWS;
+  const int bid = blockIdx.x;
+  const bool xt = FOLD && p.xcd_tiles;  // tile = bid % 8 + 8 (bid / 128), slice = (bid / 8) % 16: a tile on one XCD
+  const int j = xt ? (bid >> 3) & 15 : bid % nslice;
+  const int row0 = (xt ? (bid & 7) + 8 * (bid >> 7) : bid / nslice) * DEC_ROWS;
   const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
 
   const int t = wave & 7, kh = wave >> 3;  // FFN-1 tile, k half (4 of the 8 k64 steps)
   const f32x4 bias = *(const f32x4*)(p.b1 + j * 128 + t * 16 + 4 * fq);  // oldest load (as dec_sa_kernel)
-  dma_x(p.A, p.aL, ns, row0, p.rows, sx);
-  bf16x8 w1f[FR ? DEC_K64 : 1], w2f[FR ? 8 : 1];
+  FoldIn<FOLD ? FOLD : 1> fi;
+  if constexpr (FOLD) fold_issue<FOLD>(p.fold, row0, p.rows, smem + FOLD_PRM, fi);
+  else dma_x(p.A, p.aL, ns, row0, p.rows, sx);
+  constexpr int NW1 = DEC_K64, NW2 = 8;  // fragments per wave (the opening's vmcnt counts them)
+  bf16x8 w1f[FR ? NW1 : 1], w2f[FR ? NW2 : 1];
   if (FR) {
-    load_frags<DEC_K64>(w1f, p.W1f, (long)(j * 8 + t) * 2 * DEC_K64 + kh * DEC_K64);
-    load_frags<8>(w2f, p.W2f, (long)(j * 32 + 2 * wave) * 4);
+    load_frags<NW1>(w1f, p.W1f, (long)(j * 8 + t) * 2 * DEC_K64 + kh * DEC_K64);
+    if (!FOLD) load_frags<NW2>(w2f, p.W2f, (long)(j * 32 + 2 * wave) * 4);
+    if (FOLD) __builtin_amdgcn_sched_barrier(0);  // every W1 fragment load issued before the fold's first wait
   } else {
     const char* w1 = (const char*)(p.W1 + (long)j * 128 * DEC_D);
     for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 128, ra + k * 128 * 128);
   }
-  if (FR && NSC == 2) {
-    open_x<DEC_K64 + 8>();  // X landed; W1 / W2 fragments may still fly
+  if constexpr (FOLD) {
+    fold_finish<FOLD, 2>(p.fold, fi, row0, p.rows, smem + FOLD_PRM, sx, j == 0);
+    load_frags<NW2>(w2f, p.W2f, (long)(j * 32 + 2 * wave) * 4);
+    lds_barrier();  // the X image written
+  } else if (FR && NSC == 2) {
+    open_x<NW1 + NW2>();  // X landed; W1 / W2 fragments may still fly
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -533,7 +648,10 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
 // W2_h [512 rows][128 B] 64 KiB.  out = OUT_SPLIT (q~ planes of head h) or OUT_PARTIAL (slab h).
 // FR (ChainArgs::W1f / W2f, round 4): W1 (tile t, k-quarter kq: 4 KiB) and W2 (column tiles 2 wave, 2 wave + 1: 4 KiB)
 // fragments per wave in registers, 32 KiB of LDS (the X image) instead of 160.
-template <bool FR, int NSC = 0>
+// FOLD (round 5, FR with two planes, X shared by the heads): X = the residual LN1 of dec_sa's FOLD slabs (fold_issue /
+// fold_finish), written by the block of head 0; the 8 head blocks of a row tile then run on one XCD (xcd_tiles) so
+// the tile's slabs are read from that XCD's L2 after the first block's miss.
+template <bool FR, int NSC = 0, int FOLD = 0>
 __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* w1i = smem;                       // 64 KiB (FR: none)
@@ -543,24 +661,34 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   char* sy = sx + 12 * 64 * 16;           // Y image [1 k64][ns][16][128 B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int h = blockIdx.x % p.H, row0 = (blockIdx.x / p.H) * DEC_ROWS;
+  const int bid = blockIdx.x;
+  const bool xt = FOLD && p.xcd_tiles;  // tile = bid % 8 + 8 (bid / 64), head = (bid / 8) % 8: a tile's heads on one XCD
+  const int h = xt ? (bid >> 3) & 7 : bid % p.H;
+  const int row0 = (xt ? (bid & 7) + 8 * (bid >> 6) : bid / p.H) * DEC_ROWS;
   const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
   const int t = wave & 3, kq = wave >> 2;  // Y tile, k quarter (2 of the 8 k64 steps)
   const f32x4 bv = *(const f32x4*)(p.b1 + h * 64 + t * 16 + 4 * fq);  // oldest loads (as dec_sa_kernel)
   // (unconditional, from b1 when there is no scale: a load under a branch made hipcc wait for it at the join)
   const float bsc = *(p.b1_scale ? p.b1_scale + (long)min(row0 + fr, p.M - 1) * p.H + h : p.b1);
-  dma_x(p.X + (long)h * p.x_hstride, p.x_lo, ns, row0, p.M, sx, p.ldx);
-  bf16x8 w1f[FR ? 4 : 1], w2f[FR ? 4 : 1];
+  FoldIn<FOLD ? FOLD : 1> fi;
+  if constexpr (FOLD) fold_issue<FOLD>(p.fold, row0, p.M, smem + FOLD_PRM, fi);
+  else dma_x(p.X + (long)h * p.x_hstride, p.x_lo, ns, row0, p.M, sx, p.ldx);
+  constexpr int NW1 = 4, NW2 = 4;  // fragments per wave (the opening's vmcnt counts them)
+  bf16x8 w1f[FR ? NW1 : 1], w2f[FR ? NW2 : 1];
   if (FR) {
-    load_frags<4>(w1f, p.W1f, (long)(h * 4 + t) * 2 * DEC_K64 + kq * 4);
-    load_frags<4>(w2f, p.W2f, (long)(h * 32 + 2 * wave) * 2);
+    load_frags<NW1>(w1f, p.W1f, (long)(h * 4 + t) * 2 * DEC_K64 + kq * 4);
+    load_frags<NW2>(w2f, p.W2f, (long)(h * 32 + 2 * wave) * 2);
+    if (FOLD) __builtin_amdgcn_sched_barrier(0);  // every fragment load issued before the fold's first wait
   } else {
     const char* w1 = (const char*)(p.W1 + (long)h * 64 * DEC_D);
     for (int k = 0; k < DEC_K64; ++k) dma_rows(w1 + k * 128, DEC_D * 2, 64, w1i + k * 64 * 128, 8 * k + 2);
     dma_rows((const char*)(p.W2 + (long)h * p.w2_hstride), p.ldw2 * 2, DEC_D, w2i, 2);
   }
-  if (FR && NSC == 2) {
-    open_x<8>();  // X landed; W1 / W2 fragments may still fly
+  if constexpr (FOLD) {
+    fold_finish<FOLD, 2>(p.fold, fi, row0, p.M, smem + FOLD_PRM, sx, h == 0);
+    lds_barrier();  // the X image written
+  } else if (FR && NSC == 2) {
+    open_x<NW1 + NW2>();  // X landed; W1 / W2 fragments may still fly
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -622,6 +750,11 @@ hipError_t dec_lds_attr() {
   attr = true;
   return hipSuccess;
 }
+// a fold's arguments: the 8 producer slabs of d_model-wide rows, the LN parameters, x_out apart from x
+bool fold_ok(const RlnArgs& f, int nparts) {
+  return f.parts && f.x && f.x_out && f.x_out != f.x && f.bias && f.w && f.b && f.nparts == nparts &&
+         f.part_stride > 0;
+}
 }  // namespace
 
 hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
@@ -632,6 +765,15 @@ hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
   const hipError_t e = dec_lds_attr();
   if (e != hipSuccess) return e;
   const int blocks = (a.M + DEC_ROWS - 1) / DEC_ROWS * a.H;
+  if (a.fold.parts) {  // the residual LN1 folded in: X from dec_sa's 8 slabs
+    if (!a.W1f || a.nsplit != 2 || a.x_hstride != 0 || a.H != DEC_H || a.out != OUT_SPLIT || a.mg.tick ||
+        !fold_ok(a.fold, DEC_H))
+      return hipErrorInvalidValue;
+    ChainArgs b = a;
+    b.xcd_tiles = a.xcd_tiles && ((a.M + DEC_ROWS - 1) / DEC_ROWS) % 8 == 0;
+    hipLaunchKernelGGL((dec_chain_kernel<true, 2, DEC_H>), dim3(blocks), dim3(1024), DEC_LDS_FOLD, s, b);
+    return hipGetLastError();
+  }
   if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_chain_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else if (a.W1f) hipLaunchKernelGGL(dec_chain_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else hipLaunchKernelGGL(dec_chain_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
@@ -657,6 +799,13 @@ hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s) {
   const hipError_t e = dec_lds_attr();
   if (e != hipSuccess) return e;
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * (DEC_F / 128);
+  if (a.fold.parts) {  // the residual LN2 folded in: X from the cross-attention chain's 8 slabs
+    if (!a.W1f || a.nsplit != 2 || a.mg.tick || !fold_ok(a.fold, DEC_H)) return hipErrorInvalidValue;
+    DecFfnArgs b = a;
+    b.xcd_tiles = a.xcd_tiles && ((a.rows + DEC_ROWS - 1) / DEC_ROWS) % 8 == 0;
+    hipLaunchKernelGGL((dec_ffn_kernel<true, 2, DEC_H>), dim3(blocks), dim3(1024), DEC_LDS_FOLD, s, b);
+    return hipGetLastError();
+  }
   if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_ffn_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else if (a.W1f) hipLaunchKernelGGL(dec_ffn_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else hipLaunchKernelGGL(dec_ffn_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);

@@ -1012,7 +1012,7 @@ constexpr int MAX_KSPLIT = 16;  // partial slabs: split-K GEMMs, 8 heads (dec_sa
 constexpr int XDEC_SLABS = 33;  // the group-persistent step: 32 feed-forward slabs + the pre-LN sums
 
 struct DecodeBufs {
-  float *x, *qkv, *kc, *vc, *part;
+  float *x, *x2, *qkv, *kc, *vc, *part;  // x2: the second residual-stream buffer of the folded LayerNorms
   bf16_t *a, *q, *qt, *c, *o, *hb, *memp;
   long aL, qL, cL, hL, memL;
   size_t kvl;  // KV-cache stride between layers (of the whole buffer)
@@ -1028,7 +1028,7 @@ struct DecodeBufs {
 DecodeBufs sub_bufs(const DecodeBufs& b, const icap_model_desc& d, int r0, int Lmax, int S) {
   const int D = d.d_model, H = d.nhead;
   DecodeBufs v = b;
-  v.x += (size_t)r0 * D; v.a += (size_t)r0 * D; v.qkv += (size_t)r0 * 3 * D; v.q += (size_t)r0 * D;
+  v.x += (size_t)r0 * D; v.x2 += (size_t)r0 * D; v.a += (size_t)r0 * D; v.qkv += (size_t)r0 * 3 * D; v.q += (size_t)r0 * D;
   v.qt += (size_t)r0 * H * D; v.c += (size_t)r0 * H * D; v.o += (size_t)r0 * D; v.hb += (size_t)r0 * d.dim_ff;
   v.kc += (size_t)r0 * H * Lmax * 64; v.vc += (size_t)r0 * H * Lmax * 64;
   v.part += (size_t)r0 * D; v.memp += (size_t)r0 * S * D;
@@ -1047,7 +1047,7 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   const icap_model_desc& d = h->d;
   const int D = d.d_model, ns = h->ns, H = d.nhead;
   icap_handle::DecWS& w = h->dws[wsi];
-  w.x.ensure((size_t)rows * D * 4);
+  w.x.ensure((size_t)2 * rows * D * 4);  // x and x2
   w.a.ensure((size_t)rows * D * 2 * ns);
   w.qkv.ensure((size_t)rows * 3 * D * 4);
   w.q.ensure((size_t)rows * D * 2 * ns);
@@ -1071,7 +1071,7 @@ DecodeBufs dec_bufs(icap_handle* h, int rows, int B, int Lmax, int S, int kv_row
   }
   DecodeBufs b;
   b.tick = w.tick.as<int>();
-  b.x = w.x.as<float>(); b.a = w.a.as<bf16_t>(); b.qkv = w.qkv.as<float>();
+  b.x = w.x.as<float>(); b.x2 = b.x + (size_t)rows * D; b.a = w.a.as<bf16_t>(); b.qkv = w.qkv.as<float>();
   b.q = w.q.as<bf16_t>(); b.qt = w.qt.as<bf16_t>(); b.c = w.c.as<bf16_t>();
   b.o = w.o.as<bf16_t>(); b.hb = w.h.as<bf16_t>();
   b.kc = w.kv.as<float>();
@@ -1129,7 +1129,23 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
 #else
   constexpr int merge_knob = 0;
 #endif
+  // round 5: the residual LN1 / LN2 folded into the register-fragment blocks that consume them (the q~ chain,
+  // dec_ffn; decode.hip fold_issue / fold_finish), a mask: 1 = LN1, 2 = LN2.  A fold reads the residual from xc and
+  // writes the normalised rows to the other x buffer (the tile's other blocks still read xc), so the two buffers
+  // alternate; dec_ffn's 16 slabs then go to the second slab set (its own fold reads the chain's 8 from the first).
+#ifndef ICAP_DEC_FOLD_DEFAULT
+#define ICAP_DEC_FOLD_DEFAULT 3
+#endif
+#ifndef ICAP_DEC_XCD_DEFAULT
+#define ICAP_DEC_XCD_DEFAULT 1
+#endif
+  static const int fold_knob = icap_knob("ICAP_DEC_FOLD", ICAP_DEC_FOLD_DEFAULT);
+  static const int xcd_knob = icap_knob("ICAP_DEC_XCD", ICAP_DEC_XCD_DEFAULT);
+  const int fold = fused && ns == 2 && !merge_knob ? fold_knob : 0;
   const int merge = fused ? merge_knob : 0;
+  float* xc = b.x;                                             // the residual stream's current buffer
+  auto x_other = [&] { return xc == b.x ? b.x2 : b.x; };
+  float* const PF = (fold & 2) ? b.part + (size_t)MAX_KSPLIT * PS : b.part;  // dec_ffn's slabs
   for (int l = 0; l < d.n_dec_layers; ++l) {
     const DecLayer& L = h->dec[l];
     bool merged2 = false;
@@ -1152,8 +1168,8 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       sa.drop = dl;
       h->timed(PROF_DEC_FUSED, 2.0 * rows * (3.0 * D * D + (double)D * D), 2.0 * (4.0 * D * D + (double)rows * D * ns),
                s, [&] { HIPCHK(launch_dec_sa(sa, s)); });
-      if (!sa.mg.tick)
-        HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, H, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
+      if (!sa.mg.tick && !(fold & 1))
+        HIPCHK(launch_residual_layernorm(xc, rows, D, b.part, H, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL,
                                          ns, s, dl, 2));
     } else {
       h->wgemm(b.a, D, b.aL, L.sa_qkv.w, D, L.sa_qkv.b, rows, 3 * D, D, b.qkv, 3 * D, 0, EPI_NONE, OUT_F32, WAVE_2x2,
@@ -1180,6 +1196,11 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.C = b.qt; c.ldc = (long)H * D; c.c_lo = b.cL; c.c_hstride = D;
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_SPLIT;
       if (fused) c.W1f = L.f_caq, c.W2f = L.f_kT;
+      if (fold & 1) {  // X = LN1(x + SA): dec_sa's 8 slabs
+        c.fold = RlnArgs{xc, x_other(), b.part, H, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, dl, 2};
+        c.xcd_tiles = xcd_knob;
+        xc = x_other();
+      }
       h->chain(c, s, fused);
     }
     h->timed(PROF_CROSS_ATTN, 4.0 * rows * H * (double)S * D, 2.0 * (double)(rows / mem_rpi) * S * D, s, [&] {
@@ -1210,8 +1231,8 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       h->chain(c, s, fused);
       merged2 = c.mg.tick != nullptr;
     }
-    if (!merged2)
-      HIPCHK(launch_residual_layernorm(b.x, rows, D, b.part, wl ? KS_D : H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a,
+    if (!merged2 && !(fold & 2))
+      HIPCHK(launch_residual_layernorm(xc, rows, D, b.part, wl ? KS_D : H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a,
                                        b.aL, ns, s, dl, 4));
     // feed-forward block
     if (fused) {
@@ -1222,16 +1243,23 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       const bool head_folds = tail_ln && l + 1 == d.n_dec_layers;  // the caller's head normalises instead
       if ((merge & 4) && !head_folds)
         ff.mg = SlabMerge{b.tick, b.x, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a, b.aL, 6, dl};
-      ff.part = b.part; ff.part_stride = PS;
+      ff.part = PF; ff.part_stride = PS;
       ff.drop = dl;
+      if (fold & 2) {  // X = LN2(x + CA): the chain's 8 slabs
+        ff.fold = RlnArgs{xc, x_other(), b.part, H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, dl, 4};
+        ff.xcd_tiles = xcd_knob;
+        xc = x_other();
+      }
       h->timed(PROF_DEC_FUSED, 4.0 * rows * (double)D * F, 2.0 * (2.0 * D * F + (double)rows * D * ns), s,
                [&] { HIPCHK(launch_dec_ffn(ff, s)); });
-      const RlnArgs ln3{b.x, nullptr, b.part, F / 128, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, dl, 6};
-      if (tail_ln && l + 1 == d.n_dec_layers)
-        *tail_ln = ln3;  // the caller's head normalises
-      else if (!ff.mg.tick)
+      const RlnArgs ln3{xc, nullptr, PF, F / 128, PS, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, dl, 6};
+      if (tail_ln && l + 1 == d.n_dec_layers) {
+        *tail_ln = ln3;  // the caller's head normalises (reading x from ln3.x)
+      } else if (!ff.mg.tick) {  // back into b.x (the buffer the next layer's folds and the callers start from)
         HIPCHK(launch_residual_layernorm(b.x, rows, D, ln3.parts, ln3.nparts, PS, ln3.bias, ln3.w, ln3.b, ln3.eps, b.a,
-                                         b.aL, ns, s, dl, 6));
+                                         b.aL, ns, s, dl, 6, xc));
+        xc = b.x;
+      }
     } else {
       h->wgemm(b.a, D, b.aL, L.lin1.w, D, L.lin1.b, rows, F, D, b.hb, F, b.hL, EPI_RELU, OUT_SPLIT, WAVE_2x2, 1, 0, s,
                1, 0, 0, 0, 0, wl ? L.lin1.wl : nullptr);
@@ -1481,7 +1509,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
       }
       HeadArgs ha{};
       decoder_layers(h, v, n, 1, t, max_len, 1, S, st, nullptr, 0, nullptr, drop ? &dc : nullptr, &ha.ln);
-      ha.x = v.x; ha.rows = n; ha.Dm = D; ha.W = h->fc_w; ha.W4 = head_w4(h); ha.bias = h->fc_b; ha.V = d.vocab;
+      ha.x = ha.ln.parts ? ha.ln.x : v.x; ha.rows = n; ha.Dm = D; ha.W = h->fc_w; ha.W4 = head_w4(h); ha.bias = h->fc_b; ha.V = d.vocab;
       ha.logits = step_logits ? step_logits + ((size_t)t * B + r0) * d.vocab : nullptr;
       ha.ld_logits = d.vocab;
       ha.ids = ids + (size_t)r0 * max_len; ha.ld_ids = max_len; ha.id_col = t + 1;
@@ -1914,7 +1942,7 @@ const char* icap_knobs_set() {
       "ICAP_ENC_ATTN16_FULL", "ICAP_XATTN16_S", "ICAP_EAF_ABL", "ICAP_DEC_MERGE", "ICAP_XATTN16_WK",
       "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
       "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE", "ICAP_XDEC_TRACE", "ICAP_GEMM_NARROW",
-      "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW"};
+      "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW", "ICAP_DEC_FOLD", "ICAP_DEC_XCD"};
   for (const char* n : names)
     if (getenv(n)) return n;
   return "";
@@ -2479,15 +2507,30 @@ uint32_t icap_drop_hash_host(uint32_t seed, uint32_t site, uint32_t layer, uint3
 int icap_op_cross_attn(const uint16_t* qt, long qt_lo, const uint16_t* mem16, int rows, int rows_per_image, int S,
                        uint16_t* out, long out_lo, void* stream) {
   return guarded([&] {
-    // the key-split form's partial states and tickets (op entry: a process-wide workspace, tickets zero at rest)
-    static DevBuf xp, xc;
-    if (rows > 0 && xc.n < (size_t)rows * 4) {
-      xp.ensure(cross_attn_part_floats(rows) * 4);
-      xc.ensure((size_t)rows * 4);
-      HIPCHK(hipMemset(xc.p, 0, xc.n));
+    float* xp = nullptr;
+    int* xc = nullptr;
+#ifdef ICAP_TOOLS
+    // the tools-only key-split forms' partial states and tickets: one workspace per device, allocated only when a
+    // knob selects them, tickets zero at rest (the launch that takes a ticket resets it); callers on one device
+    // are serialised by the lock for the allocation only - the key-split op entry is a single-caller measurement
+    if (rows > 0 && (cross_attn_f16s_on() || cross_attn_f16_splits() == 2)) {
+      static std::mutex mu;
+      static std::map<int, std::pair<DevBuf, DevBuf>> per_dev;
+      int dev = 0;
+      HIPCHK(hipGetDevice(&dev));
+      std::lock_guard<std::mutex> lk(mu);
+      auto& w = per_dev[dev];
+      if (w.second.n < (size_t)rows * 4) {
+        w.first.ensure(cross_attn_part_floats(rows) * 4);
+        w.second.ensure((size_t)rows * 4);
+        HIPCHK(hipMemsetAsync(w.second.p, 0, w.second.n, (hipStream_t)stream));
+      }
+      xp = w.first.as<float>();
+      xc = w.second.as<int>();
     }
+#endif
     HIPCHK(launch_cross_attn_f16(qt, qt_lo, mem16, rows, rows_per_image, S, 0.125f, out, out_lo,
-                                 (hipStream_t)stream, DropCfg{}, nullptr, xp.as<float>(), xc.as<int>()));
+                                 (hipStream_t)stream, DropCfg{}, nullptr, xp, xc));
   });
 }
 

@@ -153,9 +153,10 @@ hipError_t launch_gemm_dec(const WaveGemmArgs& g, hipStream_t s);
 
 // A residual LayerNorm folded into the kernel that consumes it: y = LN(x + sum_{s<nparts} parts[s] + bias)
 // (dropout `site` on the sublayer output, as launch_residual_layernorm), computed by the consumer for its own
-// rows.  Used by the decode head for the last layer's LN3 (x_out unused); parts == nullptr: off.  (Folding
-// LN1 / LN2 into the 8 / 16 blocks per row tile of dec_chain / dec_ffn was measured and rejected: each
-// block's 288 KB of slab reads cost more than the separate launch)
+// rows.  Used by the decode head for the last layer's LN3 (x_out unused) and, round 5, by the register-fragment
+// decode blocks (DecSaArgs / ChainArgs / DecFfnArgs::fold, decode.hip): the block builds its X image from the fold
+// instead of the DMA of the a planes, and the tile's writer block stores the normalised rows to x_out (!= x: the
+// tile's other blocks still read x).  parts == nullptr: off.
 struct RlnArgs {
   const float* x; float* x_out; const float* parts; int nparts; long part_stride;
   const float* bias; const float* w; const float* b; float eps;
@@ -190,6 +191,8 @@ struct ChainArgs {
   // h * 32 + n x 2 k32-steps - each wave loads its own fragments straight into registers (no LDS weight staging)
   const bf16_t* W1f; const bf16_t* W2f;
   SlabMerge mg;  // dec_chain, OUT_PARTIAL only
+  RlnArgs fold;  // dec_chain FR with two planes, x_hstride 0: X = the residual LN of the producer's slabs (nparts 8)
+  int xcd_tiles;  // with fold: the 8 head blocks of a row tile on one XCD (when the tile count is a multiple of 8)
 };
 hipError_t launch_chain_dec(const ChainArgs& a, hipStream_t s);
 
@@ -207,6 +210,7 @@ struct DecSaArgs {
   // as tiles h * 32 + n x 2 k32-steps (mode 2, ksl 64)
   const bf16_t* Wqkv_f; const bf16_t* Wo_f;
   SlabMerge mg;
+  RlnArgs fold;  // FR with two planes: A = the residual LN of the producer's slabs (nparts 16)
 };
 hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s);
 // dec_ffn: slab j of 16 = relu(a W1[128j:128j+128]^T + b1) W2[:, 128j:128j+128]^T -> part[j][rows][512]
@@ -218,6 +222,8 @@ struct DecFfnArgs {
   // frag_pack images (both or neither): W1 as tiles 0..127 x 16 k32-steps, W2 as tiles j * 32 + n x 4 k32-steps
   const bf16_t* W1f; const bf16_t* W2f;
   SlabMerge mg;
+  RlnArgs fold;  // FR with two planes: A = the residual LN of the producer's slabs (nparts 8)
+  int xcd_tiles;  // with fold: the 16 slice blocks of a row tile on one XCD (when the tile count is a multiple of 8)
 };
 hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s);
 // The chained per-head cross-attention products (ChainArgs as launch_chain_dec, N2 = 512) with 16-row
@@ -309,7 +315,8 @@ hipError_t launch_layernorm(const float* x, long ldx, int rows, int D, int in_gr
 // x = LN(x + sum_{s<nparts} parts[s*part_stride + row*D + col] + bias) in place (fp32), plus planes.
 hipError_t launch_residual_layernorm(float* x, int rows, int D, const float* parts, int nparts, long part_stride,
                                     const float* bias, const float* w, const float* b, float eps, bf16_t* out_bf,
-                                    long bf_lo, int nsplit, hipStream_t s, DropCfg drop = DropCfg{}, int site = 0);
+                                    long bf_lo, int nsplit, hipStream_t s, DropCfg drop = DropCfg{}, int site = 0,
+                                    const float* x_in = nullptr);  // x_in: the residual input (default x, in place)
 hipError_t launch_im2col_patches(const float* img, int B, int C, int HW, int P, bf16_t* out, long lo,
                                  int nsplit, hipStream_t s);
 hipError_t launch_cls_rows(const float* cls, const float* pos, float* x, int B, int tokens, int D,

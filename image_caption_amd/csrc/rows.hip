@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void pack_i8_rows_kernel(const float* __restri
 constexpr int RLN_MAX_PARTS = 16;
 
 template <int NT>
-__global__ __launch_bounds__(NT) void residual_layernorm_kernel(float* __restrict__ x, int rows,
+__global__ __launch_bounds__(NT) void residual_layernorm_kernel(const float* xin, float* x, int rows,
                                                                 const float* __restrict__ parts, int nparts,
                                                                 long part_stride, const float* __restrict__ bias,
                                                                 const float* __restrict__ w,
@@ -174,12 +174,12 @@ __global__ __launch_bounds__(NT) void residual_layernorm_kernel(float* __restric
   __shared__ float red[2][NW];
   const int row = blockIdx.x, col = threadIdx.x * 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float* xr = x + (long)row * D;
+  float* xr = x + (long)row * D;  // (xin: the residual input when it is not x itself)
   f32x4 pp[RLN_MAX_PARTS];
 #pragma unroll
   for (int s = 0; s < RLN_MAX_PARTS; ++s)
     pp[s] = s < nparts ? *(const f32x4*)(parts + s * part_stride + (long)row * D + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 v = *(const f32x4*)(xr + col);
+  f32x4 v = *(const f32x4*)(xin + (long)row * D + col);
   const f32x4 bb = bias ? *(const f32x4*)(bias + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
   const f32x4 wv = *(const f32x4*)(w + col), bv = *(const f32x4*)(b + col);
   if (drop.thr == 0) {
@@ -397,14 +397,16 @@ hipError_t launch_pack_i8_rows(const float* w, int N, int K, int8_t* out, float*
 
 hipError_t launch_residual_layernorm(float* x, int rows, int D, const float* parts, int nparts, long part_stride,
                                     const float* bias, const float* w, const float* b, float eps, bf16_t* out_bf,
-                                    long bf_lo, int nsplit, hipStream_t s, DropCfg drop, int site) {
+                                    long bf_lo, int nsplit, hipStream_t s, DropCfg drop, int site,
+                                    const float* x_in) {
   if (nparts < 0 || nparts > RLN_MAX_PARTS || rows <= 0) return hipErrorInvalidValue;
   dim3 grid(rows);
+  const float* xi = x_in ? x_in : x;
   if (D == 512)
-    hipLaunchKernelGGL(residual_layernorm_kernel<128>, grid, dim3(128), 0, s, x, rows, parts, nparts, part_stride,
+    hipLaunchKernelGGL(residual_layernorm_kernel<128>, grid, dim3(128), 0, s, xi, x, rows, parts, nparts, part_stride,
                        bias, w, b, eps, out_bf, bf_lo, nsplit, drop, site);
   else if (D == 768)
-    hipLaunchKernelGGL(residual_layernorm_kernel<192>, grid, dim3(192), 0, s, x, rows, parts, nparts, part_stride,
+    hipLaunchKernelGGL(residual_layernorm_kernel<192>, grid, dim3(192), 0, s, xi, x, rows, parts, nparts, part_stride,
                        bias, w, b, eps, out_bf, bf_lo, nsplit, drop, site);
   else
     return hipErrorInvalidValue;

@@ -122,9 +122,10 @@ def test_enc_attention(cuda, B, N, H, nsplit):
 def test_cross_attn_f16(cuda, rows, rpi, S):
     """Key-absorbed decoder cross-attention over one fp16 memory plane (decode loops, beam slots and
     teacher-forced rows of an image share a block): against fp64 softmax(q~ mem^T / 8) mem on the same
-    rounded operands, ragged last chunks (S = 196, 70, 49, 1) and odd rows per image.  One row per image runs the
-    key-split form (cross_attn_f16s_kernel: two workgroups per row merged by the second to finish): S = 1 and 17
-    leave part 1 with no / one key, S = 256 fills 8 key tiles, rows not a multiple of 8 pad the grid."""
+    rounded operands, ragged last chunks (S = 196, 70, 49, 1) and odd rows per image.  The product build runs the
+    32-key chunk loop (cross_attn_f16_kernel<1, 32>) for every case: S = 1 and 17 are one partial chunk, S = 256
+    eight full ones, odd row counts leave the last block with one row.  (The key-split forms are tools-only:
+    tools/r4_tools_pytest.sh runs this test with ICAP_XATTN16_S=1 on the tools build.)"""
     L, lib = _lib()
     g = torch.Generator(device="cpu").manual_seed(rows * 7 + S)
     B = rows // rpi
@@ -141,7 +142,7 @@ def test_cross_attn_f16(cuda, rows, rpi, S):
     torch.cuda.synchronize()
     got = value(out, 2).double().cpu()
     assert (got - ref).abs().max().item() < 2e-4
-    if rpi == 1:  # the merge of the two halves is order-independent: repeated launches are bitwise equal
+    if rpi == 1:  # repeated launches are bitwise equal (the tools build's key-split merge too)
         for _ in range(3):
             again = torch.zeros_like(out)
             L.check(lib.icap_op_cross_attn(Q.data_ptr(), rows * 8 * 512, mem.to(cuda).data_ptr(), rows, rpi, S,

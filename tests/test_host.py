@@ -77,8 +77,8 @@ def test_product_build_refuses_measurement_knobs(monkeypatch):
 
 
 def test_product_build_ships_only_shipped_forms():
-    """The measured-and-rejected kernel forms (gemm_tools.hip, the persistent decode steps decstep.hip / xdec.hip) are
-    compiled into the tools build only: the product source list does not hold them and the product library's code
+    """The measured-and-rejected kernel forms (gemm_tools.hip, the persistent decode steps decstep.hip / xdec.hip, the
+    key-split and wave-owned cross-attentions) are compiled into the tools build only: the product source list does not hold them and the product library's code
     object has none of their kernels."""
     from image_caption_amd import _lib, build
 
@@ -88,7 +88,8 @@ def test_product_build_ships_only_shipped_forms():
     if lib.icap_tools_build():
         pytest.skip("tools build")
     blob = build.LIB.read_bytes()
-    for kernel in (b"dec_step_kernel", b"xdec_kernel", b"gemm_f16q_kernel", b"gemm_8ph_kernel"):
+    for kernel in (b"dec_step_kernel", b"xdec_kernel", b"gemm_f16q_kernel", b"gemm_8ph_kernel",
+                   b"cross_attn_f16s_kernel", b"cross_attn_wk_kernel", b"cross_attn_f16_kernelILi2E"):
         assert kernel not in blob, kernel
 
 
