@@ -371,7 +371,9 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   char* sc = sx + 16 * 192 * 4;           // ctx image [1 k64][ns][16][128 B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int h = blockIdx.x & (DEC_H - 1), row0 = (blockIdx.x >> 3) * DEC_ROWS;
+  const int bid = blockIdx.x;  // xcd_tiles: tile = bid % 8 + 8 (bid / 64), head = (bid / 8) % 8 (a tile on one XCD)
+  const int h = p.xcd_tiles ? (bid >> 3) & 7 : bid & (DEC_H - 1);
+  const int row0 = (p.xcd_tiles ? (bid & 7) + 8 * (bid >> 6) : bid >> 3) * DEC_ROWS;
   const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
   const char* wq = (const char*)(p.Wqkv + (long)(h * DEC_HD) * DEC_D);
   const char* wk = (const char*)(p.Wqkv + (long)(DEC_D + h * DEC_HD) * DEC_D);
@@ -662,7 +664,7 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int bid = blockIdx.x;
-  const bool xt = FOLD && p.xcd_tiles;  // tile = bid % 8 + 8 (bid / 64), head = (bid / 8) % 8: a tile's heads on one XCD
+  const bool xt = p.xcd_tiles;  // tile = bid % 8 + 8 (bid / 64), head = (bid / 8) % 8: a tile's heads on one XCD
   const int h = xt ? (bid >> 3) & 7 : bid % p.H;
   const int row0 = (xt ? (bid & 7) + 8 * (bid >> 6) : bid / p.H) * DEC_ROWS;
   const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
@@ -765,7 +767,10 @@ hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
   const hipError_t e = dec_lds_attr();
   if (e != hipSuccess) return e;
   const int blocks = (a.M + DEC_ROWS - 1) / DEC_ROWS * a.H;
-  if (a.fold.parts) {  // the residual LN1 folded in: X from dec_sa's 8 slabs
+  if (a.fold.parts) {  // the residual LN1 folded in: X from dec_sa's 8 slabs (measured slower: tools build only)
+#ifndef ICAP_TOOLS
+    return hipErrorInvalidValue;
+#else
     if (!a.W1f || a.nsplit != 2 || a.x_hstride != 0 || a.H != DEC_H || a.out != OUT_SPLIT || a.mg.tick ||
         !fold_ok(a.fold, DEC_H))
       return hipErrorInvalidValue;
@@ -773,10 +778,13 @@ hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
     b.xcd_tiles = a.xcd_tiles && ((a.M + DEC_ROWS - 1) / DEC_ROWS) % 8 == 0;
     hipLaunchKernelGGL((dec_chain_kernel<true, 2, DEC_H>), dim3(blocks), dim3(1024), DEC_LDS_FOLD, s, b);
     return hipGetLastError();
+#endif
   }
-  if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_chain_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
-  else if (a.W1f) hipLaunchKernelGGL(dec_chain_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
-  else hipLaunchKernelGGL(dec_chain_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
+  ChainArgs c = a;
+  c.xcd_tiles = a.xcd_tiles && a.H == DEC_H && ((a.M + DEC_ROWS - 1) / DEC_ROWS) % 8 == 0;
+  if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_chain_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, c);
+  else if (a.W1f) hipLaunchKernelGGL(dec_chain_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, c);
+  else hipLaunchKernelGGL(dec_chain_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, c);
   return hipGetLastError();
 }
 
@@ -787,9 +795,11 @@ hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s) {
   const hipError_t e = dec_lds_attr();
   if (e != hipSuccess) return e;
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * DEC_H;
-  if (a.Wqkv_f && a.nsplit == 2) hipLaunchKernelGGL((dec_sa_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
-  else if (a.Wqkv_f) hipLaunchKernelGGL(dec_sa_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
-  else hipLaunchKernelGGL(dec_sa_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
+  DecSaArgs b = a;
+  b.xcd_tiles = a.xcd_tiles && ((a.rows + DEC_ROWS - 1) / DEC_ROWS) % 8 == 0;
+  if (a.Wqkv_f && a.nsplit == 2) hipLaunchKernelGGL((dec_sa_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, b);
+  else if (a.Wqkv_f) hipLaunchKernelGGL(dec_sa_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, b);
+  else hipLaunchKernelGGL(dec_sa_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, b);
   return hipGetLastError();
 }
 
@@ -799,12 +809,16 @@ hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s) {
   const hipError_t e = dec_lds_attr();
   if (e != hipSuccess) return e;
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * (DEC_F / 128);
-  if (a.fold.parts) {  // the residual LN2 folded in: X from the cross-attention chain's 8 slabs
+  if (a.fold.parts) {  // the residual LN2 folded in: X from the cross-attention chain's 8 slabs (tools build only)
+#ifndef ICAP_TOOLS
+    return hipErrorInvalidValue;
+#else
     if (!a.W1f || a.nsplit != 2 || a.mg.tick || !fold_ok(a.fold, DEC_H)) return hipErrorInvalidValue;
     DecFfnArgs b = a;
     b.xcd_tiles = a.xcd_tiles && ((a.rows + DEC_ROWS - 1) / DEC_ROWS) % 8 == 0;
     hipLaunchKernelGGL((dec_ffn_kernel<true, 2, DEC_H>), dim3(blocks), dim3(1024), DEC_LDS_FOLD, s, b);
     return hipGetLastError();
+#endif
   }
   if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_ffn_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else if (a.W1f) hipLaunchKernelGGL(dec_ffn_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);

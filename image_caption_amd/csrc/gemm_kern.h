@@ -603,10 +603,39 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   const int M = p.M, nk = p.K / KS;
   const int srow = wave * IPW * 8 + (lane >> 3), schunk = (lane & 7) ^ (srow & 7);
   const int fr = lane & 15, fq = lane >> 4;
+#ifndef ICAP_F16P_PRIO
+#define ICAP_F16P_PRIO 0
+#endif
+  // ICAP_F16P_PRIO (compile-time form, round 5): the younger wave of each SIMD (waves 4-7) at priority 1 for the
+  // whole launch (cdna_hip_programming.md T5, static form) - within noise (frac 0.2913-0.2929, same box), off
+  if (ICAP_F16P_PRIO && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
 
+#ifndef ICAP_F16P_BUF
+#define ICAP_F16P_BUF 1
+#endif
+  // ICAP_F16P_BUF (compile-time form, round 5): the stage pieces as buffer loads (32-bit per-lane row offsets in the
+  // resource of A / W, the k-step in the scalar offset) instead of flat 64-bit per-lane addresses: 10 fewer VGPRs and
+  // frac 0.2924-0.2931 -> 0.2941-0.2951 on one box (profiles/r05/gemm_buf_ab.txt; 0 = the flat form)
+  const long bytesA = (long)M * p.lda * 2, bytesW = (long)p.N * p.ldw * 2;
+  const i32x4r rsA = buf_rsrc(p.A, (uint32_t)(bytesA < 0xffffffffL ? bytesA : 0xffffffffL));
+  const i32x4r rsW = buf_rsrc(p.W, (uint32_t)(bytesW < 0xffffffffL ? bytesW : 0xffffffffL));
   auto stage = [&](int t, int kt, int buf) {  // tile t (logical), k-step kt -> ring buffer buf
     const int bm = t / nbn, bn = t - bm * nbn, m0 = bm * BM, n0 = bn * BN;
     char* s0 = smem + buf * STAGE;
+    if constexpr (ICAP_F16P_BUF) {
+#pragma unroll
+      for (int i = 0; i < IPW; ++i) {
+        if (BM < 256 && (wave * IPW + i) * 8 >= BM) break;
+        const int row = min(m0 + srow + i * 8, M - 1);
+        lds_dma_buf16(rsA, (uint32_t)(row * p.lda + schunk * 8) * 2, (uint32_t)kt * KS * 2,
+                      (LDS_AS void*)(s0 + (wave * IPW + i) * 1024));
+      }
+#pragma unroll
+      for (int i = 0; i < IPW; ++i)
+        lds_dma_buf16(rsW, (uint32_t)((n0 + srow + i * 8) * p.ldw + schunk * 8) * 2, (uint32_t)kt * KS * 2,
+                      (LDS_AS void*)(s0 + OPA + (wave * IPW + i) * 1024));
+      return;
+    }
     const bf16_t* Ab = p.A + kt * KS + schunk * 8;
     const bf16_t* Wb = p.W + (long)(n0 + srow) * p.ldw + kt * KS + schunk * 8;
 #pragma unroll

@@ -1129,18 +1129,20 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
 #else
   constexpr int merge_knob = 0;
 #endif
-  // round 5: the residual LN1 / LN2 folded into the register-fragment blocks that consume them (the q~ chain,
-  // dec_ffn; decode.hip fold_issue / fold_finish), a mask: 1 = LN1, 2 = LN2.  A fold reads the residual from xc and
-  // writes the normalised rows to the other x buffer (the tile's other blocks still read xc), so the two buffers
-  // alternate; dec_ffn's 16 slabs then go to the second slab set (its own fold reads the chain's 8 from the first).
-#ifndef ICAP_DEC_FOLD_DEFAULT
-#define ICAP_DEC_FOLD_DEFAULT 3
+  // round 5, measured slower and tools-only: the residual LN1 / LN2 folded into the register-fragment blocks that
+  // consume them (the q~ chain, dec_ffn; decode.hip fold_issue / fold_finish; knob ICAP_DEC_FOLD, a mask: 1 = LN1,
+  // 2 = LN2): each block's 288 KB of slab reads cost about the 5 us launch they remove - decode 11.18-11.23 against
+  // 11.02-11.05 ms, 11.37-11.44 against 11.28-11.32 on a second box (profiles/r05/fold_ab.txt).  A fold reads the
+  // residual from xc and writes the normalised rows to the other x buffer (the tile's other blocks still read xc), so
+  // the two buffers alternate; dec_ffn's 16 slabs then go to the second slab set.  ICAP_DEC_XCD (tools), a mask: 1 = a
+  // fold's row-tile blocks on one XCD (without it the folds cost 1 ms more), 2 = dec_sa / the output chain too (their
+  // weights then leave the per-XCD L2: decode 11.36-11.41 against 11.28-11.32 ms).
+#ifdef ICAP_TOOLS
+  static const int fold_knob = icap_knob("ICAP_DEC_FOLD", 0);
+  static const int xcd_knob = icap_knob("ICAP_DEC_XCD", 1);
+#else
+  constexpr int fold_knob = 0, xcd_knob = 0;
 #endif
-#ifndef ICAP_DEC_XCD_DEFAULT
-#define ICAP_DEC_XCD_DEFAULT 1
-#endif
-  static const int fold_knob = icap_knob("ICAP_DEC_FOLD", ICAP_DEC_FOLD_DEFAULT);
-  static const int xcd_knob = icap_knob("ICAP_DEC_XCD", ICAP_DEC_XCD_DEFAULT);
   const int fold = fused && ns == 2 && !merge_knob ? fold_knob : 0;
   const int merge = fused ? merge_knob : 0;
   float* xc = b.x;                                             // the residual stream's current buffer
@@ -1166,6 +1168,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       sa.anc = anc;
       sa.part = b.part; sa.part_stride = PS;
       sa.drop = dl;
+      sa.xcd_tiles = (xcd_knob & 2) != 0;
       h->timed(PROF_DEC_FUSED, 2.0 * rows * (3.0 * D * D + (double)D * D), 2.0 * (4.0 * D * D + (double)rows * D * ns),
                s, [&] { HIPCHK(launch_dec_sa(sa, s)); });
       if (!sa.mg.tick && !(fold & 1))
@@ -1198,7 +1201,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       if (fused) c.W1f = L.f_caq, c.W2f = L.f_kT;
       if (fold & 1) {  // X = LN1(x + SA): dec_sa's 8 slabs
         c.fold = RlnArgs{xc, x_other(), b.part, H, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, dl, 2};
-        c.xcd_tiles = xcd_knob;
+        c.xcd_tiles = xcd_knob & 1;
         xc = x_other();
       }
       h->chain(c, s, fused);
@@ -1227,6 +1230,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_PARTIAL;
       if (drop) c.b1_scale = b.gs;  // the value bias weighs sum_s P_s m_s under probability dropout
       if (fused) c.W1f = L.f_cav, c.W2f = L.f_cao;
+      c.xcd_tiles = fused && (xcd_knob & 2);
       if (fused && (merge & 2)) c.mg = SlabMerge{b.tick, b.x, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL, 4, dl};
       h->chain(c, s, fused);
       merged2 = c.mg.tick != nullptr;
@@ -1247,7 +1251,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       ff.drop = dl;
       if (fold & 2) {  // X = LN2(x + CA): the chain's 8 slabs
         ff.fold = RlnArgs{xc, x_other(), b.part, H, PS, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, dl, 4};
-        ff.xcd_tiles = xcd_knob;
+        ff.xcd_tiles = xcd_knob & 1;
         xc = x_other();
       }
       h->timed(PROF_DEC_FUSED, 4.0 * rows * (double)D * F, 2.0 * (2.0 * D * F + (double)rows * D * ns), s,

@@ -192,7 +192,7 @@ struct ChainArgs {
   const bf16_t* W1f; const bf16_t* W2f;
   SlabMerge mg;  // dec_chain, OUT_PARTIAL only
   RlnArgs fold;  // dec_chain FR with two planes, x_hstride 0: X = the residual LN of the producer's slabs (nparts 8)
-  int xcd_tiles;  // with fold: the 8 head blocks of a row tile on one XCD (when the tile count is a multiple of 8)
+  int xcd_tiles;  // dec_chain: the 8 head blocks of a row tile on one XCD (when the tile count is a multiple of 8)
 };
 hipError_t launch_chain_dec(const ChainArgs& a, hipStream_t s);
 
@@ -211,6 +211,7 @@ struct DecSaArgs {
   const bf16_t* Wqkv_f; const bf16_t* Wo_f;
   SlabMerge mg;
   RlnArgs fold;  // FR with two planes: A = the residual LN of the producer's slabs (nparts 16)
+  int xcd_tiles;  // the 8 head blocks of a row tile on one XCD (when the tile count is a multiple of 8)
 };
 hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s);
 // dec_ffn: slab j of 16 = relu(a W1[128j:128j+128]^T + b1) W2[:, 128j:128j+128]^T -> part[j][rows][512]

@@ -35,7 +35,6 @@ class CaptionPipeline:
 
         self.eng = engine
         self.check_range = bool(check_range)
-        self._prev_cus = engine.encoder_cus
         self.start, self.end, self.max_len = int(start), int(end), int(max_len)
         dev = engine.device
         self._owned = []
@@ -48,8 +47,12 @@ class CaptionPipeline:
                            "icap_stream_create_cu_mask")
                 ptrs.append(p.value)
             self._owned = ptrs
-            # the persistent encoder GEMMs size their grids to the encoder stream's CUs
-            engine.set_encoder_cus(torch.cuda.get_device_properties(dev).multi_processor_count - int(decode_cus))
+            # the persistent encoder GEMMs size their grids to the encoder stream's CUs.  The engine keeps one budget;
+            # its CU-masked pipelines form a stack on it (base budget first), so destroying them in any order leaves
+            # the budget of the newest live one (or the base) in force
+            budgets = engine.__dict__.setdefault("_cu_budgets", [("base", engine.encoder_cus)])
+            budgets.append((id(self), torch.cuda.get_device_properties(dev).multi_processor_count - int(decode_cus)))
+            engine.set_encoder_cus(budgets[-1][1])
             self.dec_stream = torch.cuda.ExternalStream(ptrs[0], device=dev)
             self.enc_stream = torch.cuda.ExternalStream(ptrs[1], device=dev)
         else:
@@ -60,8 +63,10 @@ class CaptionPipeline:
 
     def __del__(self):
         if getattr(self, "_owned", []):
-            try:  # the budget this pipeline found, not 0: another pipeline on the engine may still use its own
-                self.eng.set_encoder_cus(self._prev_cus)
+            try:  # drop this pipeline's budget; the newest remaining one (or the base) applies again
+                budgets = self.eng._cu_budgets
+                budgets[:] = [b for b in budgets if b[0] != id(self)]
+                self.eng.set_encoder_cus(budgets[-1][1])
             except Exception:
                 pass
         for p in getattr(self, "_owned", []):

@@ -78,7 +78,7 @@ def test_product_build_refuses_measurement_knobs(monkeypatch):
 
 def test_product_build_ships_only_shipped_forms():
     """The measured-and-rejected kernel forms (gemm_tools.hip, the persistent decode steps decstep.hip / xdec.hip, the
-    key-split and wave-owned cross-attentions) are compiled into the tools build only: the product source list does not hold them and the product library's code
+    key-split and wave-owned cross-attentions, the LayerNorm-folding decode blocks) are compiled into the tools build only: the product source list does not hold them and the product library's code
     object has none of their kernels."""
     from image_caption_amd import _lib, build
 
@@ -89,7 +89,8 @@ def test_product_build_ships_only_shipped_forms():
         pytest.skip("tools build")
     blob = build.LIB.read_bytes()
     for kernel in (b"dec_step_kernel", b"xdec_kernel", b"gemm_f16q_kernel", b"gemm_8ph_kernel",
-                   b"cross_attn_f16s_kernel", b"cross_attn_wk_kernel", b"cross_attn_f16_kernelILi2E"):
+                   b"cross_attn_f16s_kernel", b"cross_attn_wk_kernel", b"cross_attn_f16_kernelILi2E",
+                   b"dec_chain_kernelILb1ELi2ELi8E", b"dec_ffn_kernelILb1ELi2ELi8E"):
         assert kernel not in blob, kernel
 
 
