@@ -99,21 +99,43 @@ __device__ __forceinline__ f32x4 mma_rows(f32x4 acc, const char* wimg, int wrows
 // k64-steps of ximg; the same MFMA order as mma_rows (bit-identical sums)
 // The X fragments of half-step j + 1 are read before the MFMAs of half-step j (with ns a compile-time constant in the
 // kernels' NSC forms), so each MFMA pair waits for reads issued one pair earlier instead of its own.
-template <int NK>
-__device__ __forceinline__ f32x4 mma_frag(f32x4 acc, const bf16x8* wf, const char* ximg, int ns) {
+// Hi/lo decoder weights (round 5): lo(j) is fragment j of the W_lo image and acc also takes W_lo . X_hi
+// (every operand of the product then carries 16 significand bits); the lo fragment is fetched one pair ahead with X.
+struct NoLo {
+  __device__ __forceinline__ bf16x8 operator()(int) const { return bf16x8{}; }
+};
+template <int NK, class LoF = NoLo>
+__device__ __forceinline__ f32x4 mma_frag(f32x4 acc, const bf16x8* wf, const char* ximg, int ns, LoF lo = LoF{}) {
+  constexpr bool LO = !__is_same(LoF, NoLo);
   auto xf = [&](int j, int pl) { return frag(ximg + (j >> 1) * ns * 2048 + pl * 2048, 0, j & 1); };
-  bf16x8 xh = xf(0, 0), xl = ns == 2 ? xf(0, 1) : xh;
+  bf16x8 xh = xf(0, 0), xl = ns == 2 ? xf(0, 1) : xh, wl = LO ? lo(0) : xh;
 #pragma unroll
   for (int j = 0; j < 2 * NK; ++j) {
-    bf16x8 nh = xh, nl = xl;
+    bf16x8 nh = xh, nl = xl, nw = wl;
     if (j + 1 < 2 * NK) {
       nh = xf(j + 1, 0);
       if (ns == 2) nl = xf(j + 1, 1);
+      if (LO) nw = lo(j + 1);
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the next pair's reads issued ahead of this pair's MFMAs
     acc = mfma16(wf[j], xh, acc);
     if (ns == 2) acc = mfma16(wf[j], xl, acc);
-    xh = nh, xl = nl;
+    if (LO) acc = mfma16(wl, xh, acc);
+    xh = nh, xl = nl, wl = nw;
+  }
+  return acc;
+}
+// acc += W_lo . X_hi alone (a two-plane X image): the second pass of a block whose lo fragments reuse the hi registers
+template <int NK>
+__device__ __forceinline__ f32x4 mma_frag_lo(f32x4 acc, const bf16x8* wl, const char* ximg) {
+  auto xf = [&](int j) { return frag(ximg + (j >> 1) * 2 * 2048, 0, j & 1); };
+  bf16x8 xh = xf(0);
+#pragma unroll
+  for (int j = 0; j < 2 * NK; ++j) {
+    const bf16x8 nh = j + 1 < 2 * NK ? xf(j + 1) : xh;
+    __builtin_amdgcn_sched_barrier(0);
+    acc = mfma16(wl[j], xh, acc);
+    xh = nh;
   }
   return acc;
 }
@@ -125,8 +147,10 @@ __device__ __forceinline__ f32x4 mma_frag(f32x4 acc, const bf16x8* wf, const cha
 // written as the sum of the load_frags template arguments at each call
 template <int YOUNGER>
 __device__ __forceinline__ void x_landed() {
-  static_assert(YOUNGER == 16 || YOUNGER == 8 || YOUNGER == 0, "x_landed: add the s_waitcnt form for this count");
-  if constexpr (YOUNGER == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  static_assert(YOUNGER == 24 || YOUNGER == 16 || YOUNGER == 8 || YOUNGER == 0,
+                "x_landed: add the s_waitcnt form for this count");
+  if constexpr (YOUNGER == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if constexpr (YOUNGER == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if constexpr (YOUNGER == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -362,7 +386,10 @@ __global__ void frag_pack_kernel(const bf16_t* __restrict__ W, long ldw, int nti
 // FR (DecSaArgs::Wqkv_f / Wo_f, round 4): no weight region - waves 0-11 load their q|k|v tile's 16 KiB of fragments
 // straight into registers in the same burst as the X image, and every wave its 4 KiB of Wo fragments after its QKV
 // MFMAs (behind the attention): one memory round instead of two, 32 KiB of LDS instead of 160.
-template <bool FR, int NSC = 0>
+// WLO (round 5, FR with two planes): hi/lo decoder weights - after its hi MFMAs a wave reloads the same registers with
+// its lo q|k|v fragments (one more memory round: the hi and lo images of a tile, 32 KiB per wave, do not fit beside
+// each other) and adds W_lo . X_hi; the Wo lo fragments ride with the hi ones behind the attention.
+template <bool FR, int NSC = 0, bool WLO = false>
 __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ra = smem;                        // 128 KiB weight region (FR: none)
@@ -421,9 +448,14 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
     __syncthreads();
   }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  bf16x8 wo[FR ? 4 : 1];  // FR: Wo fragments of output column tiles 2 wave, 2 wave + 1 (2 k32-steps each)
+  bf16x8 wo[FR ? 4 : 1], wol[WLO ? 4 : 1];  // FR: Wo fragments of output column tiles 2 wave, 2 wave + 1 (2 k32-steps each)
   if (FR) {
     if (wave < 12) acc = mma_frag<DEC_K64>(acc, wf, sx, ns);  // q tiles 0..3, k tiles 4..7, v tiles 8..11
+    if (WLO && wave < 12) {
+      __builtin_amdgcn_sched_barrier(0);  // the hi fragments consumed: their registers take the lo image
+      load_frags<NWQ>(wf, p.Wqkv_fl, (long)(h * 12 + wave) * 2 * DEC_K64);
+      acc = mma_frag_lo<DEC_K64>(acc, wf, sx);
+    }
   } else {
     if (wave < 8) acc = mma_rows(acc, ra, 128, wave * 16, sx, ns, 0, DEC_K64);  // q tiles 0..3, k tiles 4..7
     __syncthreads();  // Wq / Wk no longer read
@@ -435,6 +467,7 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   }
   __syncthreads();  // X image no longer read: it becomes the q|k|v rows
   if (FR) load_frags<4>(wo, p.Wo_f, (long)(h * 32 + 2 * wave) * 2);  // needed after the attention
+  if (WLO) load_frags<4>(wol, p.Wo_fl, (long)(h * 32 + 2 * wave) * 2);
   if (wave < 12) {
     const int c = wave * 16 + 4 * fq;  // column in [q | k | v] of this head
     acc += bias;
@@ -544,7 +577,8 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
-    if (FR) o = mma_frag<1>(o, wo + 2 * i, sc, ns);
+    if (WLO) o = mma_frag<1>(o, wo + 2 * i, sc, ns, [&](int j) { return wol[2 * i + j]; });
+    else if (FR) o = mma_frag<1>(o, wo + 2 * i, sc, ns);
     else o = mma_rows(o, woi, DEC_D, wave * 32 + i * 16, sc, ns, 0, 1);
     const int row = row0 + fr;
     if (row < p.rows)
@@ -564,7 +598,10 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
 // fragments (column tiles 2 wave, 2 wave + 1 of the slice: 8 KiB) into registers with the X image - one memory round.
 // FOLD (round 5, FR with two planes): X = the residual LN2 of the cross-attention chain's FOLD slabs, written by the
 // block of slice 0; the W2 fragments are then issued after the fold (register budget) and fly behind FFN-1.
-template <bool FR, int NSC = 0, int FOLD = 0>
+// WLO (round 5, FR with two planes, no fold): hi/lo decoder weights - each wave DMAs its W1 lo fragments (8 KiB) into
+// its own LDS slot behind its W1 hi loads (the 128 KiB the FR form leaves free), and loads its W2 lo fragments into the
+// registers the W1 fragments free after FFN-1.
+template <bool FR, int NSC = 0, int FOLD = 0, bool WLO = false>
 __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ra = smem;
@@ -587,9 +624,16 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   else dma_x(p.A, p.aL, ns, row0, p.rows, sx);
   constexpr int NW1 = DEC_K64, NW2 = 8;  // fragments per wave (the opening's vmcnt counts them)
   bf16x8 w1f[FR ? NW1 : 1], w2f[FR ? NW2 : 1];
+  const long w1i = (long)(j * 8 + t) * 2 * DEC_K64 + kh * DEC_K64, w2i = (long)(j * 32 + 2 * wave) * 4;
+  char* const lo1 = smem + 32 * 1024 + wave * NW1 * 1024;  // WLO: this wave's W1 lo fragments (its own slot)
   if (FR) {
-    load_frags<NW1>(w1f, p.W1f, (long)(j * 8 + t) * 2 * DEC_K64 + kh * DEC_K64);
-    if (!FOLD) load_frags<NW2>(w2f, p.W2f, (long)(j * 32 + 2 * wave) * 4);
+    load_frags<NW1>(w1f, p.W1f, w1i);
+    if (WLO) {
+#pragma unroll
+      for (int i = 0; i < NW1; ++i)
+        lds_dma16(p.W1fl + (w1i + i) * 512 + lane * 8, (LDS_AS void*)(lo1 + i * 1024));
+    }
+    if (!FOLD) load_frags<NW2>(w2f, p.W2f, w2i);
     if (FOLD) __builtin_amdgcn_sched_barrier(0);  // every W1 fragment load issued before the fold's first wait
   } else {
     const char* w1 = (const char*)(p.W1 + (long)j * 128 * DEC_D);
@@ -600,14 +644,26 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
     load_frags<NW2>(w2f, p.W2f, (long)(j * 32 + 2 * wave) * 4);
     lds_barrier();  // the X image written
   } else if (FR && NSC == 2) {
-    open_x<NW1 + NW2>();  // X landed; W1 / W2 fragments may still fly
+    open_x<NW1 + NW2 + (WLO ? NW1 : 0)>();  // X landed; W1 / W1 lo / W2 fragments may still fly
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (FR) acc = mma_frag<4>(acc, w1f, sx + kh * 4 * ns * 2048, ns);
-  else acc = mma_rows(acc, ra, 128, t * 16, sx, ns, kh * 4, kh * 4 + 4);
+  if (WLO) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW2) : "memory");  // this wave's W1 lo slot landed (W2 may fly)
+    const bf16x8* l1 = (const bf16x8*)lo1 + lane;
+    acc = mma_frag<4>(acc, w1f, sx + kh * 4 * ns * 2048, ns, [&](int i) { return l1[i * 64]; });
+  } else if (FR) {
+    acc = mma_frag<4>(acc, w1f, sx + kh * 4 * ns * 2048, ns);
+  } else {
+    acc = mma_rows(acc, ra, 128, t * 16, sx, ns, kh * 4, kh * 4 + 4);
+  }
+  bf16x8 w2l[WLO ? NW2 : 1];
+  if (WLO) {
+    __builtin_amdgcn_sched_barrier(0);  // after FFN-1: the W1 registers are free
+    load_frags<NW2>(w2l, p.W2fl, w2i);
+  }
   __syncthreads();  // W1 and X no longer read
   if (!FR) {
     const char* w2 = (const char*)(p.W2 + (long)j * 128);
@@ -631,7 +687,8 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
-    if (FR) o = mma_frag<2>(o, w2f + 4 * i, sh, ns);
+    if (WLO) o = mma_frag<2>(o, w2f + 4 * i, sh, ns, [&](int q) { return w2l[4 * i + q]; });
+    else if (FR) o = mma_frag<2>(o, w2f + 4 * i, sh, ns);
     else o = mma_rows(o, ra, DEC_D, wave * 32 + i * 16, sh, ns, 0, 2);
     const int row = row0 + fr;
     if (row < p.rows)
@@ -653,7 +710,8 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
 // FOLD (round 5, FR with two planes, X shared by the heads): X = the residual LN1 of dec_sa's FOLD slabs (fold_issue /
 // fold_finish), written by the block of head 0; the 8 head blocks of a row tile then run on one XCD (xcd_tiles) so
 // the tile's slabs are read from that XCD's L2 after the first block's miss.
-template <bool FR, int NSC = 0, int FOLD = 0>
+// WLO (round 5, FR with two planes, no fold): hi/lo decoder weights, the lo fragments in registers beside the hi ones.
+template <bool FR, int NSC = 0, int FOLD = 0, bool WLO = false>
 __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* w1i = smem;                       // 64 KiB (FR: none)
@@ -676,10 +734,14 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   if constexpr (FOLD) fold_issue<FOLD>(p.fold, row0, p.M, smem + FOLD_PRM, fi);
   else dma_x(p.X + (long)h * p.x_hstride, p.x_lo, ns, row0, p.M, sx, p.ldx);
   constexpr int NW1 = 4, NW2 = 4;  // fragments per wave (the opening's vmcnt counts them)
-  bf16x8 w1f[FR ? NW1 : 1], w2f[FR ? NW2 : 1];
+  bf16x8 w1f[FR ? NW1 : 1], w2f[FR ? NW2 : 1], w1l[WLO ? NW1 : 1], w2l[WLO ? NW2 : 1];
   if (FR) {
     load_frags<NW1>(w1f, p.W1f, (long)(h * 4 + t) * 2 * DEC_K64 + kq * 4);
     load_frags<NW2>(w2f, p.W2f, (long)(h * 32 + 2 * wave) * 2);
+    if (WLO) {
+      load_frags<NW1>(w1l, p.W1fl, (long)(h * 4 + t) * 2 * DEC_K64 + kq * 4);
+      load_frags<NW2>(w2l, p.W2fl, (long)(h * 32 + 2 * wave) * 2);
+    }
     if (FOLD) __builtin_amdgcn_sched_barrier(0);  // every fragment load issued before the fold's first wait
   } else {
     const char* w1 = (const char*)(p.W1 + (long)h * 64 * DEC_D);
@@ -690,13 +752,14 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
     fold_finish<FOLD, 2>(p.fold, fi, row0, p.M, smem + FOLD_PRM, sx, h == 0);
     lds_barrier();  // the X image written
   } else if (FR && NSC == 2) {
-    open_x<NW1 + NW2>();  // X landed; W1 / W2 fragments may still fly
+    open_x<(WLO ? 2 : 1) * (NW1 + NW2)>();  // X landed; the W1 / W2 (hi, lo) fragments may still fly
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (FR) acc = mma_frag<2>(acc, w1f, sx + kq * 2 * ns * 2048, ns);
+  if (WLO) acc = mma_frag<2>(acc, w1f, sx + kq * 2 * ns * 2048, ns, [&](int i) { return w1l[i]; });
+  else if (FR) acc = mma_frag<2>(acc, w1f, sx + kq * 2 * ns * 2048, ns);
   else acc = mma_rows(acc, w1i, 64, t * 16, sx, ns, kq * 2, kq * 2 + 2);
   __syncthreads();  // X no longer read
   if (kq) red[((kq - 1) * 4 + t) * 64 + lane] = acc;
@@ -714,7 +777,8 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
-    if (FR) o = mma_frag<1>(o, w2f + 2 * i, sy, ns);
+    if (WLO) o = mma_frag<1>(o, w2f + 2 * i, sy, ns, [&](int q) { return w2l[2 * i + q]; });
+    else if (FR) o = mma_frag<1>(o, w2f + 2 * i, sy, ns);
     else o = mma_rows(o, w2i, DEC_D, wave * 32 + i * 16, sy, ns, 0, 1);
     const int col = wave * 32 + i * 16 + 4 * fq;
     if (row >= p.M) continue;
@@ -771,7 +835,7 @@ hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
 #ifndef ICAP_TOOLS
     return hipErrorInvalidValue;
 #else
-    if (!a.W1f || a.nsplit != 2 || a.x_hstride != 0 || a.H != DEC_H || a.out != OUT_SPLIT || a.mg.tick ||
+    if (!a.W1f || a.W1fl || a.nsplit != 2 || a.x_hstride != 0 || a.H != DEC_H || a.out != OUT_SPLIT || a.mg.tick ||
         !fold_ok(a.fold, DEC_H))
       return hipErrorInvalidValue;
     ChainArgs b = a;
@@ -782,7 +846,9 @@ hipError_t launch_dec_chain(const ChainArgs& a, hipStream_t s) {
   }
   ChainArgs c = a;
   c.xcd_tiles = a.xcd_tiles && a.H == DEC_H && ((a.M + DEC_ROWS - 1) / DEC_ROWS) % 8 == 0;
-  if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_chain_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, c);
+  if (!a.W1fl != !a.W2fl || (a.W1fl && (!a.W1f || a.nsplit != 2 || a.mg.tick))) return hipErrorInvalidValue;
+  if (a.W1fl) hipLaunchKernelGGL((dec_chain_kernel<true, 2, 0, true>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, c);
+  else if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_chain_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, c);
   else if (a.W1f) hipLaunchKernelGGL(dec_chain_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, c);
   else hipLaunchKernelGGL(dec_chain_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, c);
   return hipGetLastError();
@@ -797,7 +863,9 @@ hipError_t launch_dec_sa(const DecSaArgs& a, hipStream_t s) {
   const int blocks = (a.rows + DEC_ROWS - 1) / DEC_ROWS * DEC_H;
   DecSaArgs b = a;
   b.xcd_tiles = a.xcd_tiles && ((a.rows + DEC_ROWS - 1) / DEC_ROWS) % 8 == 0;
-  if (a.Wqkv_f && a.nsplit == 2) hipLaunchKernelGGL((dec_sa_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, b);
+  if (!a.Wqkv_fl != !a.Wo_fl || (a.Wqkv_fl && (!a.Wqkv_f || a.nsplit != 2 || a.mg.tick))) return hipErrorInvalidValue;
+  if (a.Wqkv_fl) hipLaunchKernelGGL((dec_sa_kernel<true, 2, true>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, b);
+  else if (a.Wqkv_f && a.nsplit == 2) hipLaunchKernelGGL((dec_sa_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, b);
   else if (a.Wqkv_f) hipLaunchKernelGGL(dec_sa_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, b);
   else hipLaunchKernelGGL(dec_sa_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, b);
   return hipGetLastError();
@@ -813,14 +881,24 @@ hipError_t launch_dec_ffn(const DecFfnArgs& a, hipStream_t s) {
 #ifndef ICAP_TOOLS
     return hipErrorInvalidValue;
 #else
-    if (!a.W1f || a.nsplit != 2 || a.mg.tick || !fold_ok(a.fold, DEC_H)) return hipErrorInvalidValue;
+    if (!a.W1f || a.W1fl || a.nsplit != 2 || a.mg.tick || !fold_ok(a.fold, DEC_H)) return hipErrorInvalidValue;
     DecFfnArgs b = a;
     b.xcd_tiles = a.xcd_tiles && ((a.rows + DEC_ROWS - 1) / DEC_ROWS) % 8 == 0;
     hipLaunchKernelGGL((dec_ffn_kernel<true, 2, DEC_H>), dim3(blocks), dim3(1024), DEC_LDS_FOLD, s, b);
     return hipGetLastError();
 #endif
   }
-  if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_ffn_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
+  if (!a.W1fl != !a.W2fl || (a.W1fl && (!a.W1f || a.nsplit != 2 || a.mg.tick))) return hipErrorInvalidValue;
+  if (a.W1fl) {  // hi/lo weights: the W1 lo slots after the X image
+    static bool lattr = false;
+    if (!lattr) {
+      const hipError_t e2 = hipFuncSetAttribute((const void*)dec_ffn_kernel<true, 2, 0, true>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, DEC_LDS);
+      if (e2 != hipSuccess) return e2;
+      lattr = true;
+    }
+    hipLaunchKernelGGL((dec_ffn_kernel<true, 2, 0, true>), dim3(blocks), dim3(1024), DEC_LDS, s, a);
+  } else if (a.W1f && a.nsplit == 2) hipLaunchKernelGGL((dec_ffn_kernel<true, 2>), dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else if (a.W1f) hipLaunchKernelGGL(dec_ffn_kernel<true>, dim3(blocks), dim3(1024), DEC_LDS_FR, s, a);
   else hipLaunchKernelGGL(dec_ffn_kernel<false>, dim3(blocks), dim3(1024), DEC_LDS, s, a);
   return hipGetLastError();

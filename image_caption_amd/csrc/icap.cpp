@@ -113,6 +113,9 @@ struct DecLayer {
   // the blocks load them straight into registers instead of staging weight slices through LDS
   bf16_t *f_qkv = nullptr, *f_sao = nullptr, *f_caq = nullptr, *f_kT = nullptr, *f_cav = nullptr, *f_cao = nullptr,
          *f_l1 = nullptr, *f_l2 = nullptr;
+  // hi/lo decoder weights (round 5): the same images of the lo planes, so the fused blocks add W_lo . X_hi
+  bf16_t *fl_qkv = nullptr, *fl_sao = nullptr, *fl_caq = nullptr, *fl_kT = nullptr, *fl_cav = nullptr,
+         *fl_cao = nullptr, *fl_l1 = nullptr, *fl_l2 = nullptr;
 };
 
 }  // namespace
@@ -530,6 +533,16 @@ void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PA
       o.f_cao = fp(o.ca_out.w, D, 256, 2, 2, 32, 64);
       o.f_l1 = fp(o.lin1.w, D, 128, 16, 0, 0, 0);
       o.f_l2 = fp(o.lin2.w, F, 512, 4, 2, 32, 128);
+      if (h->wlo) {  // the lo planes (Lin::wl; W_k^T and W_v keep theirs at + D * D)
+        o.fl_qkv = fp(o.sa_qkv.wl, D, 96, 16, 1, 0, 0);
+        o.fl_sao = fp(o.sa_out.wl, D, 256, 2, 2, 32, 64);
+        o.fl_caq = fp(o.ca_q.wl, D, 32, 16, 0, 0, 0);
+        o.fl_kT = fp(o.ca_kT + (size_t)D * D, 64, 256, 2, 0, 0, 0);
+        o.fl_cav = fp(o.ca_v + (size_t)D * D, D, 32, 16, 0, 0, 0);
+        o.fl_cao = fp(o.ca_out.wl, D, 256, 2, 2, 32, 64);
+        o.fl_l1 = fp(o.lin1.wl, D, 128, 16, 0, 0, 0);
+        o.fl_l2 = fp(o.lin2.wl, F, 512, 4, 2, 32, 128);
+      }
     }
     h->dec.push_back(o);
   }
@@ -940,7 +953,11 @@ void encode_grid(icap_handle* h, const float* img, int B, int IH, int IW, float*
   // stage: 802k / 401k elements per image), and as fp16 hi/lo planes in layer3-4, which hold 26 of the 33 roundings
   // (CPU emulation, DESIGN.md §3: trunk features 3.2e-4 relative, memory 1.1e-3, logits 1.1e-4)
   const bool f16 = h->t16 && !bt.bn;
-  auto xpl = [&](int st) { return f16 ? (st < 2 ? 1 : 2) : ns; };  // residual-stream planes of stage st
+#ifndef ICAP_TRUNK_SINGLE
+#define ICAP_TRUNK_SINGLE 0
+#endif
+  // ICAP_TRUNK_SINGLE (compile-time form, round 5): one fp16 residual plane in layer3-4 as well
+  auto xpl = [&](int st) { return f16 ? (st < 2 || ICAP_TRUNK_SINGLE ? 1 : 2) : ns; };  // residual-stream planes
   auto t16 = [&](int a_planes, int out_planes, int res_planes = 2) {
     Trunk16 t;
     t.on = f16; t.a_planes = a_planes; t.out_planes = out_planes; t.res_planes = res_planes;
@@ -999,7 +1016,7 @@ void encode_grid(icap_handle* h, const float* img, int B, int IH, int IW, float*
     REQUIRE(hh == GH && ww == GW, "trunk output grid mismatch");
     float* fb = feats ? feats + (size_t)b0 * N * d.cnn_dim : nullptr;
     if (f16) {  // the tail reads bf16 hi/lo planes: re-split the fp16 pair (and write the fp32 features)
-      HIPCHK(launch_f16planes_to_bf16(X, aL, (long)bc * N * d.cnn_dim, Y, aL, fb, s));
+      HIPCHK(launch_f16planes_to_bf16(X, xpl(3) == 2 ? aL : 0, (long)bc * N * d.cnn_dim, Y, aL, fb, s));
       std::swap(X, Y);
     } else if (fb) {  // trunk features (both planes: the values the tail consumes)
       HIPCHK(launch_planes_to_f32(X, aL, (long)bc * N * d.cnn_dim, 2, fb, s));
@@ -1114,10 +1131,13 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
   const int KS_D = 4, KS_F = 8;    // split-K of the K=512 and K=dim_ff residual GEMMs
   // one new token per sequence (the decode loops): the fused self-attention and feed-forward blocks
   // (decode.hip); the teacher-forced / padded forms keep the separate GEMM + attention launches
-  // hi/lo decoder weights run the unfused launches (whose GEMMs take W_lo), except for the train-mode dropout
-  // sampler, which keeps the fused blocks on W_hi (the differentiated log-probs use the fp32 weights themselves)
+  // hi/lo decoder weights (a real fp32 checkpoint): the fused blocks' hi/lo forms (round 5: the lo planes' fragment
+  // images, two activation planes) - the unfused launches (whose GEMMs take W_lo) only in the bf16 mode; the train-mode
+  // dropout sampler keeps the fused blocks on W_hi (the differentiated log-probs use the fp32 weights themselves)
+  const bool lo_frags = h->wlo && ns == 2 && !h->dec.empty() && h->dec[0].fl_qkv;
   const bool fused = n_new == 1 && !klen && causal && D == 512 && H == 8 && F == 2048 && t0 < 64 && t0 < Lmax &&
-                     (!h->wlo || drop);
+                     (!h->wlo || drop || lo_frags);
+  const bool flo = fused && h->wlo && !drop;  // the fused blocks add W_lo . X_hi
   const bool wl = h->wlo && !fused;  // GEMMs add W_lo . X_hi
   REQUIRE(!drop || (fused && ns == 2 && !anc), "dropout needs the one-token decode blocks in a parity precision");
   // round 4, measured slower and tools-only: the residual LayerNorms merged into the producing decode blocks
@@ -1143,8 +1163,8 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
 #else
   constexpr int fold_knob = 0, xcd_knob = 0;
 #endif
-  const int fold = fused && ns == 2 && !merge_knob ? fold_knob : 0;
-  const int merge = fused ? merge_knob : 0;
+  const int fold = fused && ns == 2 && !merge_knob && !flo ? fold_knob : 0;
+  const int merge = fused && !flo ? merge_knob : 0;
   float* xc = b.x;                                             // the residual stream's current buffer
   auto x_other = [&] { return xc == b.x ? b.x2 : b.x; };
   float* const PF = (fold & 2) ? b.part + (size_t)MAX_KSPLIT * PS : b.part;  // dec_ffn's slabs
@@ -1163,6 +1183,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       sa.A = b.a; sa.aL = b.aL; sa.nsplit = ns; sa.rows = rows;
       sa.Wqkv = L.sa_qkv.w; sa.bqkv = L.sa_qkv.b; sa.Wo = L.sa_out.w;
       sa.Wqkv_f = L.f_qkv; sa.Wo_f = L.f_sao;
+      if (flo) sa.Wqkv_fl = L.fl_qkv, sa.Wo_fl = L.fl_sao;
       if (merge & 1) sa.mg = SlabMerge{b.tick, b.x, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, b.a, b.aL, 2, dl};
       sa.kc = b.kc + l * kv_layer; sa.vc = b.vc + l * kv_layer; sa.Lmax = Lmax; sa.t0 = t0; sa.scale = 0.125f;
       sa.anc = anc;
@@ -1199,6 +1220,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.C = b.qt; c.ldc = (long)H * D; c.c_lo = b.cL; c.c_hstride = D;
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_SPLIT;
       if (fused) c.W1f = L.f_caq, c.W2f = L.f_kT;
+      if (flo) c.W1fl = L.fl_caq, c.W2fl = L.fl_kT;
       if (fold & 1) {  // X = LN1(x + SA): dec_sa's 8 slabs
         c.fold = RlnArgs{xc, x_other(), b.part, H, PS, L.sa_out.b, L.n1.w, L.n1.b, 1e-5f, dl, 2};
         c.xcd_tiles = xcd_knob & 1;
@@ -1230,6 +1252,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       c.M = rows; c.N2 = D; c.H = H; c.nsplit = ns; c.out = OUT_PARTIAL;
       if (drop) c.b1_scale = b.gs;  // the value bias weighs sum_s P_s m_s under probability dropout
       if (fused) c.W1f = L.f_cav, c.W2f = L.f_cao;
+      if (flo) c.W1fl = L.fl_cav, c.W2fl = L.fl_cao;
       c.xcd_tiles = fused && (xcd_knob & 2);
       if (fused && (merge & 2)) c.mg = SlabMerge{b.tick, b.x, L.ca_out.b, L.n2.w, L.n2.b, 1e-5f, b.a, b.aL, 4, dl};
       h->chain(c, s, fused);
@@ -1244,6 +1267,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
       ff.A = b.a; ff.aL = b.aL; ff.nsplit = ns; ff.rows = rows;
       ff.W1 = L.lin1.w; ff.b1 = L.lin1.b; ff.W2 = L.lin2.w;
       ff.W1f = L.f_l1; ff.W2f = L.f_l2;
+      if (flo) ff.W1fl = L.fl_l1, ff.W2fl = L.fl_l2;
       const bool head_folds = tail_ln && l + 1 == d.n_dec_layers;  // the caller's head normalises instead
       if ((merge & 4) && !head_folds)
         ff.mg = SlabMerge{b.tick, b.x, L.lin2.b, L.n3.w, L.n3.b, 1e-5f, b.a, b.aL, 6, dl};

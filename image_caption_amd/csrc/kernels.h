@@ -190,6 +190,8 @@ struct ChainArgs {
   // dec_chain only (frag_pack images, both or neither): W1 of head h as tiles h * 4 + t x 16 k32-steps, W2 as tiles
   // h * 32 + n x 2 k32-steps - each wave loads its own fragments straight into registers (no LDS weight staging)
   const bf16_t* W1f; const bf16_t* W2f;
+  // dec_chain, hi/lo decoder weights (round 5): the lo planes' fragment images (both or neither; FR, two planes)
+  const bf16_t* W1fl; const bf16_t* W2fl;
   SlabMerge mg;  // dec_chain, OUT_PARTIAL only
   RlnArgs fold;  // dec_chain FR with two planes, x_hstride 0: X = the residual LN of the producer's slabs (nparts 8)
   int xcd_tiles;  // dec_chain: the 8 head blocks of a row tile on one XCD (when the tile count is a multiple of 8)
@@ -209,6 +211,7 @@ struct DecSaArgs {
   // frag_pack images (both or neither): Wqkv as tiles h * 12 + i (q 0-3, k 4-7, v 8-11) x 16 k32-steps (mode 1), Wo
   // as tiles h * 32 + n x 2 k32-steps (mode 2, ksl 64)
   const bf16_t* Wqkv_f; const bf16_t* Wo_f;
+  const bf16_t* Wqkv_fl; const bf16_t* Wo_fl;  // hi/lo decoder weights: the lo planes' images (FR, two planes)
   SlabMerge mg;
   RlnArgs fold;  // FR with two planes: A = the residual LN of the producer's slabs (nparts 16)
   int xcd_tiles;  // the 8 head blocks of a row tile on one XCD (when the tile count is a multiple of 8)
@@ -222,6 +225,7 @@ struct DecFfnArgs {
   DropCfg drop;  // site 5: the hidden activations (pos = the decode position)
   // frag_pack images (both or neither): W1 as tiles 0..127 x 16 k32-steps, W2 as tiles j * 32 + n x 4 k32-steps
   const bf16_t* W1f; const bf16_t* W2f;
+  const bf16_t* W1fl; const bf16_t* W2fl;  // hi/lo decoder weights: the lo planes' images (FR, two planes)
   SlabMerge mg;
   RlnArgs fold;  // FR with two planes: A = the residual LN of the producer's slabs (nparts 8)
   int xcd_tiles;  // with fold: the 16 slice blocks of a row tile on one XCD (when the tile count is a multiple of 8)

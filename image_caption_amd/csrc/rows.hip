@@ -309,11 +309,11 @@ __global__ void planes_to_f32_kernel(const bf16_t* src, long lo, long n, int nsp
     dst[i] = nsplit == 2 ? bf2f(src[i]) + bf2f(src[i + lo]) : bf2f(src[i]);
 }
 
-// fp16 hi/lo planes (the ICAP_PREC_F16 trunk output) -> bf16 hi/lo planes of the same values (the bf16x2 Grid
-// tail's input), and optionally their fp32 sum (the trunk features); 4 elements per thread
+// fp16 hi/lo planes (the ICAP_PREC_F16 trunk output; slo = 0: one fp16 plane) -> bf16 hi/lo planes of the same values
+// (the bf16x2 Grid tail's input), and optionally their fp32 sum (the trunk features); 4 elements per thread
 __global__ void f16planes_to_bf16_kernel(const bf16_t* src, long slo, long n4, bf16_t* dst, long dlo, float* f32) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    const u32x2 h = *(const u32x2*)(src + 4 * i), l = *(const u32x2*)(src + 4 * i + slo);
+    const u32x2 h = *(const u32x2*)(src + 4 * i), l = slo ? *(const u32x2*)(src + 4 * i + slo) : (u32x2){0u, 0u};
     f32x4 v;
     bf16_t oh[4], ol[4];
 #pragma unroll

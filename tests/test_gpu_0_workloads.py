@@ -38,6 +38,8 @@ VIT_MEM_TOL = 4e-3
 # Grid memory in the default precision (f16: the ResNet trunk on fp16 planes - the residual stream as fp16 hi/lo, the
 # bottleneck branch as one fp16 plane; CPU emulation: trunk features 2.3e-4 relative, memory 8.9e-4, logits 8e-5)
 GRID_MEM_TOL = 4e-3
+# Grid trunk features (relative to the batch maximum), per image
+GRID_FEAT_TOL = 1e-3
 
 
 def _dev_sd(sd, dev):
@@ -124,6 +126,30 @@ def test_config2_vit_b256_every_row(cuda, vit_sd):
         assert (tf - O.teacher_forced_logits(sdd, mem_o, ids.long())).abs().max().item() < 1e-3
 
 
+def test_config2_vit_b256_fp32_weights_every_row(cuda):
+    """Config 2 on weights that are NOT bf16-exact (what the reference's trainers write, train_vit_transformer.py:413-423,
+    loaded by scripts/inference_vit_transformer.py:20-62): the engine picks hi/lo decoder weights and, since round 5,
+    decodes with the fused blocks' hi/lo forms (W_lo fragment images, W_hi . (X_hi + X_lo) + W_lo . X_hi).  HIP encoder
+    -> hi/lo decoder on all 256 rows against the fp32 oracle on the same weights: memory, every step's logits within
+    1e-3, the oracle's own greedy ids (the same near-tie rule as config 2); and the fused greedy decode equals the
+    unfused teacher-forced hi/lo decoder (icap_decoder_forward) on the same ids within 1e-3."""
+    from image_caption_amd.engine import Engine
+
+    B = 256
+    sd = W.to_torch(W.vit_state_dict(3, bf16_exact=False))
+    eng = Engine(sd, "vit", {}, device=cuda)
+    assert eng.dec_weight_planes == 2
+    sdd = _dev_sd(sd, cuda)
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=7)).to(cuda)
+    mem = eng.encode(imgs)
+    ids, lg = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L, want_logits=True)
+    mem_o = _oracle_memory(O.vit_encode, sdd, imgs)
+    assert (mem - mem_o).abs().max().item() < VIT_MEM_TOL
+    _check_greedy(ids, lg, sdd, mem_o, W.END_TOKEN, "config2 fp32 weights")
+    tf = eng.decoder_forward(ids[:, :-1], mem, causal=True)
+    assert (tf - lg.permute(1, 0, 2)).abs().max().item() < 1e-3
+
+
 def test_config3_grid_b256_trunk_and_every_row(cuda, grid_sd):
     from image_caption_amd.engine import Engine
 
@@ -135,13 +161,15 @@ def test_config3_grid_b256_trunk_and_every_row(cuda, grid_sd):
     feats_o = _oracle_memory(O.resnet101_trunk, sdd, imgs, chunk=32)
     scale = feats_o.abs().max().item()
     per_img = (feats - feats_o).abs().flatten(1).amax(1)
-    assert per_img.max().item() < 1e-3 * scale, per_img.max().item() / scale
+    print(f"\n[config3] trunk features max err {per_img.max().item() / scale:.2e} of the batch maximum")
+    assert per_img.max().item() < GRID_FEAT_TOL * scale, per_img.max().item() / scale
     # discriminative: every image's error is far below its distance to the closest other image
     fo = feats_o.flatten(1)
     d = torch.cdist(fo[None], fo[None], p=float("inf"))[0] + torch.eye(B, device=cuda) * 1e30
     assert bool((per_img * 10 < d.amin(1)).all())
     with torch.no_grad():
         mem_o = O.grid_encode_tail(sdd, feats_o)
+    print(f"[config3] memory max err {(mem - mem_o).abs().max().item():.2e}")
     assert (mem - mem_o).abs().max().item() < GRID_MEM_TOL
     rows = [0, 255]
     with torch.no_grad():
