@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 4 checkpoint: the whole GPU suite (-s: the B = 256 greedy counts), smoke, the default bench line (with the CPU
-# baseline), the Grid bench line, and a rocprofv3 kernel trace + stats of the ViT bench.  usage: bash tools/r4_check.sh TAG
+# Checkpoint: the whole GPU suite (-s: the B = 256 greedy counts), smoke, the default bench line (with the CPU
+# baseline), the Grid bench line, and a rocprofv3 kernel trace + stats of the ViT bench.  usage: [ROUND=r5] bash tools/checkpoint.sh TAG
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 T=${1:-ck}
-O=gpurun_out/r4; mkdir -p $O
+O=gpurun_out/${ROUND:-r5}; mkdir -p $O
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q -s --timeout 120 --timeout-method thread > $O/${T}_tests.log 2>&1 || { tail -30 $O/${T}_tests.log; exit 1; }
 tail -1 $O/${T}_tests.log; grep "greedy vs oracle" $O/${T}_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/${T}_smoke.log 2>&1 || { tail -20 $O/${T}_smoke.log; exit 1; }

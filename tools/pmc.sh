@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round 4: HBM traffic per launch of the bench's kernels (rocprofv3 --pmc, one counter group per pass, no tracing
-# domains), ViT and Grid.  usage: bash tools/r4_pmc.sh
+# HBM traffic per launch of the bench's kernels (rocprofv3 --pmc, one counter group per pass, no tracing
+# domains), ViT and Grid.  usage: [ROUND=r5] bash tools/pmc.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 for model in vit grid; do
-  OUT=gpurun_out/r4/pmc_$model
+  OUT=gpurun_out/${ROUND:-r5}/pmc_$model
   mkdir -p $OUT
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE"; do
