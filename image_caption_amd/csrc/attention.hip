@@ -539,10 +539,14 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
 // (the maximum is taken over the raw scores).
 // abl (tools knob ICAP_EAF_ABL, timing ablations; 0 in a product build): 1 = loads only, 2 = no K / V / Q loads,
 // 3 = no output stores
-template <int NKT>
-__global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t* __restrict__ qkv, int N, int H,
-                                                                     float scale, bf16_t* out, long out_ld, int abl) {
-  constexpr int NQW = (NKT + 3) / 4;  // query tiles per wave (tiles w, w + 4, ...)
+// NW waves per workgroup (round 5, compile-time form ICAP_EAF_NW; 0 = ceil(NKT / 2), every wave at most two query
+// tiles): with 4 waves the 13 query tiles of N = 197 give wave 0 four tiles and the others three, so a workgroup
+// lasts four tile times for 3.25 tiles of work per wave.
+template <int NKT, int NW = 4>
+__global__ __launch_bounds__(NW * 64, NW <= 4 ? 3 : 2) void enc_attention_full_kernel(const bf16_t* __restrict__ qkv,
+                                                                                     int N, int H, float scale,
+                                                                                     bf16_t* out, long out_ld, int abl) {
+  constexpr int NQW = (NKT + NW - 1) / NW;  // query tiles per wave (tiles w, w + NW, ...)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int h = blockIdx.x, b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t
   {
     const int lrow = lane >> 3, lch = lane & 7;
     constexpr int ni = NKT * 2;
-    for (int i = wave; i < (abl == 2 ? 0 : 2 * ni); i += 4) {
+    for (int i = wave; i < (abl == 2 ? 0 : 2 * ni); i += NW) {
       const bool isK = i < ni;
       const int row = (isK ? i : i - ni) * 8 + lrow;
       const int ch = lch ^ (isK ? kswz(row) : vswz(row));
@@ -569,7 +573,7 @@ __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t
   bf16x8 qreg[NQW][2];
 #pragma unroll
   for (int qi = 0; qi < NQW; ++qi) {
-    const int q = min((wave + 4 * qi) * 16 + fr, N - 1);
+    const int q = min((wave + NW * qi) * 16 + fr, N - 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       qreg[qi][ks] = abl == 2 ? (bf16x8){} : *(const bf16x8*)(qb + (long)q * 64 + ks * 32 + g * 8);
@@ -584,7 +588,7 @@ __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t
   const int q4 = fr >> 2, p4 = fr & 3;
 #pragma unroll
   for (int qi = 0; qi < NQW; ++qi) {
-    const int qt = wave + 4 * qi;
+    const int qt = wave + NW * qi;
     if (qt >= NKT) continue;  // (uniform per wave)
     const bf16x8* const qh = qreg[qi];
     // raw scores: lane holds query fr, keys 16 kt + 4 g + r
@@ -660,18 +664,23 @@ __global__ __launch_bounds__(256, 3) void enc_attention_full_kernel(const bf16_t
   }
 }
 
+#ifndef ICAP_EAF_NW
+#define ICAP_EAF_NW 4
+#endif
 template <int NKT>
 hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf16_t* out, long out_ld, int abl,
                         hipStream_t s) {
   constexpr int lds = 2 * NKT * 16 * 128;
+  constexpr int NW = ICAP_EAF_NW ? ICAP_EAF_NW : (NKT + 1) / 2;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_full_kernel<NKT>,
+    const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_full_kernel<NKT, NW>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(enc_attention_full_kernel<NKT>, dim3(H, B), dim3(256), lds, s, qkv, N, H, scale, out, out_ld, abl);
+  hipLaunchKernelGGL((enc_attention_full_kernel<NKT, NW>), dim3(H, B), dim3(NW * 64), lds, s, qkv, N, H, scale, out,
+                     out_ld, abl);
   return hipGetLastError();
 }
 

@@ -613,6 +613,24 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #ifndef ICAP_F16P_BUF
 #define ICAP_F16P_BUF 1
 #endif
+#ifndef ICAP_F16P_PROD
+#define ICAP_F16P_PROD 0
+#endif
+  // ICAP_F16P_PROD (compile-time form, round 5, buffer DMA only): the stage DMA issued by waves 0-3 alone (16 pieces
+  // each), so one wave per SIMD carries the DMA issue cost and the other only MFMAs; the counted seam waits then
+  // differ per wave (a wave waits only for the pieces it issued; the barrier publishes them)
+  constexpr bool PROD = ICAP_F16P_PROD && ICAP_F16P_BUF;
+#ifndef ICAP_F16P_LB
+#define ICAP_F16P_LB 0
+#endif
+  // ICAP_F16P_LB (compile-time form, round 5): the k-step barrier moved two MFMA groups before the end of the k-step
+  // (the "late point"): there the wave waits for the next stage (vmcnt) and for its own reads of this buffer
+  // (lgkmcnt), passes the barrier, issues the stage after next into this buffer and reads the next k-step's first
+  // fragments, whose latency then hides behind this k-step's last two MFMA groups instead of stalling every wave at
+  // the top of the next k-step.  Every tile's stages 0 and 1 are issued before its k-step 0 (prologue / seam); the
+  // stage after next is issued at each late point (the next tile's stage 0 at the last-but-one k-step); the last
+  // k-step of a tile has no late point (the epilogue needs every group).
+  constexpr bool LB = ICAP_F16P_LB && XK && !PROD && ABL == 0;
   // ICAP_F16P_BUF (compile-time form, round 5): the stage pieces as buffer loads (32-bit per-lane row offsets in the
   // resource of A / W, the k-step in the scalar offset) instead of flat 64-bit per-lane addresses: 10 fewer VGPRs and
   // frac 0.2924-0.2931 -> 0.2941-0.2951 on one box (profiles/r05/gemm_buf_ab.txt; 0 = the flat form)
@@ -623,17 +641,23 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
     const int bm = t / nbn, bn = t - bm * nbn, m0 = bm * BM, n0 = bn * BN;
     char* s0 = smem + buf * STAGE;
     if constexpr (ICAP_F16P_BUF) {
+      // PROD: waves 0 .. 3 issue the pieces of waves w and w + 4 (the others issue none)
+      if (PROD && wave >= 4) return;
 #pragma unroll
-      for (int i = 0; i < IPW; ++i) {
-        if (BM < 256 && (wave * IPW + i) * 8 >= BM) break;
-        const int row = min(m0 + srow + i * 8, M - 1);
-        lds_dma_buf16(rsA, (uint32_t)(row * p.lda + schunk * 8) * 2, (uint32_t)kt * KS * 2,
-                      (LDS_AS void*)(s0 + (wave * IPW + i) * 1024));
+      for (int v = 0; v < (PROD ? 2 : 1); ++v) {
+        const int vw = wave + 4 * v, vrow = srow + v * 4 * IPW * 8;
+#pragma unroll
+        for (int i = 0; i < IPW; ++i) {
+          if (BM < 256 && (vw * IPW + i) * 8 >= BM) break;
+          const int row = min(m0 + vrow + i * 8, M - 1);
+          lds_dma_buf16(rsA, (uint32_t)(row * p.lda + schunk * 8) * 2, (uint32_t)kt * KS * 2,
+                        (LDS_AS void*)(s0 + (vw * IPW + i) * 1024));
+        }
+#pragma unroll
+        for (int i = 0; i < IPW; ++i)
+          lds_dma_buf16(rsW, (uint32_t)((n0 + vrow + i * 8) * p.ldw + schunk * 8) * 2, (uint32_t)kt * KS * 2,
+                        (LDS_AS void*)(s0 + OPA + (vw * IPW + i) * 1024));
       }
-#pragma unroll
-      for (int i = 0; i < IPW; ++i)
-        lds_dma_buf16(rsW, (uint32_t)((n0 + srow + i * 8) * p.ldw + schunk * 8) * 2, (uint32_t)kt * KS * 2,
-                      (LDS_AS void*)(s0 + OPA + (wave * IPW + i) * 1024));
       return;
     }
     const bf16_t* Ab = p.A + kt * KS + schunk * 8;
@@ -666,13 +690,87 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   int t = xbase + lb, step = 0, tcount = 0;
   if (SO || RES) load_bias(t, 0);
   stage(t, 0, 0);
+  if (LB) stage(t, 1, 1);  // LB: both stages of a tile's opening in flight before its k-step 0
   bool seam = false;  // this tile's stages 0 and 1 were issued before the previous tile's epilogue stores
   bool range_bad = false;  // SO: some stored fp16 value is not finite (p.range_flag set once, after the last tile)
   for (;;) {
     const int tn = t + nbx < xbase + xcnt ? t + nbx : -1;  // this block's next tile
+    if constexpr (LB) {
+      const int fo0 = fr * 128 + ((fq ^ (fr & 7)) << 4), fo1 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
+      bf16x8 b2[2][TN], a2[2 * TM];
+      for (int kt = 0; kt < nk; ++kt, ++step) {
+        const char* s0 = smem + (step & 1) * STAGE;
+        if (kt == 0) {  // a tile's opening: stage 0 landed (stage 1 and, after a seam, the stores may still fly)
+          if (SO && seam) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE + NSTORE) : "memory");
+          else if (RES && seam) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE) : "memory");
+          __builtin_amdgcn_s_barrier();
+#pragma unroll
+          for (int j = 0; j < TN; ++j) b2[0][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo0);
+#pragma unroll
+          for (int g = 0; g < XD; ++g) a2[g] = *(const bf16x8*)(s0 + (wm * WM + g * 16) * 128 + fo0);
+        }
+        const bool late = kt + 1 < nk;  // the last k-step of a tile has no late point
+        // a k-step entered from a late point carries its b2[0] fragments only (register budget): A fragments 0 and 1 now
+        if (kt > 0) {
+          a2[0] = *(const bf16x8*)(s0 + (wm * WM) * 128 + fo0);
+          a2[1] = *(const bf16x8*)(s0 + (wm * WM + 16) * 128 + fo0);
+        }
+        auto group = [&](int g) {  // reads two groups ahead, then group g's MFMAs
+          const int nx = g + XD;
+          if (nx == TM) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) b2[1][j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo1);
+          }
+          if (nx < 2 * TM) a2[nx] = *(const bf16x8*)(s0 + (wm * WM + (nx % TM) * 16) * 128 + (nx < TM ? fo0 : fo1));
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[g % TM][j] = mma<true>(b2[g / TM][j], a2[g], acc[g % TM][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        };
+#pragma unroll
+        for (int g = 0; g < 2 * TM - XD; ++g) group(g);
+        if (late) {
+          // the late point: the next stage landed (after a seam's k-step 0 the stores may still fly; the RES seam
+          // issued stage 1 after its stores), this wave's reads of this buffer retired, then the barrier
+          if (SO && seam && kt == 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          // the next k-step's first fragments (its buffer is the other one), then the stage after next into this one
+          const char* s1 = smem + ((step + 1) & 1) * STAGE;
+          bf16x8 nb[TN];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) nb[j] = *(const bf16x8*)(s1 + OPA + (wn * WN + j * 16) * 128 + fo0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (kt + 2 < nk) {
+            stage(t, kt + 2, step & 1);
+          } else if (tn >= 0) {  // the next tile's bias and stage 0
+            if (SO || RES) load_bias(tn, (tcount + 1) & 1);
+            stage(tn, 0, step & 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int g = 2 * TM - XD; g < 2 * TM; ++g) {  // this k-step's last groups (their fragments are in registers)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[g % TM][j] = mma<true>(b2[g / TM][j], a2[g], acc[g % TM][j]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) b2[0][j] = nb[j];
+        } else {
+#pragma unroll
+          for (int g = 2 * TM - XD; g < 2 * TM; ++g) group(g);
+        }
+      }
+    } else
     for (int kt = 0; kt < nk; ++kt, ++step) {
       // lgkmcnt(0): this wave's reads of the buffer about to be refilled are done before the barrier
-      if (SO && seam && kt == 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE + NSTORE) : "memory");
+      if (SO && seam && kt == 0) {
+        if (!PROD) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE + NSTORE) : "memory");
+        else if (wave < 4) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * PER_STAGE + NSTORE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+      }
       else if (SO && seam && kt == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
       else if (RES && seam && kt == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");

@@ -1,0 +1,11 @@
+"""GPU pytest run against a given libicap build (a variant from tools/build_variant.py).
+usage: python tools/libtest.py LIB.so PYTEST_ARGS..."""
+import sys
+
+from image_caption_amd import _lib
+
+_lib.load(sys.argv[1])
+import pytest  # noqa: E402
+
+sys.exit(pytest.main(sys.argv[2:] + ["-m", "gpu", "-x", "-q", "-p", "no:cacheprovider", "--timeout", "200",
+                                     "--timeout-method", "thread"]))
