@@ -621,7 +621,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   // differ per wave (a wave waits only for the pieces it issued; the barrier publishes them)
   constexpr bool PROD = ICAP_F16P_PROD && ICAP_F16P_BUF;
 #ifndef ICAP_F16P_LB
-#define ICAP_F16P_LB 0
+#define ICAP_F16P_LB 1
 #endif
   // ICAP_F16P_LB (compile-time form, round 5): the k-step barrier moved two MFMA groups before the end of the k-step
   // (the "late point"): there the wave waits for the next stage (vmcnt) and for its own reads of this buffer

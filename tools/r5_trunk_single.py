@@ -2,6 +2,9 @@
 layer3-4 (-DICAP_TRUNK_SINGLE=1), with the trunk-feature bar lifted so the north-star checks (memory within 4e-3, every
 step's logits within 1e-3, the diverging-row pin) are measured.  usage: python tools/r5_trunk_single.py LIB.so"""
 import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 import torch
 
