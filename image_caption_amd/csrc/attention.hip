@@ -525,6 +525,72 @@ __global__ __launch_bounds__(1024 / QPW, QPW == 2 ? 4 : 1) void enc_attention_pi
   }
 }
 
+// One 16-query tile of the whole-sequence encoder attention (enc_attention_full_kernel / enc_attention_pers_kernel):
+// K and V of the (image, head) in LDS (kswz / vswz images), the tile's Q fragments qh[2] in registers.  Returns the
+// row sum l of the exact softmax and the unnormalised O = P V (4 d-tiles: lane = query fr, d = 16 dt + 4 g + r).
+template <int NKT>
+__device__ __forceinline__ float eaf_tile(const char* Ks, const char* Vs, const bf16x8* qh, int N, float sc2, int fr,
+                                          int g, f32x4 (&o)[4]) {
+  const int q4 = fr >> 2, p4 = fr & 3;
+  // raw scores: lane holds query fr, keys 16 kt + 4 g + r
+  f32x4 s[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int row = kt * 16 + fr;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 kh = *(const bf16x8*)(Ks + row * 128 + (((ks * 4 + g) ^ kswz(row)) << 4));
+      acc = mma<true>(kh, qh[ks], acc);
+    }
+    s[kt] = acc;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)  // the last tile's keys >= N
+    if ((NKT - 1) * 16 + g * 4 + r >= N) s[NKT - 1][r] = -INFINITY;
+  // maximum over the raw scores with llvm.maximum (gfx950 v_maximum3_f32: no canonicalising v_max per MFMA result,
+  // unlike fmaxf, and a compiler-visible VALU read of the XDL results - a v_max3 from inline asm was not spaced from
+  // them by the hazard recognizer: 8-wave forms of this kernel read stale maxima, tools/attn_repeat.py); the 1/8
+  // scale is folded into the exponent's FMA
+  float mx = s[0][0];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int r = (kt == 0 ? 1 : 0); r < 4; ++r) mx = __builtin_elementwise_maximum(mx, s[kt][r]);
+  const float mxs = rows4_max(mx) * sc2;
+  f32x2 l2 = {0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+      s[kt][r] = __builtin_amdgcn_exp2f(fmaf(s[kt][r], sc2, -mxs));
+      s[kt][r + 1] = __builtin_amdgcn_exp2f(fmaf(s[kt][r + 1], sc2, -mxs));
+      l2 += (f32x2){s[kt][r], s[kt][r + 1]};
+    }
+  }
+  const float l = rows4_sum(l2[0] + l2[1]);
+  // O = P V: key-tile pairs (2 c, 2 c + 1) as one 32-deep k-step; P (fp16) element j < 4 -> key 4 g + j of the
+  // first tile, j >= 4 -> of the second (odd NKT: the last pair's second tile contributes zeros)
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < (NKT + 1) / 2; ++c) {
+    constexpr f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 s1 = 2 * c + 1 < NKT ? s[2 * c + 1 < NKT ? 2 * c + 1 : 0] : z;
+    const u32x2 p0 = pack16x4<true>(s[2 * c]), p1 = pack16x4<true>(s1);
+    const bf16x8 ph = __builtin_bit_cast(bf16x8, (u32x4){p0[0], p0[1], p1[0], p1[1]});
+    const int key0 = c * 32 + 4 * g + q4;  // and key0 + 16 (vswz has period 8)
+    const int second = 2 * c + 1 < NKT ? 16 * 128 : 0;  // past the last tile: re-read tile 2 c (finite, P = 0)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int off0 = key0 * 128 + (((dt * 2 + (p4 >> 1)) ^ vswz(key0)) << 4) + (p4 & 1) * 8;
+      const bf16x8 vh = tr_pair(Vs + off0, Vs + off0 + second);
+      o[dt] = mma<true>(vh, ph, o[dt]);
+    }
+  }
+  return l;
+}
+
 // Whole-sequence form of the f16 encoder attention (round 4; head-major fp16 qkv, N <= 256): one workgroup of 4 waves
 // per (image, head) stages ALL of its K and V (N x 64 fp16 each: 50 KiB at N = 197) in one DMA burst, and each wave
 // takes query tiles w, w + 4, ...: S^T = K Q^T over every key tile at once (13 tiles x 2 MFMA at N = 197, 52 score
@@ -585,69 +651,12 @@ __global__ __launch_bounds__(NW * 64, NW <= 4 ? 3 : 2) void enc_attention_full_k
     return;
   }
   const float sc2 = scale * 1.44269504088896341f;  // exp2 domain
-  const int q4 = fr >> 2, p4 = fr & 3;
 #pragma unroll
   for (int qi = 0; qi < NQW; ++qi) {
     const int qt = wave + NW * qi;
     if (qt >= NKT) continue;  // (uniform per wave)
-    const bf16x8* const qh = qreg[qi];
-    // raw scores: lane holds query fr, keys 16 kt + 4 g + r
-    f32x4 s[NKT];
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const int row = kt * 16 + fr;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 kh = *(const bf16x8*)(Ks + row * 128 + (((ks * 4 + g) ^ kswz(row)) << 4));
-        acc = mma<true>(kh, qh[ks], acc);
-      }
-      s[kt] = acc;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)  // the last tile's keys >= N
-      if ((NKT - 1) * 16 + g * 4 + r >= N) s[NKT - 1][r] = -INFINITY;
-    // maximum over the raw scores with llvm.maximum (gfx950 v_maximum3_f32: no canonicalising v_max per MFMA result,
-    // unlike fmaxf, and a compiler-visible VALU read of the XDL results - a v_max3 from inline asm was not spaced from
-    // them by the hazard recognizer: 8-wave forms of this kernel read stale maxima, tools/attn_repeat.py); the 1/8
-    // scale is folded into the exponent's FMA
-    float mx = s[0][0];
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int r = (kt == 0 ? 1 : 0); r < 4; ++r) mx = __builtin_elementwise_maximum(mx, s[kt][r]);
-    const float mxs = rows4_max(mx) * sc2;
-    f32x2 l2 = {0.f, 0.f};
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        s[kt][r] = __builtin_amdgcn_exp2f(fmaf(s[kt][r], sc2, -mxs));
-        s[kt][r + 1] = __builtin_amdgcn_exp2f(fmaf(s[kt][r + 1], sc2, -mxs));
-        l2 += (f32x2){s[kt][r], s[kt][r + 1]};
-      }
-    }
-    const float l = rows4_sum(l2[0] + l2[1]);
-    // O = P V: key-tile pairs (2 c, 2 c + 1) as one 32-deep k-step; P (fp16) element j < 4 -> key 4 g + j of the
-    // first tile, j >= 4 -> of the second (odd NKT: the last pair's second tile contributes zeros)
     f32x4 o[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < (NKT + 1) / 2; ++c) {
-      constexpr f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 s1 = 2 * c + 1 < NKT ? s[2 * c + 1 < NKT ? 2 * c + 1 : 0] : z;
-      const u32x2 p0 = pack16x4<true>(s[2 * c]), p1 = pack16x4<true>(s1);
-      const bf16x8 ph = __builtin_bit_cast(bf16x8, (u32x4){p0[0], p0[1], p1[0], p1[1]});
-      const int key0 = c * 32 + 4 * g + q4;  // and key0 + 16 (vswz has period 8)
-      const int second = 2 * c + 1 < NKT ? 16 * 128 : 0;  // past the last tile: re-read tile 2 c (finite, P = 0)
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int off0 = key0 * 128 + (((dt * 2 + (p4 >> 1)) ^ vswz(key0)) << 4) + (p4 & 1) * 8;
-        const bf16x8 vh = tr_pair(Vs + off0, Vs + off0 + second);
-        o[dt] = mma<true>(vh, ph, o[dt]);
-      }
-    }
+    const float l = eaf_tile<NKT>(Ks, Vs, qreg[qi], N, sc2, fr, g, o);
     // 16-byte stores: lanes g (even) and g + 1 hold d = 16 dt + 4 g .. + 7 of d-tiles dt and dt + 1
     const float inv = 1.f / l;
     const int qq = qt * 16 + fr;
@@ -664,6 +673,87 @@ __global__ __launch_bounds__(NW * 64, NW <= 4 ? 3 : 2) void enc_attention_full_k
   }
 }
 
+// Persistent whole-sequence form (round 5; ICAP_EAF_PERS).  enc_attention_full_kernel's three workgroups per CU start
+// together, DMA together and compute together, so a CU alternates between an HBM-bound phase (three 75 KiB bursts)
+// and a VALU / MFMA-bound phase (12 waves on 13 query tiles each) instead of overlapping them: ≈ 4 generations x
+// (load + compute).  Here one 8-wave workgroup per CU walks the (image, head) items it, it + G, ...: K / V live in a
+// 2-item LDS ring (2 x 52 KiB at N = 197) and the next item's K / V DMA and Q loads are issued at the top of each item,
+// so they land behind this item's compute; one barrier per item (every wave's pieces of item k landed, and every wave
+// done reading item k - 1's buffer, which the DMA then refills).  Each wave takes query tiles w and w + 8.
+// Counted wait: at the top of item k this wave's outstanding VMEM is [item k's DMA + Q loads][item k - 1's stores] (in
+// order), so vmcnt(2 NQW) leaves the stores in flight; every wave issues exactly 2 NQW buffer stores per item (a tile
+// it does not own, or rows >= N, store out of the resource's range: dropped), so the count - and the compiler's own
+// wait for the Q registers - holds on every path.
+template <int NKT>
+__global__ __launch_bounds__(512, 1) void enc_attention_pers_kernel(const bf16_t* __restrict__ qkv, int N, int H,
+                                                                    int items, float scale, bf16_t* out, long out_ld) {
+  constexpr int NW = 8, NQW = (NKT + NW - 1) / NW, MAT = NKT * 16 * 128, ni = NKT * 2;
+  static_assert(NQW == 1 || NQW == 2, "the stores-per-item count below");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, g = lane >> 4, lrow = lane >> 3, lch = lane & 7;
+  const int G = gridDim.x;
+  bf16x8 qn[NQW][2];
+  auto issue = [&](int it, int buf) {  // item it's K / V into ring slot buf, its Q fragments into qn
+    const int b = it / H, h = it - b * H;
+    const bf16_t* qb = qkv + ((long)b * 3 * H + h) * N * 64;  // [q|k|v x head][token][64]
+    const bf16_t* kb = qb + (long)H * N * 64;
+    const bf16_t* vb = qb + 2L * H * N * 64;
+    char* const d = smem + buf * 2 * MAT;
+    for (int i = wave; i < 2 * ni; i += NW) {  // rows >= N read row N - 1 (finite; masked / P = 0)
+      const bool isK = i < ni;
+      const int row = (isK ? i : i - ni) * 8 + lrow;
+      const int ch = lch ^ (isK ? kswz(row) : vswz(row));
+      lds_dma16((isK ? kb : vb) + (long)min(row, N - 1) * 64 + ch * 8,
+                (LDS_AS void*)(d + (isK ? 0 : MAT) + (isK ? i : i - ni) * 1024));
+    }
+#pragma unroll
+    for (int qi = 0; qi < NQW; ++qi) {
+      const int q = min((wave + NW * qi) * 16 + fr, N - 1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) qn[qi][ks] = *(const bf16x8*)(qb + (long)q * 64 + ks * 32 + g * 8);
+    }
+  };
+  const float sc2 = scale * 1.44269504088896341f;  // exp2 domain
+  int it = blockIdx.x;
+  if (it < items) issue(it, 0);
+  for (int k = 0; it < items; ++k, it += G) {
+    if (k == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NQW) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    bf16x8 qc[NQW][2];
+#pragma unroll
+    for (int qi = 0; qi < NQW; ++qi) qc[qi][0] = qn[qi][0], qc[qi][1] = qn[qi][1];
+    if (it + G < items) issue(it + G, (k + 1) & 1);
+    const char* Ks = smem + (k & 1) * 2 * MAT;
+    const int b = it / H, h = it - b * H;
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(out + (long)b * N * out_ld, 0, (int)(N * out_ld * 2), 0x00020000);
+#pragma unroll
+    for (int qi = 0; qi < NQW; ++qi) {
+      const int qt = wave + NW * qi;
+      f32x4 o[4] = {};
+      float l = 1.f;
+      if (qt < NKT) l = eaf_tile<NKT>(Ks, Ks + MAT, qc[qi], N, sc2, fr, g, o);  // (uniform per wave)
+      const float inv = 1.f / l;
+      const int qq = qt * 16 + fr;
+      const bool odd = g & 1;
+      // 16-byte stores: lanes g (even) and g + 1 hold d = 16 dt + 4 g .. + 7 of d-tiles dt and dt + 1
+      const uint32_t ob = (uint32_t)((qq * out_ld + h * 64 + 4 * g) * 2);
+#pragma unroll
+      for (int dt = 0; dt < 4; dt += 2) {
+        const u32x2 a0 = pack16x4<true>(o[dt] * inv), a1 = pack16x4<true>(o[dt + 1] * inv);
+        const u32x2 snd = odd ? a0 : a1;
+        const u32x2 rcv = {xor16_partner(snd[0]), xor16_partner(snd[1])};
+        const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], a1[0], a1[1]} : (u32x4){a0[0], a0[1], rcv[0], rcv[1]};
+        const uint32_t off = ob + (uint32_t)((odd ? (dt + 1) * 16 - 4 : dt * 16) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(w, ro, qq < N ? off : 0x80000000u, 0, 0);
+      }
+    }
+  }
+}
+
 #ifndef ICAP_EAF_NW
 #define ICAP_EAF_NW 4
 #endif
@@ -672,6 +762,26 @@ hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf1
                         hipStream_t s) {
   constexpr int lds = 2 * NKT * 16 * 128;
   constexpr int NW = ICAP_EAF_NW ? ICAP_EAF_NW : (NKT + 1) / 2;
+  static const int pers = icap_knob("ICAP_EAF_PERS", 0);
+  if (pers && abl == 0 && (long)N * out_ld * 2 < (1L << 31)) {  // (the dropped stores' offset is past every row)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return hipErrorInvalidValue;
+      const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_pers_kernel<NKT>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * lds);
+      if (e != hipSuccess) {
+        cus = 0;
+        return e;
+      }
+    }
+    const int items = B * H;
+    hipLaunchKernelGGL((enc_attention_pers_kernel<NKT>), dim3(std::min(items, cus)), dim3(512), 2 * lds, s, qkv, N, H,
+                       items, scale, out, out_ld);
+    return hipGetLastError();
+  }
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_full_kernel<NKT, NW>,

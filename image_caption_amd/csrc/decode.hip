@@ -31,6 +31,11 @@ namespace {
 
 constexpr int DEC_D = 512, DEC_H = 8, DEC_HD = 64, DEC_F = 2048;
 constexpr int DEC_ROWS = 16;           // rows per block
+#ifdef ICAP_TOOLS
+constexpr bool DEC_XCD_TILES = true;  // the XCD-aligned tile mapping (ICAP_DEC_XCD, measured neutral: tools build only;
+#else                                 // its runtime test delayed every block's first loads behind a kernarg wait)
+constexpr bool DEC_XCD_TILES = false;
+#endif
 constexpr int DEC_K64 = DEC_D / 64;    // 64-deep k-steps of the D-wide products
 constexpr int DEC_LDS = 160 * 1024;    // both kernels: 128 KiB weight region + 32 KiB row region
 
@@ -399,8 +404,9 @@ __global__ __launch_bounds__(1024) void dec_sa_kernel(DecSaArgs p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int bid = blockIdx.x;  // xcd_tiles: tile = bid % 8 + 8 (bid / 64), head = (bid / 8) % 8 (a tile on one XCD)
-  const int h = p.xcd_tiles ? (bid >> 3) & 7 : bid & (DEC_H - 1);
-  const int row0 = (p.xcd_tiles ? (bid & 7) + 8 * (bid >> 6) : bid >> 3) * DEC_ROWS;
+  const bool xt = DEC_XCD_TILES && p.xcd_tiles;
+  const int h = xt ? (bid >> 3) & 7 : bid & (DEC_H - 1);
+  const int row0 = (xt ? (bid & 7) + 8 * (bid >> 6) : bid >> 3) * DEC_ROWS;
   const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
   const char* wq = (const char*)(p.Wqkv + (long)(h * DEC_HD) * DEC_D);
   const char* wk = (const char*)(p.Wqkv + (long)(DEC_D + h * DEC_HD) * DEC_D);
@@ -612,7 +618,7 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   const int fr = lane & 15, fq = lane >> 4;
   const int nslice = DEC_F / 128;
   const int bid = blockIdx.x;
-  const bool xt = FOLD && p.xcd_tiles;  // tile = bid % 8 + 8 (bid / 128), slice = (bid / 8) % 16: a tile on one XCD
+  const bool xt = DEC_XCD_TILES && FOLD && p.xcd_tiles;  // tile = bid % 8 + 8 (bid / 128), slice = (bid / 8) % 16: a tile on one XCD
   const int j = xt ? (bid >> 3) & 15 : bid % nslice;
   const int row0 = (xt ? (bid & 7) + 8 * (bid >> 7) : bid / nslice) * DEC_ROWS;
   const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
@@ -722,9 +728,10 @@ __global__ __launch_bounds__(1024) void dec_chain_kernel(ChainArgs p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int bid = blockIdx.x;
-  const bool xt = p.xcd_tiles;  // tile = bid % 8 + 8 (bid / 64), head = (bid / 8) % 8: a tile's heads on one XCD
-  const int h = xt ? (bid >> 3) & 7 : bid % p.H;
-  const int row0 = (xt ? (bid & 7) + 8 * (bid >> 6) : bid / p.H) * DEC_ROWS;
+  const bool xt = DEC_XCD_TILES && p.xcd_tiles;  // tile = bid % 8 + 8 (bid / 64), head = (bid / 8) % 8 (one XCD)
+  const int H = FR ? DEC_H : p.H;  // (the FR forms run DEC_H heads: launch_dec_chain checks it)
+  const int h = xt ? (bid >> 3) & 7 : bid % H;
+  const int row0 = (xt ? (bid & 7) + 8 * (bid >> 6) : bid / H) * DEC_ROWS;
   const int ns = NSC ? NSC : p.nsplit;  // NSC: the plane count as a constant (no per-MFMA branches)
   const int t = wave & 3, kq = wave >> 2;  // Y tile, k quarter (2 of the 8 k64 steps)
   const f32x4 bv = *(const f32x4*)(p.b1 + h * 64 + t * 16 + 4 * fq);  // oldest loads (as dec_sa_kernel)

@@ -703,6 +703,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         if (kt == 0) {  // a tile's opening: stage 0 landed (stage 1 and, after a seam, the stores may still fly)
           if (SO && seam) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE + NSTORE) : "memory");
           else if (RES && seam) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          // (224-row tiles: the last wave DMAs W rows only, IPW pieces per stage - stage 1 in flight is IPW, not 8)
+          else if (BM < 256 && wave * IPW * 8 >= BM) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(IPW) : "memory");
           else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE) : "memory");
           __builtin_amdgcn_s_barrier();
 #pragma unroll
