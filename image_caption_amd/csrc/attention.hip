@@ -673,21 +673,26 @@ __global__ __launch_bounds__(NW * 64, NW <= 4 ? 3 : 2) void enc_attention_full_k
   }
 }
 
-// Persistent whole-sequence form (round 5; ICAP_EAF_PERS).  enc_attention_full_kernel's three workgroups per CU start
-// together, DMA together and compute together, so a CU alternates between an HBM-bound phase (three 75 KiB bursts)
-// and a VALU / MFMA-bound phase (12 waves on 13 query tiles each) instead of overlapping them: ≈ 4 generations x
-// (load + compute).  Here one 8-wave workgroup per CU walks the (image, head) items it, it + G, ...: K / V live in a
-// 2-item LDS ring (2 x 52 KiB at N = 197) and the next item's K / V DMA and Q loads are issued at the top of each item,
-// so they land behind this item's compute; one barrier per item (every wave's pieces of item k landed, and every wave
-// done reading item k - 1's buffer, which the DMA then refills).  Each wave takes query tiles w and w + 8.
+// Persistent whole-sequence form (round 5, the default for N <= 240; ICAP_EAF_PERS).  enc_attention_full_kernel's three
+// workgroups per CU start together, DMA together and compute together, so a CU alternates between an HBM-bound phase
+// (three 75 KiB bursts) and a latency-bound compute phase instead of overlapping them: ≈ 4 generations x (load +
+// compute).  Here one 16-wave workgroup per CU walks the (image, head) items it, it + G, ...: K / V live in a 2-item LDS
+// ring (2 x 52 KiB at N = 197) and the next item's K / V DMA and Q loads are issued at the top of each item, so they
+// land behind this item's compute; one barrier per item (every wave's pieces of item k landed, and every wave done
+// reading item k - 1's buffer, which the DMA then refills).  Wave w takes query tile w (and w + NW).
 // Counted wait: at the top of item k this wave's outstanding VMEM is [item k's DMA + Q loads][item k - 1's stores] (in
 // order), so vmcnt(2 NQW) leaves the stores in flight; every wave issues exactly 2 NQW buffer stores per item (a tile
 // it does not own, or rows >= N, store out of the resource's range: dropped), so the count - and the compiler's own
 // wait for the Q registers - holds on every path.
-template <int NKT>
-__global__ __launch_bounds__(512, 1) void enc_attention_pers_kernel(const bf16_t* __restrict__ qkv, int N, int H,
-                                                                    int items, float scale, bf16_t* out, long out_ld) {
-  constexpr int NW = 8, NQW = (NKT + NW - 1) / NW, MAT = NKT * 16 * 128, ni = NKT * 2;
+// Waves per workgroup (ICAP_EAF_PERS_NW): 16 = one query tile per wave, four waves per SIMD at 108 registers: 71.8 us
+// per ViT launch against 75.9 for enc_attention_full_kernel and 91-107 with 8 waves of two tiles (the tile's
+// S -> softmax -> P V chain is latency-bound: more waves per SIMD, not fewer larger ones; profiles/r05/attn_pers.txt).
+// The SIMD holding waves {w : w = 0 mod 4} carries 4 of the 13 tiles against 3.25 on average (the per-item barrier).
+template <int NKT, int NW = 8>
+__global__ __launch_bounds__(NW * 64, 1) void enc_attention_pers_kernel(const bf16_t* __restrict__ qkv, int N, int H,
+                                                                        int items, float scale, bf16_t* out,
+                                                                        long out_ld) {
+  constexpr int NQW = (NKT + NW - 1) / NW, MAT = NKT * 16 * 128, ni = NKT * 2;
   static_assert(NQW == 1 || NQW == 2, "the stores-per-item count below");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -762,15 +767,23 @@ hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf1
                         hipStream_t s) {
   constexpr int lds = 2 * NKT * 16 * 128;
   constexpr int NW = ICAP_EAF_NW ? ICAP_EAF_NW : (NKT + 1) / 2;
-  static const int pers = icap_knob("ICAP_EAF_PERS", 0);
-  if (pers && abl == 0 && (long)N * out_ld * 2 < (1L << 31)) {  // (the dropped stores' offset is past every row)
+#ifndef ICAP_EAF_PERS_DEFAULT
+#define ICAP_EAF_PERS_DEFAULT 1
+#endif
+  static const int pers = icap_knob("ICAP_EAF_PERS", ICAP_EAF_PERS_DEFAULT);
+#ifndef ICAP_EAF_PERS_NW
+#define ICAP_EAF_PERS_NW 16
+#endif
+  constexpr int PNW = ICAP_EAF_PERS_NW;
+  // (NKT = 16 spills at 128 registers: the whole-sequence form; the dropped stores' offset is past every row)
+  if (pers && abl == 0 && (PNW < 16 || NKT < 16) && (long)N * out_ld * 2 < (1L << 31)) {
     static int cus = 0;
     if (!cus) {
       int dev = 0;
       if (hipGetDevice(&dev) != hipSuccess ||
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         return hipErrorInvalidValue;
-      const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_pers_kernel<NKT>,
+      const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_pers_kernel<NKT, PNW>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * lds);
       if (e != hipSuccess) {
         cus = 0;
@@ -778,8 +791,8 @@ hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf1
       }
     }
     const int items = B * H;
-    hipLaunchKernelGGL((enc_attention_pers_kernel<NKT>), dim3(std::min(items, cus)), dim3(512), 2 * lds, s, qkv, N, H,
-                       items, scale, out, out_ld);
+    hipLaunchKernelGGL((enc_attention_pers_kernel<NKT, PNW>), dim3(std::min(items, cus)), dim3(PNW * 64), 2 * lds, s, qkv,
+                       N, H, items, scale, out, out_ld);
     return hipGetLastError();
   }
   static bool attr = false;

@@ -1970,7 +1970,7 @@ const char* icap_knobs_set() {
       "ICAP_ENC_ATTN16_FULL", "ICAP_XATTN16_S", "ICAP_EAF_ABL", "ICAP_DEC_MERGE", "ICAP_XATTN16_WK",
       "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
       "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE", "ICAP_XDEC_TRACE", "ICAP_GEMM_NARROW",
-      "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW", "ICAP_DEC_FOLD", "ICAP_DEC_XCD"};
+      "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW", "ICAP_DEC_FOLD", "ICAP_DEC_XCD", "ICAP_EAF_PERS"};
   for (const char* n : names)
     if (getenv(n)) return n;
   return "";

@@ -1,10 +1,15 @@
 """Run an encoder ITERS times at batch B, for kernel profiles (default the Grid encoder: HIP ResNet
-trunk + tail).  usage: python tools/encode_grid.py [ITERS] [B] [vit|grid]"""
+trunk + tail).  usage: python tools/encode_grid.py [ITERS] [B] [vit|grid]   (ICAP_LIB: a variant library)"""
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
+
+if os.environ.get("ICAP_LIB"):  # a variant library (tools/build_variant.py)
+    from image_caption_amd import _lib  # noqa: E402
+
+    _lib.load(os.environ["ICAP_LIB"])
 
 from image_caption_amd import weights as W  # noqa: E402
 from image_caption_amd.engine import Engine  # noqa: E402
