@@ -12,7 +12,7 @@ if [ -n "$TESTS" ]; then
   timeout -k 10 400 python -u -m pytest $TESTS -m gpu -x -q --timeout 120 --timeout-method thread > $O/${T}_tests.log 2>&1 || { tail -40 $O/${T}_tests.log; exit 1; }
   tail -1 $O/${T}_tests.log
 fi
-bline() { python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); p=d["roofline"]["phases"]; print(sys.argv[2], d["value"], d["ms_per_step"], "enc", p["encoder"]["ms_per_step"], "dec", p["decode"]["ms_per_step"], "frac", d["roofline"]["frac"])' $1 $2; }
+bline() { python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); p=d["roofline"].get("phases") or {}; e=p.get("encoder", {}).get("ms_per_step"); c=p.get("decode", {}).get("ms_per_step"); print(sys.argv[2], d["value"], d["ms_per_step"], "enc", e, "dec", c, "frac", d["roofline"]["frac"])' $1 $2; }
 for r in $(seq $R); do
   for L in "$@"; do
     timeout -k 10 200 python -c "
