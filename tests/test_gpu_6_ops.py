@@ -555,11 +555,14 @@ def test_enc_attention_f16(cuda, B, N, H):
     assert (out.double() - ref).abs().max().item() < 4e-3
 
 
-@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (3, 100, 8), (1, 65, 2), (2, 256, 4), (5, 208, 3)])
+@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (3, 100, 8), (1, 65, 2), (2, 256, 4), (5, 208, 3), (64, 197, 12),
+                                   (45, 197, 12), (97, 120, 8)])
 def test_enc_attention_f16_head_major(cuda, B, N, H):
-    """The f16 ViT encoder's attention on the head-major qkv its QKV GEMM writes ([B][q|k|v][H][N][64]): the
-    whole-sequence form (enc_attention_full_kernel: every key of an (image, head) in LDS, one exact softmax) against
-    fp64, ragged last key tiles (N = 197, 100, 65) and full ones (256, 208); repeated launches bitwise equal."""
+    """The f16 ViT encoder's attention on the head-major qkv its QKV GEMM writes ([B][q|k|v][H][N][64]) against fp64:
+    the persistent form (enc_attention_pers_kernel, N <= 240) and the whole-sequence form (N = 256), ragged last key
+    tiles (N = 197, 100, 65, 120) and full ones (256, 208); B x H above the CU count (768, 540, 776 items) walks the
+    two-item K / V ring of the persistent form (several items per workgroup, an uneven last round); repeated launches
+    bitwise equal."""
     L, lib = _lib()
     D = H * 64
     g = torch.Generator(device="cpu").manual_seed(B * N + H + 7)
