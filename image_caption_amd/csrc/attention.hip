@@ -759,6 +759,157 @@ __global__ __launch_bounds__(NW * 64, 1) void enc_attention_pers_kernel(const bf
   }
 }
 
+#ifndef ICAP_EAF_P32
+#define ICAP_EAF_P32 0
+#endif
+#if ICAP_EAF_P32  // (measured 4 % slower than the 16-wave persistent form: compiled only on request)
+// 32-query tiles on v_mfma_f32_32x32x16_f16 (round 5, ICAP_EAF_P32): the persistent form with one 32-query tile per
+// wave (8 waves, NB = ceil(N / 32) tiles per item, 2 waves per SIMD).  Against the 16-query tiles the MFMA issue per
+// query halves (an MFMA holds the SIMD's issue for 8 of its 32 cycles instead of 8 of 16) and every K / V fragment read
+// from LDS serves 32 queries.  S^T = K Q^T per 32-key block (lane: query l & 31, keys (r & 3) + 8 (r >> 2) + 4 (l >> 5)
+// of the block in its 16 registers; cdna_hip_programming.md §3 maps); row max / sum over the lane's 16 NB values and
+// its partner l ^ 32; P = S^T registers 8 s .. 8 s + 7 as the B operand of k-step s (the same permuted key order in
+// the transposed V^T reads); O^T per 32-dim block.  K / V images, swizzles and the ring as enc_attention_pers_kernel
+// (rows padded to 32 NB, rows >= N read row N - 1 and are masked / P = 0).  Counted wait: every wave issues exactly 4
+// buffer stores per item (2 dim blocks x 2 16-byte stores; a wave without a tile stores out of range).
+// Measured (parity exact, tests/test_gpu_6_ops.py): 75.6 against 72.6 us for the 16-wave form - 212 registers leave
+// two waves per SIMD, and the tile's S -> softmax -> P V chain stays latency-bound (profiles/r05/attn_pers.txt).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16 mma32h(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+__device__ __forceinline__ uint32_t xor32_partner(uint32_t v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (threadIdx.x & 32) ? p[0] : p[1];
+}
+template <int NB>
+__global__ __launch_bounds__(512, 1) void enc_attention_p32_kernel(const bf16_t* __restrict__ qkv, int N, int H,
+                                                                   int items, float scale, bf16_t* out, long out_ld) {
+  constexpr int NW = 8, MAT = NB * 32 * 128, ni = NB * 4;  // ni: 8-row DMA pieces per matrix
+  static_assert(NB <= NW, "one 32-query tile per wave");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c32 = lane & 31, hh = lane >> 5, lrow = lane >> 3, lch = lane & 7;
+  const int G = gridDim.x;
+  bf16x8 qn[4];
+  auto issue = [&](int it, int buf) {  // item it's K / V into ring slot buf, this wave's Q fragments into qn
+    const int b = it / H, h = it - b * H;
+    const bf16_t* qb = qkv + ((long)b * 3 * H + h) * N * 64;  // [q|k|v x head][token][64]
+    const bf16_t* kb = qb + (long)H * N * 64;
+    const bf16_t* vb = qb + 2L * H * N * 64;
+    char* const d = smem + buf * 2 * MAT;
+    for (int i = wave; i < 2 * ni; i += NW) {
+      const bool isK = i < ni;
+      const int row = (isK ? i : i - ni) * 8 + lrow;
+      const int ch = lch ^ (isK ? kswz(row) : vswz(row));
+      lds_dma16((isK ? kb : vb) + (long)min(row, N - 1) * 64 + ch * 8,
+                (LDS_AS void*)(d + (isK ? 0 : MAT) + (isK ? i : i - ni) * 1024));
+    }
+    const int q = min(wave * 32 + c32, N - 1);  // B operand of k-step ks: dims 16 ks + 8 hh .. + 7 of query q
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qn[ks] = *(const bf16x8*)(qb + (long)q * 64 + ks * 16 + hh * 8);
+  };
+  const float sc2 = scale * 1.44269504088896341f;  // exp2 domain
+  // transposed V^T reads: lane 4 qq + pp of its 16-lane group supplies row (key) qq, dims 4 pp .. 4 pp + 3 of the group's
+  // 16 dims (dims 16 ((lane >> 4) & 1) of the 32-dim block)
+  const int gi = lane & 15, tq = gi >> 2, tp = gi & 3, dsub = 16 * ((lane >> 4) & 1);
+  int it = blockIdx.x;
+  if (it < items) issue(it, 0);
+  for (int k = 0; it < items; ++k, it += G) {
+    if (k == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    bf16x8 qc[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qc[ks] = qn[ks];
+    if (it + G < items) issue(it + G, (k + 1) & 1);
+    const char* Ks = smem + (k & 1) * 2 * MAT;
+    const char* Vs = Ks + MAT;
+    const int b = it / H, h = it - b * H;
+    f32x16 o[2] = {};
+    float l = 1.f;
+    if (wave < NB) {  // (uniform per wave)
+      f32x16 sacc[NB];
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb) {
+        f32x16 a = {};
+        const int row = kb * 32 + c32;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const bf16x8 kf = *(const bf16x8*)(Ks + row * 128 + (((2 * ks + hh) ^ kswz(row)) << 4));
+          a = mma32h(kf, qc[ks], a);
+        }
+        sacc[kb] = a;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r)  // the last block's keys >= N
+        if ((NB - 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) sacc[NB - 1][r] = -INFINITY;
+      // maximum and sum as four independent chains (two waves per SIMD cannot hide one 112-long dependent chain)
+      float m4[4] = {sacc[0][0], sacc[0][1], sacc[0][2], sacc[0][3]};
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb)
+#pragma unroll
+        for (int r = (kb == 0 ? 4 : 0); r < 16; ++r) m4[r & 3] = __builtin_elementwise_maximum(m4[r & 3], sacc[kb][r]);
+      float mx = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m4[0], m4[1]),
+                                               __builtin_elementwise_maximum(m4[2], m4[3]));
+      mx = fmaxf(mx, __uint_as_float(xor32_partner(__float_as_uint(mx))));
+      const float mxs = mx * sc2;
+      f32x2 l4[4] = {};
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          sacc[kb][r] = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], sc2, -mxs));
+          sacc[kb][r + 1] = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r + 1], sc2, -mxs));
+          l4[(r >> 1) & 3] += (f32x2){sacc[kb][r], sacc[kb][r + 1]};
+        }
+      const f32x2 ls = (l4[0] + l4[1]) + (l4[2] + l4[3]);
+      l = ls[0] + ls[1];
+      l += __uint_as_float(xor32_partner(__float_as_uint(l)));
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const f32x16& x = sacc[kb];
+          const u32x2 p0 = pack16x4<true>((f32x4){x[8 * st], x[8 * st + 1], x[8 * st + 2], x[8 * st + 3]});
+          const u32x2 p1 = pack16x4<true>((f32x4){x[8 * st + 4], x[8 * st + 5], x[8 * st + 6], x[8 * st + 7]});
+          const bf16x8 ph = __builtin_bit_cast(bf16x8, (u32x4){p0[0], p0[1], p1[0], p1[1]});
+          const int key0 = kb * 32 + 16 * st + 4 * hh + tq;  // and key0 + 8 (vswz has period 8)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const int off0 = key0 * 128 + (((4 * db + (dsub >> 3) + (tp >> 1)) ^ vswz(key0)) << 4) + (tp & 1) * 8;
+            const bf16x8 vh = tr_pair(Vs + off0, Vs + off0 + 8 * 128);
+            o[db] = mma32h(vh, ph, o[db]);
+          }
+        }
+    }
+    // O^T block db: lane (query c32, half hh) holds dims 32 db + (r & 3) + 8 (r >> 2) + 4 hh; 16-byte stores of dims
+    // 8 m .. 8 m + 7 joined across the partner lane l ^ 32 (hh = 0 keeps m even, hh = 1 m odd)
+    const float inv = 1.f / l;
+    const int qq = wave * 32 + c32;
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(out + (long)b * N * out_ld, 0, (int)(N * out_ld * 2), 0x00020000);
+    const uint32_t ob = (uint32_t)((qq * out_ld + h * 64) * 2);
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int mp = 0; mp < 2; ++mp) {
+        const f32x16& x = o[db];
+        const u32x2 g0 = pack16x4<true>((f32x4){x[8 * mp], x[8 * mp + 1], x[8 * mp + 2], x[8 * mp + 3]} * inv);
+        const u32x2 g1 = pack16x4<true>((f32x4){x[8 * mp + 4], x[8 * mp + 5], x[8 * mp + 6], x[8 * mp + 7]} * inv);
+        const u32x2 snd = hh ? g0 : g1;
+        const u32x2 rcv = {xor32_partner(snd[0]), xor32_partner(snd[1])};
+        const u32x4 w = hh ? (u32x4){rcv[0], rcv[1], g1[0], g1[1]} : (u32x4){g0[0], g0[1], rcv[0], rcv[1]};
+        const int dim0 = 32 * db + 8 * (2 * mp + hh);
+        __builtin_amdgcn_raw_buffer_store_b128(w, ro, qq < N ? ob + (uint32_t)dim0 * 2 : 0x80000000u, 0, 0);
+      }
+  }
+}
+
+#endif  // ICAP_EAF_P32
+
 #ifndef ICAP_EAF_NW
 #define ICAP_EAF_NW 4
 #endif
@@ -776,6 +927,28 @@ hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf1
 #endif
   constexpr int PNW = ICAP_EAF_PERS_NW;
   // (NKT = 16 spills at 128 registers: the whole-sequence form; the dropped stores' offset is past every row)
+#if ICAP_EAF_P32
+  if (abl == 0 && (long)N * out_ld * 2 < (1L << 31)) {  // 32-query tiles (enc_attention_p32_kernel)
+    constexpr int NB = (NKT + 1) / 2;
+    static int cus32 = 0;
+    if (!cus32) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus32, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus32 <= 0)
+        return hipErrorInvalidValue;
+      const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_p32_kernel<NB>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 4 * NB * 32 * 128);
+      if (e != hipSuccess) {
+        cus32 = 0;
+        return e;
+      }
+    }
+    const int items = B * H;
+    hipLaunchKernelGGL((enc_attention_p32_kernel<NB>), dim3(std::min(items, cus32)), dim3(512), 4 * NB * 32 * 128, s,
+                       qkv, N, H, items, scale, out, out_ld);
+    return hipGetLastError();
+  }
+#endif
   if (pers && abl == 0 && (PNW < 16 || NKT < 16) && (long)N * out_ld * 2 < (1L << 31)) {
     static int cus = 0;
     if (!cus) {
