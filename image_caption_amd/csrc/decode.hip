@@ -280,6 +280,11 @@ __device__ __forceinline__ void fold_finish(const RlnArgs& f, const FoldIn<NP>& 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const float* base) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
 }
+// Product (round 5): the slabs are stored non-temporal (cache policy nt, aux bit 2).  The split-K slabs are the bulk
+// of what a decode node writes (4-8 MB per launch at B = 256) and the next node reads them once; written nt they
+// leave the kernel-end L2 write-back little to do: decode 11.06-11.14 -> 10.79-10.94 ms, same box (sc1 write-through
+// the same; nt on every decode output - LayerNorm rows, q~ / context planes, KV appends, next-token rows - only
+// 11.01-11.03: those are read right back; profiles/r05/slab_nt_ab.txt).
 __device__ __forceinline__ void slab_store(float* base, uint32_t off, f32x4 v, bool wt) {
 #ifdef ICAP_TOOLS
   if (wt) {
@@ -287,7 +292,7 @@ __device__ __forceinline__ void slab_store(float* base, uint32_t off, f32x4 v, b
     return;
   }
 #endif
-  *(f32x4*)((char*)base + off) = v;
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), slab_rsrc(base), off, 0, 2);
 }
 
 // SlabMerge (kernels.h) after this block's slab stores: the last of the NP blocks of the 16-row tile row0 merges the
