@@ -938,7 +938,10 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
             const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], pk[j + 1][0], pk[j + 1][1]}
                                 : (u32x4){pk[j][0], pk[j][1], rcv[0], rcv[1]};
             if constexpr (ABL == 11) asm volatile("" ::"v"(w), "v"(C));
-            else if (ok) *(u32x4*)(C + nb + (odd ? (j + 1) * 16 - 4 : j * 16)) = w;
+            // non-temporal (round 5): the QKV / MLP-1 outputs (232 / 310 MB) stream past the L2 - encoder 13.32-13.38
+            // -> 13.12-13.24 ms, frac 0.309-0.311 -> 0.315-0.317 on one box (profiles/r05/gemm_so_nt_ab.txt); the residual
+            // epilogue's fp32 stores nt: neutral
+            else if (ok) __builtin_nontemporal_store(w, (u32x4*)(C + nb + (odd ? (j + 1) * 16 - 4 : j * 16)));
           }
         }
       }
