@@ -938,10 +938,14 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
             const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], pk[j + 1][0], pk[j + 1][1]}
                                 : (u32x4){pk[j][0], pk[j][1], rcv[0], rcv[1]};
             if constexpr (ABL == 11) asm volatile("" ::"v"(w), "v"(C));
-            // non-temporal (round 5): the QKV / MLP-1 outputs (232 / 310 MB) stream past the L2 - encoder 13.32-13.38
-            // -> 13.12-13.24 ms, frac 0.309-0.311 -> 0.315-0.317 on one box (profiles/r05/gemm_so_nt_ab.txt); the residual
-            // epilogue's fp32 stores nt: neutral
-            else if (ok) __builtin_nontemporal_store(w, (u32x4*)(C + nb + (odd ? (j + 1) * 16 - 4 : j * 16)));
+            // streaming stores (round 5): the QKV / MLP-1 outputs (232 / 310 MB) with cache policy nt | sc1 (aux 18) stream
+            // past the L2 and leave it to the operands - plain nt: encoder 13.32-13.38 -> 13.12-13.24 ms on one box,
+            // nt | sc1 another -0.1 ms against plain nt on another, sc1 alone +0.4 ms (profiles/r05/gemm_so_nt_ab.txt);
+            // the residual epilogue's fp32 loads / stores nt: slower
+            else if (ok)
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  w, __builtin_amdgcn_make_buffer_rsrc(p.C, 0, 0x7fffffff, 0x00020000),
+                  (uint32_t)((C + nb + (odd ? (j + 1) * 16 - 4 : j * 16)) - (bf16_t*)p.C) * 2, 0, 18);
           }
         }
       }
