@@ -178,7 +178,10 @@ __global__ __launch_bounds__(NT) void residual_layernorm_kernel(const float* xin
   f32x4 pp[RLN_MAX_PARTS];
 #pragma unroll
   for (int s = 0; s < RLN_MAX_PARTS; ++s)
-    pp[s] = s < nparts ? *(const f32x4*)(parts + s * part_stride + (long)row * D + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    // (non-temporal, round 5: the slabs are read once - with the producers' nt slab stores, decode 10.93-10.95 ->
+    // 10.70-10.86 ms on one box, profiles/r05/slab_nt_ab.txt)
+    pp[s] = s < nparts ? __builtin_nontemporal_load((const f32x4*)(parts + s * part_stride + (long)row * D + col))
+                       : (f32x4){0.f, 0.f, 0.f, 0.f};
   f32x4 v = *(const f32x4*)(xin + (long)row * D + col);
   const f32x4 bb = bias ? *(const f32x4*)(bias + col) : (f32x4){0.f, 0.f, 0.f, 0.f};
   const f32x4 wv = *(const f32x4*)(w + col), bv = *(const f32x4*)(b + col);
