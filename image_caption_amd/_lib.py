@@ -108,6 +108,10 @@ SIGNATURES = {
     "icap_drop_hash_host": (ctypes.c_uint32, [ctypes.c_uint32] * 6),
     "icap_decode_sample_dropout": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_float,
                                            ctypes.c_uint32, c_void_p, c_void_p, c_void_p]),
+    "icap_decode_greedy_stop": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                        c_void_p, POINTER(c_int), c_void_p]),
+    "icap_decode_sample_stop": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_float,
+                                        ctypes.c_uint32, c_int, c_void_p, c_void_p, POINTER(c_int), c_void_p]),
     "icap_decode_beam": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                  c_void_p, c_void_p]),
     "icap_decoder_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,

@@ -915,7 +915,7 @@ __global__ __launch_bounds__(512, 1) void enc_attention_p32_kernel(const bf16_t*
 #endif
 template <int NKT>
 hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf16_t* out, long out_ld, int abl,
-                        hipStream_t s) {
+                        hipStream_t s, int max_grid) {
   constexpr int lds = 2 * NKT * 16 * 128;
   constexpr int NW = ICAP_EAF_NW ? ICAP_EAF_NW : (NKT + 1) / 2;
 #ifndef ICAP_EAF_PERS_DEFAULT
@@ -949,7 +949,8 @@ hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf1
     return hipGetLastError();
   }
 #endif
-  if (pers && abl == 0 && (PNW < 16 || NKT < 16) && (long)N * out_ld * 2 < (1L << 31)) {
+  if constexpr (PNW < 16 || NKT < 16) {  // (not instantiated where it would spill)
+  if (pers && abl == 0 && (long)N * out_ld * 2 < (1L << 31)) {
     static int cus = 0;
     if (!cus) {
       int dev = 0;
@@ -963,10 +964,13 @@ hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf1
         return e;
       }
     }
-    const int items = B * H;
-    hipLaunchKernelGGL((enc_attention_pers_kernel<NKT, PNW>), dim3(std::min(items, cus)), dim3(PNW * 64), 2 * lds, s, qkv,
-                       N, H, items, scale, out, out_ld);
+    // one 16-wave workgroup per CU: under an encoder CU budget (a CU-masked stream, icap_set_encoder_cus) only that
+    // many fit at once - a larger grid would run its surplus workgroups as a second round
+    const int items = B * H, blocks = max_grid > 0 ? std::min(max_grid, cus) : cus;
+    hipLaunchKernelGGL((enc_attention_pers_kernel<NKT, PNW>), dim3(std::min(items, blocks)), dim3(PNW * 64), 2 * lds, s,
+                       qkv, N, H, items, scale, out, out_ld);
     return hipGetLastError();
+  }
   }
   static bool attr = false;
   if (!attr) {
@@ -1002,7 +1006,8 @@ hipError_t run_enc(const bf16_t* qkv, long ld, long lo, int B, int N, int H, flo
 }  // namespace
 
 hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale,
-                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s, int head_major) {
+                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s, int head_major,
+                                int max_grid) {
   if (N <= 0 || B <= 0) return hipErrorInvalidValue;
   if (head_major && (N <= 64 || N > 256)) return hipErrorInvalidValue;  // only the pipelined form reads it
   if (N <= 64) {
@@ -1021,18 +1026,18 @@ hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int 
     if (head_major && full) {
       static const int abl = icap_knob("ICAP_EAF_ABL", 0);
       switch ((N + 15) / 16) {  // N in (64, 256]
-        case 5: return run_enc_full<5>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 6: return run_enc_full<6>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 7: return run_enc_full<7>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 8: return run_enc_full<8>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 9: return run_enc_full<9>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 10: return run_enc_full<10>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 11: return run_enc_full<11>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 12: return run_enc_full<12>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 13: return run_enc_full<13>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 14: return run_enc_full<14>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        case 15: return run_enc_full<15>(qkv, B, N, H, scale, out, out_ld, abl, s);
-        default: return run_enc_full<16>(qkv, B, N, H, scale, out, out_ld, abl, s);
+        case 5: return run_enc_full<5>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 6: return run_enc_full<6>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 7: return run_enc_full<7>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 8: return run_enc_full<8>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 9: return run_enc_full<9>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 10: return run_enc_full<10>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 11: return run_enc_full<11>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 12: return run_enc_full<12>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 13: return run_enc_full<13>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 14: return run_enc_full<14>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        case 15: return run_enc_full<15>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
+        default: return run_enc_full<16>(qkv, B, N, H, scale, out, out_ld, abl, s, max_grid);
       }
     }
     if (head_major && qpw16 == 2)

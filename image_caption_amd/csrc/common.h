@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <utility>
 
 typedef uint16_t bf16_t;  // bf16 storage (raw bits)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

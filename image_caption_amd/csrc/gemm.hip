@@ -190,6 +190,45 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ICAP_F16H (compile-time form, round 6): the ViT encoder's persistent GEMMs on gemm_f16h_kernel (one wave per SIMD,
+// half-step register double buffering - gemm_kern.h) instead of gemm_f16p_kernel
+#ifndef ICAP_F16H
+#define ICAP_F16H 0
+#endif
+// the f16h form's 32-bit offsets: A / W stage pieces (rows up to a whole tile past M) and the epilogue's byte range
+bool f16h_ok(const GemmArgs& g) {
+  const bool res = g.out == OUT_F32_RESID;
+  const long cbytes = (!res && g.hm_n) ? (long)g.M * g.N * 2 : (long)g.M * g.ldc * (res ? 4 : 2);
+  return g.bias && (!g.hm_n || g.hm_n >= 16) && cbytes < (1L << 32) && (long)(g.M + 256) * g.lda * 2 < (1L << 32) &&
+         (long)g.N * g.ldw * 2 < (1L << 32);
+}
+
+hipError_t launch_f16h(const GemmArgs& g, hipStream_t s, int blocks) {
+  static bool attrs = false;
+  if (!attrs) {
+    hipError_t e = hipSuccess;
+    for (const void* f : {(const void*)gemm_f16h_kernel<1, 0>, (const void*)gemm_f16h_kernel<1, 1>,
+                          (const void*)gemm_f16h_kernel<1, 2>})
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, f16h_lds(256));
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)gemm_f16h_kernel<2, 0, 224>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              f16h_lds(224));
+    if (e != hipSuccess) return e;
+    attrs = true;
+  }
+  if (g.out == OUT_F32_RESID) {
+    const int tiles = (g.N / 256) * ((g.M + 223) / 224);
+    hipLaunchKernelGGL((gemm_f16h_kernel<2, 0, 224>), dim3(std::min(tiles, blocks)), dim3(256), f16h_lds(224), s, g);
+  } else {
+    const int tiles = (g.N / 256) * ((g.M + 255) / 256);
+    const dim3 grid(std::min(tiles, blocks));
+    if (g.hm_n) hipLaunchKernelGGL((gemm_f16h_kernel<1, 2>), grid, dim3(256), f16h_lds(256), s, g);
+    else if (g.epi == EPI_GELU) hipLaunchKernelGGL((gemm_f16h_kernel<1, 1>), grid, dim3(256), f16h_lds(256), s, g);
+    else hipLaunchKernelGGL((gemm_f16h_kernel<1, 0>), grid, dim3(256), f16h_lds(256), s, g);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 bool gemm_f16_persistent(const GemmArgs& g) {
@@ -829,6 +868,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       // form (QKV 305 -> 265 us, MLP-1 423 -> 342 us at B = 256, tools/f16_forms_r2.sh); the residual GEMMs on
       // 224-row tiles (678 tiles = 2.65 per CU at N = 768 instead of 591 = 2.3)
       const int blocks = g.max_grid > 0 ? std::min(g.max_grid, cus) : cus;
+      if (ICAP_F16H && f16h_ok(g)) return launch_f16h(g, s, blocks);
       if (g.out == OUT_F32_RESID) {
         const int tiles224 = (g.N / 256) * ((g.M + 223) / 224);
         hipLaunchKernelGGL((gemm_f16p_kernel<2, 0, 224>), dim3(std::min(tiles224, blocks)), dim3(512),

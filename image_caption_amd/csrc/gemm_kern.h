@@ -572,6 +572,16 @@ void gemm_256_kernel(GemmArgs p) {
 // BMT: tile rows, 256 or (RES) 224 - wave tiles 112 x 64, the A stage 224 rows (wave 7 DMAs W rows only): at
 // N = 768 the 256-row tiles are 591 = 2.3 per CU (3 rounds, the last 30 % full), 224-row tiles 678 = 2.65 per CU
 // (3 rounds of 7/8 the work).
+// The LDS position of 16-byte chunk c of row r in a 64-deep (128-B row) stage of the persistent fp16 GEMMs; the stage
+// DMA reads chunk swz_chunk(l & 7, r) into lane l's slot, the fragment reads find chunk c at swz_chunk(c, r).
+// ICAP_SWZ 0: c ^ (r & 7) - conflict-free ds_read_b128 fragment reads, but the DMA's lanes then read each 64-B half-line
+// out of order and the address unit splits it (round-6 PMC: TCP accesses 2x hipBLASLt's on the same bytes, TA busy
+// 1.68x); 1: c ^ (4 ((r >> 1) & 1)) - each half-line read in order by 4 consecutive lanes, 2-way read conflicts
+#ifndef ICAP_SWZ
+#define ICAP_SWZ 0
+#endif
+__device__ __forceinline__ int swz_chunk(int c, int r) { return ICAP_SWZ ? c ^ (((r >> 1) & 1) << 2) : c ^ (r & 7); }
+
 template <int MODE, int ABL = 0, int BMT = 256>
 __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   constexpr bool SO = MODE == 1, RES = MODE == 2;
@@ -601,7 +611,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   const int nbx = ((int)gridDim.x - xcd + 7) >> 3, lb = blockIdx.x >> 3;  // blocks on this XCD, rank among them
   if (lb >= xcnt) return;
   const int M = p.M, nk = p.K / KS;
-  const int srow = wave * IPW * 8 + (lane >> 3), schunk = (lane & 7) ^ (srow & 7);
+  const int srow = wave * IPW * 8 + (lane >> 3), schunk = swz_chunk(lane & 7, srow);
   const int fr = lane & 15, fq = lane >> 4;
 #ifndef ICAP_F16P_PRIO
 #define ICAP_F16P_PRIO 0
@@ -696,7 +706,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   for (;;) {
     const int tn = t + nbx < xbase + xcnt ? t + nbx : -1;  // this block's next tile
     if constexpr (LB) {
-      const int fo0 = fr * 128 + ((fq ^ (fr & 7)) << 4), fo1 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
+      const int fo0 = fr * 128 + (swz_chunk(fq, fr) << 4), fo1 = fr * 128 + (swz_chunk(4 + fq, fr) << 4);
       bf16x8 b2[2][TN], a2[2 * TM];
       for (int kt = 0; kt < nk; ++kt, ++step) {
         const char* s0 = smem + (step & 1) * STAGE;
@@ -792,7 +802,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       if (!XK_LATE && st_t >= 0) stage(st_t, st_kt, (step + 1) & 1);
       const char* s0 = smem + (step & 1) * STAGE;
       if constexpr (XK) {
-        const int fo0 = fr * 128 + ((fq ^ (fr & 7)) << 4), fo1 = fr * 128 + (((4 + fq) ^ (fr & 7)) << 4);
+        const int fo0 = fr * 128 + (swz_chunk(fq, fr) << 4), fo1 = fr * 128 + (swz_chunk(4 + fq, fr) << 4);
         bf16x8 b2[2][TN], a2[2 * TM];
         auto rd = [&](const char* ptr) -> bf16x8 {  // ABL 9: an opaque register instead of the LDS read
           if constexpr (ABL == 9) {
@@ -831,7 +841,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int fo = fr * 128 + (((ks * 4 + fq) ^ (fr & 7)) << 4);
+        const int fo = fr * 128 + (swz_chunk(ks * 4 + fq, fr) << 4);
         bf16x8 bfr[TN];
 #pragma unroll
         for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(s0 + OPA + (wn * WN + j * 16) * 128 + fo);
@@ -941,10 +951,12 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
             // streaming stores (round 5): the QKV / MLP-1 outputs (232 / 310 MB) with cache policy nt | sc1 (aux 18) stream
             // past the L2 and leave it to the operands - plain nt: encoder 13.32-13.38 -> 13.12-13.24 ms on one box,
             // nt | sc1 another -0.1 ms against plain nt on another, sc1 alone +0.4 ms (profiles/r05/gemm_so_nt_ab.txt);
-            // the residual epilogue's fp32 loads / stores nt: slower
+            // the residual epilogue's fp32 loads / stores nt: slower.  num_records = 0xffffffff: the launcher admits
+            // outputs up to 2^31 elements = 4 GiB of fp16, the whole uint32 byte-offset range (a 2^31 - 1 byte count
+            // silently dropped every store past 2 GiB: ViT MLP-1 from B ~ 1775 - tests/test_gpu_6_ops.py)
             else if (ok)
               __builtin_amdgcn_raw_buffer_store_b128(
-                  w, __builtin_amdgcn_make_buffer_rsrc(p.C, 0, 0x7fffffff, 0x00020000),
+                  w, __builtin_amdgcn_make_buffer_rsrc(p.C, 0, -1, 0x00020000),
                   (uint32_t)((C + nb + (odd ? (j + 1) * 16 - 4 : j * 16)) - (bf16_t*)p.C) * 2, 0, 18);
           }
         }
@@ -1280,6 +1292,299 @@ __global__ __launch_bounds__(256, 1) void gemm_f16w_kernel(GemmArgs p) {
   if (SO && p.range_flag && __any(range_bad) && lane == 0) range_flag_set(p.range_flag);
 }
 constexpr int f16w_lds(int bm) { return 2 * (bm * 128 + 256 * 128) + 2048; }
+
+// ---------------------------------------------------------------------------------------------
+// Persistent fp16 encoder GEMM, one wave per SIMD, half-step register double buffering (round 6).
+// What hipBLASLt's gfx950 kernel for these shapes does that gemm_f16w_kernel did not (its main loop, disassembled from
+// torch's bundled TensileLibrary_HH_HH_HA_Bias_..._Alik_Bljk_..._gfx950.co, kernel
+// Custom_Cijk_Alik_Bljk_HHS_BH_Bias_HA_S_SAV_NTD_SK3_UserArgs_MT256x256x64_MI16x16x1):
+//  * every fragment of a k-step lives in registers: the 16 fragments of the k-step's second 32-deep half are read
+//    during the first half's 64 MFMAs (one ds_read_b128 per MFMA), and the next k-step's first-half fragments during
+//    the second half's last MFMAs - a fragment read has a whole half-step (~1000 cycles) to land, and no MFMA waits
+//    on one;
+//  * so the stage buffer of k-step i is free a quarter into k-step i: after one counted lgkmcnt(0) + barrier, the
+//    16 stage pieces of k-step i + 2 go into it, spread one per two MFMAs; they land ~1.75 k-steps later, when
+//    k-step i + 1's last quarter waits vmcnt(pieces issued since) + barrier and reads them (2 barriers per k-step,
+//    no wait at the top of a k-step).  gemm_f16w_kernel waited vmcnt(0) + barrier at the top of every k-step with
+//    reads two MFMA groups ahead; gemm_f16p_kernel's 8 waves read 192 KiB of fragments per k-step against 128 here.
+// Kept: the XCD-contiguous persistent raster, 64-deep full-line stages (chunk c of row r at c ^ (r & 7)), buffer-load
+// stage pieces (rows >= M read zeros), in-place AGPR accumulators (mfma16_f16_acc / acc_v), f16w's epilogues.  The
+// (tile, k-step) sequence of a block is one stream: the last two k-steps of a tile issue the next tile's stages 0
+// and 1 (and its bias, one 512-B LDS-DMA per wave, before stage 0), and read its k-step 0 first-half fragments, so
+// the epilogue runs between two tiles with nothing to wait for; its stores (NSTORE per wave, buffer stores: rows >= M
+// are dropped by the range check, every lane issues every store, so the count is exact) are younger than the next
+// tile's stage 1, which k-step 0 of that tile waits for with vmcnt(NSTORE + 16).
+// BMT = 224 (residual form): wave tiles 112 x 128, every wave stages 7 A pieces (28 = 224 / 8) + 8 W pieces.
+// EP (MODE 1): 0 = + bias, 1 = + bias then GELU, 2 = + bias into head-major planes.  MODE 2 = residual (C += acc + bias).
+constexpr int f16h_lds(int bm) { return 2 * (bm * 128 + 256 * 128) + 2048; }
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>) in order: a straight-line sequence whose index is a
+// constant in every copy (a 128-step `#pragma unroll` loop exceeds the unroller's threshold and leaves the fragment
+// arrays dynamically indexed, in scratch)
+template <class F, int... Ms>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, Ms...>) {
+  (f(std::integral_constant<int, Ms>{}), ...);
+}
+
+#ifndef ICAP_F16H_ABL
+#define ICAP_F16H_ABL 0  // timing ablations (variant builds only, wrong results): 1 no k-loop DMA, 2 no k-loop fragment
+#endif                   // reads, 3 no k-loop barriers, 4 no MFMAs, 5 no epilogue stores
+template <int MODE, int EP = 0, int BMT = 256>
+__global__ __launch_bounds__(256, 1) void gemm_f16h_kernel(GemmArgs p) {
+  constexpr int ABL = ICAP_F16H_ABL;
+  constexpr bool SO = MODE == 1, RES = MODE == 2;
+  static_assert(SO || RES, "store-only or residual epilogue");
+  static_assert(BMT == 256 || (RES && BMT == 224), "224-row tiles only for the residual form");
+  constexpr int BM = BMT, BN = 256, KS = 64, WM = BM / 2, WN = 128, TM = WM / 16, TN = WN / 16;
+  constexpr int OPA = BM * KS * 2, OPB = BN * KS * 2, STAGE = OPA + OPB;
+  constexpr int APW = BM / 8 / 4, WPW = 8, PIECES = APW + WPW;  // stage pieces per wave (A rows, W rows)
+  constexpr int NMF = 2 * TM * TN;                               // MFMAs per wave per k-step
+  constexpr int NSTORE = SO ? TM * TN / 2 : TM * TN;             // epilogue stores per wave per tile
+  // the k-step's event points (MFMA indices m): the second half's NR fragment reads one per two MFMAs from m = 0, the
+  // buffer barrier at RB, the bias slot + PIECES stage pieces one per DSTEP MFMAs from DMA0 (spread over the rest of
+  // the k-step: issued in a burst they queue at the CU's address unit and stall the wave's MFMA issue - round-6 timing
+  // ablations), the stage-(i + 1) wait + barrier at LW, then the next first half's reads one per two MFMAs
+  constexpr int NR = TM + TN, RB = 2 * NR, DMA0 = RB + 2, DSTEP = (NMF - 8 - DMA0) / (PIECES + 1);
+  constexpr int LW = NMF - 2 * NR - 4;
+  // stage (i + 2) pieces issued before LW (the bias DMA, when issued, is older than them: the wait then covers it too)
+  constexpr int NB_LW = (LW - DMA0 - 1) / DSTEP < PIECES ? (LW - DMA0 - 1) / DSTEP : PIECES;
+  static_assert(DSTEP >= 2 && DMA0 + PIECES * DSTEP < NMF, "stage pieces inside the k-step");
+  static_assert(LW > RB && LW + 2 * NR - 2 < NMF, "next first-half reads inside the k-step");
+  static_assert(NSTORE + NB_LW <= 63 || RES, "counted seam wait fits vmcnt");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
+  const int xcd = blockIdx.x & 7, q = nwg >> 3, r = nwg & 7;
+  const int xbase = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, xcnt = q + (xcd < r);
+  const int nbx = ((int)gridDim.x - xcd + 7) >> 3, lb = blockIdx.x >> 3;
+  if (lb >= xcnt) return;
+  const int M = p.M, nk = p.K / KS;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int schunk = swz_chunk(lane & 7, lane >> 3);  // a piece is 8 rows x 128 B; row & 7 = lane >> 3
+
+  // stage pieces: per-lane 32-bit offsets (A: this lane's row of the wave's first piece in the staged tile, stepped by
+  // 8 rows per piece; W: fixed), the tile's W rows and the k-step in the wave-uniform soffset
+  const i32x4r ra = buf_rsrc(p.A, (uint32_t)((long)M * p.lda * 2)), rw = buf_rsrc(p.W, (uint32_t)((long)p.N * p.ldw * 2));
+  const uint32_t vw = (uint32_t)(((wave * WPW * 8 + (lane >> 3)) * p.ldw + schunk * 8) * 2);
+  const uint32_t astep = (uint32_t)(8 * p.lda * 2), wstep = (uint32_t)(8 * p.ldw * 2);
+  float* sbias = (float*)(smem + 2 * STAGE);
+  // stage (tile t, k-step kt) piece i (0 .. PIECES - 1) into ring buffer buf
+  auto piece = [&](int t, int kt, int buf, int i) {
+    const int bm = t / nbn, bn = t - bm * nbn;
+    char* s0 = smem + buf * STAGE;
+    if (i < APW) {
+      const uint32_t va = (uint32_t)(((bm * BM + (wave * APW + i) * 8 + (lane >> 3)) * p.lda + schunk * 8) * 2);
+      lds_dma_buf16(ra, va, (uint32_t)(kt * KS * 2), (LDS_AS void*)(s0 + (wave * APW + i) * 1024));
+    } else {
+      const int j = i - APW;
+      lds_dma_buf16(rw, vw + j * wstep, (uint32_t)(bn * BN * p.ldw * 2 + kt * KS * 2),
+                    (LDS_AS void*)(s0 + OPA + (wave * WPW + j) * 1024));
+    }
+  };
+  (void)astep;
+  // the tile's bias: each wave DMAs the 128 values of its column half (lanes 0-31, 512 B) into slot `slot`
+  auto load_bias = [&](int t, int slot) {
+    const int n0 = (t - (t / nbn) * nbn) * BN + wn * WN;
+    if (lane < 32) lds_dma16(p.bias + n0 + lane * 4, (LDS_AS void*)(sbias + slot * 256 + wn * WN));
+  };
+  // epilogue buffer resource: rows >= M (ragged last band) fall past the byte count (the launcher keeps it < 2^32)
+  const long cbytes = EP == 2 ? (long)M * p.N * 2 : (long)M * p.ldc * (RES ? 4 : 2);
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, (int)(uint32_t)cbytes, 0x00020000);
+  const int fo0 = fr * 128 + (swz_chunk(fq, fr) << 4), fo1 = fr * 128 + (swz_chunk(4 + fq, fr) << 4);
+  const int arow = wm * WM * 128, wrow = OPA + wn * WN * 128;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[2][TM], fb[2][TN];  // [half][fragment]: this k-step's first-half (0) and second-half (1) fragments
+  int t = xbase + lb, step = 0, tcount = 0;
+  // prologue: bias, stages 0 and 1 of the first tile, then k-step 0's first-half fragments
+  load_bias(t, 0);
+#pragma unroll
+  for (int i = 0; i < PIECES; ++i) piece(t, 0, 0, i);
+  const bool two = nk > 1;
+  if (two) {
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) piece(t, 1, 1, i);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < TN; ++j) fb[0][j] = *(const bf16x8*)(smem + wrow + j * 16 * 128 + fo0);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) fa[0][i] = *(const bf16x8*)(smem + arow + i * 16 * 128 + fo0);
+  bool seam = false;       // SO: the previous tile's NSTORE stores are younger than this tile's stage 1
+  bool range_bad = false;  // SO: some stored fp16 value is not finite
+  for (;;) {
+    const int tn = t + nbx < xbase + xcnt ? t + nbx : -1;
+    int kt = 0;
+#pragma clang loop unroll(disable)
+    do {
+      const char* s0 = smem + (step & 1) * STAGE;
+      const char* s1 = smem + ((step + 1) & 1) * STAGE;
+      // the stage this k-step issues (k-step kt + 2 of this tile, else stage kt + 2 - nk of the next tile) into s0
+      // (none - the last tile's last two k-steps: a dummy re-load of this tile's last stage into the free buffer, so
+      // every k-step issues PIECES pieces and the counted waits stay the same; nothing reads it)
+      int st_t = t, st_kt = nk - 1;
+      if (kt + 2 < nk) st_kt = kt + 2;
+      else if (tn >= 0) st_t = tn, st_kt = kt + 2 - nk;
+      st_t = __builtin_amdgcn_readfirstlane(st_t);
+      st_kt = __builtin_amdgcn_readfirstlane(st_kt);
+      const bool bias_next = st_t != t && st_kt == 0;  // the next tile's bias goes with its stage 0
+      // stage kt + 1 (this tile's, or the next tile's stage 0) exists: wait for it at the late point, read its
+      // first-half fragments
+      const bool has_next = kt + 1 < nk || tn >= 0;
+      // younger than stage kt + 1 at the late point: this k-step's PIECES pieces (+ the bias DMA before them, which the
+      // wait then covers too), and (SO, k-step 0 after a seam) the NSTORE stores of the previous tile's epilogue; RES:
+      // the epilogue's own waits on its residual loads retired stage 1 already (in-order counter)
+      const bool after_seam = seam && kt == 0;
+      unroll_seq([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        // second-half fragment reads (W first: the first second-half MFMAs need all TN of them and A 0)
+        constexpr int r1 = m / 2, r0 = (m - LW) / 2;  // read slots
+        if constexpr (ABL == 2 || (m & 1)) {
+        } else if constexpr (r1 < TN) fb[1][r1] = *(const bf16x8*)(s0 + wrow + r1 * 16 * 128 + fo1);
+        else if constexpr (r1 < TN + TM) fa[1][r1 - TN] = *(const bf16x8*)(s0 + arow + (r1 - TN) * 16 * 128 + fo1);
+        if constexpr (m == RB && ABL != 3) {  // every wave's reads of this buffer are done: it takes stage kt + 2
+          // (the builtin, not asm: the compiler's waitcnt pass then knows the reads landed and adds no waits of its own
+          // for them - lgkmcnt saturates at 15, so it would otherwise stall on the next first-half reads)
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0); vmcnt / expcnt at their maxima
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
+        if constexpr (ABL != 1 && m >= DMA0 && m <= DMA0 + PIECES * DSTEP && (m - DMA0) % DSTEP == 0) {
+          constexpr int i = (m - DMA0) / DSTEP;  // 0: the bias (stage 0 of the next tile only), then the pieces
+          if constexpr (i == 0) {
+            if (bias_next) load_bias(st_t, (tcount + 1) & 1);
+          } else {
+            piece(st_t, st_kt, step & 1, i - 1);
+          }
+        }
+        if constexpr (m == LW && ABL != 3) {
+          if (has_next) {  // stage kt + 1 landed (this wave's pieces, then every wave's)
+            if (SO && after_seam) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SO ? NSTORE + NB_LW : 0) : "memory");
+            else if (!(RES && after_seam)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB_LW) : "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+          }
+        }
+        // (unconditional: without a next stage the values are never used)
+        if constexpr (ABL == 2 || m < LW || ((m - LW) & 1)) {
+        } else if constexpr (r0 < TN) fb[0][r0] = *(const bf16x8*)(s1 + wrow + r0 * 16 * 128 + fo0);
+        else if constexpr (r0 < TN + TM) fa[0][r0 - TN] = *(const bf16x8*)(s1 + arow + (r0 - TN) * 16 * 128 + fo0);
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int h = m / (TM * TN), a = (m % (TM * TN)) / TN, b = m % TN;
+        if constexpr (ABL == 4) asm volatile("" ::"v"(fb[h][b]), "v"(fa[h][a]));
+        else mfma16_f16_acc(acc[a][b], fb[h][b], fa[h][a]);
+        __builtin_amdgcn_sched_barrier(0);
+      }, std::make_integer_sequence<int, NMF>{});
+      ++step;
+    } while (++kt < nk);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");  // XDL MFMA write -> v_accvgpr_read (<= 18 states)
+    const int bm = t / nbn, bn = t - bm * nbn, mb = bm * BM + wm * WM, nb = bn * BN + wn * WN;
+    const float* bl = sbias + (tcount & 1) * 256 + wn * WN + 4 * fq;  // re-read from LDS where used
+    if constexpr (SO) {
+      int hq = 0, hr = 0;
+      if (EP == 2) {
+        hq = (mb + fr) / p.hm_n;
+        hr = mb + fr - hq * p.hm_n;
+      }
+      const uint32_t head2 = EP == 2 ? (uint32_t)(p.hm_n * 64 - 64) * 2 : 0;
+      const bool odd = fq & 1;
+      uint32_t rbits = 0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t orow;  // element offset of column nb in this lane's row
+        if (EP == 2) {
+          orow = (uint32_t)(((hq * (p.N / 64) + nb / 64) * p.hm_n + hr) * 64);
+          hr += 16;
+          if (hr >= p.hm_n) hr -= p.hm_n, ++hq;
+        } else {
+          orow = (uint32_t)((mb + i * 16 + fr) * p.ldc + nb);
+        }
+        const uint32_t ob = (orow + 4 * fq) * 2;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {  // the row tile in two halves of 4 column tiles (one 64-column head each)
+          u32x2 pk[4];
+          f32x4 av[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[j] = acc_v(acc[i][hh * 4 + j]) + *(const f32x4*)(bl + (hh * 4 + j) * 16);
+          if (EP == 1) {
+#pragma unroll
+            for (int j = 0; j < 4; j += 2) {
+              const f32x8 gv = gelu_erf_as8((f32x8){av[j][0], av[j][1], av[j][2], av[j][3], av[j + 1][0], av[j + 1][1],
+                                                     av[j + 1][2], av[j + 1][3]});
+              pk[j] = pack16x4<true>((f32x4){gv[0], gv[1], gv[2], gv[3]});
+              pk[j + 1] = pack16x4<true>((f32x4){gv[4], gv[5], gv[6], gv[7]});
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pk[j] = pack16x4<true>(av[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            rbits |= ((pk[j][0] & 0x7c007c00u) + 0x04000400u) | ((pk[j][1] & 0x7c007c00u) + 0x04000400u);
+#pragma unroll
+          for (int j = 0; j < 4; j += 2) {
+            // lanes fq (even) and fq + 1 hold columns 4 fq .. 4 fq + 7 of tiles j and j + 1: the even lane stores tile j's
+            // 8 columns, the odd lane tile j + 1's (the partner is 16 lanes away, same row); streaming stores (nt | sc1)
+            const u32x2 snd = odd ? pk[j] : pk[j + 1];
+            const u32x2 rcv = {xor16_partner(snd[0]), xor16_partner(snd[1])};
+            const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], pk[j + 1][0], pk[j + 1][1]}
+                                : (u32x4){pk[j][0], pk[j][1], rcv[0], rcv[1]};
+            const uint32_t off = ob + (uint32_t)((odd ? (hh * 4 + j + 1) * 16 - 4 : (hh * 4 + j) * 16) * 2) + (hh ? head2 : 0);
+            if constexpr (ABL == 5) asm volatile("" ::"v"(w), "v"(off));
+            else __builtin_amdgcn_raw_buffer_store_b128(w, rc, off, 0, 18);
+          }
+        }
+      }
+      // rows >= M (zeros + bias) are finite whenever the real rows' bias is: the OR over all rows is the guard
+      if (rbits & 0x80008000u) range_bad = true;
+    } else {
+      constexpr int RBK = 4;  // row tiles per residual batch (RBK x TN 16-byte loads in flight per lane)
+#pragma unroll
+      for (int h2 = 0; h2 < (TM + RBK - 1) / RBK; ++h2) {
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 rv[RBK][TN];
+#pragma unroll
+        for (int i = 0; i < RBK; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            if (h2 * RBK + i < TM)
+              rv[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rc, (uint32_t)(((mb + (h2 * RBK + i) * 16 + fr) * p.ldc + nb + j * 16 + 4 * fq) * 4),
+                                                       0, 0));
+#pragma unroll
+        for (int i = 0; i < RBK; ++i) {
+          if (h2 * RBK + i >= TM) break;
+          __builtin_amdgcn_sched_barrier(0);
+          const uint32_t orow = (uint32_t)(((mb + (h2 * RBK + i) * 16 + fr) * p.ldc + nb + 4 * fq) * 4);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            f32x4 a = acc_v(acc[h2 * RBK + i][j]) + *(const f32x4*)(bl + j * 16);
+            if constexpr (ABL == 5) asm volatile("" ::"v"(rv[i][j] + a), "v"(orow));
+            else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv[i][j] + a), rc, orow + j * 64, 0, 0);
+          }
+        }
+      }
+    }
+    seam = true;
+    if (tn < 0) break;
+    t = tn;
+    ++tcount;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup has ended
+  if (SO && p.range_flag && __any(range_bad) && lane == 0) range_flag_set(p.range_flag);
+}
 
 // ---------------------------------------------------------------------------------------------
 // Persistent fp16 encoder GEMM with the A operand two k-steps ahead (round 3; tools build only, ICAP_F16_GEMM=7:

@@ -128,13 +128,26 @@ struct DecodeGraph {
   int calls = 0;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
+  // stop-aware form (chunk > 0): one graph per chunk of `chunk` steps, each ending in the chunk's stop test, and an
+  // event per chunk (decode_loop)
+  int chunk = 0;
+  std::vector<hipGraph_t> cgraph;
+  std::vector<hipGraphExec_t> cexec;
+  std::vector<hipEvent_t> cev;
   DevBuf ids, lg, uni, lp;
   void reset() {
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
+    for (hipGraphExec_t e : cexec) (void)hipGraphExecDestroy(e);
+    for (hipGraph_t e : cgraph) (void)hipGraphDestroy(e);
+    cexec.clear();
+    cgraph.clear();
     exec = nullptr;
     graph = nullptr;
     calls = 0;
+  }
+  ~DecodeGraph() {
+    for (hipEvent_t e : cev) (void)hipEventDestroy(e);
   }
 };
 
@@ -151,7 +164,20 @@ struct icap_handle {
   static constexpr int MAX_BRANCHES = 4;
   hipStream_t aux_stream[MAX_BRANCHES] = {};  // streams of chains 1.. (chain 0 runs on the caller's)
   hipEvent_t ev_fork = nullptr, ev_join[MAX_BRANCHES] = {};
-  DecodeGraph dg[2];  // one captured loop per mode (0 greedy, 1 sample): SCST alternates them
+  DecodeGraph dg[4];  // one captured loop per mode (0 greedy, 1 sample: SCST alternates them), + 2: stop-aware (chunked)
+  // stop-aware decodes: one host-mapped stop flag per chunk and mode (written by stop_scan_kernel), and the decode
+  // steps the last stop-aware decode executed
+  static constexpr int MAX_CHUNKS = 256;
+  int* stop_host = nullptr;
+  int* stop_dev = nullptr;
+  int last_steps = 0;
+  int* stop_flags(int mode) {
+    if (!stop_host) {
+      HIPCHK(hipHostMalloc((void**)&stop_host, 2 * MAX_CHUNKS * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+      HIPCHK(hipHostGetDevicePointer((void**)&stop_dev, stop_host, 0));
+    }
+    return stop_dev + mode * MAX_CHUNKS;
+  }
   int ns = 2;  // activation planes (1 = bf16, 2 = hi/lo)
   bool i8 = false;  // ICAP_PREC_I8X2: LayerNorm-fed ViT GEMMs on int8 two-slice operands
   bool i8k = false;  // ... and MLP-2 on the block-scaled int8 GELU output (ICAP_I8_MLP2=1, opt-in)
@@ -256,6 +282,7 @@ struct icap_handle {
   }
 
   ~icap_handle() {
+    if (stop_host) (void)hipHostFree(stop_host);
     for (DecodeGraph& g : dg) {
       g.reset();
       for (DevBuf* b : {&g.ids, &g.lg, &g.uni, &g.lp}) b->release();
@@ -663,7 +690,7 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
       const double flops = 4.0 * B * d.vit_heads * (double)T * T * 64;
       const double bytes = 2.0 * B * (double)T * V * 4;
       h->timed(PROF_ENC_ATTN, flops, bytes, s, [&] {
-        HIPCHK(launch_enc_attention(qkv, 3 * V, 0, B, T, d.vit_heads, 0.125f, a, V, 0, NS_F16, s, 1));
+        HIPCHK(launch_enc_attention(qkv, 3 * V, 0, B, T, d.vit_heads, 0.125f, a, V, 0, NS_F16, s, 1, h->enc_cus));
       });
     }
     h->gemm16(a, V, L.out, M, x, V, EPI_NONE, OUT_F32_RESID, s);
@@ -1399,25 +1426,30 @@ bool step_path(const icap_handle*, int, const DropCfg*) { return false; }
 bool xdec_path(const icap_handle*, int, int, int, const DropCfg*) { return false; }
 #endif
 
+// Steps [t_begin, t_end) of the loop (t_end < 0: to the end); the prologue (start column, step-0 embedding, finished
+// flags) only with t_begin = 0 - a stop-aware decode runs the loop as consecutive ranges (decode_loop)
 void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
                        float* step_logits, const float* uniforms, float* logp, hipStream_t s,
-                       const DropCfg* drop = nullptr) {
+                       const DropCfg* drop = nullptr, int t_begin = 0, int t_end = -1) {
   const icap_model_desc& d = h->d;
   REQUIRE(B > 0 && max_len >= 1, "bad batch / max_len");
   REQUIRE(max_len <= d.pe_len, "max_len exceeds the positional-encoding table (PositionalEncoding max_len)");
   REQUIRE(S > 0 && S <= 256, "memory length must be in [1, 256]");
+  if (t_end < 0) t_end = max_len - 1;
   const int D = d.d_model, wsi = uniforms ? 1 : 0;
   DecodeBufs b = dec_bufs(h, B, B, max_len, S, 0, wsi);
   const float scale = (float)std::sqrt((double)D);
   if (mem) mem_planes(h, mem, b, s);
-  HIPCHK(launch_fill_col(ids, B, max_len, 0, start, s));
-  HIPCHK(launch_embed(nullptr, 0, start, B, 1, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s,
-                      drop ? *drop : DropCfg{}));
   uint8_t* fin = nullptr;
   if (uniforms) {
     h->dws[wsi].fin.ensure((size_t)B);
     fin = h->dws[wsi].fin.as<uint8_t>();
-    HIPCHK(launch_fill_u8(fin, B, 0, s));  // a kernel node: reset on every graph replay
+  }
+  if (t_begin == 0) {
+    HIPCHK(launch_fill_col(ids, B, max_len, 0, start, s));
+    HIPCHK(launch_embed(nullptr, 0, start, B, 1, 0, h->emb, h->pe, D, scale, b.x, b.a, b.aL, h->ns, s,
+                        drop ? *drop : DropCfg{}));
+    if (fin) HIPCHK(launch_fill_u8(fin, B, 0, s));  // a kernel node: reset on every graph replay
   }
   // The images are independent: with dec_branches = n the batch decodes as n independent chains of
   // consecutive rows on n streams (n parallel branches of the captured graph), so their latency-bound
@@ -1525,7 +1557,7 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
   }
   // step-major issue order: launched eagerly, the chains' kernels reach their streams interleaved
   // (a captured graph has the same dependencies either way)
-  for (int t = 0; t + 1 < max_len; ++t) {
+  for (int t = t_begin; t < t_end; ++t) {
     for (int part = 0; part < nb; ++part) {
       const int r0 = (int)((long)B * part / nb), n = (int)((long)B * (part + 1) / nb) - r0;
       hipStream_t st = part ? h->aux_stream[part] : s;
@@ -1562,12 +1594,27 @@ void decode_loop_eager(icap_handle* h, const float* mem, int B, int S, int max_l
 // workspace, sets kernel attributes); the second captures the whole loop on a private stream into
 // a hipGraph over handle-owned in/out buffers; later calls copy memory in, replay, copy ids out.
 // drop_p > 0 (sampling only): train-mode dropout masks under drop_seed (DropCfg, common.h)
+// chunk > 0 (stop-aware, round 6): the loop as consecutive graphs of `chunk` steps, each ending in a stop test of its
+// columns (stop_scan_kernel -> a host-mapped flag per chunk).  Before launching chunk c the host waits for chunk c - 2's
+// event and reads its flag: once a chunk reports the reference's stop (greedy: a step whose every latest token is end,
+// vit:321-323; sampling: every row finished, scst_loss:246-249) no further chunk is launched - the GPU always holds
+// one more chunk than the host has checked, so the checks add no gap, and at most one chunk past the stop runs.  The
+// columns not computed are filled (ids = end, log-probs = 0), so the callers' stop rules return the reference's
+// sequence.  *steps = decode steps executed.  The host blocks until chunk (last - 1) has run.
 void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, int start, int end, int32_t* ids,
                  float* step_logits, const float* uniforms, float* logp, hipStream_t s, float drop_p = 0.f,
-                 uint32_t drop_seed = 0) {
+                 uint32_t drop_seed = 0, int chunk = 0, int* steps = nullptr) {
   const int mode = uniforms ? 1 : 0;
-  DecodeGraph& g = h->dg[mode];
   const bool wl = step_logits != nullptr;
+  const int nsteps = max_len - 1;
+  if (chunk >= nsteps) chunk = 0;  // one chunk: the fixed-length graph
+  REQUIRE(chunk >= 0 && (chunk == 0 || (nsteps + chunk - 1) / chunk <= icap_handle::MAX_CHUNKS) && chunk <= 64,
+          "decode chunk: 0 (fixed length) or 1..64 steps, at most 256 chunks");
+#ifdef ICAP_TOOLS
+  if (chunk && (step_path(h, max_len, nullptr) || xdec_path(h, B, S, max_len, nullptr))) chunk = 0;
+#endif
+  if (steps) *steps = nsteps;
+  DecodeGraph& g = h->dg[mode + (chunk ? 2 : 0)];
   DropCfg drop{};
   if (drop_p > 0.f) {
     REQUIRE(mode == 1 && drop_p < 1.f, "dropout applies to sampling, with p in [0, 1)");
@@ -1584,17 +1631,50 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     return;
   }
   if (g.B != B || g.S != S || g.L != max_len || g.mode != mode || g.logits != wl || g.start != start ||
-      g.end != end || g.drop_thr != drop.thr || (g.exec && g.gen != g_ws_generation)) {
+      g.end != end || g.drop_thr != drop.thr || g.chunk != chunk || ((g.exec || !g.cexec.empty()) && g.gen != g_ws_generation)) {
     g.reset();
     g.B = B; g.S = S; g.L = max_len; g.mode = mode; g.logits = wl; g.start = start; g.end = end;
-    g.drop_thr = drop.thr;
+    g.drop_thr = drop.thr; g.chunk = chunk;
   }
-  if (!g.exec && g.calls++ == 0) {
-    decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s, dp);
+  const int nch = chunk ? (nsteps + chunk - 1) / chunk : 1;
+  int* flags = chunk ? h->stop_flags(mode) : nullptr;
+  // the chunk sequence with the host's stop checks (launch(c) enqueues chunk c and its stop test), then the tail fill
+  auto run_chunks = [&](auto&& launch, int32_t* ids_buf, float* lp_buf) {
+    while ((int)g.cev.size() < nch) {
+      hipEvent_t e = nullptr;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      g.cev.push_back(e);
+    }
+    int launched = 0;
+    for (int c = 0; c < nch; ++c) {
+      if (c >= 2) {
+        HIPCHK(hipEventSynchronize(g.cev[c - 2]));
+        if (__atomic_load_n(h->stop_host + mode * icap_handle::MAX_CHUNKS + c - 2, __ATOMIC_ACQUIRE)) break;
+      }
+      launch(c);
+      HIPCHK(hipEventRecord(g.cev[c], s));
+      launched = c + 1;
+    }
+    const int done = std::min(nsteps, launched * chunk);
+    if (steps) *steps = done;
+    h->last_steps = done;
+    if (done < nsteps) HIPCHK(launch_stop_tail(ids_buf, B, max_len, done, end, mode ? lp_buf : nullptr, s));
+  };
+  if (!g.exec && g.cexec.empty() && g.calls++ == 0) {
+    if (!chunk) {
+      decode_loop_eager(h, mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s, dp);
+    } else {
+      run_chunks([&](int c) {
+        const int t0 = c * chunk, t1 = std::min(nsteps, t0 + chunk);
+        decode_loop_eager(h, c ? nullptr : mem, B, S, max_len, start, end, ids, step_logits, uniforms, logp, s, dp, t0, t1);
+        HIPCHK(launch_stop_scan(ids, B, max_len, t0 + 1, t1 + 1, end, mode ? h->dws[mode].fin.as<uint8_t>() : nullptr,
+                                flags + c, s));
+      }, ids, logp);
+    }
     return;
   }
   const size_t lg_bytes = (size_t)(max_len - 1) * B * h->d.vocab * 4;
-  if (!g.exec) {
+  if (!g.exec && g.cexec.empty()) {
     g.ids.ensure((size_t)B * max_len * 4);
     if (wl) g.lg.ensure(lg_bytes);
     if (mode) {
@@ -1616,27 +1696,51 @@ void decode_loop(icap_handle* h, const float* mem, int B, int S, int max_len, in
     HIPCHK(hipStreamSynchronize(s));
     const bool prof = h->prof_on;
     h->prof_on = false;
-    HIPCHK(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
-    try {
-      decode_loop_eager(h, nullptr, B, S, max_len, start, end, g.ids.as<int32_t>(),
-                        wl ? g.lg.as<float>() : nullptr, mode ? g.uni.as<float>() : nullptr,
-                        mode ? g.lp.as<float>() : nullptr, h->cap_stream, dp);
-    } catch (...) {
-      hipGraph_t dead = nullptr;
-      (void)hipStreamEndCapture(h->cap_stream, &dead);
-      if (dead) (void)hipGraphDestroy(dead);
-      h->prof_on = prof;
-      throw;
+    for (int c = 0; c < nch; ++c) {
+      HIPCHK(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+      try {
+        const int t0 = chunk ? c * chunk : 0, t1 = chunk ? std::min(nsteps, t0 + chunk) : nsteps;
+        decode_loop_eager(h, nullptr, B, S, max_len, start, end, g.ids.as<int32_t>(),
+                          wl ? g.lg.as<float>() : nullptr, mode ? g.uni.as<float>() : nullptr,
+                          mode ? g.lp.as<float>() : nullptr, h->cap_stream, dp, t0, t1);
+        if (chunk)
+          HIPCHK(launch_stop_scan(g.ids.as<int32_t>(), B, max_len, t0 + 1, t1 + 1, end,
+                                  mode ? h->dws[mode].fin.as<uint8_t>() : nullptr, flags + c, h->cap_stream));
+      } catch (...) {
+        hipGraph_t dead = nullptr;
+        (void)hipStreamEndCapture(h->cap_stream, &dead);
+        if (dead) (void)hipGraphDestroy(dead);
+        h->prof_on = prof;
+        throw;
+      }
+      hipGraph_t gr = nullptr;
+      hipGraphExec_t ex = nullptr;
+      HIPCHK(hipStreamEndCapture(h->cap_stream, &gr));
+      const hipError_t ie = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+      if (ie != hipSuccess) {
+        (void)hipGraphDestroy(gr);
+        h->prof_on = prof;
+        HIPCHK(ie);
+      }
+      if (chunk) {
+        g.cgraph.push_back(gr);
+        g.cexec.push_back(ex);
+      } else {
+        g.graph = gr;
+        g.exec = ex;
+      }
     }
-    HIPCHK(hipStreamEndCapture(h->cap_stream, &g.graph));
-    HIPCHK(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
     h->prof_on = prof;
     g.gen = g_ws_generation;
   }
   DecodeBufs b = dec_bufs(h, B, B, max_len, S, 0, mode);  // no allocation: sized at capture
   mem_planes(h, mem, b, s);
   if (mode) HIPCHK(hipMemcpyAsync(g.uni.p, uniforms, (size_t)(max_len - 1) * B * 4, hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipGraphLaunch(g.exec, s));
+  if (!chunk) {
+    HIPCHK(hipGraphLaunch(g.exec, s));
+  } else {
+    run_chunks([&](int c) { HIPCHK(hipGraphLaunch(g.cexec[c], s)); }, g.ids.as<int32_t>(), mode ? g.lp.as<float>() : nullptr);
+  }
   HIPCHK(hipMemcpyAsync(ids, g.ids.p, (size_t)B * max_len * 4, hipMemcpyDeviceToDevice, s));
   if (wl) HIPCHK(hipMemcpyAsync(step_logits, g.lg.p, lg_bytes, hipMemcpyDeviceToDevice, s));
   if (mode) HIPCHK(hipMemcpyAsync(logp, g.lp.p, (size_t)B * (max_len - 1) * 4, hipMemcpyDeviceToDevice, s));
@@ -2229,6 +2333,31 @@ int icap_decode_sample_dropout(icap_handle* h, const float* memory, int B, int S
     REQUIRE(p >= 0.f && p < 1.f, "dropout p must be in [0, 1)");
     decode_loop(h, memory, B, S, max_len, start_token, end_token, ids, nullptr, uniforms, logp, (hipStream_t)stream,
                 p, seed);
+  });
+}
+
+namespace {
+int stop_chunk(int chunk_steps, int B) { return chunk_steps > 0 ? chunk_steps : (B <= 64 ? 4 : 8); }
+}  // namespace
+
+int icap_decode_greedy_stop(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                            int end_token, int chunk_steps, int32_t* ids, float* step_logits, int* steps_executed,
+                            void* stream) {
+  return guarded([&] {
+    REQUIRE(h && memory && ids, "bad arguments");
+    decode_loop(h, memory, B, S, max_len, start_token, end_token, ids, step_logits, nullptr, nullptr,
+                (hipStream_t)stream, 0.f, 0, stop_chunk(chunk_steps, B), steps_executed);
+  });
+}
+
+int icap_decode_sample_stop(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                            int end_token, const float* uniforms, float p, uint32_t seed, int chunk_steps, int32_t* ids,
+                            float* logp, int* steps_executed, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && memory && ids && uniforms && logp, "bad arguments");
+    REQUIRE(p >= 0.f && p < 1.f, "dropout p must be in [0, 1)");
+    decode_loop(h, memory, B, S, max_len, start_token, end_token, ids, nullptr, uniforms, logp, (hipStream_t)stream, p,
+                seed, stop_chunk(chunk_steps, B), steps_executed);
   });
 }
 

@@ -367,6 +367,11 @@ hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows
 // re-applied on the second replay of the sampled-decode graph, ROCm 7.2)
 hipError_t launch_fill_u8(uint8_t* p, long n, uint8_t value, hipStream_t s);
 hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hipStream_t s);
+// stop-aware decode (round 6): flag (host-mapped) = 1 when a column in [col0, col1) is all end (greedy) or every fin row
+// is set (fin != nullptr); the tail fill of a stopped decode (ids columns > t0 = end, logp steps >= t0 = 0)
+hipError_t launch_stop_scan(const int32_t* ids, int B, long ld, int col0, int col1, int end, const uint8_t* fin,
+                            int* flag, hipStream_t s);
+hipError_t launch_stop_tail(int32_t* ids, int B, int L, int t0, int end, float* logp, hipStream_t s);
 hipError_t launch_split_f32(const float* src, long n, bf16_t* dst, long lo, int nsplit, hipStream_t s);
 // bf16 planes -> fp32 (hi + lo)
 hipError_t launch_planes_to_f32(const bf16_t* src, long lo, long n, int nsplit, float* dst, hipStream_t s);
@@ -381,7 +386,8 @@ hipError_t launch_transpose_heads_bf16(const float* wk, int H, int hd, int D, bf
 // Encoder self-attention (non-causal) over N tokens, heads of 64, MFMA bf16 (nsplit 1 or 2).
 // head_major: qkv written with GemmArgs::hm_n = N (N in (64, 256])
 hipError_t launch_enc_attention(const bf16_t* qkv, long ld, long lo, int B, int N, int H, float scale,
-                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s, int head_major = 0);
+                                bf16_t* out, long out_ld, long out_lo, int nsplit, hipStream_t s, int head_major = 0,
+                                int max_grid = 0);  // max_grid: the encoder CU budget of the persistent form (0 = all)
 // Decoder self-attention with fp32 KV cache; n_new query rows per image starting at t0.
 hipError_t launch_dec_self_attn(const float* qkv, int B, int n_new, int t0, int H, float* kc, float* vc,
                                 int Lmax, int causal, float scale, bf16_t* out, long lo, int nsplit,

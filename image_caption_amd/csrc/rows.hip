@@ -301,6 +301,45 @@ __global__ void fill_col_kernel(int32_t* ids, int B, long ld, int col, int value
   for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x) ids[(long)b * ld + col] = value;
 }
 
+// Stop test of one chunk of a stop-aware decode (round 6): *flag = 1 when some id column in [col0, col1) holds the end
+// token in every row (greedy: _greedy_search breaks after the first such step, models/vit_transformer_model.py:321-323)
+// or, with fin, when every row has finished (sampling: scst_loss.py:246-249); flag is host-mapped memory the host reads
+// after the chunk's event.  One block.
+__global__ void stop_scan_kernel(const int32_t* ids, int B, long ld, int col0, int col1, int end, const uint8_t* fin,
+                                 int* flag) {
+  __shared__ int live[65];  // [c]: some row's token in column col0 + c is not end; [64]: some row has not finished
+  const int nc = col1 - col0;
+  for (int i = threadIdx.x; i < 65; i += blockDim.x) live[i] = 0;
+  __syncthreads();
+  for (long i = threadIdx.x; i < (long)B * nc; i += blockDim.x) {
+    const int b = (int)(i / nc), c = (int)(i - (long)b * nc);
+    if (ids[(long)b * ld + col0 + c] != end) live[c] = 1;
+  }
+  if (fin)
+    for (int b = threadIdx.x; b < B; b += blockDim.x)
+      if (!fin[b]) live[64] = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int stop = 0;
+    if (fin) stop = !live[64];
+    else
+      for (int c = 0; c < nc; ++c) stop |= !live[c];
+    __hip_atomic_store(flag, stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+  }
+}
+
+// The columns a stopped decode did not compute (steps >= t0): ids = end (the reference's generated sequence ends
+// before them; the stop rules keep it), sampled log-probs = 0 (every row had finished: masked_fill semantics)
+__global__ void stop_tail_kernel(int32_t* ids, int B, int L, int t0, int end, float* logp) {
+  const int n = L - 1 - t0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (long)B * n; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / n), t = t0 + (int)(i - (long)b * n);
+    ids[(long)b * L + t + 1] = end;
+    if (logp) logp[(long)b * (L - 1) + t] = 0.f;
+  }
+}
+
 __global__ void split_f32_kernel(const float* src, long n, bf16_t* dst, long lo, int nsplit) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     store_planes(dst, i, lo, nsplit, src[i]);
@@ -447,6 +486,19 @@ hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows
 
 hipError_t launch_fill_u8(uint8_t* p, long n, uint8_t value, hipStream_t s) {
   hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, value);
+  return hipGetLastError();
+}
+
+hipError_t launch_stop_scan(const int32_t* ids, int B, long ld, int col0, int col1, int end, const uint8_t* fin,
+                            int* flag, hipStream_t s) {
+  if (col1 <= col0 || col1 - col0 > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(stop_scan_kernel, dim3(1), dim3(256), 0, s, ids, B, ld, col0, col1, end, fin, flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_stop_tail(int32_t* ids, int B, int L, int t0, int end, float* logp, hipStream_t s) {
+  if (t0 >= L - 1) return hipSuccess;
+  hipLaunchKernelGGL(stop_tail_kernel, dim3(grid_for((long)B * (L - 1 - t0))), dim3(256), 0, s, ids, B, L, t0, end, logp);
   return hipGetLastError();
 }
 

@@ -352,16 +352,43 @@ class Engine:
               "icap_decode_greedy")
         return ids, logits
 
-    def greedy(self, memory: torch.Tensor, start: int, end: int, max_len: int) -> torch.Tensor:
+    def greedy(self, memory: torch.Tensor, start: int, end: int, max_len: int, stop_early: bool = True,
+               chunk: int = 0) -> torch.Tensor:
         """Reference-identical greedy output (int64, stop rule applied).  With the f16 encoder, a direct Engine user
-        checks range_overflowed() after encode (the drop-in models do; CaptionPipeline(check_range=True) does)."""
-        ids, _ = self.greedy_raw(memory, start, end, max_len)
+        checks range_overflowed() after encode (the drop-in models do; CaptionPipeline(check_range=True) does).
+        stop_early (default): the decode itself ends as `_greedy_search` does (icap_decode_greedy_stop: chunks of
+        `chunk` steps, 0 = auto), so a batch that ends after k steps costs about k steps, not max_len - 1;
+        last_decode_steps then holds the steps executed.  The call returns after the decode's next-to-last chunk."""
+        if not stop_early:
+            ids, _ = self.greedy_raw(memory, start, end, max_len)
+            return apply_stop_rule(ids.long(), end)
+        ids, _ = self.greedy_stop_raw(memory, start, end, max_len, chunk=chunk)
         return apply_stop_rule(ids.long(), end)
 
+    def greedy_stop_raw(self, memory: torch.Tensor, start: int, end: int, max_len: int, chunk: int = 0,
+                        want_logits: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """Stop-aware greedy decode (icap_decode_greedy_stop): ids (B,max_len) int32 whose columns after the executed
+        steps are end, optional step logits (steps not executed: unwritten); last_decode_steps = steps executed."""
+        mem = memory.to(device=self.device, dtype=torch.float32).contiguous()
+        B, S = mem.shape[0], mem.shape[1]
+        ids = torch.empty(B, max_len, device=self.device, dtype=torch.int32)
+        logits = (torch.empty(max_len - 1, B, self.vocab, device=self.device, dtype=torch.float32)
+                  if want_logits else None)
+        steps = ctypes.c_int(0)
+        check(self.lib.icap_decode_greedy_stop(self.handle, mem.data_ptr(), B, S, max_len, int(start), int(end),
+                                               int(chunk), ids.data_ptr(), _lib.ptr(logits), ctypes.byref(steps),
+                                               stream_ptr(self.device)), "icap_decode_greedy_stop")
+        self.last_decode_steps = steps.value
+        return ids, logits
+
     def sample(self, memory: torch.Tensor, uniforms: torch.Tensor, start: int, end: int,
-               max_len: int, dropout: Optional[Tuple[float, int]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Sampled ids (B,max_len) int32 and per-step log-probs (B,max_len-1), no early stop.
-        dropout = (p, seed): train-mode sampling (icap_decode_sample_dropout)."""
+               max_len: int, dropout: Optional[Tuple[float, int]] = None,
+               stop_early: bool = False, chunk: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Sampled ids (B,max_len) int32 and per-step log-probs (B,max_len-1).
+        dropout = (p, seed): train-mode sampling (icap_decode_sample_dropout).  stop_early: the decode ends once every
+        row has emitted end, as the reference's loop (icap_decode_sample_stop; columns not computed: ids = end,
+        log-probs = 0; partially blocking - off by default, so a sampler and a greedy baseline on two streams
+        still overlap)."""
         mem = memory.to(device=self.device, dtype=torch.float32).contiguous()
         B, S = mem.shape[0], mem.shape[1]
         u = uniforms.to(device=self.device, dtype=torch.float32).contiguous()
@@ -369,6 +396,15 @@ class Engine:
             raise ValueError("uniforms must be (max_len-1, B)")
         ids = torch.empty(B, max_len, device=self.device, dtype=torch.int32)
         logp = torch.empty(B, max_len - 1, device=self.device, dtype=torch.float32)
+        if stop_early:
+            p, seed = dropout if dropout is not None else (0.0, 0)
+            steps = ctypes.c_int(0)
+            check(self.lib.icap_decode_sample_stop(self.handle, mem.data_ptr(), B, S, max_len, int(start), int(end),
+                                                   u.data_ptr(), float(p), int(seed) & 0xFFFFFFFF, int(chunk),
+                                                   ids.data_ptr(), logp.data_ptr(), ctypes.byref(steps),
+                                                   stream_ptr(self.device)), "icap_decode_sample_stop")
+            self.last_decode_steps = steps.value
+            return ids, logp
         if dropout is not None and dropout[0] > 0:
             check(self.lib.icap_decode_sample_dropout(self.handle, mem.data_ptr(), B, S, max_len, int(start),
                                                       int(end), u.data_ptr(), float(dropout[0]),

@@ -51,6 +51,8 @@ class CaptionPipeline:
             # its CU-masked pipelines form a stack on it (base budget first), so destroying them in any order leaves
             # the budget of the newest live one (or the base) in force
             budgets = engine.__dict__.setdefault("_cu_budgets", [("base", engine.encoder_cus)])
+            if len(budgets) == 1:  # no live CU-masked pipeline: the caller may have changed the budget since
+                budgets[0] = ("base", engine.encoder_cus)
             budgets.append((id(self), torch.cuda.get_device_properties(dev).multi_processor_count - int(decode_cus)))
             engine.set_encoder_cus(budgets[-1][1])
             self.dec_stream = torch.cuda.ExternalStream(ptrs[0], device=dev)

@@ -185,6 +185,25 @@ int icap_preprocess(const uint8_t* pixels, const int64_t* offsets, const int32_t
 int icap_decode_greedy(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
                        int end_token, int32_t* ids, float* step_logits, void* stream);
 
+/* Stop-aware greedy decode (round 6): the same decode, ending as the reference's loop does - after the first step at
+ * which every latest token == end (models/vit_transformer_model.py:321-323, grid:248-249) - instead of running all
+ * max_len-1 steps.  The steps run as captured graphs of chunk_steps steps (<= 0: 4 for B <= 64, else 8) that end in
+ * a stop test; the host checks chunk c-2's test before launching chunk c, so at most one chunk past the stop runs
+ * and the call returns once the second-to-last launched chunk has finished (a partially blocking call).  ids columns
+ * after the executed steps are end (the stop rule's result is the reference's sequence); step_logits of steps not
+ * executed are left untouched.  steps_executed (host int, optional) = decode steps run.
+ * Replaces: _greedy_search's early break (vit:321-323) for the drop-in generate (scripts/inference_vit_transformer.py
+ * :88,108-114 calls it per image with max_len 50). */
+int icap_decode_greedy_stop(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                            int end_token, int chunk_steps, int32_t* ids, float* step_logits, int* steps_executed,
+                            void* stream);
+/* The sampled decode with the reference's stop (break once every row has emitted end, scst_loss.py:246-249), in the
+ * chunked form above; p > 0: train-mode dropout (as icap_decode_sample_dropout); log-probs of steps not executed are 0.
+ * Replaces: SCSTLoss._sample_with_log_probs's early break (utils/scst_loss.py:246-249). */
+int icap_decode_sample_stop(icap_handle* h, const float* memory, int B, int S, int max_len, int start_token,
+                            int end_token, const float* uniforms, float p, uint32_t seed, int chunk_steps, int32_t* ids,
+                            float* logp, int* steps_executed, void* stream);
+
 /* Batched beam search, beam_size K in [1, 15]: every image runs the reference's per-image beam
  * search (log-softmax scores, top-K over beam x vocab, finished beams collected and pruned so the
  * live beam count shrinks); grid_variant != 0 selects the Grid model's stop tests (completed >= live

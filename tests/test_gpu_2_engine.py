@@ -91,6 +91,42 @@ def test_pipeline_matches_sequential(cuda, vit_sd, B):
         assert torch.equal(a.cpu(), apply_stop_rule(b.long(), 108))
 
 
+def test_cu_masked_pipelines_budget_stack(cuda, vit_sd):
+    """CU-masked pipelines (decode_cus) size the engine's encoder grids (GEMMs and, round 6, the persistent encoder
+    attention) to the encoder stream's CUs; two overlapping pipelines deleted in either order leave the newest live
+    budget, then the base - and a base the caller changed between pipelines is the one restored.  The
+    masked pipeline's ids equal the sequential encode + greedy."""
+    import gc
+
+    from image_caption_amd.engine import Engine
+    from image_caption_amd.pipeline import CaptionPipeline
+
+    eng = Engine(vit_sd, "vit", {}, device=cuda)
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    for first_deleted in (0, 1):
+        assert eng.encoder_cus == 0
+        ps = [CaptionPipeline(eng, 107, 108, 30, decode_cus=32), CaptionPipeline(eng, 107, 108, 30, decode_cus=64)]
+        assert eng.encoder_cus == cus - 64
+        del ps[first_deleted]
+        gc.collect()
+        assert eng.encoder_cus == (cus - 64 if first_deleted == 0 else cus - 32)
+        del ps[0]
+        gc.collect()
+        assert eng.encoder_cus == 0
+    eng.set_encoder_cus(cus - 8)  # the caller's own budget, set while no masked pipeline is alive
+    p = CaptionPipeline(eng, 107, 108, 30, decode_cus=48)
+    assert eng.encoder_cus == cus - 48
+    batches = [torch.from_numpy(W.synthetic_images(8, seed=s)).to(cuda) for s in (21, 22)]
+    got = p.run(batches)
+    torch.cuda.synchronize()
+    del p
+    gc.collect()
+    assert eng.encoder_cus == cus - 8
+    eng.set_encoder_cus(0)
+    for a, b in zip(got, batches):
+        assert torch.equal(a.cpu(), eng.greedy_raw(eng.encode(b), 107, 108, 30)[0].cpu())
+
+
 def _tools_only():
     from image_caption_amd import _lib
 

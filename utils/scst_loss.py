@@ -167,7 +167,9 @@ class SCSTLoss(nn.Module):
                         mem, vfeats = eng.encode_vit_features(images)
                 else:  # ViT, or a Grid model whose trunk is in eval mode: the whole encoder on HIP
                     eng, mem = model.checked_encode(images)  # f16 range guard: bf16x2 re-encode on overflow
-                ids32, logp = eng.sample(mem, uniforms, start_token, end_token, max_len, dropout=drop)
+                # stop_early: the decode ends once every row has emitted <end>, as the reference's loop breaks
+                # (:246-249) - a trained model's samples end long before max_len
+                ids32, logp = eng.sample(mem, uniforms, start_token, end_token, max_len, dropout=drop, stop_early=True)
             ids = ids32.long()
             L = sample_stop_length(ids, end_token)
             ids, logp = ids[:, :L], logp[:, : L - 1]
