@@ -161,7 +161,8 @@ def main():
     ap.add_argument("--beam", type=int, default=5, help="beam width of --mode beam")
     ap.add_argument("--fp32-weights", action="store_true",
                     help="weights NOT rounded to bf16 (a real fp32 checkpoint): the engine packs the decoder's GEMM weights "
-                         "as hi/lo bf16 pairs and decodes with the unfused launches (config.dec_weight_planes = 2)")
+                         "as hi/lo bf16 pairs, which the fused decode blocks carry as lo fragment images "
+                         "(config.dec_weight_planes = 2)")
     ap.add_argument("--pipeline", action="store_true",
                     help="greedy: overlap the encode of step i+1 with the decode of step i on two streams "
                          "(image_caption_amd/pipeline.py; measured +2-4 %% with ICAP_DEC_BRANCHES=1, within noise "
@@ -400,8 +401,8 @@ def main():
                        "decode_steps": L - 1, "output_len": int(out.shape[1]) if args.mode == "greedy" else None,
                        "parallelism": f"dp{ws}",
                        "pipelined": pipe is not None,
-                       # 1: bf16-exact decoder weights (the seeded synthetic weights), fused decode blocks; 2: hi/lo pairs
-                       # (--fp32-weights, a real fp32 checkpoint), unfused decode launches
+                       # 1: bf16-exact decoder weights (the seeded synthetic weights); 2: hi/lo pairs (--fp32-weights, a
+                       # real fp32 checkpoint) - both through the fused decode blocks (round 5)
                        "dec_weight_planes": eng.dec_weight_planes},
             "roofline": roof, "cpu_baseline": cpu,
         }

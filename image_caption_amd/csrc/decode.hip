@@ -634,6 +634,10 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
   if constexpr (FOLD) fold_issue<FOLD>(p.fold, row0, p.rows, smem + FOLD_PRM, fi);
   else dma_x(p.A, p.aL, ns, row0, p.rows, sx);
   constexpr int NW1 = DEC_K64, NW2 = 8;  // fragments per wave (the opening's vmcnt counts them)
+  // the counted waits below, by what this wave issues after dma_x, in order (no other VMEM operation may go between):
+  // load_frags<NW1> (W1), WLO: NW1 lds_dma16 (W1 lo slot), load_frags<NW2> (W2)
+  constexpr int YNG_X = NW1 + (WLO ? NW1 : 0) + NW2;  // younger than the X image at the opening
+  constexpr int YNG_LO = NW2;                         // younger than the W1 lo slot (WLO's first FFN-1 wait)
   bf16x8 w1f[FR ? NW1 : 1], w2f[FR ? NW2 : 1];
   const long w1i = (long)(j * 8 + t) * 2 * DEC_K64 + kh * DEC_K64, w2i = (long)(j * 32 + 2 * wave) * 4;
   char* const lo1 = smem + 32 * 1024 + wave * NW1 * 1024;  // WLO: this wave's W1 lo fragments (its own slot)
@@ -655,14 +659,15 @@ __global__ __launch_bounds__(1024) void dec_ffn_kernel(DecFfnArgs p) {
     load_frags<NW2>(w2f, p.W2f, (long)(j * 32 + 2 * wave) * 4);
     lds_barrier();  // the X image written
   } else if (FR && NSC == 2) {
-    open_x<NW1 + NW2 + (WLO ? NW1 : 0)>();  // X landed; W1 / W1 lo / W2 fragments may still fly
+    open_x<YNG_X>();  // X landed; W1 / W1 lo / W2 fragments may still fly
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (WLO) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW2) : "memory");  // this wave's W1 lo slot landed (W2 may fly)
+    static_assert(!WLO || YNG_LO == NW2, "W2 fragments are the only loads after the W1 lo slot");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(YNG_LO) : "memory");  // this wave's W1 lo slot landed (W2 may fly)
     const bf16x8* l1 = (const bf16x8*)lo1 + lane;
     acc = mma_frag<4>(acc, w1f, sx + kh * 4 * ns * 2048, ns, [&](int i) { return l1[i * 64]; });
   } else if (FR) {

@@ -195,6 +195,7 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
 #ifndef ICAP_F16H
 #define ICAP_F16H 0
 #endif
+#if ICAP_F16H  // (a product build without the form compiles none of its kernels)
 // the f16h form's 32-bit offsets: A / W stage pieces (rows up to a whole tile past M) and the epilogue's byte range
 bool f16h_ok(const GemmArgs& g) {
   const bool res = g.out == OUT_F32_RESID;
@@ -228,6 +229,7 @@ hipError_t launch_f16h(const GemmArgs& g, hipStream_t s, int blocks) {
   }
   return hipGetLastError();
 }
+#endif
 
 }  // namespace
 
@@ -868,7 +870,9 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       // form (QKV 305 -> 265 us, MLP-1 423 -> 342 us at B = 256, tools/f16_forms_r2.sh); the residual GEMMs on
       // 224-row tiles (678 tiles = 2.65 per CU at N = 768 instead of 591 = 2.3)
       const int blocks = g.max_grid > 0 ? std::min(g.max_grid, cus) : cus;
-      if (ICAP_F16H && f16h_ok(g)) return launch_f16h(g, s, blocks);
+#if ICAP_F16H
+      if (f16h_ok(g)) return launch_f16h(g, s, blocks);
+#endif
       if (g.out == OUT_F32_RESID) {
         const int tiles224 = (g.N / 256) * ((g.M + 223) / 224);
         hipLaunchKernelGGL((gemm_f16p_kernel<2, 0, 224>), dim3(std::min(tiles224, blocks)), dim3(512),

@@ -89,7 +89,9 @@ typedef struct {
   const icap_conv_bn_w* trunk;
   /* decoder GEMM weight planes: 0 or 1 = bf16 (exact for bf16-representable weights), 2 = bf16 hi/lo
    * (hi = bf16(W), lo = bf16(W - hi): 16 significand bits, for fp32 checkpoints whose weights are not
-   * bf16-exact; the decode then runs the unfused launches, each GEMM adding W_lo . X_hi - DESIGN.md §3) */
+   * bf16-exact; every decoder product adds W_lo . X_hi - since round 5 inside the fused decode blocks too, whose
+   * fragment images then carry the lo planes; the teacher-forced / padded forms and the bf16 mode keep the unfused
+   * GEMMs - DESIGN.md §3) */
   int dec_weight_planes;
   /* rows of enc_pe (the Grid encoder's PositionalEncoding table, max_len 100 in grid:74); 0 = grid_tokens */
   int enc_pe_len;
@@ -283,8 +285,10 @@ int icap_set_decode_chains(icap_handle* h, int chains);
  * graph are not event-bracketed; bench.py times the decode phase as a whole instead). */
 #define ICAP_PROF_GEMM_128 0   /* gemm_bf16_kernel<128,128,64,64>: trunk convolutions of that tile class  */
 #define ICAP_PROF_GEMM_64 1    /* gemm_bf16_kernel<64,64,32,32>: small GEMMs (trunk layer1, N <= 128)    */
-#define ICAP_PROF_ENC_ATTN 2   /* enc_attention_pipe_kernel / enc_attention_kernel (encoder self-attention) */
-#define ICAP_PROF_CROSS_ATTN 3 /* cross_attn_mfma_kernel (decoder cross-attention)                         */
+#define ICAP_PROF_ENC_ATTN 2   /* encoder self-attention: enc_attention_pers_kernel (f16, N <= 240) /
+                                  enc_attention_full_kernel / enc_attention_pipe_kernel / enc_attention_kernel */
+#define ICAP_PROF_CROSS_ATTN 3 /* decoder cross-attention: cross_attn_f16_kernel (f16 memory plane) /
+                                  cross_attn_mfma_kernel (bf16 planes)                                     */
 #define ICAP_PROF_GEMM_WAVE 4  /* gemm_dec_kernel / chain_dec_kernel (decode-step GEMMs)                   */
 #define ICAP_PROF_GEMM_256 5   /* gemm_256_kernel: encoder GEMMs (128x256 or 256x256 tiles; fp16 residual ones) */
 #define ICAP_PROF_GEMM_I8 6    /* gemm_i8_kernel: int8 two-slice encoder GEMMs (ICAP_PREC_I8X2)            */

@@ -95,6 +95,30 @@ def test_fp32_weights_not_bf16_exact(cuda):
                                                                    ref[0].numpy()), i
 
 
+@pytest.mark.parametrize("B", [5, 37])
+def test_fp32_weights_fused_blocks_ragged_rows(cuda, B):
+    """The hi/lo (fp32-checkpoint) forms of the fused decode blocks (dec_sa / dec_chain / dec_ffn with lo fragment
+    images and counted waits, decode.hip) at batches that are not a multiple of their 16-row tiles: every KV-cached
+    greedy step's logits against the unfused teacher-forced decoder (separate hi/lo GEMMs) on the same prefix, and
+    the oracle's greedy ids."""
+    from image_caption_amd.engine import Engine
+
+    sd = W.to_torch(W.vit_state_dict(1, bf16_exact=False))
+    eng = Engine(sd, "vit", {}, device=cuda)
+    assert eng.dec_weight_planes == 2
+    mem = torch.from_numpy(np.random.Generator(np.random.PCG64(B)).standard_normal((B, 196, 512)).astype(np.float32))
+    L = 16
+    for _ in range(3):  # eager, capture, replay
+        ids, lg = eng.greedy_raw(mem.to(cuda), W.START_TOKEN, W.END_TOKEN, L, want_logits=True)
+    ids = ids.cpu().long()
+    tf = eng.decoder_forward(ids[:, :-1].to(cuda), mem.to(cuda), causal=True).cpu()  # (B, L-1, V), unfused
+    err = (lg.cpu().permute(1, 0, 2) - tf).abs().max().item()
+    ref_tf = O.teacher_forced_logits(sd, mem, ids)
+    rerr = (lg.cpu().permute(1, 0, 2) - ref_tf).abs().max().item()
+    print(f"B={B} hi/lo fused vs unfused {err:.2e}, vs fp32 oracle {rerr:.2e}")
+    assert err < 2e-4 and rerr < 1e-3
+
+
 @pytest.mark.parametrize("grid_variant", [False, True])
 def test_beam_search_large_vocabulary(cuda, grid_variant):
     """Beam search with V = 1000 (above the 512 the k x V LDS candidate array holds): beam_select takes each live
