@@ -849,7 +849,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     for (const void* f : {(const void*)gemm_f16p_kernel<1>, (const void*)gemm_f16p_kernel<2>})
-      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 64 * 1024 + 2048);
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, F16P_LDS_SO);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)gemm_f16p_kernel<2, 0, 224>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               2 * (224 * 128 + 256 * 128) + 2048);
@@ -879,7 +879,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
                            2 * (224 * 128 + 256 * 128) + 2048, s, g);
       } else {
         const int tiles = (g.N / 256) * ((g.M + 255) / 256);
-        hipLaunchKernelGGL(gemm_f16p_kernel<1>, dim3(std::min(tiles, blocks)), dim3(512), 2 * 64 * 1024 + 2048, s, g);
+        hipLaunchKernelGGL(gemm_f16p_kernel<1>, dim3(std::min(tiles, blocks)), dim3(512), F16P_LDS_SO, s, g);
       }
       return hipGetLastError();
     }

@@ -582,6 +582,16 @@ void gemm_256_kernel(GemmArgs p) {
 #endif
 __device__ __forceinline__ int swz_chunk(int c, int r) { return ICAP_SWZ ? c ^ (((r >> 1) & 1) << 2) : c ^ (r & 7); }
 
+// The LayerNorm fold of the f16 ViT encoder (GemmArgs::xh / ln_*; rows.hip launch_ln_fold_*), measured and rejected in
+// round 6 (its residual epilogue's fp16 copy of x and the store-only epilogue's row affine cost
+// more than the LayerNorm passes they remove); compiled into variant builds only (-DICAP_LN_FOLD=1 for gemm.hip and
+// icap.cpp)
+#ifndef ICAP_LN_FOLD
+#define ICAP_LN_FOLD 0
+#endif
+// dynamic LDS of gemm_f16p_kernel<1> (and <2> at 256 rows): 2 stages of 64 KiB, then the bias slots (2 x 1 KiB) and the
+// LayerNorm fold's column-sum slots (2 x 1 KiB) and row (a, b) slots (2 x 2 KiB)
+constexpr int F16P_LDS_SO = 2 * 64 * 1024 + (ICAP_LN_FOLD ? 8192 : 2048);
 // stage pieces wave w of gemm_f16p_kernel issues per stage: its A rows (8 per piece, up to the tile's BM rows) + IPW W
 constexpr int f16p_stage_pieces(int BM, int IPW, int w) {
   const int a = (BM - w * IPW * 8) / 8;
@@ -701,10 +711,24 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   // before the tile's first stage (so the counted waits below never count it) - no registers held across
   // the k-loop (the kernel is at the 256-register limit of two waves per SIMD)
   float* sbias = (float*)(smem + 2 * STAGE);
+  // LayerNorm fold (SO with p.ln_ab, kernels.h): per tile also the 256 column sums s_n (slot after the bias slots, wave
+  // 1) and the tile's 256 rows' (a, b) (wave 2: rows 0-127, wave 3: 128-255) - older than the tile's stage 0 like the
+  // bias, so no counted wait moves
+  const bool lnf = ICAP_LN_FOLD && SO && p.ln_ab != nullptr;
+  float* ssum = sbias + 2 * 256;
+  float2* sab = (float2*)(sbias + 4 * 256);
+  // (buffer-load DMAs: one per-lane 32-bit offset shared by the three sources, the tile's offset in an SGPR - 64-bit
+  // per-lane addresses held across the k-loop spilled)
+  const i32x4r rsb = buf_rsrc(p.bias, (uint32_t)p.N * 4), rss = buf_rsrc(p.ln_sum, (uint32_t)p.N * 4);
+  const i32x4r rsab = buf_rsrc(p.ln_ab, (uint32_t)(M + 256) * 8);  // (padded by a tile past M: ragged bands in bounds)
   auto load_bias = [&](int t, int slot) {
-    if (wave == 0 && p.bias) {
-      const int n0 = (t - (t / nbn) * nbn) * BN;
-      lds_dma16(p.bias + n0 + lane * 4, (LDS_AS void*)(sbias + slot * 256));
+    const int bm = t / nbn, n0 = (t - bm * nbn) * BN;
+    if (wave == 0 && p.bias) lds_dma_buf16(rsb, (uint32_t)lane * 16, (uint32_t)n0 * 4, (LDS_AS void*)(sbias + slot * 256));
+    if (lnf && wave >= 1 && wave <= 3) {
+      if (wave == 1) lds_dma_buf16(rss, (uint32_t)lane * 16, (uint32_t)n0 * 4, (LDS_AS void*)(ssum + slot * 256));
+      else
+        lds_dma_buf16(rsab, (uint32_t)lane * 16, (uint32_t)(bm * BM + (wave - 2) * 128) * 8,
+                      (LDS_AS void*)(sab + slot * 256 + (wave - 2) * 128));
     }
   };
 
@@ -902,6 +926,8 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         bj[j] = p.bias ? *(const f32x4*)(sbias + (tcount & 1) * 256 + wn * WN + j * 16 + 4 * fq) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      const float* sl = ssum + (tcount & 1) * 256 + wn * WN + 4 * fq;  // (the column sums: read per row tile, no registers
+                                                                      // held across the epilogue)
       const bool gelu = p.epi == EPI_GELU, hm_step = p.hm_n >= 16;
       int hq = 0, hr = 0;  // (row / hm_n, row % hm_n) of row tile i's row (hm_step)
       if (hm_step) {
@@ -930,6 +956,16 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
           orow = (long)min(mr, M - 1) * p.ldc;
         }
         bf16_t* C = (bf16_t*)p.C + orow + 4 * fq;
+        if (lnf) {  // LN fold: acc a_r - b_r s_n (+ the bias below)
+          const float2 ab = sab[(tcount & 1) * 256 + wm * WM + i * 16 + fr];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            f32x4 sv = *(const f32x4*)(sl + j * 16);
+            asm volatile("" : "+v"(sv));  // (read here, not hoisted over the epilogue)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaf(acc[i][j][e], ab.x, -ab.y * sv[e]);
+          }
+        }
         u32x2 pk[TN];
         if (gelu) {
           static_assert(TN % 2 == 0, "GELU in column-group pairs");
@@ -998,13 +1034,35 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         for (int i = 0; i < 4; ++i) {
           if (h2 * 4 + i >= TM) break;
           const int m = mb + (h2 * 4 + i) * 16 + fr;
-          if (tail && m >= M) continue;
+          f32x4 o[TN];
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             f32x4 a = acc[h2 * 4 + i][j];
             if (p.bias) a += *(const f32x4*)(bl + j * 16);
-            *(f32x4*)(Cb + (long)m * p.ldc + j * 16) = rv[i][j] + a;
+            o[j] = rv[i][j] + a;
           }
+          if (ICAP_LN_FOLD && p.xh) {
+            // LN fold: the new row's fp16 copy and this 64-column group's (mean, M2) - the 4 lanes fr + 16 q hold the
+            // group's 64 values of row m (rows >= M: clamped loads, nothing stored)
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) sm += (o[j][0] + o[j][1]) + (o[j][2] + o[j][3]);
+            const float mg = rows4_sum(sm) * (1.0f / 64.0f);
+            float m2 = 0.f;
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) m2 = fmaf(o[j][e] - mg, o[j][e] - mg, m2);
+            m2 = rows4_sum(m2);
+            if (!tail || m < M) {
+#pragma unroll
+              for (int j = 0; j < TN; ++j) *(u32x2*)(p.xh + (long)m * p.ldc + nb + j * 16 + 4 * fq) = pack16x4<true>(o[j]);
+              if (fq == 0) *(float2*)(p.ln_part + 2 * ((long)(nb / 64) * M + m)) = make_float2(mg, m2);
+            }
+          }
+          if (tail && m >= M) continue;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) *(f32x4*)(Cb + (long)m * p.ldc + j * 16) = o[j];
         }
       }
       if (tn >= 0) {  // stage 1 of the next tile into the last stage's buffer, after the stores

@@ -75,6 +75,97 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   if (range_flag && __any(bad) && lane == 0) range_flag_set(range_flag);
 }
 
+// ---- LayerNorm fold of the f16 ViT encoder (round 6) ----
+// LN(x) W^T + b = rstd (x W'^T) - rstd mu s + c with W' = W diag(gamma), s_n = sum_k W'_nk, c = W beta + b: the GEMM
+// reads the residual stream's fp16 copy xh and applies the row's (a, b) = (rstd, rstd mu) in its epilogue, so the
+// pre-LayerNorms run no pass of their own.
+
+// Weights: W' = fp16(W gamma) [N][K], s = row sums of the fp16 W' values (what the GEMM multiplies), c = W beta + b;
+// one 256-thread block per row n, fixed-order sums
+__global__ __launch_bounds__(256) void ln_fold_weights_kernel(const float* __restrict__ W, const float* __restrict__ b,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, int K, bf16_t* wp,
+                                                              float* c, float* sum) {
+  __shared__ float red[2][4];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float ss = 0.f, cc = 0.f;
+  for (int k = tid; k < K; k += 256) {
+    const float w = W[(long)n * K + k];
+    const bf16_t h = f2h(w * gamma[k]);
+    wp[(long)n * K + k] = h;
+    ss += h2f(h);
+    cc += w * beta[k];
+  }
+  ss = wave_sum(ss);
+  cc = wave_sum(cc);
+  if (lane == 0) red[0][wave] = ss, red[1][wave] = cc;
+  __syncthreads();
+  if (tid == 0) {
+    sum[n] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    c[n] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]) + (b ? b[n] : 0.f);
+  }
+}
+
+// A row's normalisation from G equal groups of D / G columns: mean_g and M2_g = sum (x - mean_g)^2 per group
+// (Chan et al.'s pairwise combination: no E[x^2] - mu^2 cancellation); out (a, b) = (rstd, rstd mu) as the
+// layernorm_kernel computes them (biased variance, 1 / sqrtf(var + eps))
+__device__ __forceinline__ float2 ln_fold_ab(const float2* grp, int G, int D, float eps) {
+  float mu = 0.f;
+  for (int g = 0; g < G; ++g) mu += grp[g].x;
+  mu /= (float)G;
+  float m2 = 0.f;
+  const float per = (float)(D / G);
+  for (int g = 0; g < G; ++g) {
+    const float d = grp[g].x - mu;
+    m2 += grp[g].y + per * d * d;
+  }
+  const float rstd = 1.0f / sqrtf(m2 / (float)D + eps);
+  return make_float2(rstd, rstd * mu);
+}
+
+// The residual GEMMs' epilogues leave per (row, 64-column group) (mean_g, M2_g) in part[g][rows]; one thread per row
+__global__ __launch_bounds__(256) void ln_fold_stats_kernel(const float2* __restrict__ part, int G, int rows, int D,
+                                                            float eps, float2* ab) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  float2 grp[16];
+  for (int g = 0; g < G; ++g) grp[g] = part[(long)g * rows + r];
+  ab[r] = ln_fold_ab(grp, G, D, eps);
+}
+
+// Layer 0's input (the patch embedding + class token + position rows): the fp16 copy xh and (a, b) directly, one
+// wave per row (layernorm_kernel's statistics); xh values that overflow fp16 set the range word
+template <int PER>
+__global__ __launch_bounds__(256) void ln_fold_rows_kernel(const float* __restrict__ x, int rows, float eps,
+                                                           bf16_t* xh, float2* ab, unsigned* range_flag) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = PER * 64;
+  const float* xr = x + (long)row * D;
+  float v[PER];
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < PER / 4; ++c) {
+    const f32x4 t = *(const f32x4*)(xr + c * 256 + lane * 4);
+    v[c * 4 + 0] = t[0]; v[c * 4 + 1] = t[1]; v[c * 4 + 2] = t[2]; v[c * 4 + 3] = t[3];
+    const u32x2 pk = pack16x4<true>(t);
+    bad |= f16_pair_nonfinite(pk[0]) || f16_pair_nonfinite(pk[1]);
+    *(u32x2*)(xh + (long)row * D + c * 256 + lane * 4) = pk;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) s += v[i];
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { const float d = v[i] - mean; q += d * d; }
+  const float var = wave_sum(q) / (float)D;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  if (lane == 0) ab[row] = make_float2(rstd, rstd * mean);
+  if (range_flag && __any(bad) && lane == 0) range_flag_set(range_flag);
+}
+
 // layernorm_kernel's row statistics, output as int8 two-slice planes + the row scale (one wave per row)
 template <int PER>
 __global__ __launch_bounds__(256) void layernorm_i8_kernel(const float* __restrict__ x, long ldx, int rows,
@@ -486,6 +577,28 @@ hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows
 
 hipError_t launch_fill_u8(uint8_t* p, long n, uint8_t value, hipStream_t s) {
   hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, value);
+  return hipGetLastError();
+}
+
+hipError_t launch_ln_fold_weights(const float* W, const float* b, const float* gamma, const float* beta, int N, int K,
+                                  bf16_t* wp, float* c, float* sum, hipStream_t s) {
+  if (!W || !gamma || !beta || N <= 0 || K <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_fold_weights_kernel, dim3(N), dim3(256), 0, s, W, b, gamma, beta, K, wp, c, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_ln_fold_stats(const float* part, int G, int rows, int D, float eps, float* ab, hipStream_t s) {
+  if (G <= 0 || G > 16 || D % G || rows <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_fold_stats_kernel, dim3((rows + 255) / 256), dim3(256), 0, s, (const float2*)part, G, rows, D,
+                     eps, (float2*)ab);
+  return hipGetLastError();
+}
+
+hipError_t launch_ln_fold_rows(const float* x, int rows, int D, float eps, bf16_t* xh, float* ab, unsigned* range_flag,
+                               hipStream_t s) {
+  if (D != 768 || rows <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_fold_rows_kernel<12>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, eps, xh, (float2*)ab,
+                     range_flag);
   return hipGetLastError();
 }
 

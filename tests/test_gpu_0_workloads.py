@@ -150,6 +150,42 @@ def test_config2_vit_b256_fp32_weights_every_row(cuda):
     assert (tf - lg.permute(1, 0, 2)).abs().max().item() < 1e-3
 
 
+def test_config2_fp32_weights_outlier_channels(cuda):
+    """Real ViT-B/16 checkpoints carry residual channels far above the rest; the synthetic draws do not.  Config 2 on
+    fp32 (not bf16-exact) weights whose MLP-2 rows and biases of 4 residual channels are scaled x20 in layers 2-11: the
+    default f16 encoder must keep every step's logits within 1e-3 of the fp32 oracle, and the error is the encoder's
+    (HIP memory -> oracle decoder carries it; oracle memory -> HIP decoder stays ~1e-4).  Measured (round 6,
+    tools/r6_precision.py): memory error 7.1e-3 against 2.4e-3 without outliers, logits 8.2e-4 (7.9e-4), decoder share
+    7.9e-5; the bf16x2 encoder is NOT the more precise choice for such weights (its bf16 weights: logits 6.2e-3), so the
+    drop-in keeps f16 (its fp16 range guard re-encodes only on overflow, which these weights do not reach)."""
+    from image_caption_amd.engine import Engine
+
+    B, CH = 256, [7, 200, 411, 650]
+    sd = W.to_torch(W.vit_state_dict(3, bf16_exact=False))
+    for i in range(2, 12):
+        p = f"encoder.vit.encoder.layers.encoder_layer_{i}.mlp.3"
+        sd[p + ".weight"][CH] *= 20.0
+        sd[p + ".bias"][CH] *= 20.0
+    eng = Engine(sd, "vit", {}, device=cuda)
+    sdd = _dev_sd(sd, cuda)
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=7)).to(cuda)
+    mem = eng.encode(imgs)
+    assert not eng.range_overflowed()
+    ids, lg = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L, want_logits=True)
+    ids = ids.long()
+    mem_o = _oracle_memory(O.vit_encode, sdd, imgs)
+    with torch.no_grad():
+        ref = torch.cat([O.teacher_forced_logits(sdd, mem_o[i:i + 64], ids[i:i + 64]) for i in range(0, B, 64)])
+        enc = torch.cat([O.teacher_forced_logits(sdd, mem[i:i + 64], ids[i:i + 64]) for i in range(0, B, 64)])
+    full = (lg.permute(1, 0, 2) - ref).abs().max().item()
+    dec = (eng.decoder_forward(ids[:, :-1], mem_o, causal=True) - ref).abs().max().item()
+    enc_share = (enc - ref).abs().max().item()
+    merr = (mem - mem_o).abs().max().item()
+    print(f"\n[config2 fp32 + outliers] memory err {merr:.2e}, logits {full:.2e} (encoder share {enc_share:.2e}, "
+          f"decoder share {dec:.2e})")
+    assert full < 1e-3 and dec < 2e-4 and merr < 1.5e-2
+
+
 def test_config3_grid_b256_trunk_and_every_row(cuda, grid_sd):
     from image_caption_amd.engine import Engine
 

@@ -6,7 +6,7 @@
 # run first on LIB1 (the tree's own build, image_caption_amd/libicap.so, unless named)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r5; mkdir -p $O
+O=gpurun_out/${ROUND:-r5}; mkdir -p $O
 T=$1; R=$2; shift 2
 if [ -n "$TESTS" ]; then
   timeout -k 10 400 python -u -m pytest $TESTS -m gpu -x -q --timeout 120 --timeout-method thread > $O/${T}_tests.log 2>&1 || { tail -40 $O/${T}_tests.log; exit 1; }
