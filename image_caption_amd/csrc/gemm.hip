@@ -200,6 +200,9 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
 bool f16h_ok(const GemmArgs& g) {
   const bool res = g.out == OUT_F32_RESID;
   const long cbytes = (!res && g.hm_n) ? (long)g.M * g.N * 2 : (long)g.M * g.ldc * (res ? 4 : 2);
+  // ICAP_F16H 2: the long-K residual GEMMs only (ViT MLP-2, K = 3072: 272-273 against 278-281 us on two boxes,
+  // profiles/r06/f16h_spread_ab.txt; the other shapes within +-3 %)
+  if (ICAP_F16H == 2 && !(res && g.K >= 2048)) return false;
   return g.bias && (!g.hm_n || g.hm_n >= 16) && cbytes < (1L << 32) && (long)(g.M + 256) * g.lda * 2 < (1L << 32) &&
          (long)g.N * g.ldw * 2 < (1L << 32);
 }
