@@ -1021,6 +1021,13 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       float* Cb = (float*)p.C + nb + 4 * fq;
       const float* bl = sbias + (tcount & 1) * 256 + wn * WN + 4 * fq;
       const bool tail = bm * BM + BM > M;  // ragged last row band: rows >= M neither read nor stored
+      // LN fold (variant builds): the residual stream as two fp16 planes, hi at xh and lo = fp16(x - hi) at xh + c_lo
+      // (the same 4 bytes per element as fp32; the hi plane is the store-only GEMMs' A operand)
+      const bool hl = ICAP_LN_FOLD && p.xh != nullptr;
+      auto unpack4 = [](u32x2 v) -> f32x4 {
+        return (f32x4){h2f((bf16_t)(v[0] & 0xffff)), h2f((bf16_t)(v[0] >> 16)), h2f((bf16_t)(v[1] & 0xffff)),
+                       h2f((bf16_t)(v[1] >> 16))};
+      };
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {  // row tiles [4 h2, min(TM, 4 h2 + 4))
         f32x4 rv[4][TN];
@@ -1028,8 +1035,15 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            if (h2 * 4 + i < TM)
-              rv[i][j] = *(const f32x4*)(Cb + (long)min(mb + (h2 * 4 + i) * 16 + fr, M - 1) * p.ldc + j * 16);
+            if (h2 * 4 + i < TM) {
+              const long row = min(mb + (h2 * 4 + i) * 16 + fr, M - 1);
+              if (hl) {
+                const bf16_t* hp = p.xh + row * p.ldc + nb + j * 16 + 4 * fq;
+                rv[i][j] = unpack4(*(const u32x2*)hp) + unpack4(*(const u32x2*)(hp + p.c_lo));
+              } else {
+                rv[i][j] = *(const f32x4*)(Cb + row * p.ldc + j * 16);
+              }
+            }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           if (h2 * 4 + i >= TM) break;
@@ -1041,9 +1055,9 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
             if (p.bias) a += *(const f32x4*)(bl + j * 16);
             o[j] = rv[i][j] + a;
           }
-          if (ICAP_LN_FOLD && p.xh) {
-            // LN fold: the new row's fp16 copy and this 64-column group's (mean, M2) - the 4 lanes fr + 16 q hold the
-            // group's 64 values of row m (rows >= M: clamped loads, nothing stored)
+          if (hl) {
+            // LN fold: the new row as hi / lo planes and this 64-column group's (mean, M2) - the 4 lanes fr + 16 q hold
+            // the group's 64 values of row m (rows >= M: clamped loads, nothing stored)
             float sm = 0.f;
 #pragma unroll
             for (int j = 0; j < TN; ++j) sm += (o[j][0] + o[j][1]) + (o[j][2] + o[j][3]);
@@ -1056,9 +1070,15 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
             m2 = rows4_sum(m2);
             if (!tail || m < M) {
 #pragma unroll
-              for (int j = 0; j < TN; ++j) *(u32x2*)(p.xh + (long)m * p.ldc + nb + j * 16 + 4 * fq) = pack16x4<true>(o[j]);
+              for (int j = 0; j < TN; ++j) {
+                bf16_t* hp = p.xh + (long)m * p.ldc + nb + j * 16 + 4 * fq;
+                const u32x2 hi = pack16x4<true>(o[j]);
+                *(u32x2*)hp = hi;
+                *(u32x2*)(hp + p.c_lo) = pack16x4<true>(o[j] - unpack4(hi));
+              }
               if (fq == 0) *(float2*)(p.ln_part + 2 * ((long)(nb / 64) * M + m)) = make_float2(mg, m2);
             }
+            continue;
           }
           if (tail && m >= M) continue;
 #pragma unroll

@@ -470,6 +470,7 @@ struct icap_handle {
     g.range_flag = range_word();
     g.max_grid = enc_cus;
     g.ln_ab = ab; g.ln_sum = sum; g.xh = xh; g.ln_part = part;
+    if (xh) g.c_lo = (long)M * ldc;  // the residual stream's lo plane (fold: C itself is not read or written)
     REQUIRE(gemm_f16_persistent(g), "LayerNorm fold: the persistent fp16 GEMM form only");
     run_gemm(g, s);
   }
@@ -734,12 +735,13 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
     // directly; every residual GEMM then leaves the next xh and its 12 group partials, turned into (a, b) by one small
     // pass (ln_fold_stats_kernel) - no LayerNorm pass per sub-layer
     const int G = V / 64;
-    h->e_xh.ensure((size_t)M * V * 2);
+    h->e_xh.ensure((size_t)M * V * 2 * 2);  // the residual stream's hi and lo fp16 planes
     h->e_lnp.ensure((size_t)G * M * 8);
     h->e_ab.ensure((size_t)(M + 256) * 8);
     bf16_t* xh = h->e_xh.as<bf16_t>();
     float *part = h->e_lnp.as<float>(), *ab = h->e_ab.as<float>();
-    HIPCHK(launch_ln_fold_rows(x, M, V, 1e-6f, xh, ab, rf, s));
+    const long xl = (long)M * V;
+    HIPCHK(launch_ln_fold_rows(x, M, V, 1e-6f, xh, xl, ab, rf, s));
     for (size_t li = 0; li < h->vit.size(); ++li) {
       const VitLayer& L = h->vit[li];
       const bool last = li + 1 == h->vit.size();
@@ -754,15 +756,10 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
       h->gemm16_fold(a, V, L.out, M, x, V, EPI_NONE, OUT_F32_RESID, s, 0, nullptr, nullptr, xh, part);
       HIPCHK(launch_ln_fold_stats(part, G, M, V, 1e-6f, ab, s));
       h->gemm16_fold(xh, V, L.mlp0F, M, hb, F, EPI_GELU, OUT_SPLIT, s, 0, ab, L.mlp0_s, nullptr, nullptr);
-      if (last) {
-        h->gemm16(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s);
-      } else {
-        h->gemm16_fold(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s, 0, nullptr, nullptr, xh, part);
-        HIPCHK(launch_ln_fold_stats(part, G, M, V, 1e-6f, ab, s));
-      }
+      h->gemm16_fold(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s, 0, nullptr, nullptr, xh, part);
+      if (!last) HIPCHK(launch_ln_fold_stats(part, G, M, V, 1e-6f, ab, s));
     }
-    HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, V, a, V, 0, NS_F16, s,
-                            rf));
+    HIPCHK(launch_layernorm_hilo(xh, xl, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, a, rf, s));
     h->gemm16(a, V, h->proj, B * np, memory, Dm, EPI_NONE, OUT_F32, s);
     return;
   }

@@ -382,8 +382,11 @@ hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hip
 hipError_t launch_ln_fold_weights(const float* W, const float* b, const float* gamma, const float* beta, int N, int K,
                                   bf16_t* wp, float* c, float* sum, hipStream_t s);
 hipError_t launch_ln_fold_stats(const float* part, int G, int rows, int D, float eps, float* ab, hipStream_t s);
-hipError_t launch_ln_fold_rows(const float* x, int rows, int D, float eps, bf16_t* xh, float* ab, unsigned* range_flag,
-                               hipStream_t s);
+hipError_t launch_ln_fold_rows(const float* x, int rows, int D, float eps, bf16_t* xh, long xl, float* ab,
+                               unsigned* range_flag, hipStream_t s);
+hipError_t launch_layernorm_hilo(const bf16_t* xh, long xl, int rows, int D, int in_group, long in_stride, long in_off,
+                                 const float* w, const float* b, float eps, float* out_f32, bf16_t* out_h,
+                                 unsigned* range_flag, hipStream_t s);
 // stop-aware decode (round 6): flag (host-mapped) = 1 when a column in [col0, col1) is all end (greedy) or every fin row
 // is set (fin != nullptr); the tail fill of a stopped decode (ids columns > t0 = end, logp steps >= t0 = 0)
 hipError_t launch_stop_scan(const int32_t* ids, int B, long ld, int col0, int col1, int end, const uint8_t* fin,

@@ -123,6 +123,54 @@ __device__ __forceinline__ float2 ln_fold_ab(const float2* grp, int G, int D, fl
   return make_float2(rstd, rstd * mu);
 }
 
+// The encoder's final LayerNorm over the hi / lo residual planes (the fold's stream), layernorm_kernel's arithmetic:
+// rows grouped as (row / in_group) * in_stride + in_off + row % in_group (the patch rows, no class token)
+template <int PER>
+__global__ __launch_bounds__(256) void layernorm_hilo_kernel(const bf16_t* __restrict__ xh, long xl, int rows,
+                                                             int in_group, long in_stride, long in_off,
+                                                             const float* __restrict__ w, const float* __restrict__ b,
+                                                             float eps, float* out_f32, bf16_t* out_h,
+                                                             unsigned* range_flag) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = PER * 64;
+  const long irow = (long)(row / in_group) * in_stride + in_off + row % in_group;
+  float v[PER];
+#pragma unroll
+  for (int c = 0; c < PER / 4; ++c) {
+    const bf16_t* hp = xh + irow * D + c * 256 + lane * 4;
+    const u32x2 h = *(const u32x2*)hp, l = *(const u32x2*)(hp + xl);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t hw = h[k >> 1] >> ((k & 1) * 16), lw = l[k >> 1] >> ((k & 1) * 16);
+      v[c * 4 + k] = h2f((bf16_t)(hw & 0xffff)) + h2f((bf16_t)(lw & 0xffff));
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) s += v[i];
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { const float d = v[i] - mean; q += d * d; }
+  const float var = wave_sum(q) / (float)D;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < PER / 4; ++c) {
+    const int col = c * 256 + lane * 4;
+    f32x4 wv = *(const f32x4*)(w + col), bv = *(const f32x4*)(b + col), y;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) y[k] = (v[c * 4 + k] - mean) * rstd * wv[k] + bv[k];
+    if (out_f32) *(f32x4*)(out_f32 + (long)row * D + col) = y;
+    const u32x2 pk = pack16x4<true>(y);
+    bad |= f16_pair_nonfinite(pk[0]) || f16_pair_nonfinite(pk[1]);
+    *(u32x2*)(out_h + (long)row * D + col) = pk;
+  }
+  if (range_flag && __any(bad) && lane == 0) range_flag_set(range_flag);
+}
+
 // The residual GEMMs' epilogues leave per (row, 64-column group) (mean_g, M2_g) in part[g][rows]; one thread per row
 __global__ __launch_bounds__(256) void ln_fold_stats_kernel(const float2* __restrict__ part, int G, int rows, int D,
                                                             float eps, float2* ab) {
@@ -137,7 +185,7 @@ __global__ __launch_bounds__(256) void ln_fold_stats_kernel(const float2* __rest
 // wave per row (layernorm_kernel's statistics); xh values that overflow fp16 set the range word
 template <int PER>
 __global__ __launch_bounds__(256) void ln_fold_rows_kernel(const float* __restrict__ x, int rows, float eps,
-                                                           bf16_t* xh, float2* ab, unsigned* range_flag) {
+                                                           bf16_t* xh, long xl, float2* ab, unsigned* range_flag) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -151,7 +199,11 @@ __global__ __launch_bounds__(256) void ln_fold_rows_kernel(const float* __restri
     v[c * 4 + 0] = t[0]; v[c * 4 + 1] = t[1]; v[c * 4 + 2] = t[2]; v[c * 4 + 3] = t[3];
     const u32x2 pk = pack16x4<true>(t);
     bad |= f16_pair_nonfinite(pk[0]) || f16_pair_nonfinite(pk[1]);
-    *(u32x2*)(xh + (long)row * D + c * 256 + lane * 4) = pk;
+    bf16_t* hp = xh + (long)row * D + c * 256 + lane * 4;
+    *(u32x2*)hp = pk;
+    const f32x4 hv = {h2f((bf16_t)(pk[0] & 0xffff)), h2f((bf16_t)(pk[0] >> 16)), h2f((bf16_t)(pk[1] & 0xffff)),
+                      h2f((bf16_t)(pk[1] >> 16))};
+    *(u32x2*)(hp + xl) = pack16x4<true>(t - hv);  // the lo plane: the residual stream as fp16 hi / lo from here on
   }
   float s = 0.f;
 #pragma unroll
@@ -594,11 +646,20 @@ hipError_t launch_ln_fold_stats(const float* part, int G, int rows, int D, float
   return hipGetLastError();
 }
 
-hipError_t launch_ln_fold_rows(const float* x, int rows, int D, float eps, bf16_t* xh, float* ab, unsigned* range_flag,
-                               hipStream_t s) {
+hipError_t launch_ln_fold_rows(const float* x, int rows, int D, float eps, bf16_t* xh, long xl, float* ab,
+                               unsigned* range_flag, hipStream_t s) {
   if (D != 768 || rows <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ln_fold_rows_kernel<12>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, eps, xh, (float2*)ab,
+  hipLaunchKernelGGL(ln_fold_rows_kernel<12>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, eps, xh, xl, (float2*)ab,
                      range_flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_layernorm_hilo(const bf16_t* xh, long xl, int rows, int D, int in_group, long in_stride, long in_off,
+                                 const float* w, const float* b, float eps, float* out_f32, bf16_t* out_h,
+                                 unsigned* range_flag, hipStream_t s) {
+  if (D != 768 || rows <= 0 || in_group <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(layernorm_hilo_kernel<12>, dim3((rows + 3) / 4), dim3(256), 0, s, xh, xl, rows, in_group, in_stride,
+                     in_off, w, b, eps, out_f32, out_h, range_flag);
   return hipGetLastError();
 }
 
