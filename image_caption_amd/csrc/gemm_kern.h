@@ -589,9 +589,12 @@ __device__ __forceinline__ int swz_chunk(int c, int r) { return ICAP_SWZ ? c ^ (
 #ifndef ICAP_LN_FOLD
 #define ICAP_LN_FOLD 0
 #endif
-// dynamic LDS of gemm_f16p_kernel<1> (and <2> at 256 rows): 2 stages of 64 KiB, then the bias slots (2 x 1 KiB) and the
-// LayerNorm fold's column-sum slots (2 x 1 KiB) and row (a, b) slots (2 x 2 KiB)
-constexpr int F16P_LDS_SO = 2 * 64 * 1024 + (ICAP_LN_FOLD ? 8192 : 2048);
+// dynamic LDS of gemm_f16p_kernel<1> (and <2> at 256 rows): 2 stages of 64 KiB, then the bias slots (2 x 1 KiB), the
+// LayerNorm fold's column-sum slots (2 x 1 KiB) and row (a, b) slots (2 x 2 KiB), then the stream-K ticket word
+constexpr int F16P_LDS_TAIL = ICAP_LN_FOLD ? 8192 : 2048;
+constexpr int f16p_lds(int BM) { return 2 * (BM * 128 + 256 * 128) + F16P_LDS_TAIL + 16; }
+constexpr int F16P_LDS_SO = f16p_lds(256);
+
 // stage pieces wave w of gemm_f16p_kernel issues per stage: its A rows (8 per piece, up to the tile's BM rows) + IPW W
 constexpr int f16p_stage_pieces(int BM, int IPW, int w) {
   const int a = (BM - w * IPW * 8) / 8;
@@ -639,6 +642,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
   const int M = p.M, nk = p.K / KS;
   const int srow = wave * IPW * 8 + (lane >> 3), schunk = swz_chunk(lane & 7, srow);
   const int fr = lane & 15, fq = lane >> 4;
+
 #ifndef ICAP_F16P_PRIO
 #define ICAP_F16P_PRIO 0
 #endif
@@ -732,25 +736,114 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
     }
   };
 
+  // Stream-K (round 6, ICAP_F16P_SK = 1 for gemm.hip and icap.cpp, variant builds; measured slower - DESIGN.md section 8:
+  // with the partial exchange removed the schedule alone gains nothing on MLP-1 / MLP-2, so the last partial round of
+  // whole tiles costs less than its share of tiles, and the exchange adds 20-40 us per launch; the late-barrier k-loop
+  // only).  Whole tiles leave a partial last round: 2364 MLP-1
+  // tiles are 9.23 per CU (10 rounds), the residual GEMMs' 678 tiles 2.65 (3 rounds).  Per XCD the xcnt tiles are
+  // walked by VB virtual lanes: RP whole rounds (lane v: tiles v, v + VB, ...), then the remaining T2 = xcnt - RP VB
+  // tiles (VB <= T2 < 3 VB) as one sequence of T2 nk k-steps cut into VB contiguous ranges at even k-steps - lane v
+  // runs [bnd(v), bnd(v + 1)).  Every range is >= nk + 2 k-steps long, so a tile is cut at most once: its head
+  // [0, k) ends one lane's range, its tail [k, nk) opens the next.  A cut tile's two units meet through the workspace
+  // slot of their boundary: the first to finish stores its fp32 accumulators (device-coherent stores) and raises the
+  // slot's ready word, the second adds them to its own (fp32 addition commutes: the same sums whichever comes first)
+  // and runs the tile's epilogue.  The schedule depends on the shape only (VB is fixed; a grid of fewer blocks runs
+  // several lanes per block), so the results do not depend on the grid (CU-masked encoder streams).
+  constexpr int VB = F16P_SK_VB;
+  constexpr int SKW = NW * 64 * TM * TN * 4;  // floats of one partial tile
+  static_assert(SKW <= F16P_SK_SLOT, "stream-K slot size");
+  const int xq = xcnt / VB, xr = xcnt - xq * VB;
+  int RP = -1;  // whole rounds before the stream-K part; -1: no stream-K (every tile whole, t, t + nbx, ...)
+  if (ICAP_F16P_SK && LB && (SO || RES) && p.sk_ws && p.sk_cnt && xr && nbx <= VB && (nk & 1) == 0 && nk >= 2) {
+    if (xq >= 1 && xr * nk >= 2 * VB) RP = xq - 1;  // ranges of (VB + xr) nk / VB >= nk + 2 k-steps
+    else if (xq >= 2) RP = xq - 2;                    // (2 VB + xr) nk / VB >= 2 nk
+  }
+  const bool sk = RP >= 0;
+  const int sk_t0 = xbase + (sk ? RP : 0) * VB, sk_w2h = sk ? (xcnt - RP * VB) * nk / 2 : 0;
+  auto bnd = [&](int v) { return 2 * (int)((uint32_t)v * (uint32_t)sk_w2h / (uint32_t)VB); };
+  struct Unit {
+    int t, k0, k1, v, r;  // tile (-1: none), k-steps [k0, k1), lane, whole round (r == RP: the stream-K part)
+  };
+  auto sk_unit = [&](int v, int pos) -> Unit {  // lane v's unit at k-step pos of the stream-K sequence
+    const int u = (int)((uint32_t)pos / (uint32_t)nk), k0 = pos - u * nk;
+    return Unit{sk_t0 + u, k0, min(nk, bnd(v + 1) - u * nk), v, RP};
+  };
+  auto first_unit = [&](int v) -> Unit { return RP > 0 ? Unit{xbase + v, 0, nk, v, 0} : sk_unit(v, bnd(v)); };
+  auto next_unit = [&](const Unit& c) -> Unit {
+    if (!sk) return Unit{c.t + nbx < xbase + xcnt ? c.t + nbx : -1, 0, nk, 0, 0};
+    if (c.r + 1 < RP) return Unit{xbase + c.v + (c.r + 1) * VB, 0, nk, c.v, c.r + 1};
+    if (c.r + 1 == RP) return sk_unit(c.v, bnd(c.v));
+    const int pos = (c.t + 1 - sk_t0) * nk;  // a unit ending inside its tile ends its lane's range
+    if (c.k1 == nk && pos < bnd(c.v + 1)) return Unit{c.t + 1, 0, min(nk, bnd(c.v + 1) - pos), c.v, RP};
+    return c.v + nbx < VB ? first_unit(c.v + nbx) : Unit{-1, 0, nk, 0, 0};
+  };
+
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  int t = xbase + lb, step = 0, tcount = 0;
+  Unit cu = sk ? first_unit(lb) : Unit{xbase + lb, 0, nk, 0, 0};
+  int t = cu.t, step = 0, tcount = 0;
   if (SO || RES) load_bias(t, 0);
-  stage(t, 0, 0);
-  if (LB) stage(t, 1, 1);  // LB: both stages of a tile's opening in flight before its k-step 0
+  stage(t, cu.k0, 0);
+  if (LB) stage(t, cu.k0 + 1, 1);  // LB: both stages of a tile's opening in flight before its k-step 0
   bool seam = false;  // this tile's stages 0 and 1 were issued before the previous tile's epilogue stores
   bool range_bad = false;  // SO: some stored fp16 value is not finite (p.range_flag set once, after the last tile)
+  // stream-K: the (ticket, ready) broadcast word in LDS after the bias / fold slots
+  int* const sk_word = (int*)(smem + 2 * STAGE + F16P_LDS_TAIL);
+  // a cut tile's meeting (block-uniform; every wave calls it): true = this block runs the tile's epilogue with the other
+  // unit's accumulators added.  The first unit's block stores its partial and raises ready; the second waits for ready
+  // (bounded: a lost partner ends the wait instead of hanging the grid) and loads the partial
+#ifndef ICAP_SK_ABL
+#define ICAP_SK_ABL 0
+#endif
+  auto sk_meet = [&](const Unit& c) -> bool {
+    if (ICAP_SK_ABL == 2) return c.k0 == 0;  // timing ablation (wrong sums): no exchange, the head unit stores
+    const int slot = (blockIdx.x & 7) * VB + (c.k0 > 0 ? c.v : c.v + 1);
+    int* const cnt = p.sk_cnt + 2 * slot;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.sk_ws + (long)slot * F16P_SK_SLOT, 0, SKW * 4, 0x00020000);
+    if (tid == 0) *sk_word = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const bool second = *(volatile int*)sk_word != 0;
+    if (!second) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)  // device-coherent (sc1) 16-byte stores, [i TN + j][thread]
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                                 (uint32_t)((i * TN + j) * NW * 64 + tid) * 16, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial is complete
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if (tid == 0) {
+      for (int it = 0; it < (1 << 22) && __hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; ++it)
+        __builtin_amdgcn_s_sleep(1);
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // zero at rest for the next launch
+      __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {  // one row tile at a time (registers: the accumulators fill the file)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] += __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)((i * TN + j) * NW * 64 + tid) * 16, 0, 17));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return true;
+  };
   for (;;) {
-    const int tn = t + nbx < xbase + xcnt ? t + nbx : -1;  // this block's next tile
+    const Unit un = next_unit(cu);  // this block's next unit
+    const int tn = un.t;
     if constexpr (LB) {
       const int fo0 = fr * 128 + (swz_chunk(fq, fr) << 4), fo1 = fr * 128 + (swz_chunk(4 + fq, fr) << 4);
       bf16x8 b2[2][TN], a2[2 * TM];
-      for (int kt = 0; kt < nk; ++kt, ++step) {
+      for (int kt = cu.k0; kt < cu.k1; ++kt, ++step) {
         const char* s0 = smem + (step & 1) * STAGE;
-        if (kt == 0) {  // a tile's opening: stage 0 landed (stage 1 and, after a seam, the stores may still fly)
+        if (kt == cu.k0) {  // a tile's opening: stage 0 landed (stage 1 and, after a seam, the stores may still fly)
           if (SO && seam) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE + NSTORE) : "memory");
           else if (RES && seam) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           // (224-row tiles: the last wave DMAs W rows only, IPW pieces per stage - stage 1 in flight is IPW, not 8)
@@ -762,9 +855,9 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
           for (int g = 0; g < XD; ++g) a2[g] = *(const bf16x8*)(s0 + (wm * WM + g * 16) * 128 + fo0);
         }
-        const bool late = kt + 1 < nk;  // the last k-step of a tile has no late point
+        const bool late = kt + 1 < cu.k1;  // the last k-step of a tile has no late point
         // a k-step entered from a late point carries its b2[0] fragments only (register budget): A fragments 0 and 1 now
-        if (kt > 0) {
+        if (kt > cu.k0) {
           a2[0] = *(const bf16x8*)(s0 + (wm * WM) * 128 + fo0);
           a2[1] = *(const bf16x8*)(s0 + (wm * WM + 16) * 128 + fo0);
         }
@@ -785,7 +878,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
         if (late) {
           // the late point: the next stage landed (after a seam's k-step 0 the stores may still fly; the RES seam
           // issued stage 1 after its stores), this wave's reads of this buffer retired, then the barrier
-          if (SO && seam && kt == 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
+          if (SO && seam && kt == cu.k0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORE) : "memory");
           else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
@@ -795,11 +888,11 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
 #pragma unroll
           for (int j = 0; j < TN; ++j) nb[j] = *(const bf16x8*)(s1 + OPA + (wn * WN + j * 16) * 128 + fo0);
           __builtin_amdgcn_sched_barrier(0);
-          if (kt + 2 < nk) {
+          if (kt + 2 < cu.k1) {
             stage(t, kt + 2, step & 1);
-          } else if (tn >= 0) {  // the next tile's bias and stage 0
+          } else if (tn >= 0) {  // the next unit's bias and first stage
             if (SO || RES) load_bias(tn, (tcount + 1) & 1);
-            stage(tn, 0, step & 1);
+            stage(tn, un.k0, step & 1);
           }
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -911,12 +1004,17 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       }
     }
     const int bm = t / nbn, bn = t - bm * nbn, mb = bm * BM + wm * WM, nb = bn * BN + wn * WN;
+    // stream-K: a cut tile's first unit stores its partial and skips the epilogue (its waits: sk_meet ends in vmcnt(0))
+    const bool epi = !sk || (cu.k0 == 0 && cu.k1 == nk) || sk_meet(cu);
     if constexpr (SO) {
       if (tn >= 0) {  // every wave is done reading the last stage's buffer: stage 1 of the next tile into it
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (ABL != 1 && ABL < 10) stage(tn, 1, (step + 1) & 1);  // step = the next tile's k-step 0 here; its k-step 1 reads (step + 1) & 1
+        if (ABL != 1 && ABL < 10) stage(tn, un.k0 + 1, (step + 1) & 1);  // step = the next unit's first k-step here; its second reads (step + 1) & 1
       }
+      // (no epilogue stores: the next opening's seam count would not hold - plain counted waits)
+      if (!epi) seam = false;
+      else {
       const bool tail = bm * BM + BM > M;  // the last row band of a ragged M: rows >= M are not stored
       // straight-line per row tile (no per-element branches, so the scheduler interleaves the TN x 2 independent GELU
       // chains instead of padding each dependent packed FMA with a nop): bias in registers, head-major row offsets
@@ -1017,6 +1115,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       // the counted waits of the next tile assume all NSTORE stores per wave were issued: not after a ragged tile
       // (its next tile waits vmcnt(0) and re-issues its stage 1 - the same bytes into the same buffer)
       seam = !tail;
+      }
     } else if constexpr (RES) {
       float* Cb = (float*)p.C + nb + 4 * fq;
       const float* bl = sbias + (tcount & 1) * 256 + wn * WN + 4 * fq;
@@ -1030,6 +1129,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       };
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {  // row tiles [4 h2, min(TM, 4 h2 + 4))
+        if (!epi) break;  // stream-K: the tile's other unit stores it
         f32x4 rv[4][TN];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1088,7 +1188,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
       if (tn >= 0) {  // stage 1 of the next tile into the last stage's buffer, after the stores
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (ABL != 1 && ABL < 10) stage(tn, 1, (step + 1) & 1);
+        if (ABL != 1 && ABL < 10) stage(tn, un.k0 + 1, (step + 1) & 1);
       }
       // k-step 0 of the next tile skips its vmcnt wait because the residual loads retired after its stage 0;
       // every lane loads (rows clamped), so that holds for ragged tiles too
@@ -1098,6 +1198,7 @@ __global__ __launch_bounds__(512, 1) void gemm_f16p_kernel(GemmArgs p) {
     }
     if (tn < 0) break;
     t = tn;
+    cu = un;
     ++tcount;
 #pragma unroll
     for (int i = 0; i < TM; ++i)

@@ -262,6 +262,7 @@ struct icap_handle {
 
   // workspaces
   DevBuf e_split, e_scnt;  // GEMM tail split: partial tiles + tickets (zero at rest)
+  DevBuf e_sk, e_skc;      // stream-K fp16 encoder GEMMs: partial tiles + (ticket, ready) words (zero at rest)
   int split_slots = -1;     // block slots per XCD of the 128 x 256 GEMM (2 per CU); 0 = tail split off
   DevBuf e_x, e_a, e_qkv, e_h, e_patch, e_sa, e_hs;  // encoder (e_sa: int8 row scales, e_hs: MLP block scales)
   DevBuf e_xh, e_lnp, e_ab;  // f16 LayerNorm fold: fp16 copy of x, (mean, M2) per 64-column group, (a, b) per row
@@ -308,7 +309,8 @@ struct icap_handle {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col, &t_bn}) b->release();
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt, &rflag, &step_layers})
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt, &e_sk, &e_skc, &rflag,
+                      &step_layers})
       b->release();
     for (int i = 0; i < 2; ++i) {
       step_args[i].release();
@@ -453,7 +455,23 @@ struct icap_handle {
     g.epi = epi; g.out = out;
     g.range_flag = range_word();
     g.max_grid = enc_cus;
+    stream_k(g);
     run_gemm(g, s);
+  }
+  // the persistent fp16 GEMMs' stream-K workspace (gemm_kern.h ICAP_F16P_SK), allocated on first use (the encoder is
+  // never captured); tickets zeroed once, every launch leaves them zero
+  void stream_k(GemmArgs& g) {
+    if (!ICAP_F16P_SK) return;  // (the product: whole tiles)
+#ifdef ICAP_SK_HOST_OFF  // measurement variant: the kernels' stream-K code compiled in, never engaged
+    return;
+#endif
+    if (!e_skc.p) {
+      e_sk.ensure(F16P_SK_WS_BYTES);
+      e_skc.ensure((size_t)F16P_SK_CNT_INTS * 4);
+      HIPCHK(hipMemset(e_skc.p, 0, e_skc.n));
+    }
+    g.sk_ws = e_sk.as<float>();
+    g.sk_cnt = e_skc.as<int>();
   }
   // the LayerNorm fold's GEMMs: store-only with ab / sum (A = the fp16 copy xh, W folded), or residual leaving xh and the
   // group partials (kernels.h GemmArgs::xh / ln_*)
@@ -472,6 +490,7 @@ struct icap_handle {
     g.ln_ab = ab; g.ln_sum = sum; g.xh = xh; g.ln_part = part;
     if (xh) g.c_lo = (long)M * ldc;  // the residual stream's lo plane (fold: C itself is not read or written)
     REQUIRE(gemm_f16_persistent(g), "LayerNorm fold: the persistent fp16 GEMM form only");
+    stream_k(g);
     run_gemm(g, s);
   }
   // residual-output GEMMs (N = 768 / 512: a partial last round of tiles) split their tail tiles in K when

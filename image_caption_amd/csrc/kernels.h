@@ -102,7 +102,21 @@ struct GemmArgs {
   float* ln_part;
   const float* ln_ab;
   const float* ln_sum;
+  // stream-K (round 6; gemm_f16p_kernel, gemm_kern.h ICAP_F16P_SK): fp32 partial tiles of the tiles split between two
+  // blocks (F16P_SK_WS_BYTES) and their (ticket, ready) words (F16P_SK_CNT_INTS, zero at rest); nullptr = whole tiles
+  float* sk_ws;
+  int* sk_cnt;
 };
+// ICAP_F16P_SK (round 6, variant builds: -DICAP_F16P_SK=1 for gemm.hip and icap.cpp): stream-K scheduling of the
+// persistent fp16 GEMMs (gemm_kern.h; measured slower); 0 = whole tiles, no workspace
+#ifndef ICAP_F16P_SK
+#define ICAP_F16P_SK 0
+#endif
+// stream-K workspace: 8 XCDs x F16P_SK_VB lane boundaries, one 512-thread fp32 accumulator image (<= 256 KiB) each
+constexpr int F16P_SK_VB = 32;  // virtual lanes per XCD (the schedule, and so the sums, do not depend on the grid)
+constexpr long F16P_SK_SLOT = 512L * 32 * 4;  // floats per partial tile (512 threads x 32 f32x4)
+constexpr size_t F16P_SK_WS_BYTES = (size_t)8 * F16P_SK_VB * F16P_SK_SLOT * 4;
+constexpr int F16P_SK_CNT_INTS = 8 * F16P_SK_VB * 2;
 // bytes of split_ws for split_slots block slots per XCD
 inline size_t gemm_split_ws_bytes(int split_slots) { return (size_t)8 * split_slots * 2 * 128 * 256 * 4; }
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; g.res_planes = 2; return g; }
