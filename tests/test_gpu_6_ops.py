@@ -511,6 +511,30 @@ def test_gemm_f16_persistent_repeat_bitwise(cuda, M, N, K):
         assert (got - want).abs().max().item() < tol, (epi, out)
 
 
+def test_gemm_f16_plane_past_2gib(cuda):
+    """The store-only fp16 plane of the persistent GEMM beyond a 2 GiB byte offset (a buffer resource of
+    2^31 - 1 bytes silently dropped those stores - the ViT MLP-1 output from B ~ 1775): a 2.2 GB output whose last
+    rows are checked against fp64 (the plane is prefilled with NaN, so a dropped store cannot pass)."""
+    L, lib = _lib()
+    M, N, K = 360448, 3072, 128  # M N 2 bytes = 2.21e9 > 2^31
+    g = torch.Generator(device="cpu").manual_seed(7)
+    a = torch.randn(M, K, generator=g).to(torch.float16).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.float16).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    C = torch.full((M, N), float("nan"), device=cuda, dtype=torch.float16)
+    L.check(lib.icap_op_gemm(a.data_ptr(), K, 0, -1, w.data_ptr(), bias.data_ptr(), C.data_ptr(), N, 0,
+                             M, N, K, 0, 2, L.stream_ptr()), "gemm f16 plane > 2 GiB")
+    torch.cuda.synchronize()
+    first_past = (1 << 31) // (2 * N)  # the first row with bytes past 2 GiB
+    rows = torch.cat([torch.arange(0, 64), torch.arange(first_past - 8, first_past + 8), torch.arange(M - 300, M)])
+    rows = rows.to(cuda)
+    ref = a[rows].double() @ w.double().t() + bias.double()
+    got = C[rows].double()
+    assert not torch.isnan(got).any()
+    assert (got - ref).abs().max().item() < 2 ** -10 * max(1.0, ref.abs().max().item())
+    del C
+
+
 def test_gemm_f16_head_major_via_engine_layout(cuda):
     """Identity A through the fp16 kernel: exact, and not transposed."""
     L, lib = _lib()
