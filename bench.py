@@ -43,11 +43,13 @@ PEAK_I8_TOPS = 5000.0      # dense i8 MFMA (2x bf16 per clock: 16x16x64 i8 = cyc
 PEAK_HBM_GBS = 8000.0
 # HBM-side bytes per launch from rocprofv3 PMC passes over the default bench of each greedy workload
 # (tools/r3_profile.sh); the round-2 summary is the fallback for the ViT line
-TRAFFIC_JSON = {"vit": [os.path.join(ROOT, "profiles", "r05", "pmc_traffic_vit.json"),
+TRAFFIC_JSON = {"vit": [os.path.join(ROOT, "profiles", "r06", "pmc_traffic_vit.json"),
+                        os.path.join(ROOT, "profiles", "r05", "pmc_traffic_vit.json"),
                         os.path.join(ROOT, "profiles", "r04", "pmc_traffic_vit.json"),
                         os.path.join(ROOT, "profiles", "r03", "pmc_traffic_vit.json"),
                         os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")],
-                "grid": [os.path.join(ROOT, "profiles", "r05", "pmc_traffic_grid.json"),
+                "grid": [os.path.join(ROOT, "profiles", "r06", "pmc_traffic_grid.json"),
+                         os.path.join(ROOT, "profiles", "r05", "pmc_traffic_grid.json"),
                          os.path.join(ROOT, "profiles", "r04", "pmc_traffic_grid.json"),
                          os.path.join(ROOT, "profiles", "r03", "pmc_traffic_grid.json")]}
 
