@@ -231,6 +231,9 @@ struct icap_handle {
     hipEvent_t a, b;
   };
   bool prof_on = false;
+  int prof_every = 1;     // icap_profile_enable(h, N >= 2): only ViT encoder layers li % N == 0 are bracketed
+  bool prof_gate = true;  // the current ViT layer is bracketed (set by the layer loops)
+  void prof_layer(size_t li) { prof_gate = li % (size_t)prof_every == 0; }
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<ProfRec> prof;
@@ -244,7 +247,7 @@ struct icap_handle {
   }
   template <class F>
   void timed(int cls, double flops, double bytes, hipStream_t s, F&& launch) {
-    if (!prof_on) {
+    if (!prof_on || !prof_gate) {
       launch();
       return;
     }
@@ -764,6 +767,7 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
     for (size_t li = 0; li < h->vit.size(); ++li) {
       const VitLayer& L = h->vit[li];
       const bool last = li + 1 == h->vit.size();
+      h->prof_layer(li);
       h->gemm16_fold(xh, V, L.qkvF, M, qkv, 3 * V, EPI_NONE, OUT_SPLIT, s, hm, ab, L.qkv_s, nullptr, nullptr);
       {
         const double flops = 4.0 * B * d.vit_heads * (double)T * T * 64;
@@ -778,11 +782,14 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
       h->gemm16_fold(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s, 0, nullptr, nullptr, xh, part);
       if (!last) HIPCHK(launch_ln_fold_stats(part, G, M, V, 1e-6f, ab, s));
     }
+    h->prof_gate = true;
     HIPCHK(launch_layernorm_hilo(xh, xl, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, a, rf, s));
     h->gemm16(a, V, h->proj, B * np, memory, Dm, EPI_NONE, OUT_F32, s);
     return;
   }
-  for (const VitLayer& L : h->vit) {
+  for (size_t li = 0; li < h->vit.size(); ++li) {
+    const VitLayer& L = h->vit[li];
+    h->prof_layer(li);
     HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s, rf));
     h->gemm16(a, V, L.qkv, M, qkv, 3 * V, EPI_NONE, OUT_SPLIT, s, hm);  // head-major [image][q|k|v x head][token][64]
     {
@@ -797,6 +804,7 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
     h->gemm16(a, V, L.mlp0, M, hb, F, EPI_GELU, OUT_SPLIT, s);
     h->gemm16(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s);
   }
+  h->prof_gate = true;
   // final LN on patch rows only (drop CLS), then projection 768 -> d_model
   HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, V, a, V, 0, NS_F16, s,
                           rf));
@@ -854,7 +862,9 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
     h->run_gemm(ga, s);
   }
   HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
-  for (const VitLayer& L : h->vit) {
+  for (size_t li = 0; li < h->vit.size(); ++li) {
+    const VitLayer& L = h->vit[li];
+    h->prof_layer(li);
     // QKV written head-major ([image][q|k|v x head][token][64]) for the attention's contiguous rows
     if (h->i8) {
       HIPCHK(launch_layernorm_i8(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, a8, sa, s));
@@ -879,6 +889,7 @@ void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStrea
     }
     h->gemm(hb, d.vit_mlp, hL, L.mlp3, M, x, V, 0, EPI_NONE, OUT_F32_RESID, s);
   }
+  h->prof_gate = true;
   // final LN on patch rows only (drop CLS), then projection 768 -> d_model
   const long a2L = (long)B * np * V;
   if (feats)
@@ -2558,6 +2569,8 @@ int icap_profile_enable(icap_handle* h, int enable) {
   return guarded([&] {
     REQUIRE(h, "null handle");
     h->prof_on = enable != 0;
+    h->prof_every = enable > 1 ? enable : 1;
+    h->prof_gate = true;
     h->prof.clear();
     h->ev_used = 0;
   });

@@ -471,8 +471,10 @@ class Engine:
         check(self.lib.icap_set_graphs(self.handle, int(bool(enable))), "icap_set_graphs")
 
     # ------------------------------------------------------------------ live kernel timing
-    def profile(self, enable: bool) -> None:
-        check(self.lib.icap_profile_enable(self.handle, int(bool(enable))), "icap_profile_enable")
+    def profile(self, enable: bool, every: int = 1) -> None:
+        """HIP-event timing of the hot-kernel launches (icap_profile_enable); every = N >= 2 brackets only ViT encoder
+        layers 0, N, 2N, ... (each event pair costs the stream ~3 us; the layers share their shapes)."""
+        check(self.lib.icap_profile_enable(self.handle, max(1, int(every)) if enable else 0), "icap_profile_enable")
 
     def profile_read(self, kernel_class: int) -> dict:
         """Device time of every recorded launch of one kernel class (HIP events on the launch

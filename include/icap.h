@@ -294,7 +294,10 @@ int icap_set_decode_chains(icap_handle* h, int chains);
 #define ICAP_PROF_GEMM_I8 6    /* gemm_i8_kernel: int8 two-slice encoder GEMMs (ICAP_PREC_I8X2)            */
 #define ICAP_PROF_DEC_FUSED 7  /* dec_sa_kernel / dec_ffn_kernel (fused decode-step blocks, eager launches)   */
 #define ICAP_PROF_GEMM_F16P 8  /* gemm_f16p_kernel: persistent fp16 encoder GEMMs (ViT QKV, MLP-1)          */
-/* Enable (1) / disable (0) HIP-event bracketing of every hot-kernel launch; clears records. */
+/* Enable (1) / disable (0) HIP-event bracketing of every hot-kernel launch; clears records.  enable = N >= 2: inside
+ * the ViT encoder's layer loop only layers 0, N, 2N, ... are bracketed (every other launch as with 1): each timing
+ * event pair costs the stream about 3 us of command-processor time, so bracketing all 60 encoder-layer launches of
+ * a step adds ~0.4 ms to it (tools/r6_gap.py) - the layers share their shapes, so a sample measures the same kernels. */
 int icap_profile_enable(icap_handle* h, int enable);
 /* Sum over recorded launches of one class: device ms, launch count, algorithmic flops and bytes
  * (flops count one activation plane; bytes are the operand bytes the launches must read). */

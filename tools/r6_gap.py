@@ -34,12 +34,12 @@ def timed(fn, sync_each, n=10):
     return sum(a.elapsed_time(b) for a, b in evs) / n
 
 
-for prof in (False, True):
-    eng.profile(prof)
+for prof in (0, 1, 6):  # off, every launch, layers 0 and 6 (bench.py)
+    eng.profile(prof > 0, every=max(prof, 1))
     for name, fn in (("encode", lambda: eng.encode(imgs)),
                      ("decode", lambda: eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, 30))):
         t_sync = timed(fn, True)
         t_b2b = timed(fn, False)
-        print(f"profile {int(prof)} {name}: after sync {t_sync:.3f} ms, back-to-back {t_b2b:.3f} ms, "
+        print(f"profile {prof} {name}: after sync {t_sync:.3f} ms, back-to-back {t_b2b:.3f} ms, "
               f"exposed host latency {1e3 * (t_sync - t_b2b):.0f} us", flush=True)
     eng.profile(False)
