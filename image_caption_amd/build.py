@@ -26,7 +26,7 @@ def _stale(tools: bool = False) -> bool:
     if not FLAVOR.exists() or FLAVOR.read_text().strip() != ("tools" if tools else "product"):
         return True
     t = LIB.stat().st_mtime
-    deps = [CSRC / s for s in SOURCES + (TOOLS_SOURCES if tools else [])] + list(CSRC.glob("*.h")) + [HERE.parent / "include" / "icap.h"]
+    deps = [CSRC / s for s in SOURCES + (TOOLS_SOURCES if tools else [])] + list(CSRC.glob("*.h")) + list(CSRC.glob("*.inc")) + [HERE.parent / "include" / "icap.h"]
     return any(p.stat().st_mtime > t for p in deps)
 
 

@@ -1439,98 +1439,7 @@ void decoder_layers(icap_handle* h, DecodeBufs& b, int B, int n_new, int t0, int
 // ---- persistent decode steps (decstep.hip, xdec.hip): measured slower than the launch loop, compiled
 // into the tools build only; a product build has neither kernel and icap_set_decode_step refuses modes 1 / 2.
 #ifdef ICAP_TOOLS
-// Whether the decode loop runs as one persistent launch per step: the fused blocks' shapes (d 512, 8 heads,
-// dim_ff 2048), two activation planes, decode positions below 64, the bf16 weights (hi/lo weights keep the unfused
-// launches, except for the dropout sampler as in decoder_layers).
-bool step_path(const icap_handle* h, int max_len, const DropCfg* drop) {
-  const icap_model_desc& d = h->d;
-  return h->use_step && h->ns == 2 && d.d_model == 512 && d.nhead == 8 && d.dim_ff == 2048 && max_len <= 65 &&
-         d.n_dec_layers >= 1 && d.n_dec_layers <= DEC_STEP_MAX_LAYERS && (!h->wlo || drop);
-}
-
-// The decoder layers' weight pointers in device memory (DecStepLayer[n_dec_layers]) for the persistent steps.
-const DecStepLayer* step_layers(icap_handle* h) {
-  const icap_model_desc& d = h->d;
-  const int L = d.n_dec_layers;
-  if (!h->step_layers.p) {
-    std::vector<DecStepLayer> v(L);
-    for (int l = 0; l < L; ++l) {
-      const DecLayer& o = h->dec[l];
-      DecStepLayer& x = v[l];
-      x.Wqkv = o.sa_qkv.w; x.bqkv = o.sa_qkv.b; x.Wo = o.sa_out.w; x.bo = o.sa_out.b;
-      x.n1w = o.n1.w; x.n1b = o.n1.b;
-      x.Wq = o.ca_q.w; x.bq = o.ca_q.b; x.WkT = o.ca_kT;
-      x.Wv = o.ca_v; x.bv = o.ca_vb; x.Wco = o.ca_out.w; x.bco = o.ca_out.b;
-      x.n2w = o.n2.w; x.n2b = o.n2.b;
-      x.W1 = o.lin1.w; x.b1 = o.lin1.b; x.W2 = o.lin2.w; x.b2 = o.lin2.b;
-      x.n3w = o.n3.w; x.n3b = o.n3.b;
-    }
-    h->step_layers.ensure(sizeof(DecStepLayer) * L);
-    HIPCHK(hipMemcpy(h->step_layers.p, v.data(), sizeof(DecStepLayer) * L, hipMemcpyHostToDevice));
-  }
-  return h->step_layers.as<DecStepLayer>();
-}
-
-// Whether the decode loop runs as the group-persistent step (xdec.hip): its shapes (d 512, 8 heads, dim_ff 2048,
-// at most 256 rows, one row per memory image, S <= 256), two activation planes, bf16 decoder weights, eval mode.
-bool xdec_path(const icap_handle* h, int B, int S, int max_len, const DropCfg* drop) {
-  const icap_model_desc& d = h->d;
-  return h->use_xdec && h->ns == 2 && d.d_model == 512 && d.nhead == 8 && d.dim_ff == 2048 && max_len <= 65 &&
-         B <= 256 && S <= 256 && d.n_dec_layers >= 1 && d.n_dec_layers <= DEC_STEP_MAX_LAYERS && !h->wlo && !drop &&
-         xdec_supported();
-}
-
-// The per-step argument structs of one decode configuration, built on the host and copied to device memory (the
-// kernel reads its arguments there).  Rebuilt when the configuration or the workspace changes; never during a
-// stream capture (decode_loop prepares them before it captures).
-const DecStepArgs* step_args(icap_handle* h, const DecodeBufs& b, int B, int S, int max_len, int wsi,
-                             const DropCfg* drop, hipStream_t s) {
-  const icap_model_desc& d = h->d;
-  const int L = d.n_dec_layers, steps = max_len - 1;
-  step_layers(h);
-  const size_t st_ints = dec_step_state_ints(L, B);
-  const long key[8] = {B, S, max_len, (long)g_ws_generation, drop ? (long)drop->thr : -1,
-                       drop ? (long)(intptr_t)drop->seed : 0, (long)(intptr_t)b.x, (long)st_ints};
-  h->step_state[wsi].ensure(st_ints * 4 * steps);
-  if (!h->step_args[wsi].p || h->step_args[wsi].n < sizeof(DecStepArgs) * steps ||
-      std::memcmp(key, h->step_key[wsi], sizeof(key)) != 0) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    HIPCHK(hipStreamIsCapturing(s, &cs));
-    REQUIRE(cs == hipStreamCaptureStatusNone, "internal: decode step arguments rebuilt during a capture");
-    std::vector<DecStepArgs> v(steps);
-    int* state = h->step_state[wsi].as<int>();
-    const int ntasks = L * 59 * ((B + 15) / 16);
-    static const int trace = icap_knob("ICAP_DEC_STEP_TRACE", 0);
-    if (trace) h->step_trace.ensure((size_t)steps * ntasks * 4 * 8 + 4096 * 4);
-    for (int t = 0; t < steps; ++t) {
-      DecStepArgs& a = v[t];
-      a = DecStepArgs{};
-      a.layers = h->step_layers.as<DecStepLayer>();
-      a.n_layers = L; a.rows = B; a.t0 = t; a.Lmax = max_len; a.S = S;
-      a.x = b.x; a.a = b.a; a.aL = b.aL;
-      a.kc = b.kc; a.vc = b.vc; a.kvl = (long)b.kvl;
-      a.part = b.part; a.PS = b.PS;
-      a.qt = b.qt; a.cL = b.cL; a.c = b.c; a.mem16 = b.memp; a.gs = b.gs;
-      if (drop) {
-        a.drop = *drop;
-        a.drop.row_base = 0;
-      }
-      int* blk = state + (size_t)t * st_ints;
-      a.ctr = blk;
-      a.qhead = blk + (st_ints - 4);  // the block's last 16 bytes (after every counter)
-      a.err = h->range_word();
-      if (trace) {
-        a.trace = h->step_trace.as<unsigned long long>() + (size_t)t * ntasks * 4;
-        a.trace_cur = (int*)(h->step_trace.as<unsigned long long>() + (size_t)steps * ntasks * 4);
-      }
-    }
-    h->step_args[wsi].ensure(sizeof(DecStepArgs) * steps);
-    HIPCHK(hipMemcpy(h->step_args[wsi].p, v.data(), sizeof(DecStepArgs) * steps, hipMemcpyHostToDevice));
-    std::memcpy(h->step_key[wsi], key, sizeof(key));
-  }
-  return h->step_args[wsi].as<DecStepArgs>();
-}
-
+#include "icap_tools_steps.inc"
 #else
 bool step_path(const icap_handle*, int, const DropCfg*) { return false; }
 bool xdec_path(const icap_handle*, int, int, int, const DropCfg*) { return false; }
