@@ -591,69 +591,6 @@ __device__ __forceinline__ float eaf_tile(const char* Ks, const char* Vs, const 
   return l;
 }
 
-// Key tiles [KT0, KT0 + NK) of one 16-query tile (round 6, the persistent form's split last tile): eaf_tile's S, softmax
-// and P V over that key range only, with the range's own maximum - returns the partial row sum l and the maximum mxs (exp2
-// domain), O = the unnormalised partial P V.  Merged with the other ranges' (mxs, l, O) by eaf_merge.
-template <int NKT, int KT0, int NK>
-__device__ __forceinline__ float eaf_part(const char* Ks, const char* Vs, const bf16x8* qh, int N, float sc2, int fr,
-                                          int g, f32x4 (&o)[4], float& mxs) {
-  const int q4 = fr >> 2, p4 = fr & 3;
-  f32x4 s[NK];
-#pragma unroll
-  for (int i = 0; i < NK; ++i) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const int row = (KT0 + i) * 16 + fr;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 kh = *(const bf16x8*)(Ks + row * 128 + (((ks * 4 + g) ^ kswz(row)) << 4));
-      acc = mma<true>(kh, qh[ks], acc);
-    }
-    s[i] = acc;
-  }
-  if constexpr (KT0 + NK == NKT)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)  // the last tile's keys >= N
-      if ((NKT - 1) * 16 + g * 4 + r >= N) s[NK - 1][r] = -INFINITY;
-  float mx = s[0][0];
-#pragma unroll
-  for (int i = 0; i < NK; ++i)
-#pragma unroll
-    for (int r = (i == 0 ? 1 : 0); r < 4; ++r) mx = __builtin_elementwise_maximum(mx, s[i][r]);
-  mxs = rows4_max(mx) * sc2;
-  f32x2 l2 = {0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < NK; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; r += 2) {
-      s[i][r] = __builtin_amdgcn_exp2f(fmaf(s[i][r], sc2, -mxs));
-      s[i][r + 1] = __builtin_amdgcn_exp2f(fmaf(s[i][r + 1], sc2, -mxs));
-      l2 += (f32x2){s[i][r], s[i][r + 1]};
-    }
-  }
-  const float l = rows4_sum(l2[0] + l2[1]);
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < (NK + 1) / 2; ++c) {
-    constexpr f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    const f32x4 s1 = 2 * c + 1 < NK ? s[2 * c + 1 < NK ? 2 * c + 1 : 0] : z;
-    const u32x2 p0 = pack16x4<true>(s[2 * c]), p1 = pack16x4<true>(s1);
-    const bf16x8 ph = __builtin_bit_cast(bf16x8, (u32x4){p0[0], p0[1], p1[0], p1[1]});
-    const int key0 = (KT0 + 2 * c) * 16 + 4 * g + q4;  // and key0 + 16 (vswz has period 8)
-    const int second = 2 * c + 1 < NK ? 16 * 128 : 0;  // past the range: re-read tile 2 c (finite, P = 0)
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int off0 = key0 * 128 + (((dt * 2 + (p4 >> 1)) ^ vswz(key0)) << 4) + (p4 & 1) * 8;
-      const bf16x8 vh = tr_pair(Vs + off0, Vs + off0 + second);
-      o[dt] = mma<true>(vh, ph, o[dt]);
-    }
-  }
-  return l;
-}
-// the key split of the last query tile over S waves: range j = [split_kt0(j), + split_nk(j))
-constexpr int split_nk(int NKT, int S, int j) { return NKT / S + (j < NKT % S ? 1 : 0); }
-constexpr int split_kt0(int NKT, int S, int j) { return j * (NKT / S) + (j < NKT % S ? j : NKT % S); }
-
 // Whole-sequence form of the f16 encoder attention (round 4; head-major fp16 qkv, N <= 256): one workgroup of 4 waves
 // per (image, head) stages ALL of its K and V (N x 64 fp16 each: 50 KiB at N = 197) in one DMA burst, and each wave
 // takes query tiles w, w + 4, ...: S^T = K Q^T over every key tile at once (13 tiles x 2 MFMA at N = 197, 52 score
@@ -751,40 +688,16 @@ __global__ __launch_bounds__(NW * 64, NW <= 4 ? 3 : 2) void enc_attention_full_k
 // per ViT launch against 75.9 for enc_attention_full_kernel and 91-107 with 8 waves of two tiles (the tile's
 // S -> softmax -> P V chain is latency-bound: more waves per SIMD, not fewer larger ones; profiles/r05/attn_pers.txt).
 // The SIMD holding waves {w : w = 0 mod 4} carries 4 of the 13 tiles against 3.25 on average (the per-item barrier).
-// Round 6 (ICAP_EAF_SPLIT=1, variant builds; measured equal - 76.8 against 75.5 us per launch in kernel stats, bench
-// lines within the box's spread, profiles/r06/split_ab.txt - so off in the product): with one query tile per wave and W = NW - NKT + 1 >= 2 waves for the last
-// tile, that tile's keys are split over S = min(4, W) waves (eaf_part: partial max, sum and P V), which write their
-// partials to an LDS slot of the item's parity; the first of them merges the slot at the top of the NEXT item (after
-// the item barrier) and stores the tile - so each SIMD carries 3 full tiles and a quarter instead of 4 against 3 (13
-// tiles at N = 197 on 16 waves: waves 0-11 one tile each, 12-15 a quarter of tile 12 each).  Every wave still issues
-// exactly 2 buffer stores per item (the merged tile's, or out of range), which the counted wait at the top relies on.
-#ifndef ICAP_EAF_SPLIT
-#define ICAP_EAF_SPLIT 0
-#endif
-constexpr int eaf_split_s(int NKT, int NW) {
-  return (ICAP_EAF_SPLIT && NKT <= NW && NW - NKT + 1 >= 2) ? (NW - NKT + 1 < 4 ? NW - NKT + 1 : 4) : 0;
-}
-constexpr int EAF_PART_BYTES = 64 * 16 * 4 + 64 * 8;  // one split wave's partial: O (16 floats / lane) + (mxs, l) / lane
-template <int NKT, int NW>
-constexpr int eaf_pers_lds() {  // the 2-item K / V ring + (split) the two partial slots
-  return 2 * 2 * NKT * 16 * 128 + 2 * eaf_split_s(NKT, NW) * EAF_PART_BYTES;
-}
-
 template <int NKT, int NW = 8>
 __global__ __launch_bounds__(NW * 64, 1) void enc_attention_pers_kernel(const bf16_t* __restrict__ qkv, int N, int H,
                                                                         int items, float scale, bf16_t* out,
                                                                         long out_ld) {
   constexpr int NQW = (NKT + NW - 1) / NW, MAT = NKT * 16 * 128, ni = NKT * 2;
-  constexpr int S = eaf_split_s(NKT, NW);  // waves sharing the last query tile (0: no split)
   static_assert(NQW == 1 || NQW == 2, "the stores-per-item count below");
-  static_assert(S == 0 || NQW == 1, "the split needs one query tile per wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, g = lane >> 4, lrow = lane >> 3, lch = lane & 7;
   const int G = gridDim.x;
-  char* const parts = smem + 4 * MAT;  // [item parity][S][EAF_PART_BYTES]
-  // the query tile this wave computes (split waves: the last tile)
-  auto tile_of = [&](int qi) { return S ? min(wave, NKT - 1) : wave + NW * qi; };
   bf16x8 qn[NQW][2];
   auto issue = [&](int it, int buf) {  // item it's K / V into ring slot buf, its Q fragments into qn
     const int b = it / H, h = it - b * H;
@@ -801,119 +714,48 @@ __global__ __launch_bounds__(NW * 64, 1) void enc_attention_pers_kernel(const bf
     }
 #pragma unroll
     for (int qi = 0; qi < NQW; ++qi) {
-      const int q = min(tile_of(qi) * 16 + fr, N - 1);
+      const int q = min((wave + NW * qi) * 16 + fr, N - 1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) qn[qi][ks] = *(const bf16x8*)(qb + (long)q * 64 + ks * 32 + g * 8);
     }
   };
-  // the normalised 16 x 64 output tile qt of item it (o / l): 2 buffer stores per lane (rows >= N, or store = false:
-  // out of the resource's range, dropped)
-  auto store_tile = [&](int itm, int qt, const f32x4 (&o)[4], float l, bool store) {
-    const int b = itm / H, h = itm - b * H;
-    const __amdgpu_buffer_rsrc_t ro =
-        __builtin_amdgcn_make_buffer_rsrc(out + (long)b * N * out_ld, 0, (int)(N * out_ld * 2), 0x00020000);
-    const float inv = 1.f / l;
-    const int qq = qt * 16 + fr;
-    const bool odd = g & 1;
-    // 16-byte stores: lanes g (even) and g + 1 hold d = 16 dt + 4 g .. + 7 of d-tiles dt and dt + 1
-    const uint32_t ob = (uint32_t)((qq * out_ld + h * 64 + 4 * g) * 2);
-#pragma unroll
-    for (int dt = 0; dt < 4; dt += 2) {
-      const u32x2 a0 = pack16x4<true>(o[dt] * inv), a1 = pack16x4<true>(o[dt + 1] * inv);
-      const u32x2 snd = odd ? a0 : a1;
-      const u32x2 rcv = {xor16_partner(snd[0]), xor16_partner(snd[1])};
-      const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], a1[0], a1[1]} : (u32x4){a0[0], a0[1], rcv[0], rcv[1]};
-      const uint32_t off = ob + (uint32_t)((odd ? (dt + 1) * 16 - 4 : dt * 16) * 2);
-      __builtin_amdgcn_raw_buffer_store_b128(w, ro, store && qq < N ? off : 0x80000000u, 0, 0);
-    }
-  };
-  // split: merge the S partials of slot `par` (the exact softmax over all keys: rescale each range by 2^(mxs_j - m))
-  auto merge_store = [&](int itm, int par, bool store) {
-    f32x4 o[4] = {};
-    float l = 0.f, m = -INFINITY;
-    const char* ps = parts + par * S * EAF_PART_BYTES;
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      const float2 ml = *(const float2*)(ps + j * EAF_PART_BYTES + 64 * 64 + lane * 8);
-      m = fmaxf(m, ml.x);
-    }
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      const char* pj = ps + j * EAF_PART_BYTES;
-      const float2 ml = *(const float2*)(pj + 64 * 64 + lane * 8);
-      const float f = __builtin_amdgcn_exp2f(ml.x - m);
-      l = fmaf(ml.y, f, l);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] += *(const f32x4*)(pj + (dt * 64 + lane) * 16) * f;
-    }
-    store_tile(itm, NKT - 1, o, l, store);
-  };
   const float sc2 = scale * 1.44269504088896341f;  // exp2 domain
   int it = blockIdx.x;
   if (it < items) issue(it, 0);
-  // the top of item k: its K / V and Q landed (2 NQW younger stores in flight), every wave done with item k - 1's ring
-  // slot (then refilled with item k + 1)
-  auto item_top = [&](int k) {
+  for (int k = 0; it < items; ++k, it += G) {
     if (k == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NQW) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-  };
-  if constexpr (S > 0) if (wave >= NKT - 1) {
-    // the split waves (their own loop, so the full-tile loop below keeps its registers): the previous item's split tile
-    // merged and stored by the first of them (the others: 2 dropped stores), then this item's partial over key range j
-    const int j = wave - (NKT - 1);
-    int prev = -1;
-    for (int k = 0; it < items; ++k, it += G) {
-      item_top(k);
-      const bf16x8 qc[2] = {qn[0][0], qn[0][1]};
-      if (it + G < items) issue(it + G, (k + 1) & 1);
-      const char* Ks = smem + (k & 1) * 2 * MAT;
-      if (j == 0 && prev >= 0) merge_store(prev, (k + 1) & 1, true);
-      else {
-        const f32x4 z[4] = {};
-        store_tile(it, NKT - 1, z, 1.f, false);
-      }
-      if (j < S) {
-        f32x4 o[4];
-        float mxs = 0.f, l = 0.f;
-        if (j == 0) l = eaf_part<NKT, split_kt0(NKT, S, 0), split_nk(NKT, S, 0)>(Ks, Ks + MAT, qc, N, sc2, fr, g, o, mxs);
-        else if (j == 1) l = eaf_part<NKT, split_kt0(NKT, S, 1), split_nk(NKT, S, 1)>(Ks, Ks + MAT, qc, N, sc2, fr, g, o, mxs);
-        else if (j == 2) l = eaf_part<NKT, split_kt0(NKT, S, 2 % S), split_nk(NKT, S, 2 % S)>(Ks, Ks + MAT, qc, N, sc2, fr, g, o, mxs);
-        else l = eaf_part<NKT, split_kt0(NKT, S, 3 % S), split_nk(NKT, S, 3 % S)>(Ks, Ks + MAT, qc, N, sc2, fr, g, o, mxs);
-        char* pj = parts + ((k & 1) * S + j) * EAF_PART_BYTES;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) *(f32x4*)(pj + (dt * 64 + lane) * 16) = o[dt];
-        *(float2*)(pj + 64 * 64 + lane * 8) = make_float2(mxs, l);
-      }
-      prev = it;
-    }
-    // the last item's split tile (every wave's partial written before this barrier)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (j == 0 && prev >= 0) merge_store(prev, ((prev - (int)blockIdx.x) / G) & 1, true);
-    return;
-  }
-  for (int k = 0; it < items; ++k, it += G) {
-    item_top(k);
     bf16x8 qc[NQW][2];
 #pragma unroll
     for (int qi = 0; qi < NQW; ++qi) qc[qi][0] = qn[qi][0], qc[qi][1] = qn[qi][1];
     if (it + G < items) issue(it + G, (k + 1) & 1);
     const char* Ks = smem + (k & 1) * 2 * MAT;
+    const int b = it / H, h = it - b * H;
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(out + (long)b * N * out_ld, 0, (int)(N * out_ld * 2), 0x00020000);
 #pragma unroll
     for (int qi = 0; qi < NQW; ++qi) {
       const int qt = wave + NW * qi;
       f32x4 o[4] = {};
       float l = 1.f;
       if (qt < NKT) l = eaf_tile<NKT>(Ks, Ks + MAT, qc[qi], N, sc2, fr, g, o);  // (uniform per wave)
-      store_tile(it, qt, o, l, true);
+      const float inv = 1.f / l;
+      const int qq = qt * 16 + fr;
+      const bool odd = g & 1;
+      // 16-byte stores: lanes g (even) and g + 1 hold d = 16 dt + 4 g .. + 7 of d-tiles dt and dt + 1
+      const uint32_t ob = (uint32_t)((qq * out_ld + h * 64 + 4 * g) * 2);
+#pragma unroll
+      for (int dt = 0; dt < 4; dt += 2) {
+        const u32x2 a0 = pack16x4<true>(o[dt] * inv), a1 = pack16x4<true>(o[dt + 1] * inv);
+        const u32x2 snd = odd ? a0 : a1;
+        const u32x2 rcv = {xor16_partner(snd[0]), xor16_partner(snd[1])};
+        const u32x4 w = odd ? (u32x4){rcv[0], rcv[1], a1[0], a1[1]} : (u32x4){a0[0], a0[1], rcv[0], rcv[1]};
+        const uint32_t off = ob + (uint32_t)((odd ? (dt + 1) * 16 - 4 : dt * 16) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(w, ro, qq < N ? off : 0x80000000u, 0, 0);
+      }
     }
-  }
-  if constexpr (S > 0) {  // (the split waves' final merge barrier)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
   }
 }
 
@@ -1116,7 +958,7 @@ hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf1
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         return hipErrorInvalidValue;
       const hipError_t e = hipFuncSetAttribute((const void*)enc_attention_pers_kernel<NKT, PNW>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, eaf_pers_lds<NKT, PNW>());
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 2 * lds);
       if (e != hipSuccess) {
         cus = 0;
         return e;
@@ -1125,8 +967,7 @@ hipError_t run_enc_full(const bf16_t* qkv, int B, int N, int H, float scale, bf1
     // one 16-wave workgroup per CU: under an encoder CU budget (a CU-masked stream, icap_set_encoder_cus) only that
     // many fit at once - a larger grid would run its surplus workgroups as a second round
     const int items = B * H, blocks = max_grid > 0 ? std::min(max_grid, cus) : cus;
-    constexpr int plds = eaf_pers_lds<NKT, PNW>();
-    hipLaunchKernelGGL((enc_attention_pers_kernel<NKT, PNW>), dim3(std::min(items, blocks)), dim3(PNW * 64), plds, s,
+    hipLaunchKernelGGL((enc_attention_pers_kernel<NKT, PNW>), dim3(std::min(items, blocks)), dim3(PNW * 64), 2 * lds, s,
                        qkv, N, H, items, scale, out, out_ld);
     return hipGetLastError();
   }

@@ -196,6 +196,7 @@ hipError_t run(const GemmArgs& g, hipStream_t s) {
 #define ICAP_F16H 0
 #endif
 #if ICAP_F16H  // (a product build without the form compiles none of its kernels)
+#include "gemm_variants.h"
 // the f16h form's 32-bit offsets: A / W stage pieces (rows up to a whole tile past M) and the epilogue's byte range
 bool f16h_ok(const GemmArgs& g) {
   const bool res = g.out == OUT_F32_RESID;
@@ -855,7 +856,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, F16P_LDS_SO);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)gemm_f16p_kernel<2, 0, 224>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              f16p_lds(224));
+                              2 * (224 * 128 + 256 * 128) + 2048);
     if (e != hipSuccess) {
       cus = 0;
       return e;
@@ -879,7 +880,7 @@ hipError_t launch_gemm_256_(const GemmArgs& g, hipStream_t s) {
       if (g.out == OUT_F32_RESID) {
         const int tiles224 = (g.N / 256) * ((g.M + 223) / 224);
         hipLaunchKernelGGL((gemm_f16p_kernel<2, 0, 224>), dim3(std::min(tiles224, blocks)), dim3(512),
-                           f16p_lds(224), s, g);
+                           2 * (224 * 128 + 256 * 128) + 2048, s, g);
       } else {
         const int tiles = (g.N / 256) * ((g.M + 255) / 256);
         hipLaunchKernelGGL(gemm_f16p_kernel<1>, dim3(std::min(tiles, blocks)), dim3(512), F16P_LDS_SO, s, g);

@@ -7,6 +7,7 @@
 #error "gemm_tools.hip belongs to the tools build only (-DICAP_TOOLS)"
 #endif
 #include "gemm_kern.h"
+#include "gemm_variants.h"
 
 #include <algorithm>
 
@@ -408,7 +409,7 @@ bool launch_gemm_256_tools(const GemmArgs& g, hipStream_t s, int cus, hipError_t
     return e == hipSuccess;
   };
   constexpr int lds2 = 3 * 3 * 256 * 32 * 2, lds1 = 4 * 2 * 256 * 32 * 2;
-  constexpr int LP = F16P_LDS_SO, LP224 = f16p_lds(224);
+  constexpr int LP = F16P_LDS_SO, LP224 = 2 * (224 * 128 + 256 * 128) + 2048;
   if (g.f16) {
     // ICAP_F16_GEMM: 1 / 2 = 256 x 256 8-phase (64-B / 128-B LDS rows); 3 / 4 = 128 x 256 tiles with 64-deep
     // stages, 2 / 3 stages; 5 = 256 x 256 tiles, 64-deep stages; 6 = persistent for every fp16 GEMM

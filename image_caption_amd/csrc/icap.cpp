@@ -15,9 +15,6 @@
 #include <string>
 #include <vector>
 
-#ifndef ICAP_LN_FOLD
-#define ICAP_LN_FOLD 0  // the f16 encoder's LayerNorm fold: measured slower; variant builds only
-#endif
 
 #include "../../include/icap.h"
 #include "kernels.h"
@@ -96,10 +93,6 @@ struct VitLayer {
   LN ln1, ln2;
   Lin qkv, out, mlp0, mlp3;
   Lin8 qkv8, mlp08, mlp38;
-  // f16 LayerNorm fold (round 6): W' = fp16(W gamma) with bias c = W beta + b, and s = row sums of W' (ln_1 into QKV,
-  // ln_2 into MLP-1; rows.hip launch_ln_fold_weights)
-  Lin qkvF, mlp0F;
-  float *qkv_s = nullptr, *mlp0_s = nullptr;
 };
 struct EncLayer {
   Lin qkv, out, lin1, lin2;
@@ -190,9 +183,6 @@ struct icap_handle {
   bool i8 = false;  // ICAP_PREC_I8X2: LayerNorm-fed ViT GEMMs on int8 two-slice operands
   bool i8k = false;  // ... and MLP-2 on the block-scaled int8 GELU output (ICAP_I8_MLP2=1, opt-in)
   bool f16 = false;  // ICAP_PREC_F16: the ViT encoder on single fp16 planes (fp16 MFMA); the decoder stays bf16x2
-  // f16 ViT encoder: the pre-LayerNorms folded into the QKV / MLP-1 GEMMs (round 6; the compile-time
-  // default ICAP_LN_FOLD selects it, variant builds A/B it)
-  bool ln_fold = ICAP_LN_FOLD;
   // ICAP_PREC_F16 on a Grid model: the eval ResNet trunk on fp16 planes - the residual stream as one fp16 plane in
   // layer1-2 and as fp16 hi/lo planes (~22 bits) in layer3-4, the bottleneck branch (conv1 / conv2 outputs) as one
   // fp16 plane, fp16 weights and MFMA (encode_grid); the tail and the decoder stay bf16x2, train-mode
@@ -265,10 +255,8 @@ struct icap_handle {
 
   // workspaces
   DevBuf e_split, e_scnt;  // GEMM tail split: partial tiles + tickets (zero at rest)
-  DevBuf e_sk, e_skc;      // stream-K fp16 encoder GEMMs: partial tiles + (ticket, ready) words (zero at rest)
   int split_slots = -1;     // block slots per XCD of the 128 x 256 GEMM (2 per CU); 0 = tail split off
   DevBuf e_x, e_a, e_qkv, e_h, e_patch, e_sa, e_hs;  // encoder (e_sa: int8 row scales, e_hs: MLP block scales)
-  DevBuf e_xh, e_lnp, e_ab;  // f16 LayerNorm fold: fp16 copy of x, (mean, M2) per 64-column group, (a, b) per row
   DevBuf t_x, t_y, t_1, t_2, t_r, t_col;  // ResNet trunk (NHWC planes)
   DevBuf t_bn;                            // train-mode BatchNorm: partial sums + scale / shift
   // decoder workspaces, one set per decode mode (0: greedy / beam / teacher-forced, 1: sampled), so
@@ -312,7 +300,7 @@ struct icap_handle {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col, &t_bn}) b->release();
-    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt, &e_sk, &e_skc, &rflag,
+    for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt, &rflag,
                       &step_layers})
       b->release();
     for (int i = 0; i < 2; ++i) {
@@ -393,17 +381,6 @@ struct icap_handle {
   }
   LN ln(const icap_ln_w& p, int D, hipStream_t s) { return LN{own_f32(p.w, D, s), own_f32(p.b, D, s)}; }
   // nn.Linear fed by LayerNorm ln, folded (f16 encoder): fp16 W' = W diag(gamma), bias c = W beta + b, *sum = row sums of W'
-  Lin fold_lin(const float* w, const float* b, const icap_ln_w& ln, int N, int K, hipStream_t s, float** sum) {
-    REQUIRE(w && ln.w && ln.b, "missing parameter pointer");
-    Lin l;
-    l.w = (bf16_t*)alloc((size_t)N * K * 2);
-    l.b = (float*)alloc((size_t)N * 4);
-    *sum = (float*)alloc((size_t)N * 4);
-    HIPCHK(launch_ln_fold_weights(w, b, ln.w, ln.b, N, K, l.w, l.b, *sum, s));
-    l.N = N;
-    l.K = K;
-    return l;
-  }
   Conv pack_conv(const icap_conv_bn_w& c, hipStream_t s) {
     REQUIRE(c.w && c.bn_w && c.bn_b && c.bn_mean && c.bn_var, "missing trunk parameter pointer");
     REQUIRE(c.cout % 64 == 0 && c.k % 2 == 1 && (c.stride == 1 || c.stride == 2), "unsupported trunk conv");
@@ -458,42 +435,6 @@ struct icap_handle {
     g.epi = epi; g.out = out;
     g.range_flag = range_word();
     g.max_grid = enc_cus;
-    stream_k(g);
-    run_gemm(g, s);
-  }
-  // the persistent fp16 GEMMs' stream-K workspace (gemm_kern.h ICAP_F16P_SK), allocated on first use (the encoder is
-  // never captured); tickets zeroed once, every launch leaves them zero
-  void stream_k(GemmArgs& g) {
-    if (!ICAP_F16P_SK) return;  // (the product: whole tiles)
-#ifdef ICAP_SK_HOST_OFF  // measurement variant: the kernels' stream-K code compiled in, never engaged
-    return;
-#endif
-    if (!e_skc.p) {
-      e_sk.ensure(F16P_SK_WS_BYTES);
-      e_skc.ensure((size_t)F16P_SK_CNT_INTS * 4);
-      HIPCHK(hipMemset(e_skc.p, 0, e_skc.n));
-    }
-    g.sk_ws = e_sk.as<float>();
-    g.sk_cnt = e_skc.as<int>();
-  }
-  // the LayerNorm fold's GEMMs: store-only with ab / sum (A = the fp16 copy xh, W folded), or residual leaving xh and the
-  // group partials (kernels.h GemmArgs::xh / ln_*)
-  void gemm16_fold(const bf16_t* A, long lda, const Lin& W, int M, void* C, long ldc, int epi, int out, hipStream_t s,
-                   int hm_n, const float* ab, const float* sum, bf16_t* xh, float* part) {
-    GemmArgs g = gemm_args();
-    g.hm_n = hm_n;
-    g.A = A; g.lda = lda;
-    g.W = W.w; g.ldw = W.K;
-    g.bias = W.b;
-    g.C = C; g.ldc = ldc;
-    g.M = M; g.N = W.N; g.K = W.K; g.nsplit = 1; g.c_planes = 1; g.f16 = 1;
-    g.epi = epi; g.out = out;
-    g.range_flag = range_word();
-    g.max_grid = enc_cus;
-    g.ln_ab = ab; g.ln_sum = sum; g.xh = xh; g.ln_part = part;
-    if (xh) g.c_lo = (long)M * ldc;  // the residual stream's lo plane (fold: C itself is not read or written)
-    REQUIRE(gemm_f16_persistent(g), "LayerNorm fold: the persistent fp16 GEMM form only");
-    stream_k(g);
     run_gemm(g, s);
   }
   // residual-output GEMMs (N = 768 / 512: a partial last round of tiles) split their tail tiles in K when
@@ -661,10 +602,6 @@ void pack(icap_handle* h, hipStream_t s, int parts = ICAP_PART_DECODER | ICAP_PA
       o.ln2 = h->ln(L.ln_2, V, s);
       o.mlp0 = h->lin(L.mlp0_w, L.mlp0_b, d.vit_mlp, V, s, hf);
       o.mlp3 = h->lin(L.mlp3_w, L.mlp3_b, V, d.vit_mlp, s, hf);
-      if (hf && ICAP_LN_FOLD) {
-        o.qkvF = h->fold_lin(L.attn.in_w, L.attn.in_b, L.ln_1, 3 * V, V, s, &o.qkv_s);
-        o.mlp0F = h->fold_lin(L.mlp0_w, L.mlp0_b, L.ln_2, d.vit_mlp, V, s, &o.mlp0_s);
-      }
       if (h->i8) {
         o.qkv8 = h->lin8(L.attn.in_w, L.attn.in_b, 3 * V, V, s);
         o.mlp08 = h->lin8(L.mlp0_w, L.mlp0_b, d.vit_mlp, V, s);
@@ -752,41 +689,6 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
     h->run_gemm(ga, s);
   }
   HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
-  if (ICAP_LN_FOLD && h->ln_fold && V == 768 && M >= 256) {  // (M < 256: the GEMMs are not the persistent form)
-    // the pre-LayerNorms folded into QKV / MLP-1 (kernels.h GemmArgs::ln_*): layer 0's input rows give xh and (a, b)
-    // directly; every residual GEMM then leaves the next xh and its 12 group partials, turned into (a, b) by one small
-    // pass (ln_fold_stats_kernel) - no LayerNorm pass per sub-layer
-    const int G = V / 64;
-    h->e_xh.ensure((size_t)M * V * 2 * 2);  // the residual stream's hi and lo fp16 planes
-    h->e_lnp.ensure((size_t)G * M * 8);
-    h->e_ab.ensure((size_t)(M + 256) * 8);
-    bf16_t* xh = h->e_xh.as<bf16_t>();
-    float *part = h->e_lnp.as<float>(), *ab = h->e_ab.as<float>();
-    const long xl = (long)M * V;
-    HIPCHK(launch_ln_fold_rows(x, M, V, 1e-6f, xh, xl, ab, rf, s));
-    for (size_t li = 0; li < h->vit.size(); ++li) {
-      const VitLayer& L = h->vit[li];
-      const bool last = li + 1 == h->vit.size();
-      h->prof_layer(li);
-      h->gemm16_fold(xh, V, L.qkvF, M, qkv, 3 * V, EPI_NONE, OUT_SPLIT, s, hm, ab, L.qkv_s, nullptr, nullptr);
-      {
-        const double flops = 4.0 * B * d.vit_heads * (double)T * T * 64;
-        const double bytes = 2.0 * B * (double)T * V * 4;
-        h->timed(PROF_ENC_ATTN, flops, bytes, s, [&] {
-          HIPCHK(launch_enc_attention(qkv, 3 * V, 0, B, T, d.vit_heads, 0.125f, a, V, 0, NS_F16, s, 1, h->enc_cus));
-        });
-      }
-      h->gemm16_fold(a, V, L.out, M, x, V, EPI_NONE, OUT_F32_RESID, s, 0, nullptr, nullptr, xh, part);
-      HIPCHK(launch_ln_fold_stats(part, G, M, V, 1e-6f, ab, s));
-      h->gemm16_fold(xh, V, L.mlp0F, M, hb, F, EPI_GELU, OUT_SPLIT, s, 0, ab, L.mlp0_s, nullptr, nullptr);
-      h->gemm16_fold(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s, 0, nullptr, nullptr, xh, part);
-      if (!last) HIPCHK(launch_ln_fold_stats(part, G, M, V, 1e-6f, ab, s));
-    }
-    h->prof_gate = true;
-    HIPCHK(launch_layernorm_hilo(xh, xl, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, a, rf, s));
-    h->gemm16(a, V, h->proj, B * np, memory, Dm, EPI_NONE, OUT_F32, s);
-    return;
-  }
   for (size_t li = 0; li < h->vit.size(); ++li) {
     const VitLayer& L = h->vit[li];
     h->prof_layer(li);

@@ -93,30 +93,7 @@ struct GemmArgs {
   // stream owns (batch pipelining, icap_set_encoder_cus)
   int max_grid;
   int no_pre;     // tools (ICAP_CONV_PRE=0): the 64-deep conv forms load the residual after the k-loop
-  // LayerNorm fold (round 6; the f16 ViT encoder, gemm_f16p_kernel only - rows.hip launch_ln_fold_*):
-  //  residual form (out = OUT_F32_RESID), xh != nullptr: the epilogue also stores fp16(C) at xh[row * ldc + col] and
-  //    each (row, 64-column group)'s (mean, M2) of the new C row at ln_part[(col / 64) * M + row] (float2);
-  //  store-only form, ln_ab != nullptr: A is such an xh and the epilogue computes acc a_r - b_r ln_sum[col] +
-  //    bias[col] with (a_r, b_r) = ln_ab[row] (float2) - LN(x) W^T + b with W = W' / gamma, bias = W beta + b
-  bf16_t* xh;
-  float* ln_part;
-  const float* ln_ab;
-  const float* ln_sum;
-  // stream-K (round 6; gemm_f16p_kernel, gemm_kern.h ICAP_F16P_SK): fp32 partial tiles of the tiles split between two
-  // blocks (F16P_SK_WS_BYTES) and their (ticket, ready) words (F16P_SK_CNT_INTS, zero at rest); nullptr = whole tiles
-  float* sk_ws;
-  int* sk_cnt;
 };
-// ICAP_F16P_SK (round 6, variant builds: -DICAP_F16P_SK=1 for gemm.hip and icap.cpp): stream-K scheduling of the
-// persistent fp16 GEMMs (gemm_kern.h; measured slower); 0 = whole tiles, no workspace
-#ifndef ICAP_F16P_SK
-#define ICAP_F16P_SK 0
-#endif
-// stream-K workspace: 8 XCDs x F16P_SK_VB lane boundaries, one 512-thread fp32 accumulator image (<= 256 KiB) each
-constexpr int F16P_SK_VB = 32;  // virtual lanes per XCD (the schedule, and so the sums, do not depend on the grid)
-constexpr long F16P_SK_SLOT = 512L * 32 * 4;  // floats per partial tile (512 threads x 32 f32x4)
-constexpr size_t F16P_SK_WS_BYTES = (size_t)8 * F16P_SK_VB * F16P_SK_SLOT * 4;
-constexpr int F16P_SK_CNT_INTS = 8 * F16P_SK_VB * 2;
 // bytes of split_ws for split_slots block slots per XCD
 inline size_t gemm_split_ws_bytes(int split_slots) { return (size_t)8 * split_slots * 2 * 128 * 256 * 4; }
 inline GemmArgs gemm_args() { GemmArgs g{}; g.batch = 1; g.nsplit = 1; g.c_planes = 2; g.res_planes = 2; return g; }
@@ -390,17 +367,6 @@ hipError_t launch_embed(const int32_t* tok, long tok_ld, int fixed_tok, int rows
 // re-applied on the second replay of the sampled-decode graph, ROCm 7.2)
 hipError_t launch_fill_u8(uint8_t* p, long n, uint8_t value, hipStream_t s);
 hipError_t launch_fill_col(int32_t* ids, int B, long ld, int col, int value, hipStream_t s);
-// LayerNorm fold of the f16 ViT encoder (round 6, rows.hip): folded weights W' = fp16(W gamma), c = W beta + b,
-// s = row sums of W'; (a, b) = (rstd, rstd mean) per row from the residual epilogues' per-group (mean, M2) partials
-// part[G][rows] (float2), or straight from x rows (layer 0: also the fp16 copy xh)
-hipError_t launch_ln_fold_weights(const float* W, const float* b, const float* gamma, const float* beta, int N, int K,
-                                  bf16_t* wp, float* c, float* sum, hipStream_t s);
-hipError_t launch_ln_fold_stats(const float* part, int G, int rows, int D, float eps, float* ab, hipStream_t s);
-hipError_t launch_ln_fold_rows(const float* x, int rows, int D, float eps, bf16_t* xh, long xl, float* ab,
-                               unsigned* range_flag, hipStream_t s);
-hipError_t launch_layernorm_hilo(const bf16_t* xh, long xl, int rows, int D, int in_group, long in_stride, long in_off,
-                                 const float* w, const float* b, float eps, float* out_f32, bf16_t* out_h,
-                                 unsigned* range_flag, hipStream_t s);
 // stop-aware decode (round 6): flag (host-mapped) = 1 when a column in [col0, col1) is all end (greedy) or every fin row
 // is set (fin != nullptr); the tail fill of a stopped decode (ids columns > t0 = end, logp steps >= t0 = 0)
 hipError_t launch_stop_scan(const int32_t* ids, int B, long ld, int col0, int col1, int end, const uint8_t* fin,

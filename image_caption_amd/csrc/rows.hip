@@ -75,155 +75,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   if (range_flag && __any(bad) && lane == 0) range_flag_set(range_flag);
 }
 
-// ---- LayerNorm fold of the f16 ViT encoder (round 6; measured slower, variant builds only:
-// -DICAP_LN_FOLD=1 for gemm.hip, icap.cpp and rows.hip) ----
-#ifndef ICAP_LN_FOLD
-#define ICAP_LN_FOLD 0
-#endif
-#if ICAP_LN_FOLD
-// LN(x) W^T + b = rstd (x W'^T) - rstd mu s + c with W' = W diag(gamma), s_n = sum_k W'_nk, c = W beta + b: the GEMM
-// reads the residual stream's fp16 copy xh and applies the row's (a, b) = (rstd, rstd mu) in its epilogue, so the
-// pre-LayerNorms run no pass of their own.
-
-// Weights: W' = fp16(W gamma) [N][K], s = row sums of the fp16 W' values (what the GEMM multiplies), c = W beta + b;
-// one 256-thread block per row n, fixed-order sums
-__global__ __launch_bounds__(256) void ln_fold_weights_kernel(const float* __restrict__ W, const float* __restrict__ b,
-                                                              const float* __restrict__ gamma,
-                                                              const float* __restrict__ beta, int K, bf16_t* wp,
-                                                              float* c, float* sum) {
-  __shared__ float red[2][4];
-  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float ss = 0.f, cc = 0.f;
-  for (int k = tid; k < K; k += 256) {
-    const float w = W[(long)n * K + k];
-    const bf16_t h = f2h(w * gamma[k]);
-    wp[(long)n * K + k] = h;
-    ss += h2f(h);
-    cc += w * beta[k];
-  }
-  ss = wave_sum(ss);
-  cc = wave_sum(cc);
-  if (lane == 0) red[0][wave] = ss, red[1][wave] = cc;
-  __syncthreads();
-  if (tid == 0) {
-    sum[n] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    c[n] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]) + (b ? b[n] : 0.f);
-  }
-}
-
-// A row's normalisation from G equal groups of D / G columns: mean_g and M2_g = sum (x - mean_g)^2 per group
-// (Chan et al.'s pairwise combination: no E[x^2] - mu^2 cancellation); out (a, b) = (rstd, rstd mu) as the
-// layernorm_kernel computes them (biased variance, 1 / sqrtf(var + eps))
-__device__ __forceinline__ float2 ln_fold_ab(const float2* grp, int G, int D, float eps) {
-  float mu = 0.f;
-  for (int g = 0; g < G; ++g) mu += grp[g].x;
-  mu /= (float)G;
-  float m2 = 0.f;
-  const float per = (float)(D / G);
-  for (int g = 0; g < G; ++g) {
-    const float d = grp[g].x - mu;
-    m2 += grp[g].y + per * d * d;
-  }
-  const float rstd = 1.0f / sqrtf(m2 / (float)D + eps);
-  return make_float2(rstd, rstd * mu);
-}
-
-// The encoder's final LayerNorm over the hi / lo residual planes (the fold's stream), layernorm_kernel's arithmetic:
-// rows grouped as (row / in_group) * in_stride + in_off + row % in_group (the patch rows, no class token)
-template <int PER>
-__global__ __launch_bounds__(256) void layernorm_hilo_kernel(const bf16_t* __restrict__ xh, long xl, int rows,
-                                                             int in_group, long in_stride, long in_off,
-                                                             const float* __restrict__ w, const float* __restrict__ b,
-                                                             float eps, float* out_f32, bf16_t* out_h,
-                                                             unsigned* range_flag) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  constexpr int D = PER * 64;
-  const long irow = (long)(row / in_group) * in_stride + in_off + row % in_group;
-  float v[PER];
-#pragma unroll
-  for (int c = 0; c < PER / 4; ++c) {
-    const bf16_t* hp = xh + irow * D + c * 256 + lane * 4;
-    const u32x2 h = *(const u32x2*)hp, l = *(const u32x2*)(hp + xl);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t hw = h[k >> 1] >> ((k & 1) * 16), lw = l[k >> 1] >> ((k & 1) * 16);
-      v[c * 4 + k] = h2f((bf16_t)(hw & 0xffff)) + h2f((bf16_t)(lw & 0xffff));
-    }
-  }
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) s += v[i];
-  const float mean = wave_sum(s) / (float)D;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) { const float d = v[i] - mean; q += d * d; }
-  const float var = wave_sum(q) / (float)D;
-  const float rstd = 1.0f / sqrtf(var + eps);
-  bool bad = false;
-#pragma unroll
-  for (int c = 0; c < PER / 4; ++c) {
-    const int col = c * 256 + lane * 4;
-    f32x4 wv = *(const f32x4*)(w + col), bv = *(const f32x4*)(b + col), y;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) y[k] = (v[c * 4 + k] - mean) * rstd * wv[k] + bv[k];
-    if (out_f32) *(f32x4*)(out_f32 + (long)row * D + col) = y;
-    const u32x2 pk = pack16x4<true>(y);
-    bad |= f16_pair_nonfinite(pk[0]) || f16_pair_nonfinite(pk[1]);
-    *(u32x2*)(out_h + (long)row * D + col) = pk;
-  }
-  if (range_flag && __any(bad) && lane == 0) range_flag_set(range_flag);
-}
-
-// The residual GEMMs' epilogues leave per (row, 64-column group) (mean_g, M2_g) in part[g][rows]; one thread per row
-__global__ __launch_bounds__(256) void ln_fold_stats_kernel(const float2* __restrict__ part, int G, int rows, int D,
-                                                            float eps, float2* ab) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  float2 grp[16];
-  for (int g = 0; g < G; ++g) grp[g] = part[(long)g * rows + r];
-  ab[r] = ln_fold_ab(grp, G, D, eps);
-}
-
-// Layer 0's input (the patch embedding + class token + position rows): the fp16 copy xh and (a, b) directly, one
-// wave per row (layernorm_kernel's statistics); xh values that overflow fp16 set the range word
-template <int PER>
-__global__ __launch_bounds__(256) void ln_fold_rows_kernel(const float* __restrict__ x, int rows, float eps,
-                                                           bf16_t* xh, long xl, float2* ab, unsigned* range_flag) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  constexpr int D = PER * 64;
-  const float* xr = x + (long)row * D;
-  float v[PER];
-  bool bad = false;
-#pragma unroll
-  for (int c = 0; c < PER / 4; ++c) {
-    const f32x4 t = *(const f32x4*)(xr + c * 256 + lane * 4);
-    v[c * 4 + 0] = t[0]; v[c * 4 + 1] = t[1]; v[c * 4 + 2] = t[2]; v[c * 4 + 3] = t[3];
-    const u32x2 pk = pack16x4<true>(t);
-    bad |= f16_pair_nonfinite(pk[0]) || f16_pair_nonfinite(pk[1]);
-    bf16_t* hp = xh + (long)row * D + c * 256 + lane * 4;
-    *(u32x2*)hp = pk;
-    const f32x4 hv = {h2f((bf16_t)(pk[0] & 0xffff)), h2f((bf16_t)(pk[0] >> 16)), h2f((bf16_t)(pk[1] & 0xffff)),
-                      h2f((bf16_t)(pk[1] >> 16))};
-    *(u32x2*)(hp + xl) = pack16x4<true>(t - hv);  // the lo plane: the residual stream as fp16 hi / lo from here on
-  }
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) s += v[i];
-  const float mean = wave_sum(s) / (float)D;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) { const float d = v[i] - mean; q += d * d; }
-  const float var = wave_sum(q) / (float)D;
-  const float rstd = 1.0f / sqrtf(var + eps);
-  if (lane == 0) ab[row] = make_float2(rstd, rstd * mean);
-  if (range_flag && __any(bad) && lane == 0) range_flag_set(range_flag);
-}
-#endif  // ICAP_LN_FOLD
-
 // layernorm_kernel's row statistics, output as int8 two-slice planes + the row scale (one wave per row)
 template <int PER>
 __global__ __launch_bounds__(256) void layernorm_i8_kernel(const float* __restrict__ x, long ldx, int rows,
@@ -637,48 +488,6 @@ hipError_t launch_fill_u8(uint8_t* p, long n, uint8_t value, hipStream_t s) {
   hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, value);
   return hipGetLastError();
 }
-
-#if ICAP_LN_FOLD
-hipError_t launch_ln_fold_weights(const float* W, const float* b, const float* gamma, const float* beta, int N, int K,
-                                  bf16_t* wp, float* c, float* sum, hipStream_t s) {
-  if (!W || !gamma || !beta || N <= 0 || K <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ln_fold_weights_kernel, dim3(N), dim3(256), 0, s, W, b, gamma, beta, K, wp, c, sum);
-  return hipGetLastError();
-}
-
-hipError_t launch_ln_fold_stats(const float* part, int G, int rows, int D, float eps, float* ab, hipStream_t s) {
-  if (G <= 0 || G > 16 || D % G || rows <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ln_fold_stats_kernel, dim3((rows + 255) / 256), dim3(256), 0, s, (const float2*)part, G, rows, D,
-                     eps, (float2*)ab);
-  return hipGetLastError();
-}
-
-hipError_t launch_ln_fold_rows(const float* x, int rows, int D, float eps, bf16_t* xh, long xl, float* ab,
-                               unsigned* range_flag, hipStream_t s) {
-  if (D != 768 || rows <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ln_fold_rows_kernel<12>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, eps, xh, xl, (float2*)ab,
-                     range_flag);
-  return hipGetLastError();
-}
-
-hipError_t launch_layernorm_hilo(const bf16_t* xh, long xl, int rows, int D, int in_group, long in_stride, long in_off,
-                                 const float* w, const float* b, float eps, float* out_f32, bf16_t* out_h,
-                                 unsigned* range_flag, hipStream_t s) {
-  if (D != 768 || rows <= 0 || in_group <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(layernorm_hilo_kernel<12>, dim3((rows + 3) / 4), dim3(256), 0, s, xh, xl, rows, in_group, in_stride,
-                     in_off, w, b, eps, out_f32, out_h, range_flag);
-  return hipGetLastError();
-}
-#else  // the product build: the fold's entry points refuse (icap.cpp never takes the fold path there)
-hipError_t launch_ln_fold_weights(const float*, const float*, const float*, const float*, int, int, bf16_t*, float*,
-                                  float*, hipStream_t) { return hipErrorInvalidValue; }
-hipError_t launch_ln_fold_stats(const float*, int, int, int, float, float*, hipStream_t) { return hipErrorInvalidValue; }
-hipError_t launch_ln_fold_rows(const float*, int, int, float, bf16_t*, long, float*, unsigned*, hipStream_t) {
-  return hipErrorInvalidValue;
-}
-hipError_t launch_layernorm_hilo(const bf16_t*, long, int, int, int, long, long, const float*, const float*, float,
-                                 float*, bf16_t*, unsigned*, hipStream_t) { return hipErrorInvalidValue; }
-#endif
 
 hipError_t launch_stop_scan(const int32_t* ids, int B, long ld, int col0, int col1, int end, const uint8_t* fin,
                             int* flag, hipStream_t s) {

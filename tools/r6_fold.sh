@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: the variant this script measured was removed from the sources after the measurement - see DESIGN.md;
+# build it from the commit named there to rerun.)
 # Round 6: the LayerNorm fold - the encoder / workload parity tests on the tree's library (fold on), then bench lines
 # alternating fold on / off (tools/ab/libicap_nofold.so).
 set -o pipefail

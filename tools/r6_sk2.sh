@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: the variant this script measured was removed from the sources after the measurement - see DESIGN.md;
+# build it from the commit named there to rerun.)
 # Round 6: where stream-K's time goes - per-launch encoder GEMM durations of one bench step (kernel trace, first ViT
 # layer of the last step) for stream-K on / compiled-in but off / not compiled, then bench lines.
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: the variant this script measured was removed from the sources after the measurement - see DESIGN.md;
+# build it from the commit named there to rerun.)
 # Round 6: stream-K timing ablation - per-launch encoder GEMM durations (first ViT layer of a bench step) with the
 # partial exchange removed (ICAP_SK_ABL=2: wrong sums, timing only) against stream-K and whole tiles.
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Historical: the variant this script measured was removed from the sources after the measurement - see DESIGN.md;
+# build it from the commit named there to rerun.)
 # Round 6: the split last query tile of the persistent encoder attention - op and workload parity on the tree's library,
 # then kernel stats and bench lines against the unsplit form (tools/ab/libicap_nosplit.so).
 set -o pipefail
