@@ -257,6 +257,10 @@ struct icap_handle {
   DevBuf e_split, e_scnt;  // GEMM tail split: partial tiles + tickets (zero at rest)
   int split_slots = -1;     // block slots per XCD of the 128 x 256 GEMM (2 per CU); 0 = tail split off
   DevBuf e_x, e_a, e_qkv, e_h, e_patch, e_sa, e_hs;  // encoder (e_sa: int8 row scales, e_hs: MLP block scales)
+  // the f16 ViT encoder's second half batch (encode_vit: two halves on two streams) - its own residual stream, planes
+  DevBuf e2_x, e2_a, e2_qkv, e2_h, e2_patch;
+  hipStream_t enc_aux = nullptr;
+  hipEvent_t enc_fork = nullptr, enc_join = nullptr;
   DevBuf t_x, t_y, t_1, t_2, t_r, t_col;  // ResNet trunk (NHWC planes)
   DevBuf t_bn;                            // train-mode BatchNorm: partial sums + scale / shift
   // decoder workspaces, one set per decode mode (0: greedy / beam / teacher-forced, 1: sampled), so
@@ -301,8 +305,11 @@ struct icap_handle {
     for (void* p : owned) (void)hipFree(p);
     for (DevBuf* b : {&t_x, &t_y, &t_1, &t_2, &t_r, &t_col, &t_bn}) b->release();
     for (DevBuf* b : {&e_x, &e_a, &e_qkv, &e_h, &e_patch, &e_sa, &e_hs, &d_beam, &e_split, &e_scnt, &rflag,
-                      &step_layers})
+                      &step_layers, &e2_x, &e2_a, &e2_qkv, &e2_h, &e2_patch})
       b->release();
+    if (enc_aux) (void)hipStreamDestroy(enc_aux);
+    if (enc_fork) (void)hipEventDestroy(enc_fork);
+    if (enc_join) (void)hipEventDestroy(enc_join);
     for (int i = 0; i < 2; ++i) {
       step_args[i].release();
       step_state[i].release();
@@ -659,37 +666,58 @@ void enc_layer_postln(icap_handle* h, const EncLayer& L, int B, int N, float* x,
 
 // ICAP_PREC_F16 form of encode_vit: every GEMM and the attention on single fp16 planes (fp16 MFMA, fp32
 // accumulate); the residual stream, LayerNorm statistics, softmax and GELU stay fp32.
-void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipStream_t s, float* feats = nullptr) {
-  const icap_model_desc& d = h->d;
-  const int V = d.vit_dim, g = d.image / d.patch, np = g * g, T = np + 1, M = B * T, Dm = d.d_model;
-  const int Kp = 3 * d.patch * d.patch, F = d.vit_mlp;
-  const int hm = T > 64 && T <= 256 ? T : 0;
-  REQUIRE(hm, "ICAP_PREC_F16 encoder needs 64 < tokens <= 256");
-  h->e_patch.ensure((size_t)B * np * Kp * 2);
-  h->e_x.ensure((size_t)M * V * 4);
-  h->e_a.ensure((size_t)M * V * 2);
-  h->e_qkv.ensure((size_t)M * 3 * V * 2);
-  h->e_h.ensure((size_t)M * F * 2);
-  bf16_t *patch = h->e_patch.as<bf16_t>(), *a = h->e_a.as<bf16_t>(), *qkv = h->e_qkv.as<bf16_t>(),
-         *hb = h->e_h.as<bf16_t>();
-  float* x = h->e_x.as<float>();
-  // range guard (DESIGN.md §3, f16 range contract): every LayerNorm and store-only GEMM output is fp16; a value
-  // that overflows (or a non-finite residual row, which any earlier overflow becomes) sets the sticky word
-  unsigned* rf = h->range_word();
-  HIPCHK(launch_im2col_patches(img, B, 3, d.image, d.patch, patch, 0, NS_F16, s));
-  {  // patch-embed GEMM: rows (b, p) -> x[b*T + 1 + p] with conv bias + pos[1 + p]
-    GemmArgs ga = gemm_args();
-    ga.A = patch; ga.lda = Kp;
-    ga.W = h->conv.w; ga.ldw = Kp; ga.bias = h->conv.b;
-    ga.C = x; ga.ldc = V;
-    ga.M = B * np; ga.N = V; ga.K = Kp; ga.nsplit = 1; ga.c_planes = 1; ga.f16 = 1;
-    ga.epi = EPI_NONE; ga.out = OUT_F32;
-    ga.rm_group = np; ga.rm_stride = T; ga.rm_off = 1;
-    ga.addend = h->pos; ga.add_ld = V; ga.add_group = np; ga.add_off = 1;
-    h->run_gemm(ga, s);
+// One f16 ViT encode of B images on stream s (ws = 0: the handle's encoder workspaces, 1: the second half batch's, see
+// encode_vit), in three parts - the prologue (patch embedding, class rows), layer li, the epilogue (final LayerNorm,
+// projection) - so that encode_vit can enqueue two half batches layer by layer.
+struct VitF16Run {
+  icap_handle* h;
+  hipStream_t s;
+  int B, V, np, T, M, Dm, Kp, F, hm;
+  const float* img;
+  float* memory;
+  float* feats;
+  bf16_t *patch, *a, *qkv, *hb;
+  float* x;
+  unsigned* rf;
+  VitF16Run(icap_handle* h_, const float* img_, int B_, float* memory_, hipStream_t s_, float* feats_, int ws)
+      : h(h_), s(s_), B(B_), img(img_), memory(memory_), feats(feats_) {
+    const icap_model_desc& d = h->d;
+    V = d.vit_dim;
+    const int g = d.image / d.patch;
+    np = g * g, T = np + 1, M = B * T, Dm = d.d_model, Kp = 3 * d.patch * d.patch, F = d.vit_mlp;
+    hm = T > 64 && T <= 256 ? T : 0;
+    REQUIRE(hm, "ICAP_PREC_F16 encoder needs 64 < tokens <= 256");
+    DevBuf &wpatch = ws ? h->e2_patch : h->e_patch, &wx = ws ? h->e2_x : h->e_x, &wa = ws ? h->e2_a : h->e_a,
+           &wqkv = ws ? h->e2_qkv : h->e_qkv, &wh = ws ? h->e2_h : h->e_h;
+    wpatch.ensure((size_t)B * np * Kp * 2);
+    wx.ensure((size_t)M * V * 4);
+    wa.ensure((size_t)M * V * 2);
+    wqkv.ensure((size_t)M * 3 * V * 2);
+    wh.ensure((size_t)M * F * 2);
+    patch = wpatch.as<bf16_t>(), a = wa.as<bf16_t>(), qkv = wqkv.as<bf16_t>(), hb = wh.as<bf16_t>();
+    x = wx.as<float>();
+    // range guard (DESIGN.md §3, f16 range contract): every LayerNorm and store-only GEMM output is fp16; a value
+    // that overflows (or a non-finite residual row, which any earlier overflow becomes) sets the sticky word
+    rf = h->range_word();
   }
-  HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
-  for (size_t li = 0; li < h->vit.size(); ++li) {
+  void prologue() {
+    const icap_model_desc& d = h->d;
+    HIPCHK(launch_im2col_patches(img, B, 3, d.image, d.patch, patch, 0, NS_F16, s));
+    {  // patch-embed GEMM: rows (b, p) -> x[b*T + 1 + p] with conv bias + pos[1 + p]
+      GemmArgs ga = gemm_args();
+      ga.A = patch; ga.lda = Kp;
+      ga.W = h->conv.w; ga.ldw = Kp; ga.bias = h->conv.b;
+      ga.C = x; ga.ldc = V;
+      ga.M = B * np; ga.N = V; ga.K = Kp; ga.nsplit = 1; ga.c_planes = 1; ga.f16 = 1;
+      ga.epi = EPI_NONE; ga.out = OUT_F32;
+      ga.rm_group = np; ga.rm_stride = T; ga.rm_off = 1;
+      ga.addend = h->pos; ga.add_ld = V; ga.add_group = np; ga.add_off = 1;
+      h->run_gemm(ga, s);
+    }
+    HIPCHK(launch_cls_rows(h->cls, h->pos, x, B, T, V, s));
+  }
+  void layer(size_t li) {
+    const icap_model_desc& d = h->d;
     const VitLayer& L = h->vit[li];
     h->prof_layer(li);
     HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln1.w, L.ln1.b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s, rf));
@@ -705,18 +733,61 @@ void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipS
     HIPCHK(launch_layernorm(x, V, M, V, 0, 0, 0, L.ln2.w, L.ln2.b, 1e-6f, nullptr, 0, a, V, 0, NS_F16, s, rf));
     h->gemm16(a, V, L.mlp0, M, hb, F, EPI_GELU, OUT_SPLIT, s);
     h->gemm16(hb, F, L.mlp3, M, x, V, EPI_NONE, OUT_F32_RESID, s);
+    h->prof_gate = true;
   }
-  h->prof_gate = true;
-  // final LN on patch rows only (drop CLS), then projection 768 -> d_model
-  HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, V, a, V, 0, NS_F16, s,
-                          rf));
-  h->gemm16(a, V, h->proj, B * np, memory, Dm, EPI_NONE, OUT_F32, s);
+  void epilogue() {  // final LN on patch rows only (drop CLS), then projection 768 -> d_model
+    HIPCHK(launch_layernorm(x, V, B * np, V, np, T, 1, h->vit_ln_w, h->vit_ln_b, 1e-6f, feats, V, a, V, 0, NS_F16, s,
+                            rf));
+    h->gemm16(a, V, h->proj, B * np, memory, Dm, EPI_NONE, OUT_F32, s);
+  }
+};
+void encode_vit_f16(icap_handle* h, const float* img, int B, float* memory, hipStream_t s, float* feats = nullptr) {
+  VitF16Run r(h, img, B, memory, s, feats, 0);
+  r.prologue();
+  for (size_t li = 0; li < h->vit.size(); ++li) r.layer(li);
+  r.epilogue();
 }
 
 // feats (optional): the final-LayerNorm output of the patch tokens, (B, 196, 768) fp32 - the projection's input
+// ICAP_ENC_SPLIT (round 6, variant builds): the f16 encoder runs a batch of B >= ENC_SPLIT_MIN images as two half
+// batches on two streams (the caller's and the handle's enc_aux, forked / joined by events, enqueued layer by layer):
+// one half's kernels fill the other's kernel tails and launch gaps.  Encodes back to back: 12.68-12.74 -> 11.89-11.92
+// ms at B = 256, the memory bit-identical (every output row depends on its own image only); but an encode that follows
+// a decode and a host sync, as every bench / serving step does, gains 0.05-0.25 ms only (tools/r6_enc_time.py), and
+// per-launch timing of overlapping half-batch kernels no longer measures one kernel - off.  Not
+// under an encoder CU budget (icap_set_encoder_cus: the aux stream is not masked).
+#ifndef ICAP_ENC_SPLIT
+#define ICAP_ENC_SPLIT 0
+#endif
+constexpr int ENC_SPLIT_MIN = 64;
 void encode_vit(icap_handle* h, const float* img, int B, float* memory, hipStream_t s, float* feats = nullptr) {
   if (h->f16) {
-    encode_vit_f16(h, img, B, memory, s, feats);
+    if (!ICAP_ENC_SPLIT || B < ENC_SPLIT_MIN || h->enc_cus > 0) {
+      encode_vit_f16(h, img, B, memory, s, feats);
+      return;
+    }
+    const icap_model_desc& d = h->d;
+    const int np = (d.image / d.patch) * (d.image / d.patch), B1 = (B + 1) / 2, B2 = B - B1;
+    if (!h->enc_aux) HIPCHK(hipStreamCreateWithFlags(&h->enc_aux, hipStreamNonBlocking));
+    if (!h->enc_fork) HIPCHK(hipEventCreateWithFlags(&h->enc_fork, hipEventDisableTiming));
+    if (!h->enc_join) HIPCHK(hipEventCreateWithFlags(&h->enc_join, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(h->enc_fork, s));
+    HIPCHK(hipStreamWaitEvent(h->enc_aux, h->enc_fork, 0));
+    // enqueued layer by layer, alternating halves (one half enqueued whole before the other started the second half
+    // only after the first half's ~60 launches: no gain at all in a bench step)
+    VitF16Run r1(h, img, B1, memory, s, feats, 0);
+    VitF16Run r2(h, img + (long)B1 * 3 * d.image * d.image, B2, memory + (long)B1 * np * d.d_model, h->enc_aux,
+                 feats ? feats + (long)B1 * np * d.vit_dim : nullptr, 1);
+    r1.prologue();
+    r2.prologue();
+    for (size_t li = 0; li < h->vit.size(); ++li) {
+      r1.layer(li);
+      r2.layer(li);
+    }
+    r1.epilogue();
+    r2.epilogue();
+    HIPCHK(hipEventRecord(h->enc_join, h->enc_aux));
+    HIPCHK(hipStreamWaitEvent(s, h->enc_join, 0));
     return;
   }
   const icap_model_desc& d = h->d;
