@@ -91,6 +91,28 @@ def test_pipeline_matches_sequential(cuda, vit_sd, B):
         assert torch.equal(a.cpu(), apply_stop_rule(b.long(), 108))
 
 
+def test_profile_sampled_layers(cuda, vit_sd):
+    """Live launch timing (icap_profile_enable, bench.py's roofline): every = 6 brackets ViT encoder layers 0 and 6 only
+    - 8 of the 48 persistent-GEMM launches and 2 of the 12 attentions of an f16 encode at B = 64 - every = 1 all of
+    them, with positive device times; the patch / projection GEMMs (another class) are bracketed either way."""
+    from image_caption_amd import _lib
+    from image_caption_amd.engine import Engine
+
+    eng = Engine(vit_sd, "vit", {}, device=cuda)
+    imgs = torch.from_numpy(W.synthetic_images(64, seed=3)).to(cuda)
+    eng.encode(imgs)
+    for every, gemms, attns in ((1, 48, 12), (6, 8, 2)):
+        eng.profile(True, every=every)
+        eng.encode(imgs)
+        torch.cuda.synchronize()
+        g = eng.profile_read(_lib.PROF_GEMM_F16P)
+        a = eng.profile_read(_lib.PROF_ENC_ATTN)
+        p = eng.profile_read(_lib.PROF_GEMM_256)
+        eng.profile(False)
+        assert (g["launches"], a["launches"], p["launches"]) == (gemms, attns, 2), (every, g, a, p)
+        assert g["ms"] > 0 and a["ms"] > 0
+
+
 def test_cu_masked_pipelines_budget_stack(cuda, vit_sd):
     """CU-masked pipelines (decode_cus) size the engine's encoder grids (GEMMs and, round 6, the persistent encoder
     attention) to the encoder stream's CUs; two overlapping pipelines deleted in either order leave the newest live
