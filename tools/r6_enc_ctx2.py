@@ -15,6 +15,8 @@ from image_caption_amd.engine import Engine
 
 dev = torch.device("cuda", 0)
 eng = Engine(W.to_torch(W.vit_state_dict(0)), "vit", {}, device=dev)
+if os.environ.get("R6_EAGER"):  # eager decode launches (rocprofv3 --pmc crashed on the decode graph's replays)
+    eng.set_graphs(False)
 imgs = torch.from_numpy(W.synthetic_images(256, seed=1)).to(dev)
 m = eng.encode(imgs)
 eng.greedy_raw(m, W.START_TOKEN, W.END_TOKEN, 30)
