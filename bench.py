@@ -167,10 +167,12 @@ def main():
                     help="weights NOT rounded to bf16 (a real fp32 checkpoint): the engine packs the decoder's GEMM weights "
                          "as hi/lo bf16 pairs, which the fused decode blocks carry as lo fragment images "
                          "(config.dec_weight_planes = 2)")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="greedy: overlap the encode of step i+1 with the decode of step i on two streams "
-                         "(image_caption_amd/pipeline.py; measured +2-4 %% with ICAP_DEC_BRANCHES=1, within noise "
-                         "of the default, profiles/r01/v16_pipeline_sweep.txt)")
+    ap.add_argument("--sequential", action="store_true",
+                    help="greedy: run each step's encode, decode and stop rule one after the other (the round-5 "
+                         "line) instead of the default batch pipeline - the encode of batch i+1 on its own stream "
+                         "beside the decode of batch i (image_caption_amd/pipeline.py; round 6: +3.7-4.3 %% on one "
+                         "box, profiles/r06/pipe_ab.txt)")
+    ap.add_argument("--pipeline", action="store_true", help="(the default for greedy; kept for old command lines)")
     args = ap.parse_args()
 
     # BENCH_DIST_BACKEND / BENCH_ONE_DEVICE: rehearsal of the N > 1 flow on a one-GPU box (every rank on cuda:0,
@@ -271,7 +273,8 @@ def main():
             return gid
 
     pipe = None
-    if args.mode == "greedy" and trunk is None and args.pipeline:
+    pipe_ev = []  # pipelined steps: per batch (encode start, end, decode start, end) on the two streams
+    if args.mode == "greedy" and trunk is None and not args.sequential:
         from image_caption_amd.pipeline import CaptionPipeline
 
         dcus = int(os.environ.get("ICAP_PIPE_DECODE_CUS", "0")) or None
@@ -285,7 +288,7 @@ def main():
 
     def run_steps(n):
         if pipe is not None:  # n steps = n batches, encode(i+1) overlapping decode(i)
-            return pipe.run([imgs] * n, post)[-1] if n else None
+            return pipe.run([imgs] * n, post, timing=pipe_ev if recording[0] else None)[-1] if n else None
         o = None
         for _ in range(n):
             o = step()
@@ -319,11 +322,17 @@ def main():
     prof = [eng.profile_read(c) for c in sorted(_lib.PROF_NAMES)]
     eng.profile(False)
     phases = None
-    if phase_ev:  # encoder = MFMA-bound phase, decode = HBM-bound phase (SURVEY.md §8(d) phase-wise roofline)
-        n = len(phase_ev)
-        enc_ms = sum(a.elapsed_time(b) for a, b, _, _ in phase_ev) / n
-        dec_ms = sum(b.elapsed_time(c) for _, b, c, _ in phase_ev) / n
-        gat_ms = sum(c.elapsed_time(d) for _, _, c, d in phase_ev) / n
+    if phase_ev or pipe_ev:  # encoder = MFMA-bound phase, decode = HBM-bound phase (SURVEY.md §8(d) phase-wise roofline)
+        if pipe_ev:  # pipelined: each phase on its own stream (batch i's decode overlaps batch i + 1's encode)
+            n = len(pipe_ev)
+            enc_ms = sum(a.elapsed_time(b) for a, b, _, _ in pipe_ev) / n
+            dec_ms = sum(c.elapsed_time(d) for _, _, c, d in pipe_ev) / n
+            gat_ms = 0.0  # (the all-gather runs inside the decode stream's post step, not timed apart)
+        else:
+            n = len(phase_ev)
+            enc_ms = sum(a.elapsed_time(b) for a, b, _, _ in phase_ev) / n
+            dec_ms = sum(b.elapsed_time(c) for _, b, c, _ in phase_ev) / n
+            gat_ms = sum(c.elapsed_time(d) for _, _, c, d in phase_ev) / n
         if ws > 1:  # the slowest rank's phases
             t = torch.tensor([enc_ms, dec_ms, gat_ms], device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -340,10 +349,12 @@ def main():
                                f"{L - 1} steps"},
             "allgather_ms_per_step": round(gat_ms, 3),
         }
+        if pipe_ev:
+            phases["overlapped"] = True  # encoder and decode ms of one batch; consecutive batches' phases overlap
     # multi-GPU self-check: the stop rule on the gathered ids equals the all-reduce form of SURVEY.md §8(e)
     # (each rank's per-column "every row ended" mask AND-reduced over ranks), so the line can be verified alone
     stop_check = None
-    if args.mode == "greedy" and pipe is None:
+    if args.mode == "greedy":
         mem = encode()
         ids, _ = eng.greedy_raw(mem, W.START_TOKEN, W.END_TOKEN, L)
         col = (ids[:, 1:] == W.END_TOKEN).all(dim=0).to(torch.int32)

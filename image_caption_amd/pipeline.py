@@ -80,11 +80,14 @@ class CaptionPipeline:
         self._owned = []
 
     def run(self, batches: Iterable[torch.Tensor],
-            post: Optional[Callable[[torch.Tensor], object]] = None) -> List[object]:
+            post: Optional[Callable[[torch.Tensor], object]] = None,
+            timing: Optional[list] = None) -> List[object]:
         """Greedy-caption every batch; returns post(ids) per batch (default: the raw int32 ids
         (B, max_len) before the stop rule).  `post` runs on the decode stream right after its batch's
         decode was enqueued and the NEXT batch's encode was enqueued, so a host sync inside it (the stop
-        rule's length) waits for this decode while the encoder keeps the GPU busy."""
+        rule's length) waits for this decode while the encoder keeps the GPU busy.  timing: a list that
+        receives per batch (encode start, encode end, decode start, decode end) timing events, recorded on the
+        encoder / decode streams (the two phases of consecutive batches overlap)."""
         eng, E, D = self.eng, self.enc_stream, self.dec_stream
         cur = torch.cuda.current_stream(eng.device)
         it = iter(batches)
@@ -94,19 +97,35 @@ class CaptionPipeline:
             return outs
         E.wait_stream(cur)  # inputs produced on the caller's stream
         D.wait_stream(cur)
-        with torch.cuda.stream(E):
-            mem = eng.encode(first)
+
+        def mark(stream):
+            if timing is None:
+                return None
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            return e
+
+        def encode(batch):
+            with torch.cuda.stream(E):
+                e0 = mark(E)
+                m = eng.encode(batch)
+                return m, (e0, mark(E))
+
+        mem, enc_ev = encode(first)
         nxt = next(it, None)
         while mem is not None:
             ev = E.record_event()
             D.wait_event(ev)
             mem.record_stream(D)
             with torch.cuda.stream(D):
+                d0 = mark(D)
                 ids, _ = eng.greedy_raw(mem, self.start, self.end, self.max_len)
+                d1 = mark(D)
+            if timing is not None:
+                timing.append((enc_ev[0], enc_ev[1], d0, d1))
             mem = None
             if nxt is not None:
-                with torch.cuda.stream(E):
-                    mem = eng.encode(nxt)
+                mem, enc_ev = encode(nxt)
                 nxt = next(it, None)
             with torch.cuda.stream(D):
                 outs.append(post(ids) if post is not None else ids)
