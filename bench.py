@@ -170,8 +170,8 @@ def main():
     ap.add_argument("--sequential", action="store_true",
                     help="greedy: run each step's encode, decode and stop rule one after the other (the round-5 "
                          "line) instead of the default batch pipeline - the encode of batch i+1 on its own stream "
-                         "beside the decode of batch i (image_caption_amd/pipeline.py; round 6: +3.7-4.3 %% on one "
-                         "box, profiles/r06/pipe_ab.txt)")
+                         "beside the decode of batch i, on 160 of the 256 CUs (image_caption_amd/pipeline.py; round 6: "
+                         "12,246-12,349 against 10,617 sequential, profiles/r06/pipe_cus_ab.txt, pipe_ab.txt)")
     ap.add_argument("--pipeline", action="store_true", help="(the default for greedy; kept for old command lines)")
     args = ap.parse_args()
 
@@ -279,7 +279,9 @@ def main():
 
         dcus = int(os.environ.get("ICAP_PIPE_DECODE_CUS", "0")) or None
         dprio = int(os.environ.get("ICAP_PIPE_DECODE_PRIORITY", "-1"))
-        pipe = CaptionPipeline(eng, W.START_TOKEN, W.END_TOKEN, L, decode_priority=dprio, decode_cus=dcus)
+        ecus = os.environ.get("ICAP_PIPE_ENC_CUS")  # measurement knob: the overlapped encodes' CU budget (0 = all CUs)
+        pipe = CaptionPipeline(eng, W.START_TOKEN, W.END_TOKEN, L, decode_priority=dprio, decode_cus=dcus,
+                               encoder_cus=int(ecus) if ecus else None)
 
         def post(ids):
             if ws > 1:
@@ -403,6 +405,13 @@ def main():
                      "launches_timed_per_step": dom["launches"] // args.steps,
                      "avg_launch_us": round(avg_ms * 1e3, 2),
                      "share_of_step": round(dom["ms"] * dom["scale"] / args.steps / step_ms, 3)})
+        if pipe is not None and pipe.overlap_cus and dom["kernel"] in sampled:
+            # pipelined: the overlapped encodes' persistent grids hold overlap_cus of the CUs (the first timed encode
+            # all of them), the rest left to the decode stream - frac of the CUs the kernel was given beside frac
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            granted = (cus + (args.steps - 1) * pipe.overlap_cus) / args.steps
+            roof["cus_granted_avg"] = round(granted, 1)
+            roof["frac_of_granted_cus"] = round(roof["frac"] * cus / granted, 4)
         cpu = None
         if roof["traffic"] is not None:
             roof["traffic_unit"] = f"bytes/launch (HBM-side, rocprofv3 PMC, {traffic_source(workload)})"
@@ -424,6 +433,7 @@ def main():
                        "decode_steps": L - 1, "output_len": int(out.shape[1]) if args.mode == "greedy" else None,
                        "parallelism": f"dp{ws}",
                        "pipelined": pipe is not None,
+                       "encoder_cus_overlapped": pipe.overlap_cus if pipe is not None else None,
                        # 1: bf16-exact decoder weights (the seeded synthetic weights); 2: hi/lo pairs (--fp32-weights, a
                        # real fp32 checkpoint) - both through the fused decode blocks (round 5)
                        "dec_weight_planes": eng.dec_weight_planes},

@@ -26,11 +26,20 @@ class CaptionPipeline:
     decode stream runs on n CUs and the encoder stream on the others (icap_stream_create_cu_mask),
     so neither phase waits for the other's workgroups to retire before it gets a CU."""
 
+    # the encoder CU budget of an encode that overlaps a decode (unmasked streams): round 6, bench sweep of 96-256 CUs
+    # (profiles/r06/pipe_tune.txt): 160-192 of 256 CUs leave the decode's small launches free CUs and give the
+    # best steps (21.1-21.4 against 23.2 ms with the encoder on every CU; 128 and below starve the encoder)
+    OVERLAP_CU_SHARE = 0.625
+
     def __init__(self, engine: Engine, start: int, end: int, max_len: int, decode_priority: int = -1,
-                 decode_cus: Optional[int] = None, check_range: bool = False):
+                 decode_cus: Optional[int] = None, check_range: bool = False, encoder_cus: Optional[int] = None):
         """check_range: after each run(), raise if the f16 encoder's fp16 range guard fired for any batch
         (Engine.range_overflowed, DESIGN.md §3: those memories must be re-encoded in bf16x2, which the drop-in
-        models do by themselves; a direct Engine / pipeline user opts in here).  Costs one stream sync per run."""
+        models do by themselves; a direct Engine / pipeline user opts in here).  Costs one stream sync per run.
+        encoder_cus (unmasked streams only): the persistent encoder grids' CU budget for the encodes that overlap a
+        decode (None = OVERLAP_CU_SHARE of the device's CUs, a multiple of 8 = whole CUs on each XCD, for an f16 ViT
+        engine - the budget sizes its persistent encoder grids - and 0 otherwise; 0 = every CU).
+        The first batch's encode, which has no decode beside it, runs at the engine's own budget."""
         import ctypes
 
         self.eng = engine
@@ -62,6 +71,14 @@ class CaptionPipeline:
             prio = max(min(decode_priority, lo), hi)
             self.enc_stream = torch.cuda.Stream(device=dev, priority=0)
             self.dec_stream = torch.cuda.Stream(device=dev, priority=prio)
+        self.overlap_cus = 0
+        if not decode_cus:
+            if encoder_cus is None and not (engine.kind == "vit" and engine.precision == "f16"):
+                encoder_cus = 0  # the budget sizes the f16 ViT encoder's persistent grids only
+            if encoder_cus is None:
+                cus = torch.cuda.get_device_properties(dev).multi_processor_count
+                encoder_cus = max(8, int(cus * self.OVERLAP_CU_SHARE) // 8 * 8)
+            self.overlap_cus = int(encoder_cus)
 
     def __del__(self):
         if getattr(self, "_owned", []):
@@ -113,6 +130,22 @@ class CaptionPipeline:
 
         mem, enc_ev = encode(first)
         nxt = next(it, None)
+        base = eng.encoder_cus
+        try:
+            self._overlap(outs, mem, enc_ev, nxt, it, post, timing, encode, mark)
+        finally:
+            if self.overlap_cus and eng.encoder_cus != base:
+                eng.set_encoder_cus(base)
+        cur.wait_stream(D)
+        cur.wait_stream(E)
+        if self.check_range and eng.range_overflowed():
+            raise RuntimeError("fp16 range guard: an f16 encoder activation overflowed in this run; re-encode the "
+                               "batches with a bf16x2 engine (Engine(..., precision='bf16x2'))")
+        return outs
+
+    def _overlap(self, outs, mem, enc_ev, nxt, it, post, timing, encode, mark):
+        """The steady state of run(): decode batch i on D, then encode batch i + 1 on E under the overlap budget."""
+        eng, E, D = self.eng, self.enc_stream, self.dec_stream
         while mem is not None:
             ev = E.record_event()
             D.wait_event(ev)
@@ -125,13 +158,9 @@ class CaptionPipeline:
                 timing.append((enc_ev[0], enc_ev[1], d0, d1))
             mem = None
             if nxt is not None:
+                if self.overlap_cus and eng.encoder_cus != self.overlap_cus:
+                    eng.set_encoder_cus(self.overlap_cus)
                 mem, enc_ev = encode(nxt)
                 nxt = next(it, None)
             with torch.cuda.stream(D):
                 outs.append(post(ids) if post is not None else ids)
-        cur.wait_stream(D)
-        cur.wait_stream(E)
-        if self.check_range and eng.range_overflowed():
-            raise RuntimeError("fp16 range guard: an f16 encoder activation overflowed in this run; re-encode the "
-                               "batches with a bf16x2 engine (Engine(..., precision='bf16x2'))")
-        return outs

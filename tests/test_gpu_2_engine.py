@@ -89,6 +89,16 @@ def test_pipeline_matches_sequential(cuda, vit_sd, B):
     got2 = CaptionPipeline(eng, 107, 108, 30).run(batches, lambda ids: apply_stop_rule(ids.long(), 108))
     for a, b in zip(got2, seq):
         assert torch.equal(a.cpu(), apply_stop_rule(b.long(), 108))
+    # the overlapped encodes run under an encoder CU budget (default OVERLAP_CU_SHARE of the CUs, round 6) that the
+    # run restores; the ids do not depend on it (each tile's k-loop is the same whichever block takes the tile)
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    assert eng.encoder_cus == 0
+    assert CaptionPipeline(eng, 107, 108, 30).overlap_cus == int(cus * CaptionPipeline.OVERLAP_CU_SHARE) // 8 * 8
+    for budget in (0, 96):
+        got3 = CaptionPipeline(eng, 107, 108, 30, encoder_cus=budget).run(batches)
+        assert eng.encoder_cus == 0
+        for a, b in zip(got3, seq):
+            assert torch.equal(a.cpu(), b)
 
 
 def test_profile_sampled_layers(cuda, vit_sd):

@@ -14,7 +14,7 @@ tail -1 $O/${T}_vit.json
 timeout -k 10 300 python bench.py --model grid --no-cpu-baseline > $O/${T}_grid.json 2> $O/${T}_grid.err || { tail -20 $O/${T}_grid.err; exit 1; }
 tail -1 $O/${T}_grid.json
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/${T}_prof.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof -o run -- python3 bench.py ${PROF_ARGS:---steps 3 --warmup 1} --no-cpu-baseline > $O/${T}_prof.log 2>&1 || exit 1
 f=$(find $O/${T}_prof -name "*kernel_trace.csv" | head -1)
 python3 tools/trace_decode.py $f > $O/${T}_decode_trace.txt 2>&1
 cp $(find $O/${T}_prof -name "*kernel_stats.csv" | head -1) $O/${T}_kernel_stats.csv
