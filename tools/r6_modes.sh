@@ -9,3 +9,5 @@ run beam5_vit --mode beam
 run beam5_grid --mode beam --model grid
 run vit_fp32w --fp32-weights
 run vit_fp32w_beam5 --fp32-weights --mode beam
+# (pipelined greedy is the default since the end of round 6: the other precisions through the pipeline, and sequential)
+[ -n "$R6_MODES_ALL" ] && { run vit_bf16x2 --precision bf16x2; run vit_i8x2 --precision i8x2; run vit_seq_fp32w --fp32-weights --sequential; run grid_seq --model grid --sequential; }
