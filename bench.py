@@ -280,8 +280,9 @@ def main():
         dcus = int(os.environ.get("ICAP_PIPE_DECODE_CUS", "0")) or None
         dprio = int(os.environ.get("ICAP_PIPE_DECODE_PRIORITY", "-1"))
         ecus = os.environ.get("ICAP_PIPE_ENC_CUS")  # measurement knob: the overlapped encodes' CU budget (0 = all CUs)
+        acus = os.environ.get("ICAP_PIPE_ENC_ATTN_CUS")  # and their attention's (0 = the GEMMs' budget)
         pipe = CaptionPipeline(eng, W.START_TOKEN, W.END_TOKEN, L, decode_priority=dprio, decode_cus=dcus,
-                               encoder_cus=int(ecus) if ecus else None)
+                               encoder_cus=int(ecus) if ecus else None, attention_cus=int(acus) if acus else None)
 
         def post(ids):
             if ws > 1:
@@ -434,6 +435,7 @@ def main():
                        "parallelism": f"dp{ws}",
                        "pipelined": pipe is not None,
                        "encoder_cus_overlapped": pipe.overlap_cus if pipe is not None else None,
+                       "attention_cus_overlapped": pipe.overlap_attn_cus if pipe is not None else None,
                        # 1: bf16-exact decoder weights (the seeded synthetic weights); 2: hi/lo pairs (--fp32-weights, a
                        # real fp32 checkpoint) - both through the fused decode blocks (round 5)
                        "dec_weight_planes": eng.dec_weight_planes},

@@ -120,6 +120,7 @@ SIGNATURES = {
     "icap_set_decode_chains": (c_int, [c_void_p, c_int]),
     "icap_set_decode_step": (c_int, [c_void_p, c_int]),
     "icap_set_encoder_cus": (c_int, [c_void_p, c_int]),
+    "icap_set_encoder_attention_cus": (c_int, [c_void_p, c_int]),
     "icap_range_check": (c_int, [c_void_p, c_void_p, POINTER(c_int)]),
     "icap_grid_tokens": (c_int, [c_void_p, c_int, c_int, POINTER(c_int)]),
     "icap_encode_grid_hw": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),

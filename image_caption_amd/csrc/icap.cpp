@@ -189,6 +189,7 @@ struct icap_handle {
   // BatchNorm stays on the bf16x2 trunk
   bool t16 = false;
   int enc_cus = 0;  // icap_set_encoder_cus: persistent encoder GEMM grids sized for a CU-masked stream (0 = all CUs)
+  int enc_attn_cus = 0;  // icap_set_encoder_attention_cus: the persistent encoder attention's own budget (0 = enc_cus)
   // hi/lo decoder weights (icap_model_desc.dec_weight_planes = 2: fp32 checkpoints that are not bf16-exact): every
   // decoder GEMM weight is packed as hi = bf16(W) and lo = bf16(W - hi) and the decode runs the unfused launches,
   // whose GEMMs add W_lo . X_hi; the train-mode dropout sampler keeps the fused blocks (W_hi only)
@@ -442,6 +443,13 @@ struct icap_handle {
     g.epi = epi; g.out = out;
     g.range_flag = range_word();
     g.max_grid = enc_cus;
+#ifdef ICAP_TOOLS
+    // (round 6, tools: per-GEMM-class overrides of a pipelined encode's CU budget)
+    if (enc_cus > 0) {
+      const int o = out == OUT_F32_RESID ? icap_knob("ICAP_PIPE_RESID_CUS", 0) : icap_knob("ICAP_PIPE_SO_CUS", 0);
+      if (o > 0) g.max_grid = o;
+    }
+#endif
     run_gemm(g, s);
   }
   // residual-output GEMMs (N = 768 / 512: a partial last round of tiles) split their tail tiles in K when
@@ -726,7 +734,11 @@ struct VitF16Run {
       const double flops = 4.0 * B * d.vit_heads * (double)T * T * 64;
       const double bytes = 2.0 * B * (double)T * V * 4;
       h->timed(PROF_ENC_ATTN, flops, bytes, s, [&] {
-        HIPCHK(launch_enc_attention(qkv, 3 * V, 0, B, T, d.vit_heads, 0.125f, a, V, 0, NS_F16, s, 1, h->enc_cus));
+        int acus = h->enc_attn_cus > 0 ? h->enc_attn_cus : h->enc_cus;
+#ifdef ICAP_TOOLS
+        if (h->enc_cus > 0 && icap_knob("ICAP_PIPE_ATTN_CUS", -1) >= 0) acus = icap_knob("ICAP_PIPE_ATTN_CUS", 0);
+#endif
+        HIPCHK(launch_enc_attention(qkv, 3 * V, 0, B, T, d.vit_heads, 0.125f, a, V, 0, NS_F16, s, 1, acus));
       });
     }
     h->gemm16(a, V, L.out, M, x, V, EPI_NONE, OUT_F32_RESID, s);
@@ -2066,7 +2078,8 @@ const char* icap_knobs_set() {
       "ICAP_ENC_ATTN16_FULL", "ICAP_XATTN16_S", "ICAP_EAF_ABL", "ICAP_DEC_MERGE", "ICAP_XATTN16_WK",
       "ICAP_F16P_ABL", "ICAP_F16_RES_BM", "ICAP_XATTN16_NB",
       "ICAP_HEAD_W4", "ICAP_DEC_STEP", "ICAP_DEC_STEP_TRACE", "ICAP_XDEC_TRACE", "ICAP_GEMM_NARROW",
-      "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW", "ICAP_DEC_FOLD", "ICAP_DEC_XCD", "ICAP_EAF_PERS"};
+      "ICAP_GEMM_C3", "ICAP_CONV_PRE", "ICAP_CONV_RMW", "ICAP_DEC_FOLD", "ICAP_DEC_XCD", "ICAP_EAF_PERS",
+      "ICAP_PIPE_RESID_CUS", "ICAP_PIPE_SO_CUS", "ICAP_PIPE_ATTN_CUS"};
   for (const char* n : names)
     if (getenv(n)) return n;
   return "";
@@ -2402,6 +2415,13 @@ int icap_set_encoder_cus(icap_handle* h, int cus) {
   return guarded([&] {
     REQUIRE(h && cus >= 0, "null handle / negative CU count");
     h->enc_cus = cus;
+  });
+}
+
+int icap_set_encoder_attention_cus(icap_handle* h, int cus) {
+  return guarded([&] {
+    REQUIRE(h && cus >= 0, "null handle / negative CU count");
+    h->enc_attn_cus = cus;
   });
 }
 

@@ -466,6 +466,15 @@ class Engine:
     def encoder_cus(self) -> int:
         return getattr(self, "_encoder_cus", 0)
 
+    def set_encoder_attention_cus(self, cus: int) -> None:
+        """The persistent encoder attention's own CU budget (0 = follow set_encoder_cus, the default)."""
+        check(self.lib.icap_set_encoder_attention_cus(self.handle, int(cus)), "icap_set_encoder_attention_cus")
+        self._encoder_attention_cus = int(cus)
+
+    @property
+    def encoder_attention_cus(self) -> int:
+        return getattr(self, "_encoder_attention_cus", 0)
+
     def set_graphs(self, enable: bool) -> None:
         """hipGraph replay of the decode loop (default on)."""
         check(self.lib.icap_set_graphs(self.handle, int(bool(enable))), "icap_set_graphs")

@@ -30,16 +30,22 @@ class CaptionPipeline:
     # (profiles/r06/pipe_tune.txt): 160-192 of 256 CUs leave the decode's small launches free CUs and give the
     # best steps (21.1-21.4 against 23.2 ms with the encoder on every CU; 128 and below starve the encoder)
     OVERLAP_CU_SHARE = 0.625
+    # and the persistent encoder attention's: 96 or 128 CUs against the GEMMs' 160 (+1-2 %, 96 ahead in two of three
+    # same-box sweeps, 48-64 starve it; profiles/r06/pipe_attn_ab.txt, pipe_attn_sweep.txt)
+    OVERLAP_ATTN_CU_SHARE = 0.375
 
     def __init__(self, engine: Engine, start: int, end: int, max_len: int, decode_priority: int = -1,
-                 decode_cus: Optional[int] = None, check_range: bool = False, encoder_cus: Optional[int] = None):
+                 decode_cus: Optional[int] = None, check_range: bool = False, encoder_cus: Optional[int] = None,
+                 attention_cus: Optional[int] = None):
         """check_range: after each run(), raise if the f16 encoder's fp16 range guard fired for any batch
         (Engine.range_overflowed, DESIGN.md §3: those memories must be re-encoded in bf16x2, which the drop-in
         models do by themselves; a direct Engine / pipeline user opts in here).  Costs one stream sync per run.
         encoder_cus (unmasked streams only): the persistent encoder grids' CU budget for the encodes that overlap a
         decode (None = OVERLAP_CU_SHARE of the device's CUs, a multiple of 8 = whole CUs on each XCD, for an f16 ViT
         engine - the budget sizes its persistent encoder grids - and 0 otherwise; 0 = every CU).
-        The first batch's encode, which has no decode beside it, runs at the engine's own budget."""
+        attention_cus: the same for the persistent encoder attention (None = OVERLAP_ATTN_CU_SHARE of the CUs when
+        the GEMMs have a budget).  The first batch's encode, which has no decode beside it, runs at the engine's own
+        budgets."""
         import ctypes
 
         self.eng = engine
@@ -71,14 +77,17 @@ class CaptionPipeline:
             prio = max(min(decode_priority, lo), hi)
             self.enc_stream = torch.cuda.Stream(device=dev, priority=0)
             self.dec_stream = torch.cuda.Stream(device=dev, priority=prio)
-        self.overlap_cus = 0
+        self.overlap_cus = self.overlap_attn_cus = 0
         if not decode_cus:
             if encoder_cus is None and not (engine.kind == "vit" and engine.precision == "f16"):
                 encoder_cus = 0  # the budget sizes the f16 ViT encoder's persistent grids only
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count
             if encoder_cus is None:
-                cus = torch.cuda.get_device_properties(dev).multi_processor_count
                 encoder_cus = max(8, int(cus * self.OVERLAP_CU_SHARE) // 8 * 8)
             self.overlap_cus = int(encoder_cus)
+            if attention_cus is None:
+                attention_cus = max(8, int(cus * self.OVERLAP_ATTN_CU_SHARE) // 8 * 8) if self.overlap_cus else 0
+            self.overlap_attn_cus = int(attention_cus)
 
     def __del__(self):
         if getattr(self, "_owned", []):
@@ -130,12 +139,13 @@ class CaptionPipeline:
 
         mem, enc_ev = encode(first)
         nxt = next(it, None)
-        base = eng.encoder_cus
+        base = (eng.encoder_cus, eng.encoder_attention_cus)
         try:
             self._overlap(outs, mem, enc_ev, nxt, it, post, timing, encode, mark)
         finally:
-            if self.overlap_cus and eng.encoder_cus != base:
-                eng.set_encoder_cus(base)
+            if (eng.encoder_cus, eng.encoder_attention_cus) != base:
+                eng.set_encoder_cus(base[0])
+                eng.set_encoder_attention_cus(base[1])
         cur.wait_stream(D)
         cur.wait_stream(E)
         if self.check_range and eng.range_overflowed():
@@ -160,6 +170,7 @@ class CaptionPipeline:
             if nxt is not None:
                 if self.overlap_cus and eng.encoder_cus != self.overlap_cus:
                     eng.set_encoder_cus(self.overlap_cus)
+                    eng.set_encoder_attention_cus(self.overlap_attn_cus)
                 mem, enc_ev = encode(nxt)
                 nxt = next(it, None)
             with torch.cuda.stream(D):

@@ -271,10 +271,17 @@ int icap_range_check(icap_handle* h, void* stream, int* overflowed);
  * another order). */
 int icap_set_decode_step(icap_handle* h, int mode);
 
-/* Encoder CU budget (batch pipelining, image_caption_amd/pipeline.py): the persistent encoder GEMMs launch at most
- * `cus` workgroups - the CUs of the CU-masked stream the encoder runs on while the previous batch decodes on the
- * others (0 = one per CU of the device, the default).  Results are unchanged. */
+/* Encoder CU budget (batch pipelining, image_caption_amd/pipeline.py): the persistent encoder GEMMs (and attention)
+ * launch at most `cus` workgroups - the CUs of the CU-masked stream the encoder runs on while the previous batch decodes
+ * on the others, or (unmasked streams, the pipeline's default) the CUs the encoder may hold so that the decode's
+ * launches find free ones (0 = one per CU of the device, the default).  Results are unchanged. */
 int icap_set_encoder_cus(icap_handle* h, int cus);
+
+/* The persistent encoder attention's own CU budget (0 = follow icap_set_encoder_cus, the default).  Round 6: an encode
+ * overlapping a decode on unmasked streams runs its GEMMs on 160 and its attention on 96 of 256 CUs (the attention's
+ * 16-wave workgroups at a 160-CU grid delay the decode more than they gain; profiles/r06/pipe_attn_ab.txt).  Results
+ * are unchanged. */
+int icap_set_encoder_attention_cus(icap_handle* h, int cus);
 
 /* Number of independent decode chains a batch is split into (1..4, default 1 since round 4; used from 80 rows per
  * chain): the chains are parallel branches of the captured decode graph (DESIGN.md §4 "Decode, round 4"). */

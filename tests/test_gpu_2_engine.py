@@ -94,9 +94,11 @@ def test_pipeline_matches_sequential(cuda, vit_sd, B):
     cus = torch.cuda.get_device_properties(cuda).multi_processor_count
     assert eng.encoder_cus == 0
     assert CaptionPipeline(eng, 107, 108, 30).overlap_cus == int(cus * CaptionPipeline.OVERLAP_CU_SHARE) // 8 * 8
-    for budget in (0, 96):
-        got3 = CaptionPipeline(eng, 107, 108, 30, encoder_cus=budget).run(batches)
-        assert eng.encoder_cus == 0
+    p = CaptionPipeline(eng, 107, 108, 30)
+    assert p.overlap_attn_cus == int(cus * CaptionPipeline.OVERLAP_ATTN_CU_SHARE) // 8 * 8
+    for budget, attn in ((0, None), (96, None), (160, 40)):
+        got3 = CaptionPipeline(eng, 107, 108, 30, encoder_cus=budget, attention_cus=attn).run(batches)
+        assert (eng.encoder_cus, eng.encoder_attention_cus) == (0, 0)
         for a, b in zip(got3, seq):
             assert torch.equal(a.cpu(), b)
 
