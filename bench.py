@@ -42,12 +42,15 @@ PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA, MI355X_MICROARCH.md chip table
 PEAK_I8_TOPS = 5000.0      # dense i8 MFMA (2x bf16 per clock: 16x16x64 i8 = cycles of 16x16x32 bf16), same table
 PEAK_HBM_GBS = 8000.0
 # HBM-side bytes per launch from rocprofv3 PMC passes over the default bench of each greedy workload
-# (tools/r3_profile.sh); the round-2 summary is the fallback for the ViT line
+# (tools/pmc.sh; the ViT line since the pipelined default: MODELS=vit PMC_ARGS="--steps 10 --warmup 3", the budgeted
+# persistent GEMMs fetch more per launch than on every CU; "vit_sequential" = the --sequential line's summary); the
+# round-2 summary is the fallback for the ViT line
 TRAFFIC_JSON = {"vit": [os.path.join(ROOT, "profiles", "r06", "pmc_traffic_vit.json"),
                         os.path.join(ROOT, "profiles", "r05", "pmc_traffic_vit.json"),
                         os.path.join(ROOT, "profiles", "r04", "pmc_traffic_vit.json"),
                         os.path.join(ROOT, "profiles", "r03", "pmc_traffic_vit.json"),
                         os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")],
+                "vit_sequential": [os.path.join(ROOT, "profiles", "r06", "pmc_traffic_vit_sequential.json")],
                 "grid": [os.path.join(ROOT, "profiles", "r06", "pmc_traffic_grid.json"),
                          os.path.join(ROOT, "profiles", "r05", "pmc_traffic_grid.json"),
                          os.path.join(ROOT, "profiles", "r04", "pmc_traffic_grid.json"),
@@ -379,6 +382,8 @@ def main():
             p["scale"] = prof_every if p["kernel"] in sampled else 1
         dom = max(prof, key=lambda p: p["ms"] * p["scale"])
         workload = args.model if args.mode == "greedy" else None  # the PMC summaries' workloads
+        if workload == "vit" and pipe is None:
+            workload = "vit_sequential"
         avg_ms = dom["ms"] / max(dom["launches"], 1)
         for p in prof:
             if not p["launches"]:
