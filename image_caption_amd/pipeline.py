@@ -22,9 +22,11 @@ from .engine import Engine
 
 
 class CaptionPipeline:
-    """decode_cus = None: two ordinary streams, the decode one at high priority.  decode_cus = n: the
-    decode stream runs on n CUs and the encoder stream on the others (icap_stream_create_cu_mask),
-    so neither phase waits for the other's workgroups to retire before it gets a CU."""
+    """decode_cus = None (the default): two ordinary streams, the decode one at high priority, and the encodes that
+    overlap a decode hold their persistent grids to a CU budget (encoder_cus / attention_cus) so the decode's launches
+    find free CUs.  decode_cus = n: the decode stream runs on n CUs and the encoder stream on the others
+    (icap_stream_create_cu_mask), so neither phase waits for the other's workgroups to retire before it gets a CU
+    (measured slower)."""
 
     # the encoder CU budget of an encode that overlaps a decode (unmasked streams): round 6, bench sweep of 96-256 CUs
     # (profiles/r06/pipe_tune.txt): 160-192 of 256 CUs leave the decode's small launches free CUs and give the
@@ -168,9 +170,10 @@ class CaptionPipeline:
                 timing.append((enc_ev[0], enc_ev[1], d0, d1))
             mem = None
             if nxt is not None:
-                if self.overlap_cus and eng.encoder_cus != self.overlap_cus:
-                    eng.set_encoder_cus(self.overlap_cus)
-                    eng.set_encoder_attention_cus(self.overlap_attn_cus)
+                target = (self.overlap_cus, self.overlap_attn_cus)
+                if any(target) and (eng.encoder_cus, eng.encoder_attention_cus) != target:
+                    eng.set_encoder_cus(target[0])
+                    eng.set_encoder_attention_cus(target[1])
                 mem, enc_ev = encode(nxt)
                 nxt = next(it, None)
             with torch.cuda.stream(D):
