@@ -286,6 +286,7 @@ def main():
         acus = os.environ.get("ICAP_PIPE_ENC_ATTN_CUS")  # and their attention's (0 = the GEMMs' budget)
         pipe = CaptionPipeline(eng, W.START_TOKEN, W.END_TOKEN, L, decode_priority=dprio, decode_cus=dcus,
                                encoder_cus=int(ecus) if ecus else None, attention_cus=int(acus) if acus else None)
+        pipe.defer_post = os.environ.get("ICAP_PIPE_DEFER_POST", "1") != "0"  # measurement knob (0: post not deferred)
 
         def post(ids):
             if ws > 1:

@@ -79,6 +79,8 @@ class CaptionPipeline:
             prio = max(min(decode_priority, lo), hi)
             self.enc_stream = torch.cuda.Stream(device=dev, priority=0)
             self.dec_stream = torch.cuda.Stream(device=dev, priority=prio)
+        self.post_stream = torch.cuda.Stream(device=dev)  # run()'s post steps, one batch behind the decode
+        self.defer_post = True
         self.overlap_cus = self.overlap_attn_cus = 0
         if not decode_cus:
             if encoder_cus is None and not (engine.kind == "vit" and engine.precision == "f16"):
@@ -111,9 +113,9 @@ class CaptionPipeline:
             post: Optional[Callable[[torch.Tensor], object]] = None,
             timing: Optional[list] = None) -> List[object]:
         """Greedy-caption every batch; returns post(ids) per batch (default: the raw int32 ids
-        (B, max_len) before the stop rule).  `post` runs on the decode stream right after its batch's
-        decode was enqueued and the NEXT batch's encode was enqueued, so a host sync inside it (the stop
-        rule's length) waits for this decode while the encoder keeps the GPU busy.  timing: a list that
+        (B, max_len) before the stop rule).  `post(ids)` of batch i runs on its own stream, ordered after batch i's
+        decode, once decode i + 1 and encode i + 2 are queued, so a host sync inside it (the stop rule's length)
+        waits for batch i's decode while both streams hold work.  timing: a list that
         receives per batch (encode start, encode end, decode start, decode end) timing events, recorded on the
         encoder / decode streams (the two phases of consecutive batches overlap)."""
         eng, E, D = self.eng, self.enc_stream, self.dec_stream
@@ -150,14 +152,29 @@ class CaptionPipeline:
                 eng.set_encoder_attention_cus(base[1])
         cur.wait_stream(D)
         cur.wait_stream(E)
+        cur.wait_stream(self.post_stream)
         if self.check_range and eng.range_overflowed():
             raise RuntimeError("fp16 range guard: an f16 encoder activation overflowed in this run; re-encode the "
                                "batches with a bf16x2 engine (Engine(..., precision='bf16x2'))")
         return outs
 
     def _overlap(self, outs, mem, enc_ev, nxt, it, post, timing, encode, mark):
-        """The steady state of run(): decode batch i on D, then encode batch i + 1 on E under the overlap budget."""
-        eng, E, D = self.eng, self.enc_stream, self.dec_stream
+        """The steady state of run(): decode batch i on D, then encode batch i + 1 on E under the overlap budget, then
+        the post step of batch i - 1 on its own stream P.  Round 6: with the post step of batch i on D right after
+        its encode was queued, the host sat in that step's sync until decode i ended and only then queued decode
+        i + 1 and encode i + 2, so every other batch both streams idled ≈ 0.8 ms (tools/r6_pipe_gaps.py,
+        profiles/r06/pipe_gaps.txt); one batch later, behind an event on decode i - 1 alone, the host waits while
+        decode i and encode i + 1 are already queued."""
+        eng, E, D, P = self.eng, self.enc_stream, self.dec_stream, self.post_stream
+        pending = None
+
+        def flush(item):
+            ids, done = item
+            P.wait_event(done)
+            ids.record_stream(P)
+            with torch.cuda.stream(P):
+                outs.append(post(ids) if post is not None else ids)
+
         while mem is not None:
             ev = E.record_event()
             D.wait_event(ev)
@@ -176,5 +193,11 @@ class CaptionPipeline:
                     eng.set_encoder_attention_cus(target[1])
                 mem, enc_ev = encode(nxt)
                 nxt = next(it, None)
-            with torch.cuda.stream(D):
-                outs.append(post(ids) if post is not None else ids)
+            if pending is not None:
+                flush(pending)
+            pending = (ids, D.record_event())
+            if not self.defer_post:  # (measurement: the round-6 form, the host waits for this batch's decode now)
+                flush(pending)
+                pending = None
+        if pending is not None:
+            flush(pending)
